@@ -1,0 +1,127 @@
+"""Synthetic relations for the join path.
+
+Counter-based splitmix64: ``v(seed, rel, col, row) = splitmix64(((seed<<40)|(rel<<36)|(col<<32)) + row)``.
+Column kinds:
+
+* ``("mod", M)``  -> ``v % M``       (join keys; SURVEY uses M = N)
+* ``("hi32",)``   -> ``v >> 32``     (filter / payload column, uniform in [0, 2^32))
+* ``("zipf", D, theta, perm_seed)``  -> Zipf(theta) rank over [0, D) mapped through a shared
+  rank->key permutation (config 5 shape)
+
+The same generator runs on the GPU inside libqe (``qe_gen_column``); tests check the two agree
+bit for bit.  Files use the reference's binary layout: ``u64 rows, u64 ncols`` then the columns
+column-major (reference src/utilities.c:105-121).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+GOLDEN_GAMMA = np.uint64(0x9E3779B97F4A7C15)
+MUL1 = np.uint64(0xBF58476D1CE4E5B9)
+MUL2 = np.uint64(0x94D049BB133111EB)
+
+
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    """Vectorised splitmix64 finaliser on uint64 (wrapping arithmetic)."""
+    with np.errstate(over="ignore"):
+        z = x.astype(np.uint64) + GOLDEN_GAMMA
+        z = (z ^ (z >> np.uint64(30))) * MUL1
+        z = (z ^ (z >> np.uint64(27))) * MUL2
+        return z ^ (z >> np.uint64(31))
+
+
+def splitmix64_int(x: int) -> int:
+    m = (1 << 64) - 1
+    z = (x + 0x9E3779B97F4A7C15) & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return z ^ (z >> 31)
+
+
+def stream_base(seed: int, rel: int, col: int) -> int:
+    return ((seed << 40) | (rel << 36) | (col << 32)) & ((1 << 64) - 1)
+
+
+def raw_column(seed: int, rel: int, col: int, rows: int, start: int = 0) -> np.ndarray:
+    base = np.uint64(stream_base(seed, rel, col))
+    idx = np.arange(start, start + rows, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        return splitmix64(idx + base)
+
+
+def zipf_cdf(domain: int, theta: float) -> np.ndarray:
+    """Cumulative Zipf(theta) weights over ranks 1..domain, normalised to [0, 1]."""
+    w = 1.0 / np.power(np.arange(1, domain + 1, dtype=np.float64), theta)
+    c = np.cumsum(w)
+    return c / c[-1]
+
+
+def zipf_perm(domain: int, perm_seed: int) -> np.ndarray:
+    """Rank -> key permutation shared by both sides of a skewed join (seeded)."""
+    keys = splitmix64(np.arange(domain, dtype=np.uint64) + np.uint64(stream_base(perm_seed, 15, 15)))
+    return np.argsort(keys, kind="stable").astype(np.uint64)
+
+
+def column(seed: int, rel: int, col: int, rows: int, kind: tuple, start: int = 0) -> np.ndarray:
+    v = raw_column(seed, rel, col, rows, start)
+    if kind[0] == "mod":
+        return v % np.uint64(kind[1])
+    if kind[0] == "hi32":
+        return v >> np.uint64(32)
+    if kind[0] == "zipf":
+        domain, theta, perm_seed = int(kind[1]), float(kind[2]), int(kind[3])
+        u = (v >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)   # 53-bit uniform
+        rank = np.searchsorted(zipf_cdf(domain, theta), u, side="right")
+        rank = np.minimum(rank, domain - 1)
+        return zipf_perm(domain, perm_seed)[rank]
+    raise ValueError(f"unknown column kind {kind!r}")
+
+
+@dataclass
+class RelSpec:
+    rows: int
+    kinds: list = field(default_factory=list)   # one kind tuple per column
+
+
+def chain_spec(n_rels: int, rows: int, key_domain: int | None = None) -> list[RelSpec]:
+    """every relation has c0 = v % N, c1 = v % N, c2 = v >> 32."""
+    d = key_domain if key_domain is not None else rows
+    return [RelSpec(rows, [("mod", d), ("mod", d), ("hi32",)]) for _ in range(n_rels)]
+
+
+def make_relations(specs: list[RelSpec], seed: int) -> list[list[np.ndarray]]:
+    return [[column(seed, r, c, s.rows, k) for c, k in enumerate(s.kinds)] for r, s in enumerate(specs)]
+
+
+def write_relation(path: str, cols: list[np.ndarray]) -> None:
+    rows = len(cols[0]) if cols else 0
+    with open(path, "wb") as f:
+        np.array([rows, len(cols)], dtype=np.uint64).tofile(f)
+        for c in cols:
+            np.ascontiguousarray(c, dtype=np.uint64).tofile(f)
+
+
+def read_relation(path: str) -> list[np.ndarray]:
+    m = np.fromfile(path, dtype=np.uint64)
+    rows, ncols = int(m[0]), int(m[1])
+    return [m[2 + j * rows: 2 + (j + 1) * rows] for j in range(ncols)]
+
+
+def write_dataset(dirpath: str, rels: list[list[np.ndarray]]) -> list[str]:
+    os.makedirs(dirpath, exist_ok=True)
+    paths = []
+    for i, cols in enumerate(rels):
+        p = os.path.join(dirpath, f"r{i}")
+        write_relation(p, cols)
+        paths.append(p)
+    return paths
+
+
+def protocol_input(paths: list[str], queries: str) -> str:
+    """stdin for the reference protocol: paths, Done, query lines (main/queries_main.c)."""
+    q = queries if queries.endswith("\n") or not queries else queries + "\n"
+    return "".join(p + "\n" for p in paths) + "Done\n" + q
