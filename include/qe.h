@@ -1,0 +1,152 @@
+/*
+ * qe.h -- C ABI of libqe, the MI355X-native sort-merge-join executor.
+ *
+ * The reference (giorgosLiako/Query-Compiler-Executor) has no FFI: its operator seam is two
+ * C functions called by execute_query (src/utilities.c:262-269) plus the static print_sums
+ * (src/utilities.c:197).  libqe replaces that seam at two levels:
+ *
+ *   1. the executor level -- qe_run_queries() runs a whole query batch with the reference's
+ *      stdin/stdout semantics (main/queries_main.c:24-68, src/utilities.c:258-300): the host-C
+ *      restatement of parsing.c / pred_arrange.c / the mid_result state machine drives the
+ *      device primitives below, and `queries` (host/qe_main.c) is the drop-in binary;
+ *   2. the primitive level -- one entry point per hot-path step,
+ *      each citing the reference function it replaces.
+ *
+ * Conventions: every call returns 0 on success and a negative QE_E* code on
+ * failure (qe_last_error() has the message); no exceptions cross the ABI; device buffers are
+ * plain pointers owned by the qe_ctx that allocated them (release with qe_list_free /
+ * qe_pairs_free); one host thread drives one ctx; work is ordered on the ctx's HIP stream and
+ * every call that returns a host-visible size or value synchronises that stream.
+ * Rowids are uint32 (relations below 2^32 rows), keys/values uint64, sums wrap mod 2^64.
+ */
+#ifndef QE_H
+#define QE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QE_ABI_VERSION 1
+
+enum {
+    QE_OK = 0,
+    QE_EINVAL = -1,      /* bad argument / reference-undefined input */
+    QE_EHIP = -2,        /* HIP runtime error */
+    QE_ENOMEM = -3,      /* device allocation failed */
+    QE_EEXIT = -4,       /* the reference would have called exit(EXIT_FAILURE) here */
+};
+
+typedef struct qe_ctx qe_ctx;
+
+/* A device column: `n` uint64 values (one column of a relation in HBM). */
+typedef struct { const uint64_t* d; uint64_t n; } qe_col;
+
+/* A device rowid list -- the reference's payload DArray (src/DArray.h, src/structs.h:44-49).
+ * flags bit 0 (QE_LIST_DISTINCT): no rowid occurs twice. */
+typedef struct { uint32_t* d; uint64_t n; uint64_t cap; uint32_t flags; } qe_list;
+#define QE_LIST_DISTINCT 1u
+
+/* Join input: (key, rowid) pairs in SoA -- the reference's `relation` of `tuple`s
+ * (src/structs.h:7-15).  `val == NULL` means rowid i for every i (a base column).
+ * flags: QE_PAIRS_DISTINCT (no rowid twice), QE_PAIRS_SORTED (ascending by key).
+ * owns: bit 0 key buffer, bit 1 val buffer belong to the pairs (freed by qe_pairs_free). */
+typedef struct { uint64_t* key; uint32_t* val; uint64_t n; uint32_t flags; uint32_t owns; } qe_pairs;
+#define QE_PAIRS_DISTINCT 1u
+#define QE_PAIRS_SORTED 2u
+
+/* Per-kernel statistics (profiling, qe_set_profiling). */
+typedef struct {
+    char     name[48];
+    uint64_t launches;
+    double   total_ms;        /* sum of HIP-event durations on the ctx stream */
+    double   alg_bytes;       /* algorithmic bytes summed over launches */
+} qe_kstat;
+
+/* ---- lifecycle --------------------------------------------------------------------------- */
+qe_ctx*     qe_init(int device);
+void        qe_fini(qe_ctx*);
+const char* qe_last_error(qe_ctx*);
+int         qe_abi_version(void);
+int         qe_device_name(qe_ctx*, char* out, size_t cap);
+int         qe_sync(qe_ctx*);
+
+/* ---- relations (loader: src/utilities.c:105-162) ------------------------------------------ */
+/* Copy a column-major host relation into HBM; returns the relation id (= load order) or <0. */
+int qe_load_relation(qe_ctx*, uint64_t rows, uint64_t ncols, const uint64_t* const* host_cols);
+/* Generate a relation on the device with the splitmix64 generator of SURVEY.md §9.1.
+ * kinds[c]: 0 = v % mod[c], 1 = v >> 32. Returns the relation id or <0. */
+int qe_gen_relation(qe_ctx*, uint64_t rows, uint64_t ncols, const int* kinds, const uint64_t* mods,
+                    uint64_t seed, uint32_t gen_rel, uint64_t row_start);
+int qe_relation_count(qe_ctx*);
+int qe_relation_column(qe_ctx*, int rel, int col, qe_col* out);
+int qe_relation_rows(qe_ctx*, int rel, uint64_t* rows);
+int qe_drop_relations(qe_ctx*);
+
+/* ---- executor (src/utilities.c:258-300 + main/queries_main.c) ------------------------------ */
+/* Run every query line of `text` (relation ids = load order) and return the exact stdout bytes
+ * the reference would print in a malloc'd buffer (free with qe_free_host).  Returns 0, QE_EEXIT
+ * when the reference would have exited with status 1 (output up to that point is returned), or
+ * another negative code. */
+int  qe_run_queries(qe_ctx*, const char* text, char** out, size_t* outlen);
+void qe_free_host(void*);
+
+/* ---- device primitives ---------------------------------------------------- */
+/* a1: exec_filter_rel_no_exists (src/filter.c:37-64): rowids i with col[i] op v, ascending. */
+int qe_filter_scan(qe_ctx*, qe_col col, char op, uint64_t v, qe_list* out);
+/* a2: exec_filter_rel_exists (src/filter.c:3-35): keep rowids r of `in` with col[r] op v, in
+ * order (the count is the stray stdout line of src/filter.c:32; printing is the caller's). */
+int qe_filter_refine(qe_ctx*, qe_col col, char op, uint64_t v, qe_list* inout);
+/* a3/a4: allocate_relation / allocate_relation_mid_results (src/join.c:96-142):
+ * (key = col[rowid], rowid) for rows == NULL (every row) or for each rowid of *rows in order. */
+int qe_gather_pairs(qe_ctx*, qe_col col, const qe_list* rows, qe_pairs* out);
+/* a5-a7: iterative_sort + quicksort (src/join.c:5-94, src/quicksort.c): ascending by key,
+ * stable (LSD radix over the key bits that vary). */
+int qe_sort_pairs(qe_ctx*, qe_pairs* inout);
+int qe_is_sorted(qe_ctx*, const qe_pairs*, int* sorted);
+/* a8: join_relations (src/join.c:325-392): aligned payload lists in key, R, S order.  Runs the
+ * merge-path kernel when both inputs are sorted and the exact two-pointer semantics otherwise. */
+int qe_merge_join(qe_ctx*, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS);
+/* a9: scan_join (src/join.c:395-423). */
+int qe_scan_join(qe_ctx*, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS);
+/* a8 dedup: the multiset non_duplicates[mode] of a join (src/join.c:358-367) as a dense count
+ * array over rowids [0, rows): counts[x] = #distinct (pR,pS) pairs whose mode-side rowid is x.
+ * R/S (nullable) are the join's inputs: when both are QE_PAIRS_SORTED and the other side is
+ * QE_PAIRS_DISTINCT the counts come from one annotated merge pass; otherwise from an exact
+ * sort + unique of the packed pairs (outR[i], outS[i]).  join_payloads only ever uses the
+ * driver as a sorted multiset (src/join.c:436-445), so counts are all it needs. */
+int qe_driver_counts(qe_ctx*, const qe_pairs* R, const qe_pairs* S, const qe_list* outR, const qe_list* outS,
+                     int mode, uint64_t rows, uint32_t** d_counts);
+/* a10: join_payloads (src/join.c:426-484): edit[i] repeated counts[last[i]] times, ordered by
+ * last[i] (stable).  |edit| < |last| is undefined in the reference -> QE_EINVAL. */
+int qe_join_payloads(qe_ctx*, const uint32_t* d_counts, uint64_t rows, const qe_list* last,
+                     const qe_list* edit, qe_list* out);
+/* a12: print_sums' inner loop (src/utilities.c:216-219): sum of col[rowid] mod 2^64. */
+int qe_checksum(qe_ctx*, qe_col col, const qe_list* rows, uint64_t* sum);
+
+/* ---- buffers ------------------------------------------------------------------------------- */
+int  qe_list_alloc(qe_ctx*, uint64_t n, qe_list* out);
+int  qe_list_from_host(qe_ctx*, const uint32_t* h, uint64_t n, uint32_t flags, qe_list* out);
+int  qe_list_to_host(qe_ctx*, const qe_list*, uint32_t* h);
+void qe_list_free(qe_ctx*, qe_list*);
+int  qe_pairs_from_host(qe_ctx*, const uint64_t* key, const uint32_t* val, uint64_t n, qe_pairs* out);
+int  qe_pairs_to_host(qe_ctx*, const qe_pairs*, uint64_t* key, uint32_t* val);
+void qe_pairs_free(qe_ctx*, qe_pairs*);
+void qe_counts_free(qe_ctx*, uint32_t*);
+int  qe_counts_to_host(qe_ctx*, const uint32_t* d, uint64_t n, uint32_t* h);
+/* device memory in use / cached by the ctx allocator (bytes) */
+int  qe_mem_stats(qe_ctx*, uint64_t* in_use, uint64_t* cached);
+int  qe_mem_trim(qe_ctx*);
+
+/* ---- profiling ----------------------------------------------------------------------------- */
+int qe_set_profiling(qe_ctx*, int on);
+int qe_reset_stats(qe_ctx*);
+/* fills up to `max` entries, returns the number of kernels with statistics */
+int qe_kernel_stats(qe_ctx*, qe_kstat* out, int max);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QE_H */

@@ -1,0 +1,170 @@
+// qe_device.h -- device helpers for gfx950 (wave64): lane masks, wave scans, and the
+// decoupled-lookback chained scan used by every single-pass compaction / radix pass.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "qe_internal.h"
+
+namespace qe {
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+__device__ __forceinline__ int wave_id() { return (int)(threadIdx.x >> 6); }
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    int l = lane_id();
+    return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    lo = (uint32_t)__shfl((int)lo, src, 64);
+    hi = (uint32_t)__shfl((int)hi, src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    lo = (uint32_t)__shfl_xor((int)lo, m, 64);
+    hi = (uint32_t)__shfl_xor((int)hi, m, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += shfl_xor_u64(v, m);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += (uint32_t)__shfl_xor((int)v, m, 64);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        uint32_t o = (uint32_t)__shfl_xor((int)v, m, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+// inclusive wave scan (u32)
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+    int l = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t o = (uint32_t)__shfl_up((int)v, d, 64);
+        if (l >= d) v += o;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
+    int l = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, d, 64);
+        uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d, 64);
+        uint64_t o = ((uint64_t)hi << 32) | lo;
+        if (l >= d) v += o;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// status word = [epoch:16 | flag:2 | value:46]: one 8-byte agent-scope store carries both the
+// value and its flag (the data is the flag, MI355X_MICROARCH "R2 granule"), so no fence is
+// needed and a word from an older launch (other epoch) reads as "not ready".
+__device__ __forceinline__ uint64_t lb_word(uint32_t epoch, uint64_t flag, uint64_t v) {
+    return ((uint64_t)epoch << 48) | (flag << 46) | (v & LB_VAL_MASK);
+}
+__device__ __forceinline__ uint32_t lb_flag(uint64_t w, uint32_t epoch) {
+    return ((uint32_t)(w >> 48) == epoch) ? (uint32_t)((w >> 46) & 3u) : 0u;
+}
+
+// Dynamic tile id: blocks take tickets in the order they start, so every predecessor of a
+// running tile is itself resident -- the lookback below cannot deadlock whatever the
+// dispatch order (cdna_hip_programming.md §1: dispatch order is undefined).
+__device__ __forceinline__ uint32_t take_ticket(uint32_t* ticket, uint32_t* lds_slot) {
+    if (threadIdx.x == 0) *lds_slot = atomicAdd(ticket, 1u);
+    __syncthreads();
+    uint32_t t = *lds_slot;
+    return t;
+}
+
+// Wave-parallel lookback for ONE running total per tile.  Called by a whole wave; returns the
+// exclusive prefix (same in every lane) and publishes the inclusive one.
+__device__ __forceinline__ uint64_t lookback_wave(uint64_t* status, uint32_t epoch, uint32_t tile,
+                                                  uint64_t agg) {
+    const int l = lane_id();
+    if (tile == 0) {
+        if (l == 0) st_agent(&status[0], lb_word(epoch, LB_FLAG_INC, agg));
+        return 0;
+    }
+    if (l == 0) st_agent(&status[tile], lb_word(epoch, LB_FLAG_AGG, agg));
+    uint64_t excl = 0;
+    int64_t base = (int64_t)tile - 1;
+    for (;;) {
+        int64_t idx = base - l;
+        uint64_t w = 0;
+        uint32_t f;
+        uint32_t spins = 0;
+        for (;;) {
+            if (idx >= 0) {
+                w = ld_agent(&status[idx]);
+                f = lb_flag(w, epoch);
+            } else {
+                w = 0;
+                f = (uint32_t)LB_FLAG_INC;
+            }
+            if (!__any(f == 0)) break;
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 24)) break;   // bounded spin: never hang the GPU
+        }
+        uint64_t inc = __ballot(f == LB_FLAG_INC);
+        int first = inc ? (__ffsll((unsigned long long)inc) - 1) : 64;
+        uint64_t v = (l <= first && idx >= 0) ? (w & LB_VAL_MASK) : 0;
+        excl += wave_sum_u64(v);
+        if (first < 64) break;
+        base -= 64;
+    }
+    if (l == 0) st_agent(&status[tile], lb_word(epoch, LB_FLAG_INC, excl + agg));
+    return excl;
+}
+
+// Thread-serial lookback for one of many per-tile totals (radix digits): `stride` words per
+// tile, this thread owns column `col`.  The aggregate must already be published.
+__device__ __forceinline__ uint64_t lookback_serial(uint64_t* status, uint32_t epoch, uint32_t tile,
+                                                    uint32_t stride, uint32_t col) {
+    uint64_t excl = 0;
+    int64_t idx = (int64_t)tile - 1;
+    uint32_t spins = 0;
+    while (idx >= 0) {
+        uint64_t w = ld_agent(&status[(uint64_t)idx * stride + col]);
+        uint32_t f = lb_flag(w, epoch);
+        if (f == 0) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 24)) break;
+            continue;
+        }
+        excl += w & LB_VAL_MASK;
+        if (f == LB_FLAG_INC) break;
+        --idx;
+    }
+    return excl;
+}
+
+}  // namespace qe

@@ -1,0 +1,155 @@
+// qe_internal.h -- shared internals of libqe (HIP C++ for gfx950).  Not part of the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/qe.h"
+
+namespace qe {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define QE_HIP(call)                                                                           \
+    do {                                                                                       \
+        hipError_t e_ = (call);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            throw ::qe::Error(QE_EHIP, std::string(#call) + ": " + hipGetErrorString(e_));    \
+    } while (0)
+
+struct Relation {
+    uint64_t rows = 0;
+    std::vector<uint64_t*> cols;
+};
+
+struct PendingEvent {
+    int kernel;
+    hipEvent_t a, b;
+    double bytes;
+};
+
+struct KStat {
+    std::string name;
+    uint64_t launches = 0;
+    double ms = 0, bytes = 0;
+};
+
+// Status words of the decoupled-lookback scans: [epoch:16 | flag:2 | value:46].
+constexpr uint64_t LB_FLAG_AGG = 1ull;
+constexpr uint64_t LB_FLAG_INC = 2ull;
+constexpr int LB_VAL_BITS = 46;
+constexpr uint64_t LB_VAL_MASK = (1ull << LB_VAL_BITS) - 1;
+constexpr int LB_MAX_COUNTERS = 65536;
+
+}  // namespace qe
+
+struct qe_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // caching device allocator: exact size classes, stream-ordered reuse on the one stream
+    std::multimap<size_t, void*> free_blocks;
+    std::unordered_map<void*, size_t> live;
+    uint64_t in_use = 0, cached = 0;
+
+    std::vector<qe::Relation> rels;
+
+    // decoupled-lookback state: status words + per-launch tile tickets, epoch-tagged so that
+    // nothing is cleared between launches (cleared when the 16-bit epoch wraps)
+    uint64_t* lb_status = nullptr;
+    size_t lb_status_words = 0;
+    uint32_t* lb_tickets = nullptr;
+    uint32_t lb_epoch = 0;
+
+    // small device scratch + pinned host mirror for scalar results
+    uint64_t* d_scratch = nullptr;   // 64 words
+    uint64_t* h_scratch = nullptr;   // pinned, 64 words
+
+    // profiling
+    bool prof = false;
+    std::vector<qe::PendingEvent> pending;
+    std::vector<hipEvent_t> event_pool;
+    std::vector<qe::KStat> kstats;
+    std::map<std::string, int> kindex;
+};
+
+namespace qe {
+
+void* dalloc(qe_ctx* c, size_t bytes);
+void dfree(qe_ctx* c, void* p);
+template <class T>
+T* dalloc_t(qe_ctx* c, size_t n) { return static_cast<T*>(dalloc(c, n * sizeof(T))); }
+
+// one epoch per lookback launch: returns (status base, ticket counter, epoch tag)
+struct LBSlot {
+    uint64_t* status;
+    uint32_t* ticket;
+    uint32_t epoch;
+};
+LBSlot lb_acquire(qe_ctx* c, size_t words);
+
+// profiling-aware launch bracket
+struct Timed {
+    qe_ctx* c;
+    int k = -1;
+    hipEvent_t a = nullptr, b = nullptr;
+    double bytes;
+    Timed(qe_ctx* c_, const char* name, double alg_bytes);
+    ~Timed();
+};
+
+void sync(qe_ctx* c);
+uint64_t read_u64(qe_ctx* c, const uint64_t* d);
+void read_words(qe_ctx* c, const uint64_t* d, uint64_t* h, int n);
+
+inline unsigned grid_for(uint64_t n, unsigned per_block, unsigned cap = 0x7fffffffu) {
+    uint64_t g = (n + per_block - 1) / per_block;
+    if (g == 0) g = 1;
+    return (unsigned)(g < cap ? g : cap);
+}
+
+// ---- primitives shared between translation units ------------------------------------------
+// compaction family (qe_scan.hip)
+uint64_t filter_scan(qe_ctx* c, const uint64_t* col, uint64_t n, char op, uint64_t v, uint32_t* out);
+uint64_t filter_refine(qe_ctx* c, const uint64_t* col, const uint32_t* in, uint64_t n, char op, uint64_t v,
+                       uint32_t* out);
+uint64_t scan_join_k(qe_ctx* c, const uint64_t* rk, const uint32_t* rv, const uint64_t* sk, const uint32_t* sv,
+                     uint64_t n, uint32_t* outR, uint32_t* outS);
+uint64_t compact_nonzero_pairs(qe_ctx* c, const uint32_t* counts, const uint32_t* last, const uint32_t* edit,
+                               uint64_t n, uint32_t* out_last, uint32_t* out_edit);
+
+// sort (qe_sort.hip): stable LSD radix; returns buffers (may alias inputs when 0 passes needed)
+struct SortOut {
+    void* keys;
+    uint32_t* vals;
+    bool keys_new, vals_new;
+};
+SortOut radix_sort_u64(qe_ctx* c, const uint64_t* keys, const uint32_t* vals /*nullable: iota*/, uint64_t n,
+                       bool with_vals);
+SortOut radix_sort_u32(qe_ctx* c, const uint32_t* keys, const uint32_t* vals, uint64_t n);
+
+}  // namespace qe
+
+#define QE_API_BEGIN(ctx) \
+    try {
+#define QE_API_END(ctx)                                                                         \
+    }                                                                                           \
+    catch (const ::qe::Error& e) {                                                              \
+        if (ctx) (ctx)->err = e.what();                                                         \
+        return e.code;                                                                          \
+    }                                                                                           \
+    catch (const std::exception& e) {                                                           \
+        if (ctx) (ctx)->err = e.what();                                                         \
+        return QE_EINVAL;                                                                       \
+    }

@@ -1,0 +1,742 @@
+// qe_join.hip -- merge join, payload propagation, gathers and checksums on gfx950.
+//
+// merge join (reference join_relations, src/join.c:325-392) on sorted inputs:
+//   mj_partition -- one binary search pair per R tile: the S window [lo, hi) the tile can match
+//   mj_tile<0>   -- per tile: R keys + the S window staged in LDS, each thread walks its 8
+//                   consecutive R keys through the window (merge walk, binary search past 16
+//                   steps), tile match count -> global exclusive scan (tile_scan)
+//   mj_tile<1>   -- recompute, block scan, then a load-balanced expansion: output slot o of the
+//                   tile finds its R element by binary search over the tile's prefix sums, so
+//                   every write of outR/outS is coalesced whatever the fan-out
+// Output order = key, then R order, then S order: exactly the reference's nested loop.
+// Unsorted inputs (possible in the reference's state machine) take
+// seq_merge_kernel, the literal two-pointer loop, so results stay identical there too.
+#include <algorithm>
+
+#include "qe_device.h"
+#include "qe_internal.h"
+
+namespace qe {
+
+constexpr int MJB = 256;
+constexpr int MJ_ITEMS = 8;
+constexpr int MJ_TILE = MJB * MJ_ITEMS;   // 2048 R elements per tile
+constexpr int MJ_WIN = 4096;              // S keys staged in LDS (32 KiB)
+constexpr int MJ_WALK = 16;               // linear steps before falling back to binary search
+
+enum : uint32_t { MJF_R_FANOUT = 1u, MJF_S_DUP = 2u, MJF_ERR = 4u };
+
+template <class F>
+__device__ __forceinline__ uint64_t lower_bound_f(uint64_t lo, uint64_t hi, uint64_t key, F at) {
+    while (lo < hi) {
+        uint64_t mid = lo + ((hi - lo) >> 1);
+        if (at(mid) < key) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+template <class F>
+__device__ __forceinline__ uint64_t upper_bound_f(uint64_t lo, uint64_t hi, uint64_t key, F at) {
+    while (lo < hi) {
+        uint64_t mid = lo + ((hi - lo) >> 1);
+        if (at(mid) <= key) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(256) mj_partition(const uint64_t* __restrict__ rk, uint64_t nR,
+                                                    const uint64_t* __restrict__ sk, uint64_t nS, uint32_t ntiles,
+                                                    uint64_t* __restrict__ win) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntiles) return;
+    uint64_t first = (uint64_t)t * MJ_TILE;
+    uint64_t last = std::min<uint64_t>(nR, first + MJ_TILE) - 1;
+    auto at = [&](uint64_t i) { return sk[i]; };
+    win[2 * t] = lower_bound_f(0, nS, rk[first], at);
+    win[2 * t + 1] = upper_bound_f(0, nS, rk[last], at);
+}
+
+// exclusive scan of `n` uint64 counts in place, single block (n = tiles, small); total -> *total
+__global__ void __launch_bounds__(1024) tile_scan_kernel(uint64_t* __restrict__ v, uint64_t n, uint64_t* total) {
+    __shared__ uint64_t wsum[16];
+    __shared__ uint64_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint64_t base = 0; base < n; base += 1024) {
+        uint64_t i = base + threadIdx.x;
+        uint64_t x = i < n ? v[i] : 0;
+        uint64_t inc = wave_incl_scan_u64(x);
+        if (lane_id() == 63) wsum[wave_id()] = inc;
+        __syncthreads();
+        uint64_t add = carry;
+        for (int w = 0; w < wave_id(); w++) add += wsum[w];
+        if (i < n) v[i] = inc - x + add;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = add + inc;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+// WRITE = 0: per-tile counts + flags (+ optional driver-count annotation)
+// WRITE = 1: expansion into outR / outS at tile offsets
+template <int WRITE>
+__global__ void __launch_bounds__(MJB) mj_tile(const uint64_t* __restrict__ rk, const uint32_t* __restrict__ rv,
+                                               uint64_t nR, const uint64_t* __restrict__ sk,
+                                               const uint32_t* __restrict__ sv, uint64_t nS,
+                                               const uint64_t* __restrict__ win, uint64_t* __restrict__ tile_counts,
+                                               uint32_t* __restrict__ outR, uint32_t* __restrict__ outS,
+                                               uint32_t* __restrict__ flags, uint32_t* __restrict__ annot) {
+    __shared__ uint64_t s_r[MJ_TILE];
+    __shared__ uint64_t s_s[MJ_WIN];
+    __shared__ uint32_t s_lo[WRITE ? MJ_TILE : 1];    // window-relative S start per R element
+    __shared__ uint32_t s_off[WRITE ? MJ_TILE : 1];   // tile-relative output offset per R element
+    __shared__ uint64_t s_red[MJB / 64];
+    __shared__ uint32_t s_flag;
+
+    const uint32_t tile = blockIdx.x;
+    const uint64_t base = (uint64_t)tile * MJ_TILE;
+    const uint32_t tn = (uint32_t)std::min<uint64_t>(MJ_TILE, nR - base);
+    const uint64_t wlo = win[2 * tile], whi = win[2 * tile + 1];
+    const uint64_t wn = whi - wlo;
+    const bool in_lds = wn <= MJ_WIN;
+    if (threadIdx.x == 0) s_flag = 0;
+    for (uint32_t i = threadIdx.x; i < tn; i += MJB) s_r[i] = rk[base + i];
+    if (in_lds)
+        for (uint32_t i = threadIdx.x; i < wn; i += MJB) s_s[i] = sk[wlo + i];
+    __syncthreads();
+
+    auto S = [&](uint64_t i) -> uint64_t { return in_lds ? s_s[i] : sk[wlo + i]; };
+
+    uint32_t cnt[MJ_ITEMS];
+    uint32_t lo_rel[MJ_ITEMS];
+    uint64_t tsum = 0;
+    uint32_t myflag = 0;
+    const uint32_t e0 = threadIdx.x * MJ_ITEMS;
+    uint64_t p = 0;   // walk pointer (window-relative)
+    bool have_p = false;
+    uint64_t prev_key = 0, prev_lo = 0, prev_hi = 0;
+#pragma unroll
+    for (int j = 0; j < MJ_ITEMS; j++) {
+        uint32_t e = e0 + j;
+        cnt[j] = 0;
+        lo_rel[j] = 0;
+        if (e >= tn) continue;
+        uint64_t key = s_r[e];
+        uint64_t lo, hi;
+        if (have_p && key == prev_key) {
+            lo = prev_lo;
+            hi = prev_hi;
+        } else {
+            if (!have_p) {
+                lo = lower_bound_f(0, wn, key, S);
+            } else {
+                lo = p;
+                int steps = 0;
+                while (lo < wn && S(lo) < key && steps < MJ_WALK) {
+                    lo++;
+                    steps++;
+                }
+                if (lo < wn && S(lo) < key) lo = lower_bound_f(lo, wn, key, S);
+            }
+            hi = lo;
+            int steps = 0;
+            while (hi < wn && S(hi) == key && steps < MJ_WALK) {
+                hi++;
+                steps++;
+            }
+            if (hi < wn && S(hi) == key) hi = upper_bound_f(hi, wn, key, S);
+            have_p = true;
+            p = hi;
+            prev_key = key;
+            prev_lo = lo;
+            prev_hi = hi;
+        }
+        uint32_t c = (uint32_t)(hi - lo);
+        cnt[j] = c;
+        lo_rel[j] = (uint32_t)lo;
+        tsum += c;
+        if (!WRITE) {
+            if (c > 1) myflag |= MJF_R_FANOUT;
+            if (c > 0) {
+                uint64_t nxt = e + 1 < tn ? s_r[e + 1] : (base + e + 1 < nR ? rk[base + e + 1] : ~key);
+                if (nxt == key) myflag |= MJF_S_DUP;
+                if (annot) annot[rv ? rv[base + e] : (uint32_t)(base + e)] = c;
+            }
+        }
+    }
+
+    if (!WRITE) {
+        uint64_t s = wave_sum_u64(tsum);
+        if (lane_id() == 0) s_red[wave_id()] = s;
+        if (myflag) atomicOr(&s_flag, myflag);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint64_t t = 0;
+            for (int w = 0; w < MJB / 64; w++) t += s_red[w];
+            tile_counts[tile] = t;
+            if (s_flag) atomicOr(flags, s_flag);
+        }
+        return;
+    }
+
+    // block exclusive scan of per-thread sums
+    uint64_t inc = wave_incl_scan_u64(tsum);
+    if (lane_id() == 63) s_red[wave_id()] = inc;
+    __syncthreads();
+    uint64_t add = 0;
+    for (int w = 0; w < wave_id(); w++) add += s_red[w];
+    uint64_t run = inc - tsum + add;
+    uint64_t btotal = 0;
+    for (int w = 0; w < MJB / 64; w++) btotal += s_red[w];
+#pragma unroll
+    for (int j = 0; j < MJ_ITEMS; j++) {
+        uint32_t e = e0 + j;
+        if (e < tn) {
+            s_off[e] = (uint32_t)run;
+            s_lo[e] = lo_rel[j];
+            run += cnt[j];
+        }
+    }
+    __syncthreads();
+    const uint64_t gofs = tile_counts[tile];
+    for (uint64_t o = threadIdx.x; o < btotal; o += MJB) {
+        // last element with s_off[e] <= o
+        uint32_t a = 0, b = tn;
+        while (b - a > 1) {
+            uint32_t m = (a + b) >> 1;
+            if (s_off[m] <= o) a = m;
+            else b = m;
+        }
+        uint64_t k = o - s_off[a];
+        uint64_t sidx = wlo + s_lo[a] + k;
+        outR[gofs + o] = rv ? rv[base + a] : (uint32_t)(base + a);
+        outS[gofs + o] = sv ? sv[sidx] : (uint32_t)sidx;
+    }
+}
+
+// The reference's two-pointer loop verbatim (src/join.c:342-377) for inputs that are not
+// sorted.  One lane: it is only reached by state-machine paths the reference itself runs on
+// unsorted lists (SURVEY.md A.2 consequences), never on the measured configs.
+// MODE 0 counts, MODE 1 writes (optionally only R, for join_payloads' merge).
+template <int MODE>
+__global__ void seq_merge_kernel(const uint64_t* rk, const uint32_t* rv, uint64_t nR, const uint64_t* sk,
+                                 const uint32_t* sv, uint64_t nS, uint32_t* outR, uint32_t* outS, uint64_t* total) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    uint64_t pr = 0, s_start = 0, o = 0;
+    while (pr < nR && s_start < nS) {
+        uint64_t ps = s_start;
+        int flag = 0;
+        uint64_t key = rk[pr];
+        while (ps < nS) {
+            uint64_t skey = sk[ps];
+            if (key < skey) break;
+            if (key > skey) {
+                ps++;
+                if (flag == 0) s_start = ps;
+            } else {
+                if (MODE == 1) {
+                    outR[o] = rv ? rv[pr] : (uint32_t)pr;
+                    if (outS) outS[o] = sv ? sv[ps] : (uint32_t)ps;
+                }
+                o++;
+                flag = 1;
+                ps++;
+            }
+        }
+        pr++;
+    }
+    *total = o;
+}
+
+__global__ void __launch_bounds__(256) is_sorted_kernel(const uint64_t* __restrict__ k, uint64_t n, uint32_t* bad) {
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    bool b = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += stride)
+        b |= k[i] > k[i + 1];
+    if (__any(b) && lane_id() == 0) atomicOr(bad, 1u);
+}
+
+__global__ void __launch_bounds__(256) gather_keys_kernel(const uint64_t* __restrict__ col,
+                                                          const uint32_t* __restrict__ rows, uint64_t n,
+                                                          uint64_t* __restrict__ out) {
+    uint64_t i4 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i4 + 3 < n) {
+        uint4 r = *reinterpret_cast<const uint4*>(rows + i4);
+        ulonglong2 a, b;
+        a.x = col[r.x];
+        a.y = col[r.y];
+        b.x = col[r.z];
+        b.y = col[r.w];
+        *reinterpret_cast<ulonglong2*>(out + i4) = a;
+        *reinterpret_cast<ulonglong2*>(out + i4 + 2) = b;
+    } else {
+        for (uint64_t i = i4; i < n; i++) out[i] = col[rows[i]];
+    }
+}
+
+__global__ void __launch_bounds__(256) widen_u32_kernel(const uint32_t* __restrict__ in, uint64_t n,
+                                                        uint64_t* __restrict__ out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = in[i];
+}
+
+// sum of col[rowid] mod 2^64 (print_sums, src/utilities.c:216-219); rows == null: whole column
+__global__ void __launch_bounds__(256) checksum_kernel(const uint64_t* __restrict__ col,
+                                                       const uint32_t* __restrict__ rows, uint64_t n,
+                                                       unsigned long long* __restrict__ out) {
+    uint64_t s = 0;
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 4;
+    for (uint64_t i4 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i4 < n; i4 += stride) {
+        if (i4 + 3 < n) {
+            if (rows) {
+                uint4 r = *reinterpret_cast<const uint4*>(rows + i4);
+                s += col[r.x] + col[r.y] + col[r.z] + col[r.w];
+            } else {
+                ulonglong2 a = *reinterpret_cast<const ulonglong2*>(col + i4);
+                ulonglong2 b = *reinterpret_cast<const ulonglong2*>(col + i4 + 2);
+                s += a.x + a.y + b.x + b.y;
+            }
+        } else {
+            for (uint64_t i = i4; i < n; i++) s += col[rows ? rows[i] : i];
+        }
+    }
+    s = wave_sum_u64(s);
+    __shared__ uint64_t red[4];
+    if (lane_id() == 0) red[wave_id()] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(out, (unsigned long long)(red[0] + red[1] + red[2] + red[3]));
+}
+
+// ---- join_payloads expansion (src/join.c:452-476 on sorted inputs) -------------------------------
+// element i (sorted by last) is emitted counts[last[i]] times
+constexpr int XB = 256, X_ITEMS = 8, X_TILE = XB * X_ITEMS;
+
+template <int WRITE>
+__global__ void __launch_bounds__(XB) expand_kernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                                    uint64_t n, const uint32_t* __restrict__ counts,
+                                                    uint64_t* __restrict__ tile_counts, uint32_t* __restrict__ out,
+                                                    uint32_t* __restrict__ flags) {
+    __shared__ uint32_t s_off[WRITE ? X_TILE : 1];
+    __shared__ uint64_t s_red[XB / 64];
+    const uint32_t tile = blockIdx.x;
+    const uint64_t base = (uint64_t)tile * X_TILE;
+    const uint32_t tn = (uint32_t)std::min<uint64_t>(X_TILE, n - base);
+    uint32_t c[X_ITEMS];
+    uint64_t tsum = 0;
+    uint32_t mx = 0;
+    const uint32_t e0 = threadIdx.x * X_ITEMS;
+#pragma unroll
+    for (int j = 0; j < X_ITEMS; j++) {
+        uint32_t e = e0 + j;
+        c[j] = e < tn ? counts[keys[base + e]] : 0;
+        tsum += c[j];
+        mx = c[j] > mx ? c[j] : mx;
+    }
+    if (!WRITE) {
+        uint64_t s = wave_sum_u64(tsum);
+        mx = wave_max_u32(mx);
+        if (lane_id() == 0) {
+            s_red[wave_id()] = s;
+            if (mx > 1) atomicOr(flags, 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) tile_counts[tile] = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+        return;
+    }
+    uint64_t inc = wave_incl_scan_u64(tsum);
+    if (lane_id() == 63) s_red[wave_id()] = inc;
+    __syncthreads();
+    uint64_t add = 0;
+    for (int w = 0; w < wave_id(); w++) add += s_red[w];
+    uint64_t run = inc - tsum + add;
+    uint64_t btotal = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+#pragma unroll
+    for (int j = 0; j < X_ITEMS; j++) {
+        uint32_t e = e0 + j;
+        if (e < tn) {
+            s_off[e] = (uint32_t)run;
+            run += c[j];
+        }
+    }
+    __syncthreads();
+    const uint64_t gofs = tile_counts[tile];
+    for (uint64_t o = threadIdx.x; o < btotal; o += XB) {
+        uint32_t a = 0, b = tn;
+        while (b - a > 1) {
+            uint32_t m = (a + b) >> 1;
+            if (s_off[m] <= o) a = m;
+            else b = m;
+        }
+        out[gofs + o] = vals[base + a];
+    }
+}
+
+// ---- general driver counts: exact distinct (pR, pS) pairs by sort + unique -------------------------
+__global__ void __launch_bounds__(256) pack_pairs_kernel(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
+                                                         uint64_t n, uint64_t* __restrict__ out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = ((uint64_t)a[i] << 32) | b[i];
+}
+
+__global__ void __launch_bounds__(256) unique_count_kernel(const uint64_t* __restrict__ p, uint64_t n, int mode,
+                                                           uint32_t* __restrict__ counts, uint64_t rows,
+                                                           uint32_t* __restrict__ err) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (i > 0 && p[i] == p[i - 1]) return;
+    uint32_t x = mode == 0 ? (uint32_t)(p[i] >> 32) : (uint32_t)p[i];
+    if (x < rows) atomicAdd(&counts[x], 1u);
+    else atomicOr(err, 1u);
+}
+
+}  // namespace qe
+
+using namespace qe;
+
+// =============================================================================================
+// C ABI: device primitives
+// =============================================================================================
+namespace {
+
+enum : uint32_t { PF_DISTINCT = 1u, PF_SORTED = 2u };
+
+const char* op_ok(char op) { return (op == '=' || op == '<' || op == '>') ? nullptr : "Wrong operator"; }
+
+// merge join on sorted inputs; returns pair count and flags
+void merge_sorted(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS, uint32_t* oflags) {
+    const uint64_t nR = R->n, nS = S->n;
+    outR->n = outS->n = 0;
+    *oflags = 0;
+    if (nR == 0 || nS == 0) {
+        outR->d = dalloc_t<uint32_t>(c, 1);
+        outS->d = dalloc_t<uint32_t>(c, 1);
+        outR->cap = outS->cap = 0;
+        return;
+    }
+    const uint32_t nt = (uint32_t)((nR + MJ_TILE - 1) / MJ_TILE);
+    uint64_t* win = dalloc_t<uint64_t>(c, 2 * (uint64_t)nt);
+    uint64_t* tc = dalloc_t<uint64_t>(c, nt);
+    uint32_t* d_flags = (uint32_t*)(c->d_scratch + 16);
+    QE_HIP(hipMemsetAsync(d_flags, 0, 4, c->stream));
+    {
+        Timed t(c, "mj_partition", 0);
+        hipLaunchKernelGGL(mj_partition, dim3((nt + 255) / 256), dim3(256), 0, c->stream, R->key, nR, S->key, nS, nt,
+                           win);
+        QE_HIP(hipGetLastError());
+    }
+    {
+        Timed t(c, "mj_count", 8.0 * nR + 8.0 * nS);
+        hipLaunchKernelGGL(mj_tile<0>, dim3(nt), dim3(MJB), 0, c->stream, R->key, R->val, nR, S->key, S->val, nS, win,
+                           tc, nullptr, nullptr, d_flags, nullptr);
+        QE_HIP(hipGetLastError());
+        hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, c->stream, tc, (uint64_t)nt, c->d_scratch + 17);
+        QE_HIP(hipGetLastError());
+    }
+    uint64_t h[2];
+    read_words(c, c->d_scratch + 16, h, 2);
+    const uint64_t P = h[1];
+    *oflags = (uint32_t)h[0];
+    outR->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(P, 1));
+    outS->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(P, 1));
+    outR->cap = outS->cap = P;
+    outR->n = outS->n = P;
+    if (P) {
+        Timed t(c, "mj_write", 12.0 * nR + 12.0 * nS + 8.0 * P);
+        hipLaunchKernelGGL(mj_tile<1>, dim3(nt), dim3(MJB), 0, c->stream, R->key, R->val, nR, S->key, S->val, nS, win,
+                           tc, outR->d, outS->d, nullptr, nullptr);
+        QE_HIP(hipGetLastError());
+    }
+    dfree(c, win);
+    dfree(c, tc);
+}
+
+void merge_sequential(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS) {
+    uint64_t* d_total = c->d_scratch + 20;
+    {
+        Timed t(c, "seq_merge", 0);
+        hipLaunchKernelGGL(seq_merge_kernel<0>, dim3(1), dim3(64), 0, c->stream, R->key, R->val, R->n, S->key, S->val,
+                           S->n, nullptr, nullptr, d_total);
+        QE_HIP(hipGetLastError());
+    }
+    uint64_t P = read_u64(c, d_total);
+    outR->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(P, 1));
+    outS->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(P, 1));
+    outR->n = outS->n = outR->cap = outS->cap = P;
+    if (P) {
+        Timed t(c, "seq_merge", 0);
+        hipLaunchKernelGGL(seq_merge_kernel<1>, dim3(1), dim3(64), 0, c->stream, R->key, R->val, R->n, S->key, S->val,
+                           S->n, outR->d, outS->d, d_total);
+        QE_HIP(hipGetLastError());
+    }
+}
+
+bool pairs_sorted(qe_ctx* c, const qe_pairs* p) {
+    if (p->flags & PF_SORTED) return true;
+    if (p->n < 2) return true;
+    uint32_t* bad = (uint32_t*)(c->d_scratch + 24);
+    QE_HIP(hipMemsetAsync(bad, 0, 4, c->stream));
+    {
+        Timed t(c, "is_sorted", 8.0 * p->n);
+        hipLaunchKernelGGL(is_sorted_kernel, dim3(grid_for(p->n, 256 * 8, 4096)), dim3(256), 0, c->stream, p->key,
+                           p->n, bad);
+        QE_HIP(hipGetLastError());
+    }
+    return (read_u64(c, c->d_scratch + 24) & 0xFFFFFFFFull) == 0;
+}
+
+// dense driver counts by exact sort + unique of the packed pairs (any input order)
+uint32_t* driver_counts_general(qe_ctx* c, const qe_list* outR, const qe_list* outS, int mode, uint64_t rows) {
+    uint32_t* cnt = dalloc_t<uint32_t>(c, std::max<uint64_t>(rows, 1));
+    QE_HIP(hipMemsetAsync(cnt, 0, std::max<uint64_t>(rows, 1) * 4, c->stream));
+    const uint64_t n = outR->n;
+    if (n == 0) return cnt;
+    uint64_t* packed = dalloc_t<uint64_t>(c, n);
+    {
+        Timed t(c, "dedup_pack", 16.0 * n);
+        hipLaunchKernelGGL(pack_pairs_kernel, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, outR->d, outS->d, n,
+                           packed);
+        QE_HIP(hipGetLastError());
+    }
+    SortOut so = radix_sort_u64(c, packed, nullptr, n, false);
+    const uint64_t* sp = (const uint64_t*)so.keys;
+    uint32_t* err = (uint32_t*)(c->d_scratch + 26);
+    QE_HIP(hipMemsetAsync(err, 0, 4, c->stream));
+    {
+        Timed t(c, "dedup_count", 8.0 * n);
+        hipLaunchKernelGGL(unique_count_kernel, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, sp, n, mode, cnt, rows,
+                           err);
+        QE_HIP(hipGetLastError());
+    }
+    if (so.keys_new) dfree(c, so.keys);
+    dfree(c, packed);
+    if (read_u64(c, c->d_scratch + 26) & 0xFFFFFFFFull) throw Error(QE_EINVAL, "driver rowid out of range");
+    return cnt;
+}
+
+// fast path: sorted merge inputs whose partner side is distinct -> the count of a rowid is the
+// length of its partner's equal-key run (every pair of that run is distinct)
+uint32_t* driver_counts_sorted(qe_ctx* c, const qe_pairs* A, const qe_pairs* B, uint64_t rows) {
+    uint32_t* cnt = dalloc_t<uint32_t>(c, std::max<uint64_t>(rows, 1));
+    QE_HIP(hipMemsetAsync(cnt, 0, std::max<uint64_t>(rows, 1) * 4, c->stream));
+    if (A->n == 0 || B->n == 0) return cnt;
+    const uint32_t nt = (uint32_t)((A->n + MJ_TILE - 1) / MJ_TILE);
+    uint64_t* win = dalloc_t<uint64_t>(c, 2 * (uint64_t)nt);
+    uint64_t* tc = dalloc_t<uint64_t>(c, nt);
+    uint32_t* d_flags = (uint32_t*)(c->d_scratch + 28);
+    {
+        Timed t(c, "mj_annotate", 12.0 * A->n + 8.0 * B->n);
+        hipLaunchKernelGGL(mj_partition, dim3((nt + 255) / 256), dim3(256), 0, c->stream, A->key, A->n, B->key, B->n,
+                           nt, win);
+        QE_HIP(hipGetLastError());
+        hipLaunchKernelGGL(mj_tile<0>, dim3(nt), dim3(MJB), 0, c->stream, A->key, A->val, A->n, B->key, B->val, B->n,
+                           win, tc, nullptr, nullptr, d_flags, cnt);
+        QE_HIP(hipGetLastError());
+    }
+    dfree(c, win);
+    dfree(c, tc);
+    return cnt;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qe_filter_scan(qe_ctx* c, qe_col col, char op, uint64_t v, qe_list* out) {
+    QE_API_BEGIN(c)
+    if (op_ok(op)) throw Error(QE_EINVAL, op_ok(op));
+    out->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(col.n, 1));
+    out->cap = col.n;
+    out->n = filter_scan(c, col.d, col.n, op, v, out->d);
+    out->flags = QE_LIST_DISTINCT;
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_filter_refine(qe_ctx* c, qe_col col, char op, uint64_t v, qe_list* inout) {
+    QE_API_BEGIN(c)
+    if (op_ok(op)) throw Error(QE_EINVAL, op_ok(op));
+    if (inout->n == 0) return 0;
+    uint32_t* o = dalloc_t<uint32_t>(c, inout->n);
+    uint64_t m = filter_refine(c, col.d, inout->d, inout->n, op, v, o);
+    dfree(c, inout->d);
+    inout->d = o;
+    inout->cap = inout->n;
+    inout->n = m;
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_gather_pairs(qe_ctx* c, qe_col col, const qe_list* rows, qe_pairs* out) {
+    QE_API_BEGIN(c)
+    if (!rows) {
+        out->key = const_cast<uint64_t*>(col.d);
+        out->val = nullptr;
+        out->n = col.n;
+        out->flags = PF_DISTINCT;
+        out->owns = 0;
+        return 0;
+    }
+    const uint64_t n = rows->n;
+    out->key = dalloc_t<uint64_t>(c, std::max<uint64_t>(n, 1));
+    out->val = rows->d;   // borrowed: the caller keeps the list alive while the pairs live
+    out->n = n;
+    out->flags = (rows->flags & QE_LIST_DISTINCT) ? PF_DISTINCT : 0;
+    out->owns = 1;
+    if (n) {
+        Timed t(c, "gather_keys", 12.0 * n + 8.0 * n);
+        hipLaunchKernelGGL(gather_keys_kernel, dim3(grid_for((n + 3) / 4, 256)), dim3(256), 0, c->stream, col.d,
+                           rows->d, n, out->key);
+        QE_HIP(hipGetLastError());
+    }
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_sort_pairs(qe_ctx* c, qe_pairs* p) {
+    QE_API_BEGIN(c)
+    if (p->flags & PF_SORTED) return 0;
+    SortOut so = radix_sort_u64(c, p->key, p->val, p->n, true);
+    if (so.keys_new) {
+        if (p->owns & 1) dfree(c, p->key);
+        p->key = (uint64_t*)so.keys;
+        p->owns |= 1;
+    }
+    if (so.vals_new) {
+        if (p->owns & 2) dfree(c, p->val);
+        p->val = so.vals;
+        p->owns |= 2;
+    }
+    p->flags |= PF_SORTED;
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_is_sorted(qe_ctx* c, const qe_pairs* p, int* sorted) {
+    QE_API_BEGIN(c)
+    *sorted = pairs_sorted(c, p) ? 1 : 0;
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_merge_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS) {
+    QE_API_BEGIN(c)
+    const bool sorted = pairs_sorted(c, R) && pairs_sorted(c, S);
+    uint32_t fl = MJF_R_FANOUT | MJF_S_DUP;
+    if (sorted) merge_sorted(c, R, S, outR, outS, &fl);
+    else merge_sequential(c, R, S, outR, outS);
+    outR->flags = ((R->flags & PF_DISTINCT) && sorted && !(fl & MJF_R_FANOUT)) ? QE_LIST_DISTINCT : 0;
+    outS->flags = ((S->flags & PF_DISTINCT) && sorted && !(fl & MJF_S_DUP)) ? QE_LIST_DISTINCT : 0;
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_scan_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS) {
+    QE_API_BEGIN(c)
+    uint64_t n = std::min(R->n, S->n);
+    outR->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
+    outS->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
+    outR->cap = outS->cap = n;
+    uint64_t m = scan_join_k(c, R->key, R->val, S->key, S->val, n, outR->d, outS->d);
+    outR->n = outS->n = m;
+    outR->flags = (R->flags & PF_DISTINCT) ? QE_LIST_DISTINCT : 0;
+    outS->flags = (S->flags & PF_DISTINCT) ? QE_LIST_DISTINCT : 0;
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_driver_counts(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const qe_list* outR, const qe_list* outS,
+                     int mode, uint64_t rows, uint32_t** d_counts) {
+    QE_API_BEGIN(c)
+    if (mode != 0 && mode != 1) throw Error(QE_EINVAL, "mode");
+    const bool sorted_inputs = R && S && (R->flags & PF_SORTED) && (S->flags & PF_SORTED);
+    if (sorted_inputs && mode == 0 && (S->flags & PF_DISTINCT)) *d_counts = driver_counts_sorted(c, R, S, rows);
+    else if (sorted_inputs && mode == 1 && (R->flags & PF_DISTINCT)) *d_counts = driver_counts_sorted(c, S, R, rows);
+    else *d_counts = driver_counts_general(c, outR, outS, mode, rows);
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_join_payloads(qe_ctx* c, const uint32_t* d_counts, uint64_t rows, const qe_list* last, const qe_list* edit,
+                     qe_list* out) {
+    QE_API_BEGIN(c)
+    (void)rows;
+    if (edit->n < last->n) throw Error(QE_EINVAL, "join_payloads: |edit| < |last| (reference-undefined)");
+    const uint64_t n = last->n;
+    out->n = 0;
+    out->flags = 0;
+    if (n == 0) {
+        out->d = dalloc_t<uint32_t>(c, 1);
+        out->cap = 0;
+        out->flags = QE_LIST_DISTINCT;
+        return 0;
+    }
+    // 1. drop (last, edit) whose driver count is 0 -- they emit nothing
+    uint32_t* pl = dalloc_t<uint32_t>(c, n);
+    uint32_t* pe = dalloc_t<uint32_t>(c, n);
+    uint64_t m = compact_nonzero_pairs(c, d_counts, last->d, edit->d, n, pl, pe);
+    // 2. stable sort by `last` (the reference sorts R = (last, edit) by key, src/join.c:444)
+    SortOut so = radix_sort_u32(c, pl, pe, m);
+    const uint32_t* sk = (const uint32_t*)so.keys;
+    const uint32_t* sv = so.vals;
+    // 3. emit edit x driver multiplicity, in sorted order
+    uint64_t P = 0;
+    uint32_t mflag = 0;
+    if (m) {
+        const uint32_t nt = (uint32_t)((m + X_TILE - 1) / X_TILE);
+        uint64_t* tc = dalloc_t<uint64_t>(c, nt);
+        uint32_t* d_flags = (uint32_t*)(c->d_scratch + 30);
+        QE_HIP(hipMemsetAsync(d_flags, 0, 4, c->stream));
+        {
+            Timed t(c, "payload_count", 8.0 * m);
+            hipLaunchKernelGGL(expand_kernel<0>, dim3(nt), dim3(XB), 0, c->stream, sk, sv, m, d_counts, tc, nullptr,
+                               d_flags);
+            QE_HIP(hipGetLastError());
+            hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, c->stream, tc, (uint64_t)nt,
+                               c->d_scratch + 31);
+            QE_HIP(hipGetLastError());
+        }
+        uint64_t h[2];
+        read_words(c, c->d_scratch + 30, h, 2);
+        mflag = (uint32_t)h[0];
+        P = h[1];
+        out->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(P, 1));
+        if (P) {
+            Timed t(c, "payload_expand", 12.0 * m + 4.0 * P);
+            hipLaunchKernelGGL(expand_kernel<1>, dim3(nt), dim3(XB), 0, c->stream, sk, sv, m, d_counts, tc, out->d,
+                               nullptr);
+            QE_HIP(hipGetLastError());
+        }
+        dfree(c, tc);
+    } else {
+        out->d = dalloc_t<uint32_t>(c, 1);
+    }
+    out->n = P;
+    out->cap = P;
+    out->flags = ((edit->flags & QE_LIST_DISTINCT) && !(mflag & 1u)) ? QE_LIST_DISTINCT : 0;
+    if (so.keys_new) dfree(c, so.keys);
+    if (so.vals_new) dfree(c, so.vals);
+    dfree(c, pl);
+    dfree(c, pe);
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_checksum(qe_ctx* c, qe_col col, const qe_list* rows, uint64_t* sum) {
+    QE_API_BEGIN(c)
+    uint64_t n = rows ? rows->n : col.n;
+    unsigned long long* d = (unsigned long long*)(c->d_scratch + 40);
+    QE_HIP(hipMemsetAsync(d, 0, 8, c->stream));
+    if (n) {
+        Timed t(c, "checksum", rows ? 12.0 * n : 8.0 * n);
+        hipLaunchKernelGGL(checksum_kernel, dim3(grid_for(n, 256 * 16, 8192)), dim3(256), 0, c->stream, col.d,
+                           rows ? rows->d : nullptr, n, d);
+        QE_HIP(hipGetLastError());
+    }
+    *sum = read_u64(c, (const uint64_t*)d);
+    return 0;
+    QE_API_END(c)
+}
+
+}  // extern "C"

@@ -1,0 +1,470 @@
+// qe_runtime.hip -- libqe context, caching HBM allocator, lookback state, profiling, the
+// relation loader (reference src/utilities.c:105-162) and the on-device splitmix64 generator.
+#include <algorithm>
+#include <cstring>
+
+#include "qe_device.h"
+#include "qe_internal.h"
+
+namespace qe {
+
+// ---------------------------------------------------------------------------------------------
+// allocator: exact size classes (rounded), blocks reused in stream order on the ctx's single
+// stream, so no hipMalloc/hipFree inside a steady-state query (cdna_hip_programming.md G9)
+// ---------------------------------------------------------------------------------------------
+static size_t round_size(size_t b) {
+    if (b < 256) return 256;
+    if (b <= (64u << 20)) {
+        size_t p = 256;
+        while (p < b) p <<= 1;
+        // quarter steps between powers of two keep waste under 25 %
+        size_t q = p >> 2;
+        size_t r = ((b + q - 1) / q) * q;
+        return r;
+    }
+    const size_t g = 32u << 20;
+    return ((b + g - 1) / g) * g;
+}
+
+void* dalloc(qe_ctx* c, size_t bytes) {
+    size_t sz = round_size(bytes);
+    auto it = c->free_blocks.lower_bound(sz);
+    if (it != c->free_blocks.end() && it->first <= sz + sz / 8) {
+        void* p = it->second;
+        size_t got = it->first;
+        c->free_blocks.erase(it);
+        c->cached -= got;
+        c->live[p] = got;
+        c->in_use += got;
+        return p;
+    }
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, sz);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        // release the cache and retry once
+        QE_HIP(hipStreamSynchronize(c->stream));
+        for (auto& kv : c->free_blocks) (void)hipFree(kv.second);
+        c->free_blocks.clear();
+        c->cached = 0;
+        e = hipMalloc(&p, sz);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            throw Error(QE_ENOMEM, "hipMalloc(" + std::to_string(sz) + ") failed");
+        }
+    }
+    c->live[p] = sz;
+    c->in_use += sz;
+    return p;
+}
+
+void dfree(qe_ctx* c, void* p) {
+    if (!p) return;
+    auto it = c->live.find(p);
+    if (it == c->live.end()) return;   // not ours (e.g. a relation column)
+    size_t sz = it->second;
+    c->live.erase(it);
+    c->in_use -= sz;
+    c->free_blocks.emplace(sz, p);
+    c->cached += sz;
+}
+
+LBSlot lb_acquire(qe_ctx* c, size_t words) {
+    if (words > c->lb_status_words) {
+        if (c->lb_status) {
+            QE_HIP(hipStreamSynchronize(c->stream));
+            QE_HIP(hipFree(c->lb_status));
+        }
+        size_t w = std::max(words, (size_t)1 << 20);
+        QE_HIP(hipMalloc(&c->lb_status, w * sizeof(uint64_t)));
+        QE_HIP(hipMemsetAsync(c->lb_status, 0, w * sizeof(uint64_t), c->stream));
+        c->lb_status_words = w;
+    }
+    c->lb_epoch++;
+    if (c->lb_epoch >= (uint32_t)LB_MAX_COUNTERS) {
+        // epoch wrap: clear every status word and ticket, restart at 1
+        QE_HIP(hipMemsetAsync(c->lb_status, 0, c->lb_status_words * sizeof(uint64_t), c->stream));
+        QE_HIP(hipMemsetAsync(c->lb_tickets, 0, LB_MAX_COUNTERS * sizeof(uint32_t), c->stream));
+        c->lb_epoch = 1;
+    }
+    return LBSlot{c->lb_status, c->lb_tickets + c->lb_epoch, c->lb_epoch};
+}
+
+// ---------------------------------------------------------------------------------------------
+// profiling: HIP events on the ctx stream around each launch (bench.py reads these)
+// ---------------------------------------------------------------------------------------------
+static hipEvent_t get_event(qe_ctx* c) {
+    if (!c->event_pool.empty()) {
+        hipEvent_t e = c->event_pool.back();
+        c->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    QE_HIP(hipEventCreate(&e));
+    return e;
+}
+
+static void drain_events(qe_ctx* c) {
+    if (c->pending.empty()) return;
+    QE_HIP(hipStreamSynchronize(c->stream));
+    for (auto& p : c->pending) {
+        float ms = 0;
+        QE_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+        KStat& k = c->kstats[p.kernel];
+        k.launches++;
+        k.ms += ms;
+        k.bytes += p.bytes;
+        c->event_pool.push_back(p.a);
+        c->event_pool.push_back(p.b);
+    }
+    c->pending.clear();
+}
+
+Timed::Timed(qe_ctx* c_, const char* name, double alg_bytes) : c(c_), bytes(alg_bytes) {
+    if (!c->prof) return;
+    auto it = c->kindex.find(name);
+    if (it == c->kindex.end()) {
+        k = (int)c->kstats.size();
+        c->kindex[name] = k;
+        KStat s;
+        s.name = name;
+        c->kstats.push_back(s);
+    } else {
+        k = it->second;
+    }
+    a = get_event(c);
+    b = get_event(c);
+    QE_HIP(hipEventRecord(a, c->stream));
+}
+
+Timed::~Timed() {
+    if (!c->prof || k < 0) return;
+    if (hipEventRecord(b, c->stream) != hipSuccess) return;
+    c->pending.push_back(PendingEvent{k, a, b, bytes});
+    if (c->pending.size() > 4096) {
+        try {
+            drain_events(c);
+        } catch (...) {
+        }
+    }
+}
+
+void sync(qe_ctx* c) { QE_HIP(hipStreamSynchronize(c->stream)); }
+
+uint64_t read_u64(qe_ctx* c, const uint64_t* d) {
+    QE_HIP(hipMemcpyAsync(c->h_scratch, d, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    QE_HIP(hipStreamSynchronize(c->stream));
+    return c->h_scratch[0];
+}
+
+void read_words(qe_ctx* c, const uint64_t* d, uint64_t* h, int n) {
+    QE_HIP(hipMemcpyAsync(c->h_scratch, d, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    QE_HIP(hipStreamSynchronize(c->stream));
+    memcpy(h, c->h_scratch, n * sizeof(uint64_t));
+}
+
+// ---------------------------------------------------------------------------------------------
+// generator: v = splitmix64(((seed<<40)|(rel<<36)|(col<<32)) + row)  
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(256) gen_column_kernel(uint64_t* out, uint64_t rows, uint64_t base,
+                                                         uint64_t row_start, int kind, uint64_t mod) {
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows; i += stride) {
+        uint64_t v = splitmix64(base + row_start + i);
+        out[i] = kind == 0 ? v % mod : (v >> 32);
+    }
+}
+
+}  // namespace qe
+
+using namespace qe;
+
+// =============================================================================================
+// C ABI: lifecycle, relations, buffers, profiling
+// =============================================================================================
+extern "C" {
+
+int qe_abi_version(void) { return QE_ABI_VERSION; }
+
+qe_ctx* qe_init(int device) {
+    qe_ctx* c = new qe_ctx();
+    c->device = device;
+    try {
+        QE_HIP(hipSetDevice(device));
+        QE_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        QE_HIP(hipMalloc(&c->lb_tickets, LB_MAX_COUNTERS * sizeof(uint32_t)));
+        QE_HIP(hipMemsetAsync(c->lb_tickets, 0, LB_MAX_COUNTERS * sizeof(uint32_t), c->stream));
+        QE_HIP(hipMalloc(&c->d_scratch, 64 * sizeof(uint64_t)));
+        QE_HIP(hipHostMalloc((void**)&c->h_scratch, 64 * sizeof(uint64_t), hipHostMallocDefault));
+        QE_HIP(hipStreamSynchronize(c->stream));
+    } catch (const Error& e) {
+        fprintf(stderr, "qe_init(%d): %s\n", device, e.what());
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
+void qe_fini(qe_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (auto& r : c->rels)
+        for (auto* p : r.cols) (void)hipFree(p);
+    for (auto& kv : c->free_blocks) (void)hipFree(kv.second);
+    for (auto& kv : c->live) (void)hipFree(kv.first);
+    for (auto& p : c->pending) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    for (auto e : c->event_pool) (void)hipEventDestroy(e);
+    if (c->lb_status) (void)hipFree(c->lb_status);
+    if (c->lb_tickets) (void)hipFree(c->lb_tickets);
+    if (c->d_scratch) (void)hipFree(c->d_scratch);
+    if (c->h_scratch) (void)hipHostFree(c->h_scratch);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* qe_last_error(qe_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int qe_device_name(qe_ctx* c, char* out, size_t cap) {
+    QE_API_BEGIN(c)
+    hipDeviceProp_t p;
+    QE_HIP(hipGetDeviceProperties(&p, c->device));
+    snprintf(out, cap, "%s (%s, %d CUs)", p.name, p.gcnArchName, p.multiProcessorCount);
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_sync(qe_ctx* c) {
+    QE_API_BEGIN(c)
+    sync(c);
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_load_relation(qe_ctx* c, uint64_t rows, uint64_t ncols, const uint64_t* const* host_cols) {
+    QE_API_BEGIN(c)
+    if (rows >= 0xFFFFFFFFull) throw Error(QE_EINVAL, "relation too large for uint32 rowids");
+    Relation r;
+    r.rows = rows;
+    for (uint64_t j = 0; j < ncols; j++) {
+        uint64_t* d = nullptr;
+        QE_HIP(hipMalloc(&d, std::max<uint64_t>(rows, 1) * sizeof(uint64_t)));
+        if (rows) QE_HIP(hipMemcpyAsync(d, host_cols[j], rows * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+        r.cols.push_back(d);
+    }
+    QE_HIP(hipStreamSynchronize(c->stream));
+    c->rels.push_back(std::move(r));
+    return (int)c->rels.size() - 1;
+    QE_API_END(c)
+}
+
+int qe_gen_relation(qe_ctx* c, uint64_t rows, uint64_t ncols, const int* kinds, const uint64_t* mods,
+                    uint64_t seed, uint32_t gen_rel, uint64_t row_start) {
+    QE_API_BEGIN(c)
+    if (rows >= 0xFFFFFFFFull) throw Error(QE_EINVAL, "relation too large for uint32 rowids");
+    Relation r;
+    r.rows = rows;
+    for (uint64_t j = 0; j < ncols; j++) {
+        uint64_t* d = nullptr;
+        QE_HIP(hipMalloc(&d, std::max<uint64_t>(rows, 1) * sizeof(uint64_t)));
+        uint64_t base = (seed << 40) | ((uint64_t)gen_rel << 36) | ((uint64_t)j << 32);
+        if (kinds[j] == 0 && mods[j] == 0) throw Error(QE_EINVAL, "mod 0");
+        if (rows)
+            hipLaunchKernelGGL(gen_column_kernel, dim3(grid_for(rows, 256 * 8, 8192)), dim3(256), 0, c->stream, d,
+                               rows, base, row_start, kinds[j], mods[j]);
+        QE_HIP(hipGetLastError());
+        r.cols.push_back(d);
+    }
+    QE_HIP(hipStreamSynchronize(c->stream));
+    c->rels.push_back(std::move(r));
+    return (int)c->rels.size() - 1;
+    QE_API_END(c)
+}
+
+int qe_relation_count(qe_ctx* c) { return c ? (int)c->rels.size() : QE_EINVAL; }
+
+int qe_relation_column(qe_ctx* c, int rel, int col, qe_col* out) {
+    if (!c || rel < 0 || rel >= (int)c->rels.size() || col < 0 || col >= (int)c->rels[rel].cols.size())
+        return QE_EINVAL;
+    out->d = c->rels[rel].cols[col];
+    out->n = c->rels[rel].rows;
+    return 0;
+}
+
+int qe_relation_rows(qe_ctx* c, int rel, uint64_t* rows) {
+    if (!c || rel < 0 || rel >= (int)c->rels.size()) return QE_EINVAL;
+    *rows = c->rels[rel].rows;
+    return 0;
+}
+
+int qe_drop_relations(qe_ctx* c) {
+    QE_API_BEGIN(c)
+    sync(c);
+    for (auto& r : c->rels)
+        for (auto* p : r.cols) QE_HIP(hipFree(p));
+    c->rels.clear();
+    return 0;
+    QE_API_END(c)
+}
+
+void qe_free_host(void* p) { free(p); }
+
+int qe_list_alloc(qe_ctx* c, uint64_t n, qe_list* out) {
+    QE_API_BEGIN(c)
+    out->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
+    out->n = 0;
+    out->cap = n;
+    out->flags = 0;
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_list_from_host(qe_ctx* c, const uint32_t* h, uint64_t n, uint32_t flags, qe_list* out) {
+    QE_API_BEGIN(c)
+    out->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
+    if (n) QE_HIP(hipMemcpyAsync(out->d, h, n * 4, hipMemcpyHostToDevice, c->stream));
+    QE_HIP(hipStreamSynchronize(c->stream));
+    out->n = n;
+    out->cap = n;
+    out->flags = flags;
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_list_to_host(qe_ctx* c, const qe_list* l, uint32_t* h) {
+    QE_API_BEGIN(c)
+    if (l->n) QE_HIP(hipMemcpyAsync(h, l->d, l->n * 4, hipMemcpyDeviceToHost, c->stream));
+    QE_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+    QE_API_END(c)
+}
+
+void qe_list_free(qe_ctx* c, qe_list* l) {
+    if (!c || !l) return;
+    dfree(c, l->d);
+    l->d = nullptr;
+    l->n = l->cap = 0;
+}
+
+int qe_pairs_from_host(qe_ctx* c, const uint64_t* key, const uint32_t* val, uint64_t n, qe_pairs* out) {
+    QE_API_BEGIN(c)
+    out->key = dalloc_t<uint64_t>(c, std::max<uint64_t>(n, 1));
+    out->val = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
+    if (n) {
+        QE_HIP(hipMemcpyAsync(out->key, key, n * 8, hipMemcpyHostToDevice, c->stream));
+        QE_HIP(hipMemcpyAsync(out->val, val, n * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    QE_HIP(hipStreamSynchronize(c->stream));
+    out->n = n;
+    out->flags = 0;
+    out->owns = 3;
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_pairs_to_host(qe_ctx* c, const qe_pairs* p, uint64_t* key, uint32_t* val) {
+    QE_API_BEGIN(c)
+    if (p->n) {
+        if (key) QE_HIP(hipMemcpyAsync(key, p->key, p->n * 8, hipMemcpyDeviceToHost, c->stream));
+        if (val) {
+            if (p->val) {
+                QE_HIP(hipMemcpyAsync(val, p->val, p->n * 4, hipMemcpyDeviceToHost, c->stream));
+            } else {
+                QE_HIP(hipStreamSynchronize(c->stream));
+                for (uint64_t i = 0; i < p->n; i++) val[i] = (uint32_t)i;
+            }
+        }
+    }
+    QE_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+    QE_API_END(c)
+}
+
+void qe_pairs_free(qe_ctx* c, qe_pairs* p) {
+    if (!c || !p) return;
+    if (p->owns & 1) dfree(c, p->key);
+    if (p->owns & 2) dfree(c, p->val);
+    p->key = nullptr;
+    p->val = nullptr;
+    p->n = 0;
+    p->owns = 0;
+}
+
+void qe_counts_free(qe_ctx* c, uint32_t* d) {
+    if (c) dfree(c, d);
+}
+
+int qe_counts_to_host(qe_ctx* c, const uint32_t* d, uint64_t n, uint32_t* h) {
+    QE_API_BEGIN(c)
+    if (n) QE_HIP(hipMemcpyAsync(h, d, n * 4, hipMemcpyDeviceToHost, c->stream));
+    QE_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_mem_stats(qe_ctx* c, uint64_t* in_use, uint64_t* cached) {
+    if (!c) return QE_EINVAL;
+    *in_use = c->in_use;
+    *cached = c->cached;
+    return 0;
+}
+
+int qe_mem_trim(qe_ctx* c) {
+    QE_API_BEGIN(c)
+    sync(c);
+    for (auto& kv : c->free_blocks) QE_HIP(hipFree(kv.second));
+    c->free_blocks.clear();
+    c->cached = 0;
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_set_profiling(qe_ctx* c, int on) {
+    QE_API_BEGIN(c)
+    drain_events(c);
+    c->prof = on != 0;
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_reset_stats(qe_ctx* c) {
+    QE_API_BEGIN(c)
+    drain_events(c);
+    for (auto& k : c->kstats) {
+        k.launches = 0;
+        k.ms = 0;
+        k.bytes = 0;
+    }
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_kernel_stats(qe_ctx* c, qe_kstat* out, int max) {
+    QE_API_BEGIN(c)
+    drain_events(c);
+    int n = 0;
+    for (auto& k : c->kstats) {
+        if (n < max && out) {
+            memset(&out[n], 0, sizeof(qe_kstat));
+            strncpy(out[n].name, k.name.c_str(), sizeof(out[n].name) - 1);
+            out[n].launches = k.launches;
+            out[n].total_ms = k.ms;
+            out[n].alg_bytes = k.bytes;
+        }
+        n++;
+    }
+    return n;
+    QE_API_END(c)
+}
+
+}  // extern "C"

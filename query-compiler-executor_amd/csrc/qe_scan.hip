@@ -1,0 +1,247 @@
+// qe_scan.hip -- order-preserving stream compaction on gfx950, one pass over HBM.
+//
+// Used for the filter scan (reference src/filter.c:37-64), the order-preserving filter
+// refinement (src/filter.c:3-35, whose O(n^2) DArray_remove it replaces), scan_join
+// (src/join.c:395-423) and join_payloads' zero-count pruning.
+//
+// One workgroup = 256 threads = 4 waves owns a tile of ITEMS x VEC x 256 consecutive elements.
+// Each lane loads VEC elements per step with one 16-byte load (coalesced: a wave moves 1 KiB
+// per instruction).  Flags are ranked with one ballot per (step, vec slot) + popcount -- no LDS
+// scan -- then the tile total goes through a wave-parallel decoupled lookback (qe_device.h) to
+// get the tile's output offset.  Survivors are staged in LDS in order and written out as one
+// contiguous, coalesced run.  HBM traffic = input bytes + output bytes (+ gathers for refine).
+#include "qe_device.h"
+#include "qe_internal.h"
+
+namespace qe {
+
+constexpr int CB = 256;   // block
+constexpr int CNW = CB / 64;
+
+enum { OP_EQ = 0, OP_GT = 1, OP_LT = 2 };
+
+template <int OP>
+__device__ __forceinline__ bool cmp_op(uint64_t k, uint64_t v) {
+    if (OP == OP_EQ) return k == v;
+    if (OP == OP_GT) return k > v;
+    return k < v;
+}
+
+// ---- element producers ------------------------------------------------------------------------
+// load(base, n, f[VEC], v0[VEC], v1[VEC]) for elements base..base+VEC-1 (valid when < n)
+
+template <int OP>
+struct FilterScanOp {          // exec_filter_rel_no_exists: rowid i if col[i] op v
+    static constexpr int VEC = 2;
+    const uint64_t* col;
+    uint64_t v;
+    __device__ __forceinline__ void load(uint64_t base, uint64_t n, bool* f, uint32_t* v0, uint32_t*) const {
+        if (base + 1 < n) {
+            ulonglong2 x = *reinterpret_cast<const ulonglong2*>(col + base);
+            f[0] = cmp_op<OP>(x.x, v);
+            f[1] = cmp_op<OP>(x.y, v);
+        } else {
+            f[0] = base < n && cmp_op<OP>(col[base], v);
+            f[1] = false;
+        }
+        v0[0] = (uint32_t)base;
+        v0[1] = (uint32_t)(base + 1);
+    }
+};
+
+template <int OP>
+struct FilterRefineOp {        // exec_filter_rel_exists: keep rowid r if col[r] op v, in order
+    static constexpr int VEC = 4;
+    const uint64_t* col;
+    const uint32_t* in;
+    uint64_t v;
+    __device__ __forceinline__ void load(uint64_t base, uint64_t n, bool* f, uint32_t* v0, uint32_t*) const {
+        uint32_t r[4];
+        if (base + 3 < n) {
+            uint4 x = *reinterpret_cast<const uint4*>(in + base);
+            r[0] = x.x; r[1] = x.y; r[2] = x.z; r[3] = x.w;
+#pragma unroll
+            for (int k = 0; k < 4; k++) f[k] = true;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                f[k] = base + k < n;
+                r[k] = f[k] ? in[base + k] : 0;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (f[k]) f[k] = cmp_op<OP>(col[r[k]], v);
+            v0[k] = r[k];
+        }
+    }
+};
+
+struct ScanJoinOp {            // scan_join: positional key equality, both payloads out
+    static constexpr int VEC = 2;
+    const uint64_t *rk, *sk;
+    const uint32_t *rv, *sv;   // nullable: iota (base column)
+    __device__ __forceinline__ void load(uint64_t base, uint64_t n, bool* f, uint32_t* v0, uint32_t* v1) const {
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            uint64_t i = base + k;
+            bool ok = i < n;
+            f[k] = ok && rk[i] == sk[i];
+            v0[k] = ok ? (rv ? rv[i] : (uint32_t)i) : 0;
+            v1[k] = ok ? (sv ? sv[i] : (uint32_t)i) : 0;
+        }
+    }
+};
+
+struct NonzeroPairsOp {        // join_payloads: keep (last[i], edit[i]) whose driver count > 0
+    static constexpr int VEC = 4;
+    const uint32_t *counts, *last, *edit;
+    __device__ __forceinline__ void load(uint64_t base, uint64_t n, bool* f, uint32_t* v0, uint32_t* v1) const {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            uint64_t i = base + k;
+            bool ok = i < n;
+            uint32_t l = ok ? last[i] : 0;
+            f[k] = ok && counts[l] != 0;
+            v0[k] = l;
+            v1[k] = ok ? edit[i] : 0;
+        }
+    }
+};
+
+// ---- the kernel -------------------------------------------------------------------------------
+template <int ITEMS, int NOUT, class Op>
+__global__ void __launch_bounds__(CB) compact_kernel(Op op, uint64_t n, uint32_t ntiles, uint64_t* status,
+                                                     uint32_t* ticket, uint32_t epoch, uint32_t* __restrict__ out0,
+                                                     uint32_t* __restrict__ out1, uint64_t* total_out) {
+    constexpr int VEC = Op::VEC;
+    constexpr int TILE = CB * ITEMS * VEC;
+    static_assert(ITEMS * CNW <= 64, "one wave scans the (step, wave) table");
+    __shared__ uint32_t s_vals[NOUT][TILE];
+    __shared__ uint32_t s_cnt[ITEMS * CNW];
+    __shared__ uint32_t s_ticket;
+    __shared__ uint64_t s_excl;
+    __shared__ uint32_t s_total;
+
+    const uint32_t tile = take_ticket(ticket, &s_ticket);
+    const uint64_t tile_base = (uint64_t)tile * TILE;
+    const int w = wave_id(), l = lane_id();
+    const uint64_t lt = lanemask_lt();
+
+    bool f[ITEMS][VEC];
+    uint32_t v0[ITEMS][VEC], v1[ITEMS][VEC];
+    uint32_t rank[ITEMS][VEC];
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) {
+        uint64_t base = tile_base + (uint64_t)j * (CB * VEC) + (uint64_t)threadIdx.x * VEC;
+        op.load(base, n, f[j], v0[j], v1[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) {
+        uint32_t pre = 0, tot = 0;
+#pragma unroll
+        for (int k = 0; k < VEC; k++) {
+            uint64_t m = __ballot(f[j][k]);
+            pre += (uint32_t)__popcll(m & lt);
+            tot += (uint32_t)__popcll(m);
+        }
+        uint32_t r = pre;
+#pragma unroll
+        for (int k = 0; k < VEC; k++) {
+            rank[j][k] = r;
+            r += f[j][k] ? 1u : 0u;
+        }
+        if (l == 0) s_cnt[j * CNW + w] = tot;
+    }
+    __syncthreads();
+    if (w == 0) {
+        uint32_t c = l < ITEMS * CNW ? s_cnt[l] : 0;
+        uint32_t inc = wave_incl_scan_u32(c);
+        uint32_t total = (uint32_t)__shfl((int)inc, ITEMS * CNW - 1, 64);
+        if (l < ITEMS * CNW) s_cnt[l] = inc - c;
+        uint64_t excl = lookback_wave(status, epoch, tile, total);
+        if (l == 0) {
+            s_excl = excl;
+            s_total = total;
+            if (tile == ntiles - 1) *total_out = excl + total;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) {
+        uint32_t b = s_cnt[j * CNW + w];
+#pragma unroll
+        for (int k = 0; k < VEC; k++) {
+            if (f[j][k]) {
+                s_vals[0][b + rank[j][k]] = v0[j][k];
+                if (NOUT == 2) s_vals[NOUT - 1][b + rank[j][k]] = v1[j][k];
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t total = s_total;
+    const uint64_t off = s_excl;
+    for (uint32_t i = threadIdx.x; i < total; i += CB) {
+        out0[off + i] = s_vals[0][i];
+        if (NOUT == 2) out1[off + i] = s_vals[NOUT - 1][i];
+    }
+}
+
+// `bytes` = algorithmic input bytes; 4 B per output list per survivor is added once the count
+// is known (SURVEY.md §8(d) byte model).
+template <int ITEMS, int NOUT, class Op>
+static uint64_t run_compact(qe_ctx* c, const char* name, double bytes, const Op& op, uint64_t n, uint32_t* out0,
+                            uint32_t* out1) {
+    if (n == 0) return 0;
+    constexpr int TILE = CB * ITEMS * Op::VEC;
+    uint64_t nt = (n + TILE - 1) / TILE;
+    if (nt >= (1ull << 31)) throw Error(QE_EINVAL, "input too large");
+    LBSlot s = lb_acquire(c, nt);
+    uint64_t* d_total = c->d_scratch;
+    {
+        Timed t(c, name, bytes);
+        hipLaunchKernelGGL((compact_kernel<ITEMS, NOUT, Op>), dim3((unsigned)nt), dim3(CB), 0, c->stream, op, n,
+                           (uint32_t)nt, s.status, s.ticket, s.epoch, out0, out1, d_total);
+        QE_HIP(hipGetLastError());
+    }
+    uint64_t m = read_u64(c, d_total);
+    if (c->prof && !c->pending.empty()) c->pending.back().bytes += 4.0 * NOUT * m;
+    return m;
+}
+
+uint64_t filter_scan(qe_ctx* c, const uint64_t* col, uint64_t n, char op, uint64_t v, uint32_t* out) {
+    // read 8 B/row; the 4 B/survivor write is added by the caller-visible count below
+    double b = 8.0 * n;
+    uint64_t m;
+    switch (op) {
+    case '=': m = run_compact<8, 1>(c, "filter_scan", b, FilterScanOp<OP_EQ>{col, v}, n, out, nullptr); break;
+    case '>': m = run_compact<8, 1>(c, "filter_scan", b, FilterScanOp<OP_GT>{col, v}, n, out, nullptr); break;
+    case '<': m = run_compact<8, 1>(c, "filter_scan", b, FilterScanOp<OP_LT>{col, v}, n, out, nullptr); break;
+    default: throw Error(QE_EINVAL, "Wrong operator");
+    }
+    return m;
+}
+
+uint64_t filter_refine(qe_ctx* c, const uint64_t* col, const uint32_t* in, uint64_t n, char op, uint64_t v,
+                       uint32_t* out) {
+    double b = 12.0 * n;
+    switch (op) {
+    case '=': return run_compact<4, 1>(c, "filter_refine", b, FilterRefineOp<OP_EQ>{col, in, v}, n, out, nullptr);
+    case '>': return run_compact<4, 1>(c, "filter_refine", b, FilterRefineOp<OP_GT>{col, in, v}, n, out, nullptr);
+    case '<': return run_compact<4, 1>(c, "filter_refine", b, FilterRefineOp<OP_LT>{col, in, v}, n, out, nullptr);
+    default: throw Error(QE_EINVAL, "Wrong operator");
+    }
+}
+
+uint64_t scan_join_k(qe_ctx* c, const uint64_t* rk, const uint32_t* rv, const uint64_t* sk, const uint32_t* sv,
+                     uint64_t n, uint32_t* outR, uint32_t* outS) {
+    return run_compact<8, 2>(c, "scan_join", 24.0 * n, ScanJoinOp{rk, sk, rv, sv}, n, outR, outS);
+}
+
+uint64_t compact_nonzero_pairs(qe_ctx* c, const uint32_t* counts, const uint32_t* last, const uint32_t* edit,
+                               uint64_t n, uint32_t* out_last, uint32_t* out_edit) {
+    return run_compact<4, 2>(c, "payload_prune", 12.0 * n, NonzeroPairsOp{counts, last, edit}, n, out_last,
+                             out_edit);
+}
+
+}  // namespace qe

@@ -1,0 +1,615 @@
+/*
+ * qe_exec.c -- the host side of libqe: the reference's query frontend and executor, restated
+ * in C over the device primitives of include/qe.h.  This is the drop-in for the reference's
+ * execute_queries / execute_query / execute_filter / execute_join / print_sums seam
+ * (src/utilities.c:258-300, src/filter.c:66-100, src/join.c:630-679, src/utilities.c:197-224).
+ *
+ * Host work only: parsing (src/parsing.c), predicate arrangement with its quirks
+ * (src/pred_arrange.c), and the mid_result state machine (src/join.c:152-292, 486-628).  Every
+ * row-sized step (scan, refine, gather, sort, merge, payload propagation, checksum) runs on the
+ * GPU through qe_* calls; rowid lists stay in HBM as qe_list and never visit the host.
+ */
+#define _GNU_SOURCE
+#include <setjmp.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/qe.h"
+
+/* ------------------------------------------------------------------------------------------ */
+/* model                                                                                        */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct {                 /* mid_result (src/structs.h:44-49), list in HBM */
+    uint64_t relation, pid;
+    int32_t lcs;
+    qe_list* list;
+} mid_t;
+
+typedef struct { mid_t* e; size_t n, cap; } entity_t;
+typedef struct { entity_t** v; size_t n, cap; } mra_t;
+
+typedef struct {                 /* predicate (src/structs.h:29-34) */
+    int type;                    /* 0 join, 1 filter, -1 unparsed */
+    uint64_t frel, fcol, srel, scol;   /* filter: srel = constant, scol = 0 (what is_match reads) */
+    char op;
+    uint64_t cval;               /* uint32 constant, zero-extended (src/filter.c:70) */
+} pred_t;
+
+typedef struct {
+    uint32_t* rels; size_t nrels;
+    pred_t* preds; size_t npreds;
+    uint64_t* sel; size_t nsel;
+} query_t;
+
+typedef struct { ptrdiff_t ent, idx; } exists_t;
+
+enum { CLASSIC_JOIN = 1, JOIN_SORT_LHS = 2, JOIN_SORT_RHS = 3, SCAN_JOIN = 4, DO_NOTHING = 5 };
+
+typedef struct {
+    qe_ctx* q;
+    FILE* out;
+    jmp_buf jb;                  /* reference exit(EXIT_FAILURE) or a device error */
+    int jb_code;
+    qe_list** lists;             /* every list made for the current query (freed at its end) */
+    size_t nlists, caplists;
+} exec_t;
+
+static void fail(exec_t* x, int code, const char* msg) {
+    if (msg) fprintf(stderr, "[ERROR] %s\n", msg);
+    x->jb_code = code;
+    longjmp(x->jb, 1);
+}
+
+static void chk(exec_t* x, int rc) {
+    if (rc != 0) {
+        fprintf(stderr, "[ERROR] libqe: %s\n", qe_last_error(x->q));
+        fail(x, rc, NULL);
+    }
+}
+
+static qe_list* new_list(exec_t* x) {
+    qe_list* l = (qe_list*)calloc(1, sizeof(qe_list));
+    if (x->nlists == x->caplists) {
+        x->caplists = x->caplists ? 2 * x->caplists : 64;
+        x->lists = (qe_list**)realloc(x->lists, x->caplists * sizeof(qe_list*));
+    }
+    x->lists[x->nlists++] = l;
+    return l;
+}
+
+static void free_lists(exec_t* x) {
+    for (size_t i = 0; i < x->nlists; i++) {
+        qe_list_free(x->q, x->lists[i]);
+        free(x->lists[i]);
+    }
+    x->nlists = 0;
+}
+
+static void entity_push(entity_t* E, mid_t m) {
+    if (E->n == E->cap) {
+        E->cap = E->cap ? 2 * E->cap : 4;
+        E->e = (mid_t*)realloc(E->e, E->cap * sizeof(mid_t));
+    }
+    E->e[E->n++] = m;
+}
+
+static entity_t* new_entity(mra_t* M) {          /* create_entity_mid_results, src/join.c:145-150 */
+    if (M->n == M->cap) {
+        M->cap = M->cap ? 2 * M->cap : 4;
+        M->v = (entity_t**)realloc(M->v, M->cap * sizeof(entity_t*));
+    }
+    entity_t* E = (entity_t*)calloc(1, sizeof(entity_t));
+    M->v[M->n++] = E;
+    return E;
+}
+
+static void mra_free(mra_t* M) {
+    for (size_t i = 0; i < M->n; i++) {
+        free(M->v[i]->e);
+        free(M->v[i]);
+    }
+    free(M->v);
+    memset(M, 0, sizeof(*M));
+}
+
+/* relation_exists: newest entity first, first match (src/utilities.c:164-181) */
+static exists_t relation_exists(const mra_t* M, uint64_t relation, uint64_t pid) {
+    exists_t ex = {-1, -1};
+    for (ptrdiff_t i = (ptrdiff_t)M->n - 1; i >= 0; i--)
+        for (size_t j = 0; j < M->v[i]->n; j++)
+            if (M->v[i]->e[j].relation == relation && M->v[i]->e[j].pid == pid) {
+                ex.ent = i;
+                ex.idx = (ptrdiff_t)j;
+                return ex;
+            }
+    return ex;
+}
+
+/* relation_exists_current: last match in one entity (src/utilities.c:183-194) */
+static ptrdiff_t relation_exists_current(const entity_t* E, uint64_t relation, uint64_t pid) {
+    ptrdiff_t f = -1;
+    for (size_t i = 0; i < E->n; i++)
+        if (E->e[i].relation == relation && E->e[i].pid == pid) f = (ptrdiff_t)i;
+    return f;
+}
+
+static qe_col column(exec_t* x, uint64_t relation, uint64_t col) {
+    qe_col c;
+    if (qe_relation_column(x->q, (int)relation, (int)col, &c) != 0) fail(x, QE_EINVAL, "no such relation/column");
+    return c;
+}
+
+static uint64_t rows_of(exec_t* x, uint64_t relation) {
+    uint64_t r = 0;
+    if (qe_relation_rows(x->q, (int)relation, &r) != 0) fail(x, QE_EINVAL, "no such relation");
+    return r;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* joins                                                                                         */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct {
+    qe_list* res[2];             /* join_result.results[0/1] */
+    qe_pairs* R;                 /* the join inputs, kept for the driver-count fast path */
+    qe_pairs* S;
+} jres_t;
+
+/* allocate_relation (src/join.c:122-142) / allocate_relation_mid_results (src/join.c:96-120) */
+static void gather(exec_t* x, qe_pairs* out, uint64_t relation, uint64_t col, const qe_list* rows) {
+    chk(x, qe_gather_pairs(x->q, column(x, relation, col), rows, out));
+}
+
+static void ensure_sorted_flag(exec_t* x, qe_pairs* p) {
+    if (p->flags & QE_PAIRS_SORTED) return;
+    int s = 0;
+    chk(x, qe_is_sorted(x->q, p, &s));
+    if (s) p->flags |= QE_PAIRS_SORTED;
+}
+
+/* non_duplicates[mode] as driver counts, then join_payloads for every other entry of the
+ * entity (fix_all_mid_results, src/join.c:486-505) */
+static void fix_all(exec_t* x, const jres_t* jr, exists_t ex, mra_t* M, uint32_t relR, uint32_t relS, mid_t tmp,
+                    int mode) {
+    entity_t* E = M->v[ex.ent];
+    qe_list* update = E->e[ex.idx].list;
+    int needed = 0;
+    for (size_t i = 0; i < E->n; i++)
+        if (E->e[i].relation != relR && E->e[i].relation != relS) needed = 1;
+    if (needed) {
+        uint64_t rows = rows_of(x, E->e[ex.idx].relation);
+        uint32_t* counts = NULL;
+        chk(x, qe_driver_counts(x->q, jr->R, jr->S, jr->res[0], jr->res[1], mode, rows, &counts));
+        for (size_t i = 0; i < E->n; i++) {
+            mid_t* ed = &E->e[i];
+            if (ed->relation != relR && ed->relation != relS) {
+                qe_list* nl = new_list(x);
+                int rc = qe_join_payloads(x->q, counts, rows, update, ed->list, nl);
+                if (rc == QE_EINVAL) {
+                    qe_counts_free(x->q, counts);
+                    fail(x, QE_EINVAL, "join_payloads on lists of different lengths (reference-undefined)");
+                }
+                chk(x, rc);
+                ed->list = nl;
+            }
+        }
+        qe_counts_free(x->q, counts);
+    }
+    E->e[ex.idx] = tmp;
+}
+
+/* update_mid_results (src/join.c:507-628) */
+static void update_mid_results(exec_t* x, const jres_t* jr, mra_t* M, uint64_t relR, uint64_t predR, uint64_t colR,
+                               uint64_t relS, uint64_t predS, uint64_t colS, int join_id) {
+    mid_t tR = {relR, predR, (int32_t)colR, jr->res[0]};
+    mid_t tS = {relS, predS, (int32_t)colS, jr->res[1]};
+    exists_t ex;
+    switch (join_id) {
+    case CLASSIC_JOIN:
+        ex = relation_exists(M, relR, predR);
+        if (ex.idx == -1) entity_push(M->v[M->n - 1], tR);
+        else fix_all(x, jr, ex, M, (uint32_t)relR, (uint32_t)relS, tR, 0);
+        ex = relation_exists(M, relS, predS);
+        if (ex.idx == -1) entity_push(M->v[M->n - 1], tS);
+        else fix_all(x, jr, ex, M, (uint32_t)relR, (uint32_t)relS, tS, 1);
+        break;
+    case JOIN_SORT_LHS:
+        ex = relation_exists(M, relR, predR);
+        if (ex.idx == -1) entity_push(M->v[M->n - 1], tR);
+        else M->v[ex.ent]->e[ex.idx] = tR;
+        ex = relation_exists(M, relS, predS);
+        if (ex.idx == -1) fail(x, QE_EEXIT, "Something went really wrong");
+        fix_all(x, jr, ex, M, (uint32_t)relR, (uint32_t)relS, tS, 1);
+        break;
+    case JOIN_SORT_RHS:
+        ex = relation_exists(M, relS, predS);
+        if (ex.idx == -1) entity_push(M->v[M->n - 1], tS);
+        else M->v[ex.ent]->e[ex.idx] = tS;
+        ex = relation_exists(M, relR, predR);
+        if (ex.idx == -1) fail(x, QE_EEXIT, "Something went really wrong");
+        fix_all(x, jr, ex, M, (uint32_t)relR, (uint32_t)relS, tR, 0);
+        break;
+    case SCAN_JOIN:
+        ex = relation_exists(M, relR, predR);
+        if (ex.idx == -1) fail(x, QE_EEXIT, "Something went really wrong");
+        M->v[ex.ent]->e[ex.idx].list = jr->res[0];
+        ex = relation_exists(M, relS, predS);
+        if (ex.idx == -1) fail(x, QE_EEXIT, "Something went really wrong");
+        M->v[ex.ent]->e[ex.idx].list = jr->res[1];
+        break;
+    }
+}
+
+/* build_relations (src/join.c:152-292): pick the variant, gather both inputs */
+static int build_relations(exec_t* x, const query_t* q, const pred_t* p, mra_t* M, qe_pairs rel[2]) {
+    uint64_t lhs_rel = q->rels[p->frel], lhs_col = p->fcol;
+    uint64_t rhs_rel = q->rels[p->srel], rhs_col = p->scol;
+    if (lhs_rel == rhs_rel && lhs_col == rhs_col) return DO_NOTHING;
+    entity_t* E = M->n == 0 ? new_entity(M) : M->v[M->n - 1];
+    ptrdiff_t li = relation_exists_current(E, lhs_rel, p->frel);
+    ptrdiff_t ri = relation_exists_current(E, rhs_rel, p->srel);
+    if (li != -1 && ri == -1) {
+        gather(x, &rel[0], lhs_rel, lhs_col, E->e[li].list);
+        exists_t ex = relation_exists(M, rhs_rel, p->srel);
+        mid_t* T = NULL;
+        if (ex.idx == -1) gather(x, &rel[1], rhs_rel, rhs_col, NULL);
+        else {
+            T = &M->v[ex.ent]->e[ex.idx];
+            gather(x, &rel[1], rhs_rel, rhs_col, T->list);
+        }
+        mid_t* mid = &E->e[li];
+        if (!T) {
+            if (mid->lcs == (int32_t)lhs_col) return JOIN_SORT_RHS;
+            mid->lcs = (int32_t)lhs_col;
+            return CLASSIC_JOIN;
+        }
+        if (mid->lcs == (int32_t)lhs_col && T->lcs == (int32_t)rhs_col) return SCAN_JOIN;
+        if (mid->lcs == (int32_t)lhs_col) return JOIN_SORT_RHS;
+        if (T->lcs == (int32_t)rhs_col) return JOIN_SORT_LHS;
+        return CLASSIC_JOIN;
+    }
+    if (li != -1 && ri != -1) {
+        gather(x, &rel[0], lhs_rel, lhs_col, E->e[li].list);
+        gather(x, &rel[1], rhs_rel, rhs_col, E->e[ri].list);
+        return SCAN_JOIN;
+    }
+    if (li == -1 && ri != -1) {
+        gather(x, &rel[1], rhs_rel, rhs_col, E->e[ri].list);
+        exists_t ex = relation_exists(M, lhs_rel, p->frel);
+        mid_t* T = NULL;
+        if (ex.idx == -1) gather(x, &rel[0], lhs_rel, lhs_col, NULL);
+        else {
+            T = &M->v[ex.ent]->e[ex.idx];
+            gather(x, &rel[0], lhs_rel, lhs_col, T->list);
+        }
+        mid_t* mid = &E->e[ri];
+        if (!T) {
+            if (mid->lcs == (int32_t)rhs_col) return JOIN_SORT_LHS;
+            mid->lcs = (int32_t)rhs_col;
+            return CLASSIC_JOIN;
+        }
+        if (mid->lcs == (int32_t)rhs_col && T->lcs == (int32_t)lhs_col) return SCAN_JOIN;
+        if (mid->lcs == (int32_t)rhs_col) return JOIN_SORT_RHS;   /* reference quirk, src/join.c:258-259 */
+        if (mid->lcs == (int32_t)lhs_col) return JOIN_SORT_LHS;   /* reference quirk, src/join.c:261-262 */
+        return CLASSIC_JOIN;
+    }
+    new_entity(M);                                                /* src/join.c:270-285 */
+    gather(x, &rel[1], rhs_rel, rhs_col, NULL);
+    gather(x, &rel[0], lhs_rel, lhs_col, NULL);
+    if (rhs_rel != lhs_rel || p->frel != p->srel) return CLASSIC_JOIN;
+    return SCAN_JOIN;
+}
+
+/* execute_join (src/join.c:630-679) */
+static int execute_join(exec_t* x, const query_t* q, const pred_t* p, mra_t* M) {
+    qe_pairs rel[2];
+    memset(rel, 0, sizeof(rel));
+    int v = build_relations(x, q, p, M, rel);
+    if (v == DO_NOTHING) return 0;
+    jres_t jr;
+    jr.res[0] = new_list(x);
+    jr.res[1] = new_list(x);
+    jr.R = &rel[0];
+    jr.S = &rel[1];
+    switch (v) {
+    case CLASSIC_JOIN:
+        chk(x, qe_sort_pairs(x->q, &rel[0]));
+        chk(x, qe_sort_pairs(x->q, &rel[1]));
+        chk(x, qe_merge_join(x->q, &rel[0], &rel[1], jr.res[0], jr.res[1]));
+        break;
+    case JOIN_SORT_LHS:
+        chk(x, qe_sort_pairs(x->q, &rel[0]));
+        ensure_sorted_flag(x, &rel[1]);
+        chk(x, qe_merge_join(x->q, &rel[0], &rel[1], jr.res[0], jr.res[1]));
+        break;
+    case JOIN_SORT_RHS:
+        chk(x, qe_sort_pairs(x->q, &rel[1]));
+        ensure_sorted_flag(x, &rel[0]);
+        chk(x, qe_merge_join(x->q, &rel[0], &rel[1], jr.res[0], jr.res[1]));
+        break;
+    case SCAN_JOIN:
+        chk(x, qe_scan_join(x->q, &rel[0], &rel[1], jr.res[0], jr.res[1]));
+        break;
+    default:
+        return -1;
+    }
+    update_mid_results(x, &jr, M, q->rels[p->frel], p->frel, p->fcol, q->rels[p->srel], p->srel, p->scol, v);
+    qe_pairs_free(x->q, &rel[0]);
+    qe_pairs_free(x->q, &rel[1]);
+    return 0;
+}
+
+static int op_valid(char op) { return op == '=' || op == '<' || op == '>'; }
+
+/* execute_filter (src/filter.c:66-100) */
+static int execute_filter(exec_t* x, const query_t* q, const pred_t* p, mra_t* M) {
+    uint64_t relation = q->rels[p->frel];
+    qe_col col = column(x, relation, p->fcol);
+    entity_t* E = M->n == 0 ? new_entity(M) : M->v[M->n - 1];
+    exists_t ex = relation_exists(M, relation, p->frel);
+    if (ex.idx != -1) {                                           /* exec_filter_rel_exists */
+        qe_list* l = M->v[ex.ent]->e[ex.idx].list;
+        if (!op_valid(p->op)) {
+            if (l->n != 0) {
+                fprintf(stderr, "[ERROR] Wrong operator\n");
+                return -1;
+            }
+        } else {
+            chk(x, qe_filter_refine(x->q, col, p->op, p->cval, l));
+        }
+        fprintf(x->out, "%d\n", (int)(uint32_t)l->n);             /* src/filter.c:32 */
+    } else {                                                      /* exec_filter_rel_no_exists */
+        mid_t m = {relation, p->frel, -1, new_list(x)};
+        entity_push(E, m);
+        qe_list* l = m.list;
+        if (!op_valid(p->op)) {
+            l->n = 0;
+            if (col.n != 0) {
+                fprintf(stderr, "[ERROR] Wrong operator\n");
+                return -1;
+            }
+            return 0;
+        }
+        chk(x, qe_filter_scan(x->q, col, p->op, p->cval, l));
+    }
+    return 0;
+}
+
+/* print_sums (src/utilities.c:197-224) */
+static void print_sums(exec_t* x, const query_t* q, const mra_t* M) {
+    for (size_t i = 0; i < q->nsel; i++) {
+        uint64_t b = q->sel[2 * i], colno = q->sel[2 * i + 1];
+        uint32_t relation = q->rels[b];
+        exists_t ex = relation_exists(M, relation, b);
+        if (ex.idx == -1) fail(x, QE_EEXIT, "Something went really wrong...");
+        const qe_list* l = M->v[ex.ent]->e[ex.idx].list;
+        if (l->n == 0) {
+            fputs("NULL ", x->out);
+        } else {
+            uint64_t s = 0;
+            chk(x, qe_checksum(x->q, column(x, relation, colno), l, &s));
+            fprintf(x->out, "%lu ", (unsigned long)s);
+        }
+    }
+    fputc('\n', x->out);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* frontend                                                                                     */
+/* ------------------------------------------------------------------------------------------ */
+
+static void parse_relations(const char* s, query_t* q) {         /* src/parsing.c:4-28 */
+    size_t sp = 0;
+    for (size_t i = 0; s[i]; i++) sp += s[i] == ' ';
+    q->nrels = sp + 1;
+    q->rels = (uint32_t*)calloc(q->nrels, sizeof(uint32_t));
+    char cur[16];
+    const char* ptr = s;
+    int adv;
+    size_t i = 0;
+    while (i < q->nrels && sscanf(ptr, "%15[^ ]%n", cur, &adv) == 1) {
+        ptr += adv;
+        q->rels[i++] = (uint32_t)(int)strtol(cur, NULL, 10);
+        if (*ptr != ' ') break;
+        ptr++;
+    }
+}
+
+static void parse_predicates(const char* s, query_t* q) {        /* src/parsing.c:30-88 */
+    size_t amp = 0;
+    for (size_t i = 0; s[i]; i++) amp += s[i] == '&';
+    q->npreds = amp + 1;
+    q->preds = (pred_t*)calloc(q->npreds, sizeof(pred_t));
+    for (size_t i = 0; i < q->npreds; i++) q->preds[i].type = -1;
+    char cur[128];
+    const char* ptr = s;
+    int adv;
+    size_t i = 0;
+    while (i < q->npreds && sscanf(ptr, "%127[^&]%n", cur, &adv) == 1) {
+        ptr += adv;
+        int a, b, c2, d;
+        unsigned ua, ub, uc;
+        char op;
+        if (sscanf(cur, "%d.%d%c%d.%d", &a, &b, &op, &c2, &d) == 5) {
+            pred_t* p = &q->preds[i++];
+            p->type = 0;
+            p->frel = (uint32_t)a;
+            p->fcol = (uint32_t)b;
+            p->srel = (uint32_t)c2;
+            p->scol = (uint32_t)d;
+            p->op = op;
+        } else if (sscanf(cur, "%u.%u%c%u", &ua, &ub, &op, &uc) == 4) {
+            pred_t* p = &q->preds[i++];
+            p->type = 1;
+            p->frel = ua;
+            p->fcol = ub;
+            p->op = op;
+            p->cval = (uint64_t)uc;
+            p->srel = (uint64_t)uc;
+            p->scol = 0;
+        }
+        if (*ptr != '&') break;
+        ptr++;
+    }
+}
+
+static void parse_select(const char* s, query_t* q) {           /* src/parsing.c:90-116 */
+    size_t sp = 0;
+    for (size_t i = 0; s[i]; i++) sp += s[i] == ' ';
+    q->nsel = sp + 1;
+    q->sel = (uint64_t*)calloc(2 * q->nsel, sizeof(uint64_t));
+    char tmp[128];
+    const char* ptr = s;
+    int adv;
+    size_t i = 0;
+    while (i < q->nsel && sscanf(ptr, "%127[^ ]%n", tmp, &adv) == 1) {
+        ptr += adv;
+        int r = 0, c = 0;
+        sscanf(tmp, "%d.%d", &r, &c);
+        q->sel[2 * i] = (uint64_t)(int64_t)r;
+        q->sel[2 * i + 1] = (uint64_t)(int64_t)c;
+        i++;
+        if (*ptr != ' ') break;
+        ptr++;
+    }
+}
+
+static void swap_preds(query_t* q, ptrdiff_t i, ptrdiff_t j) {
+    if (i == j) return;
+    pred_t t = q->preds[i];
+    q->preds[i] = q->preds[j];
+    q->preds[j] = t;
+}
+
+static int is_match(const pred_t* l, const pred_t* r) {         /* src/pred_arrange.c:29-48 */
+    return (l->fcol == r->fcol && l->frel == r->frel) || (l->fcol == r->scol && l->frel == r->srel) ||
+           (l->scol == r->fcol && l->srel == r->frel) || (l->scol == r->scol && l->srel == r->srel);
+}
+
+static void arrange_predicates(query_t* q) {                    /* src/pred_arrange.c:50-93 */
+    ptrdiff_t n = (ptrdiff_t)q->npreds, index = 0;
+    for (ptrdiff_t i = 1; i < n; i++) {                          /* group_filters: p[0] never examined */
+        if (q->preds[i].type == 1) {
+            ptrdiff_t s = i;
+            for (ptrdiff_t j = 0; j < i - index; j++, s--) swap_preds(q, s, s - 1);
+            index++;
+        }
+    }
+    for (ptrdiff_t i = index; i < n - 1;) {                      /* group_matches, index lag kept */
+        int swapped = 0;
+        for (ptrdiff_t j = i + 1; j < n; j++)
+            if (is_match(&q->preds[i], &q->preds[j])) {
+                swap_preds(q, ++index, j);
+                swapped = 1;
+            }
+        i = swapped ? index : i + 1;
+    }
+}
+
+static int query_valid(exec_t* x, const query_t* q) {
+    int nrel = qe_relation_count(x->q);
+    for (size_t i = 0; i < q->nrels; i++)
+        if ((int)q->rels[i] >= nrel) return 0;
+    for (size_t i = 0; i < q->npreds; i++) {
+        const pred_t* p = &q->preds[i];
+        if (p->type < 0 || p->frel >= q->nrels) return 0;
+        qe_col c;
+        if (qe_relation_column(x->q, (int)q->rels[p->frel], (int)p->fcol, &c) != 0) return 0;
+        if (p->type == 0) {
+            if (p->srel >= q->nrels) return 0;
+            if (qe_relation_column(x->q, (int)q->rels[p->srel], (int)p->scol, &c) != 0) return 0;
+        }
+    }
+    for (size_t i = 0; i < q->nsel; i++) {
+        qe_col c;
+        if (q->sel[2 * i] >= q->nrels) return 0;
+        if (qe_relation_column(x->q, (int)q->rels[q->sel[2 * i]], (int)q->sel[2 * i + 1], &c) != 0) return 0;
+    }
+    return 1;
+}
+
+/* execute_query (src/utilities.c:258-287): a failed predicate drops the output line */
+static void execute_query(exec_t* x, query_t* q) {
+    mra_t M;
+    memset(&M, 0, sizeof(M));
+    int ok = query_valid(x, q);   /* out-of-range ids are undefined in the reference: no line */
+    for (size_t i = 0; ok && i < q->npreds; i++) {
+        const pred_t* p = &q->preds[i];
+        int r = p->type == 1 ? execute_filter(x, q, p, &M) : execute_join(x, q, p, &M);
+        if (r == -1) ok = 0;
+    }
+    if (ok) print_sums(x, q, &M);
+    mra_free(&M);
+    free_lists(x);
+}
+
+/* execute_queries (src/utilities.c:289-300); a reference exit(EXIT_FAILURE) or a device
+ * error unwinds here */
+static int run_all(exec_t* x, query_t* qs, size_t nq) {
+    if (setjmp(x->jb) != 0) {
+        free_lists(x);
+        return x->jb_code;
+    }
+    for (size_t qi = 0; qi < nq; qi++) {
+        arrange_predicates(&qs[qi]);
+        execute_query(x, &qs[qi]);
+    }
+    return 0;
+}
+
+int qe_run_queries(qe_ctx* ctx, const char* text, char** out, size_t* outlen) {
+    exec_t x;
+    memset(&x, 0, sizeof(x));
+    x.q = ctx;
+    *out = NULL;
+    *outlen = 0;
+    x.out = open_memstream(out, outlen);
+    if (!x.out) return QE_ENOMEM;
+
+    /* parser() (src/parsing.c:118-148): every line until EOF, 'F' lines skipped, the three
+     * scan buffers persist across lines as the reference's stack arrays do */
+    size_t len = strlen(text);
+    char* rb = (char*)calloc(len + 2, 1);
+    char* pb = (char*)calloc(len + 2, 1);
+    char* sb = (char*)calloc(len + 2, 1);
+    char* line = (char*)malloc(len + 2);
+    size_t nq_ = 0, capq = 16;  /* parsed before anything runs (main/queries_main.c:31-37) */
+    query_t* qs_ = (query_t*)malloc(capq * sizeof(query_t));
+    const char* s = text;
+    while (*s) {
+        const char* e = strchr(s, '\n');
+        size_t ll = e ? (size_t)(e - s) + 1 : strlen(s);
+        memcpy(line, s, ll);
+        line[ll] = 0;
+        s += ll;
+        if (line[0] == 'F') continue;
+        sscanf(line, "%[0-9 ]%*[|]%[0-9.=<>&]%*[|]%[0-9. ]", rb, pb, sb);
+        if (nq_ == capq) {
+            capq *= 2;
+            qs_ = (query_t*)realloc(qs_, capq * sizeof(query_t));
+        }
+        parse_relations(rb, &qs_[nq_]);
+        parse_predicates(pb, &qs_[nq_]);
+        parse_select(sb, &qs_[nq_]);
+        nq_++;
+    }
+    query_t* qs = qs_;
+    size_t nq = nq_;
+    free(line);
+    free(rb);
+    free(pb);
+    free(sb);
+
+    int rc = run_all(&x, qs, nq);
+    for (size_t i = 0; i < nq; i++) {
+        free(qs[i].rels);
+        free(qs[i].preds);
+        free(qs[i].sel);
+    }
+    free(qs);
+    free(x.lists);
+    fclose(x.out);
+    return rc;
+}

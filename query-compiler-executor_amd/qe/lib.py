@@ -1,0 +1,289 @@
+"""ctypes binding of libqe (include/qe.h).
+
+The product path is native: every call goes into build/libqe.so (HIP kernels for gfx950 + the
+host-C executor).  There is no Python or CPU fallback -- if the library is missing or no GPU
+is usable, these calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG, "build", "libqe.so")
+HEADER = os.path.join(os.path.dirname(PKG), "include", "qe.h")
+
+QE_EINVAL, QE_EHIP, QE_ENOMEM, QE_EEXIT = -1, -2, -3, -4
+LIST_DISTINCT = 1
+PAIRS_DISTINCT, PAIRS_SORTED = 1, 2
+
+
+class Col(C.Structure):
+    _fields_ = [("d", C.c_void_p), ("n", C.c_uint64)]
+
+
+class List(C.Structure):
+    _fields_ = [("d", C.c_void_p), ("n", C.c_uint64), ("cap", C.c_uint64), ("flags", C.c_uint32)]
+
+
+class Pairs(C.Structure):
+    _fields_ = [("key", C.c_void_p), ("val", C.c_void_p), ("n", C.c_uint64), ("flags", C.c_uint32),
+                ("owns", C.c_uint32)]
+
+
+class KStat(C.Structure):
+    _fields_ = [("name", C.c_char * 48), ("launches", C.c_uint64), ("total_ms", C.c_double),
+                ("alg_bytes", C.c_double)]
+
+
+class QEError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"libqe error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    """Load libqe.so; raises if it has not been built (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"{path} missing: build it with __graft_entry__.build() or "
+                                f"`make -C query-compiler-executor_amd` (libqe has no CPU fallback)")
+    lib = C.CDLL(path)
+    P, U64, I, VP = C.c_void_p, C.c_uint64, C.c_int, C.c_void_p
+    sig = {
+        "qe_init": (P, [I]),
+        "qe_fini": (None, [P]),
+        "qe_last_error": (C.c_char_p, [P]),
+        "qe_abi_version": (I, []),
+        "qe_device_name": (I, [P, C.c_char_p, C.c_size_t]),
+        "qe_sync": (I, [P]),
+        "qe_load_relation": (I, [P, U64, U64, C.POINTER(C.c_void_p)]),
+        "qe_gen_relation": (I, [P, U64, U64, C.POINTER(C.c_int), C.POINTER(C.c_uint64), U64, C.c_uint32, U64]),
+        "qe_relation_count": (I, [P]),
+        "qe_relation_column": (I, [P, I, I, C.POINTER(Col)]),
+        "qe_relation_rows": (I, [P, I, C.POINTER(C.c_uint64)]),
+        "qe_drop_relations": (I, [P]),
+        "qe_run_queries": (I, [P, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+        "qe_free_host": (None, [VP]),
+        "qe_filter_scan": (I, [P, Col, C.c_char, U64, C.POINTER(List)]),
+        "qe_filter_refine": (I, [P, Col, C.c_char, U64, C.POINTER(List)]),
+        "qe_gather_pairs": (I, [P, Col, C.POINTER(List), C.POINTER(Pairs)]),
+        "qe_sort_pairs": (I, [P, C.POINTER(Pairs)]),
+        "qe_is_sorted": (I, [P, C.POINTER(Pairs), C.POINTER(C.c_int)]),
+        "qe_merge_join": (I, [P, C.POINTER(Pairs), C.POINTER(Pairs), C.POINTER(List), C.POINTER(List)]),
+        "qe_scan_join": (I, [P, C.POINTER(Pairs), C.POINTER(Pairs), C.POINTER(List), C.POINTER(List)]),
+        "qe_driver_counts": (I, [P, C.POINTER(Pairs), C.POINTER(Pairs), C.POINTER(List), C.POINTER(List), I, U64,
+                                 C.POINTER(C.c_void_p)]),
+        "qe_join_payloads": (I, [P, C.c_void_p, U64, C.POINTER(List), C.POINTER(List), C.POINTER(List)]),
+        "qe_checksum": (I, [P, Col, C.POINTER(List), C.POINTER(C.c_uint64)]),
+        "qe_list_alloc": (I, [P, U64, C.POINTER(List)]),
+        "qe_list_from_host": (I, [P, VP, U64, C.c_uint32, C.POINTER(List)]),
+        "qe_list_to_host": (I, [P, C.POINTER(List), VP]),
+        "qe_list_free": (None, [P, C.POINTER(List)]),
+        "qe_pairs_from_host": (I, [P, VP, VP, U64, C.POINTER(Pairs)]),
+        "qe_pairs_to_host": (I, [P, C.POINTER(Pairs), VP, VP]),
+        "qe_pairs_free": (None, [P, C.POINTER(Pairs)]),
+        "qe_counts_free": (None, [P, C.c_void_p]),
+        "qe_counts_to_host": (I, [P, C.c_void_p, U64, VP]),
+        "qe_mem_stats": (I, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+        "qe_mem_trim": (I, [P]),
+        "qe_set_profiling": (I, [P, I]),
+        "qe_reset_stats": (I, [P]),
+        "qe_kernel_stats": (I, [P, C.POINTER(KStat), I]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+def declared_symbols(header: str = HEADER) -> list[str]:
+    """Every function name include/qe.h declares."""
+    import re
+    txt = open(header).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(qe_[a-z0-9_]+)\s*\(", txt)))
+
+
+class Ctx:
+    """One device context (one HIP stream, one caching allocator)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        self.h = self.lib.qe_init(device)
+        if not self.h:
+            raise QEError(QE_EHIP, f"qe_init({device}) failed: no usable GPU (libqe has no CPU path)")
+        self.device = device
+
+    def close(self):
+        if self.h:
+            self.lib.qe_fini(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _chk(self, rc):
+        if rc < 0:
+            raise QEError(rc, self.lib.qe_last_error(self.h).decode())
+        return rc
+
+    def device_name(self) -> str:
+        b = C.create_string_buffer(256)
+        self._chk(self.lib.qe_device_name(self.h, b, 256))
+        return b.value.decode()
+
+    # ---- relations ----
+    def load_relation(self, cols: list[np.ndarray]) -> int:
+        cols = [np.ascontiguousarray(c, dtype=np.uint64) for c in cols]
+        rows = len(cols[0]) if cols else 0
+        arr = (C.c_void_p * max(1, len(cols)))(*[c.ctypes.data for c in cols])
+        return self._chk(self.lib.qe_load_relation(self.h, rows, len(cols), arr))
+
+    def gen_relation(self, rows: int, kinds: list[tuple], seed: int, gen_rel: int, row_start: int = 0) -> int:
+        k = (C.c_int * len(kinds))(*[0 if kd[0] == "mod" else 1 for kd in kinds])
+        m = (C.c_uint64 * len(kinds))(*[int(kd[1]) if kd[0] == "mod" else 0 for kd in kinds])
+        return self._chk(self.lib.qe_gen_relation(self.h, rows, len(kinds), k, m, seed, gen_rel, row_start))
+
+    def drop_relations(self):
+        self._chk(self.lib.qe_drop_relations(self.h))
+
+    def column(self, rel: int, col: int) -> Col:
+        c = Col()
+        self._chk(self.lib.qe_relation_column(self.h, rel, col, C.byref(c)))
+        return c
+
+    # ---- executor ----
+    def run(self, text: str) -> tuple[str, int]:
+        out = C.c_void_p()
+        n = C.c_size_t()
+        rc = self.lib.qe_run_queries(self.h, text.encode(), C.byref(out), C.byref(n))
+        s = C.string_at(out, n.value).decode("latin-1") if out.value else ""
+        if out.value:
+            self.lib.qe_free_host(out)
+        if rc not in (0, QE_EEXIT):
+            raise QEError(rc, self.lib.qe_last_error(self.h).decode())
+        return s, (1 if rc == QE_EEXIT else 0)
+
+    # ---- primitives (tests / bench) ----
+    def list_from_host(self, a: np.ndarray, flags: int = 0) -> List:
+        a = np.ascontiguousarray(a, dtype=np.uint32)
+        l = List()
+        self._chk(self.lib.qe_list_from_host(self.h, a.ctypes.data, len(a), flags, C.byref(l)))
+        return l
+
+    def list_to_host(self, l: List) -> np.ndarray:
+        a = np.empty(l.n, dtype=np.uint32)
+        self._chk(self.lib.qe_list_to_host(self.h, C.byref(l), a.ctypes.data))
+        return a
+
+    def list_free(self, l: List):
+        self.lib.qe_list_free(self.h, C.byref(l))
+
+    def pairs_from_host(self, key: np.ndarray, val: np.ndarray) -> Pairs:
+        key = np.ascontiguousarray(key, dtype=np.uint64)
+        val = np.ascontiguousarray(val, dtype=np.uint32)
+        p = Pairs()
+        self._chk(self.lib.qe_pairs_from_host(self.h, key.ctypes.data, val.ctypes.data, len(key), C.byref(p)))
+        return p
+
+    def pairs_to_host(self, p: Pairs) -> tuple[np.ndarray, np.ndarray]:
+        k = np.empty(p.n, dtype=np.uint64)
+        v = np.empty(p.n, dtype=np.uint32)
+        self._chk(self.lib.qe_pairs_to_host(self.h, C.byref(p), k.ctypes.data, v.ctypes.data))
+        return k, v
+
+    def pairs_free(self, p: Pairs):
+        self.lib.qe_pairs_free(self.h, C.byref(p))
+
+    def filter_scan(self, col: Col, op: str, v: int) -> List:
+        l = List()
+        self._chk(self.lib.qe_filter_scan(self.h, col, op.encode(), v, C.byref(l)))
+        return l
+
+    def filter_refine(self, col: Col, op: str, v: int, l: List) -> List:
+        self._chk(self.lib.qe_filter_refine(self.h, col, op.encode(), v, C.byref(l)))
+        return l
+
+    def gather_pairs(self, col: Col, rows: List | None) -> Pairs:
+        p = Pairs()
+        self._chk(self.lib.qe_gather_pairs(self.h, col, C.byref(rows) if rows is not None else None, C.byref(p)))
+        return p
+
+    def sort_pairs(self, p: Pairs) -> Pairs:
+        self._chk(self.lib.qe_sort_pairs(self.h, C.byref(p)))
+        return p
+
+    def is_sorted(self, p: Pairs) -> bool:
+        s = C.c_int()
+        self._chk(self.lib.qe_is_sorted(self.h, C.byref(p), C.byref(s)))
+        return bool(s.value)
+
+    def merge_join(self, R: Pairs, S: Pairs) -> tuple[List, List]:
+        a, b = List(), List()
+        self._chk(self.lib.qe_merge_join(self.h, C.byref(R), C.byref(S), C.byref(a), C.byref(b)))
+        return a, b
+
+    def scan_join(self, R: Pairs, S: Pairs) -> tuple[List, List]:
+        a, b = List(), List()
+        self._chk(self.lib.qe_scan_join(self.h, C.byref(R), C.byref(S), C.byref(a), C.byref(b)))
+        return a, b
+
+    def driver_counts(self, R: Pairs | None, S: Pairs | None, outR: List, outS: List, mode: int, rows: int):
+        d = C.c_void_p()
+        self._chk(self.lib.qe_driver_counts(self.h, C.byref(R) if R is not None else None,
+                                            C.byref(S) if S is not None else None, C.byref(outR), C.byref(outS),
+                                            mode, rows, C.byref(d)))
+        return d
+
+    def counts_to_host(self, d, n: int) -> np.ndarray:
+        a = np.empty(n, dtype=np.uint32)
+        self._chk(self.lib.qe_counts_to_host(self.h, d, n, a.ctypes.data))
+        return a
+
+    def counts_free(self, d):
+        self.lib.qe_counts_free(self.h, d)
+
+    def join_payloads(self, counts, rows: int, last: List, edit: List) -> List:
+        out = List()
+        self._chk(self.lib.qe_join_payloads(self.h, counts, rows, C.byref(last), C.byref(edit), C.byref(out)))
+        return out
+
+    def checksum(self, col: Col, rows: List | None) -> int:
+        s = C.c_uint64()
+        self._chk(self.lib.qe_checksum(self.h, col, C.byref(rows) if rows is not None else None, C.byref(s)))
+        return s.value
+
+    def sync(self):
+        self._chk(self.lib.qe_sync(self.h))
+
+    def mem_stats(self) -> tuple[int, int]:
+        a, b = C.c_uint64(), C.c_uint64()
+        self._chk(self.lib.qe_mem_stats(self.h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    # ---- profiling ----
+    def set_profiling(self, on: bool):
+        self._chk(self.lib.qe_set_profiling(self.h, 1 if on else 0))
+
+    def reset_stats(self):
+        self._chk(self.lib.qe_reset_stats(self.h))
+
+    def kernel_stats(self) -> dict:
+        n = self._chk(self.lib.qe_kernel_stats(self.h, None, 0))
+        arr = (KStat * max(1, n))()
+        self._chk(self.lib.qe_kernel_stats(self.h, arr, n))
+        return {arr[i].name.decode(): {"launches": arr[i].launches, "ms": arr[i].total_ms,
+                                       "alg_bytes": arr[i].alg_bytes} for i in range(n)}

@@ -13,3 +13,12 @@ for p in (PKG, os.path.join(ROOT, "tests")):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box via gpurun)")
     config.addinivalue_line("markers", "slow: long-running (full-size) case")
+
+
+@pytest.fixture(scope="session")
+def ctx():
+    """One libqe device context for the whole GPU session (native path only, no fallback)."""
+    from qe import lib
+    c = lib.Ctx(0)
+    yield c
+    c.close()

@@ -1,0 +1,263 @@
+"""GPU parity of every device primitive (through the C ABI) against numpy restatements of
+the reference functions on the same seeded inputs.  Integer work: bit-exact."""
+import numpy as np
+import pytest
+
+from qe import datagen as dg
+from qe import lib
+
+pytestmark = pytest.mark.gpu
+
+OPS = {"=": np.equal, ">": np.greater, "<": np.less}
+
+
+def _col(ctx, arr):
+    rel = ctx.load_relation([arr])
+    return ctx.column(rel, 0)
+
+
+def _ref_merge(rk, rv, sk, sv):
+    """join_relations (src/join.c:342-377), the literal loop (valid for unsorted input)."""
+    outR, outS = [], []
+    pr, s_start = 0, 0
+    nR, nS = len(rk), len(sk)
+    while pr < nR and s_start < nS:
+        ps, flag = s_start, 0
+        while ps < nS:
+            if rk[pr] < sk[ps]:
+                break
+            if rk[pr] > sk[ps]:
+                ps += 1
+                if flag == 0:
+                    s_start = ps
+            else:
+                outR.append(rv[pr])
+                outS.append(sv[ps])
+                flag = 1
+                ps += 1
+        pr += 1
+    return np.array(outR, dtype=np.uint32), np.array(outS, dtype=np.uint32)
+
+
+def _vec_merge(rk, rv, sk, sv):
+    """Same output for sorted inputs, vectorised (key, R order, S order)."""
+    lo = np.searchsorted(sk, rk, side="left")
+    hi = np.searchsorted(sk, rk, side="right")
+    c = hi - lo
+    outR = np.repeat(rv, c)
+    starts = np.repeat(lo - np.concatenate([[0], np.cumsum(c)[:-1]]), c)
+    outS = sv[starts + np.arange(c.sum())]
+    return outR.astype(np.uint32), outS.astype(np.uint32)
+
+
+def test_gpu_generator_matches_numpy(ctx):
+    rows = 1_000_003
+    kinds = [("mod", 1_000_000), ("mod", 777), ("hi32",)]
+    rel = ctx.gen_relation(rows, kinds, seed=1, gen_rel=2)
+    for j, k in enumerate(kinds):
+        want = dg.column(1, 2, j, rows, k)
+        col = ctx.column(rel, j)
+        assert ctx.checksum(col, None) == int(np.sum(want, dtype=np.uint64))
+        l = ctx.list_from_host(np.array([0, 1, 2, rows - 1], dtype=np.uint32))
+        got = sum(int(want[i]) for i in [0, 1, 2, rows - 1]) & ((1 << 64) - 1)
+        assert ctx.checksum(col, l) == got
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 4096, 4097, 100_000, 3_000_001])
+@pytest.mark.parametrize("op", ["<", ">", "="])
+def test_filter_scan(ctx, n, op):
+    rng = np.random.default_rng(n + ord(op))
+    a = rng.integers(0, 1000, n, dtype=np.uint64)
+    col = _col(ctx, a)
+    v = 500 if op != "=" else 7
+    l = ctx.filter_scan(col, op, v)
+    want = np.nonzero(OPS[op](a, np.uint64(v)))[0].astype(np.uint32)
+    np.testing.assert_array_equal(ctx.list_to_host(l), want)
+    ctx.list_free(l)
+
+
+@pytest.mark.parametrize("n", [1, 5, 8191, 500_000])
+def test_filter_refine_keeps_order(ctx, n):
+    rng = np.random.default_rng(n)
+    a = rng.integers(0, 1 << 32, 2 * n + 10, dtype=np.uint64)
+    col = _col(ctx, a)
+    rows = rng.integers(0, len(a), n).astype(np.uint32)    # arbitrary order, duplicates
+    l = ctx.list_from_host(rows)
+    ctx.filter_refine(col, ">", 1 << 31, l)
+    want = rows[a[rows] > np.uint64(1 << 31)]
+    np.testing.assert_array_equal(ctx.list_to_host(l), want)
+
+
+def test_filter_bad_operator_raises(ctx):
+    col = _col(ctx, np.arange(10, dtype=np.uint64))
+    with pytest.raises(lib.QEError):
+        ctx.filter_scan(col, "!", 3)
+
+
+@pytest.mark.parametrize("n,domain", [(2, 3), (1000, 10), (70_000, 1 << 20), (1_000_000, 1_000_000),
+                                      (2_000_000, 1 << 62), (300_000, 1)])
+def test_sort_pairs_stable(ctx, n, domain):
+    rng = np.random.default_rng(n)
+    k = rng.integers(0, domain, n, dtype=np.uint64)
+    v = rng.permutation(n).astype(np.uint32)
+    p = ctx.pairs_from_host(k, v)
+    ctx.sort_pairs(p)
+    gk, gv = ctx.pairs_to_host(p)
+    order = np.argsort(k, kind="stable")
+    np.testing.assert_array_equal(gk, k[order])
+    np.testing.assert_array_equal(gv, v[order])
+    assert ctx.is_sorted(p)
+    ctx.pairs_free(p)
+
+
+def test_sort_base_column_generates_rowids(ctx):
+    a = dg.column(5, 0, 0, 123_457, ("mod", 50_000))
+    col = _col(ctx, a)
+    p = ctx.gather_pairs(col, None)
+    ctx.sort_pairs(p)
+    gk, gv = ctx.pairs_to_host(p)
+    order = np.argsort(a, kind="stable")
+    np.testing.assert_array_equal(gk, a[order])
+    np.testing.assert_array_equal(gv, order.astype(np.uint32))
+
+
+def test_gather_pairs_list_order(ctx):
+    a = dg.column(6, 0, 1, 10_000, ("mod", 999))
+    col = _col(ctx, a)
+    rows = np.random.default_rng(0).integers(0, 10_000, 33_333).astype(np.uint32)
+    l = ctx.list_from_host(rows)
+    p = ctx.gather_pairs(col, l)
+    gk, gv = ctx.pairs_to_host(p)
+    np.testing.assert_array_equal(gk, a[rows])
+    np.testing.assert_array_equal(gv, rows)
+
+
+@pytest.mark.parametrize("nR,nS,dom", [(1, 1, 1), (10, 20, 5), (5000, 7000, 3000), (1_000_000, 1_000_000, 1_000_000),
+                                       (300_000, 50_000, 40), (100, 200_000, 3), (0, 10, 4), (10, 0, 4)])
+def test_merge_join_sorted(ctx, nR, nS, dom):
+    rng = np.random.default_rng(nR * 7 + nS)
+    rk = np.sort(rng.integers(0, dom, nR, dtype=np.uint64))
+    sk = np.sort(rng.integers(0, dom, nS, dtype=np.uint64))
+    rv = rng.integers(0, 1 << 31, nR).astype(np.uint32)
+    sv = rng.integers(0, 1 << 31, nS).astype(np.uint32)
+    R, S = ctx.pairs_from_host(rk, rv), ctx.pairs_from_host(sk, sv)
+    a, b = ctx.merge_join(R, S)
+    wa, wb = _vec_merge(rk, rv, sk, sv)
+    np.testing.assert_array_equal(ctx.list_to_host(a), wa)
+    np.testing.assert_array_equal(ctx.list_to_host(b), wb)
+
+
+def test_merge_join_skewed_window(ctx):
+    # one key matching 100k S rows: the S window does not fit LDS -> global-memory search path
+    rk = np.array([1, 5, 5, 5, 9], dtype=np.uint64)
+    sk = np.sort(np.concatenate([np.full(100_000, 5, np.uint64), np.arange(10, 20, dtype=np.uint64)]))
+    rv = np.arange(5, dtype=np.uint32)
+    sv = np.arange(len(sk), dtype=np.uint32)
+    R, S = ctx.pairs_from_host(rk, rv), ctx.pairs_from_host(sk, sv)
+    a, b = ctx.merge_join(R, S)
+    wa, wb = _vec_merge(rk, rv, sk, sv)
+    np.testing.assert_array_equal(ctx.list_to_host(a), wa)
+    np.testing.assert_array_equal(ctx.list_to_host(b), wb)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_merge_join_unsorted_matches_reference_loop(ctx, seed):
+    rng = np.random.default_rng(seed)
+    nR, nS = int(rng.integers(1, 300)), int(rng.integers(1, 300))
+    rk = rng.integers(0, 20, nR, dtype=np.uint64)
+    sk = rng.integers(0, 20, nS, dtype=np.uint64)
+    if seed % 2:
+        sk = np.sort(sk)   # one sorted side, one not
+    rv = np.arange(nR, dtype=np.uint32)
+    sv = np.arange(nS, dtype=np.uint32)
+    R, S = ctx.pairs_from_host(rk, rv), ctx.pairs_from_host(sk, sv)
+    a, b = ctx.merge_join(R, S)
+    wa, wb = _ref_merge(list(rk), list(rv), list(sk), list(sv))
+    np.testing.assert_array_equal(ctx.list_to_host(a), wa)
+    np.testing.assert_array_equal(ctx.list_to_host(b), wb)
+
+
+@pytest.mark.parametrize("nR,nS", [(0, 5), (1000, 999), (100_000, 123_456)])
+def test_scan_join(ctx, nR, nS):
+    rng = np.random.default_rng(nR)
+    rk = rng.integers(0, 4, nR, dtype=np.uint64)
+    sk = rng.integers(0, 4, nS, dtype=np.uint64)
+    rv = rng.integers(0, 1 << 30, nR).astype(np.uint32)
+    sv = rng.integers(0, 1 << 30, nS).astype(np.uint32)
+    R, S = ctx.pairs_from_host(rk, rv), ctx.pairs_from_host(sk, sv)
+    a, b = ctx.scan_join(R, S)
+    m = min(nR, nS)
+    eq = rk[:m] == sk[:m]
+    np.testing.assert_array_equal(ctx.list_to_host(a), rv[:m][eq])
+    np.testing.assert_array_equal(ctx.list_to_host(b), sv[:m][eq])
+
+
+def _ref_nondup_counts(outR, outS, mode, rows):
+    seen = set()
+    cnt = np.zeros(rows, dtype=np.uint32)
+    for r, s in zip(outR.tolist(), outS.tolist()):
+        if (r, s) not in seen:
+            seen.add((r, s))
+            cnt[r if mode == 0 else s] += 1
+    return cnt
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("dupR,dupS", [(False, False), (True, False), (False, True), (True, True)])
+def test_driver_counts(ctx, mode, dupR, dupS):
+    rng = np.random.default_rng(mode * 4 + dupR * 2 + dupS)
+    rows = 3000
+    colR = rng.integers(0, 500, rows, dtype=np.uint64)
+    colS = rng.integers(0, 500, rows, dtype=np.uint64)
+    lr = rng.integers(0, rows, 4000) if dupR else rng.permutation(rows)[:2000]
+    ls = rng.integers(0, rows, 4000) if dupS else rng.permutation(rows)[:2500]
+    lr, ls = lr.astype(np.uint32), ls.astype(np.uint32)
+    LR = ctx.list_from_host(lr, 0 if dupR else lib.LIST_DISTINCT)
+    LS = ctx.list_from_host(ls, 0 if dupS else lib.LIST_DISTINCT)
+    cR, cS = _col(ctx, colR), _col(ctx, colS)
+    R, S = ctx.gather_pairs(cR, LR), ctx.gather_pairs(cS, LS)
+    ctx.sort_pairs(R)
+    ctx.sort_pairs(S)
+    a, b = ctx.merge_join(R, S)
+    ha, hb = ctx.list_to_host(a), ctx.list_to_host(b)
+    want = _ref_nondup_counts(ha, hb, mode, rows)
+    for use_inputs in (True, False):
+        d = ctx.driver_counts(R if use_inputs else None, S if use_inputs else None, a, b, mode, rows)
+        np.testing.assert_array_equal(ctx.counts_to_host(d, rows), want)
+        ctx.counts_free(d)
+
+
+def _ref_join_payloads(counts, last, edit):
+    order = np.argsort(last, kind="stable")
+    l, e = last[order], edit[order]
+    return np.repeat(e, counts[l]).astype(np.uint32)
+
+
+@pytest.mark.parametrize("n", [0, 1, 1000, 300_000])
+def test_join_payloads(ctx, n):
+    rng = np.random.default_rng(n)
+    rows = max(1, n // 2)
+    counts = rng.integers(0, 4, rows).astype(np.uint32)
+    last = rng.integers(0, rows, n).astype(np.uint32)
+    edit = rng.integers(0, 1 << 31, n + 3).astype(np.uint32)
+    L, E = ctx.list_from_host(last), ctx.list_from_host(edit)
+    dc = ctx.list_from_host(counts)   # any device u32 buffer works as a count array
+    out = ctx.join_payloads(dc.d, rows, L, E)
+    np.testing.assert_array_equal(ctx.list_to_host(out), _ref_join_payloads(counts, last, edit[:n]))
+
+
+def test_join_payloads_short_edit_is_error(ctx):
+    L = ctx.list_from_host(np.array([0, 1, 2], dtype=np.uint32))
+    E = ctx.list_from_host(np.array([5], dtype=np.uint32))
+    dc = ctx.list_from_host(np.ones(3, dtype=np.uint32))
+    with pytest.raises(lib.QEError):
+        ctx.join_payloads(dc.d, 3, L, E)
+
+
+@pytest.mark.parametrize("n", [0, 3, 1_000_001])
+def test_checksum_wraps_mod_2_64(ctx, n):
+    a = np.full(2 * n + 1, (1 << 63) + 12345, dtype=np.uint64)
+    col = _col(ctx, a)
+    rows = np.random.default_rng(n).integers(0, len(a), n).astype(np.uint32)
+    l = ctx.list_from_host(rows)
+    assert ctx.checksum(col, l) == int(np.sum(a[rows], dtype=np.uint64))
