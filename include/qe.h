@@ -92,6 +92,10 @@ int qe_drop_relations(qe_ctx*);
  * another negative code. */
 int  qe_run_queries(qe_ctx*, const char* text, char** out, size_t* outlen);
 void qe_free_host(void*);
+/* Row count of the first selected binding's list in the last query that printed sums (the
+ * join's output cardinality for the relational shapes; bench "joined tuples"). */
+int  qe_last_result_rows(qe_ctx*, uint64_t* rows);
+int  qe_set_last_result_rows(qe_ctx*, uint64_t rows);
 
 /* ---- device primitives ---------------------------------------------------- */
 /* a1: exec_filter_rel_no_exists (src/filter.c:37-64): rowids i with col[i] op v, ascending. */

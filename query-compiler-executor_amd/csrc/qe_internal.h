@@ -64,6 +64,7 @@ struct qe_ctx {
     uint64_t in_use = 0, cached = 0;
 
     std::vector<qe::Relation> rels;
+    uint64_t last_result_rows = 0;
 
     // decoupled-lookback state: status words + per-launch tile tickets, epoch-tagged so that
     // nothing is cleared between launches (cleared when the 16-bit epoch wraps)

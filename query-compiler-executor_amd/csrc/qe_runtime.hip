@@ -291,6 +291,18 @@ int qe_gen_relation(qe_ctx* c, uint64_t rows, uint64_t ncols, const int* kinds, 
     QE_API_END(c)
 }
 
+int qe_last_result_rows(qe_ctx* c, uint64_t* rows) {
+    if (!c) return QE_EINVAL;
+    *rows = c->last_result_rows;
+    return 0;
+}
+
+int qe_set_last_result_rows(qe_ctx* c, uint64_t rows) {
+    if (!c) return QE_EINVAL;
+    c->last_result_rows = rows;
+    return 0;
+}
+
 int qe_relation_count(qe_ctx* c) { return c ? (int)c->rels.size() : QE_EINVAL; }
 
 int qe_relation_column(qe_ctx* c, int rel, int col, qe_col* out) {

@@ -379,6 +379,10 @@ static int execute_filter(exec_t* x, const query_t* q, const pred_t* p, mra_t* M
 
 /* print_sums (src/utilities.c:197-224) */
 static void print_sums(exec_t* x, const query_t* q, const mra_t* M) {
+    if (q->nsel > 0) {
+        exists_t e0 = relation_exists(M, q->rels[q->sel[0]], q->sel[0]);
+        if (e0.idx != -1) qe_set_last_result_rows(x->q, M->v[e0.ent]->e[e0.idx].list->n);
+    }
     for (size_t i = 0; i < q->nsel; i++) {
         uint64_t b = q->sel[2 * i], colno = q->sel[2 * i + 1];
         uint32_t relation = q->rels[b];

@@ -72,6 +72,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "qe_drop_relations": (I, [P]),
         "qe_run_queries": (I, [P, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
         "qe_free_host": (None, [VP]),
+        "qe_last_result_rows": (I, [P, C.POINTER(C.c_uint64)]),
+        "qe_set_last_result_rows": (I, [P, U64]),
         "qe_filter_scan": (I, [P, Col, C.c_char, U64, C.POINTER(List)]),
         "qe_filter_refine": (I, [P, Col, C.c_char, U64, C.POINTER(List)]),
         "qe_gather_pairs": (I, [P, Col, C.POINTER(List), C.POINTER(Pairs)]),
@@ -176,6 +178,11 @@ class Ctx:
         if rc not in (0, QE_EEXIT):
             raise QEError(rc, self.lib.qe_last_error(self.h).decode())
         return s, (1 if rc == QE_EEXIT else 0)
+
+    def last_result_rows(self) -> int:
+        r = C.c_uint64()
+        self._chk(self.lib.qe_last_result_rows(self.h, C.byref(r)))
+        return r.value
 
     # ---- primitives (tests / bench) ----
     def list_from_host(self, a: np.ndarray, flags: int = 0) -> List:
