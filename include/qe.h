@@ -130,6 +130,25 @@ int qe_join_payloads(qe_ctx*, const uint32_t* d_counts, uint64_t rows, const qe_
 /* a12: print_sums' inner loop (src/utilities.c:216-219): sum of col[rowid] mod 2^64. */
 int qe_checksum(qe_ctx*, qe_col col, const qe_list* rows, uint64_t* sum);
 
+/* ---- multi-GPU plan; the exchange itself is an RCCL all-to-all -------------- */
+/* Hash-partition n rows on their key: dest = fmix64(key) % nparts (murmur3 finaliser).  Rows go
+ * to contiguous per-destination segments (dest order, input order kept inside a segment) of the
+ * caller's device buffers out_keys / out_cols[c] (capacity n each); counts[p] (host) = rows for
+ * destination p.  ncols <= 4 uint32 rowid columns travel with each key. */
+int qe_partition(qe_ctx*, const uint64_t* keys, uint64_t n, const uint32_t* const* cols, int ncols,
+                 uint32_t nparts, uint64_t* counts, uint64_t* out_keys, uint32_t* const* out_cols);
+/* a1 on a row range [start, end) of a column, rowids numbered globally (a rank's slice). */
+int qe_filter_scan_range(qe_ctx*, qe_col col, uint64_t start, uint64_t end, char op, uint64_t v, qe_list* out);
+/* rowids start .. start+n-1 (an unfiltered slice). */
+int qe_iota(qe_ctx*, uint64_t start, uint64_t n, qe_list* out);
+/* out[i] = src[idx[i]] (carry a rowid column through a join's index lists). */
+int qe_take_u32(qe_ctx*, const uint32_t* src, const qe_list* idx, qe_list* out);
+/* Equi-join of two key arrays (a rank's bucket): sort both, merge, return aligned row indices. */
+int qe_join_indices(qe_ctx*, const uint64_t* keysA, uint64_t nA, const uint64_t* keysB, uint64_t nB, qe_list* ia,
+                    qe_list* ib);
+/* The ctx's HIP stream (hipStream_t), for callers that order their own work against it. */
+int qe_sync_stream_ptr(qe_ctx*, void** stream);
+
 /* ---- buffers ------------------------------------------------------------------------------- */
 int  qe_list_alloc(qe_ctx*, uint64_t n, qe_list* out);
 int  qe_list_from_host(qe_ctx*, const uint32_t* h, uint64_t n, uint32_t flags, qe_list* out);

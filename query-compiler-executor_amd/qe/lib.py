@@ -85,6 +85,13 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
                                  C.POINTER(C.c_void_p)]),
         "qe_join_payloads": (I, [P, C.c_void_p, U64, C.POINTER(List), C.POINTER(List), C.POINTER(List)]),
         "qe_checksum": (I, [P, Col, C.POINTER(List), C.POINTER(C.c_uint64)]),
+        "qe_partition": (I, [P, C.c_void_p, U64, C.POINTER(C.c_void_p), I, C.c_uint32, C.POINTER(C.c_uint64),
+                             C.c_void_p, C.POINTER(C.c_void_p)]),
+        "qe_filter_scan_range": (I, [P, Col, U64, U64, C.c_char, U64, C.POINTER(List)]),
+        "qe_iota": (I, [P, U64, U64, C.POINTER(List)]),
+        "qe_take_u32": (I, [P, C.c_void_p, C.POINTER(List), C.POINTER(List)]),
+        "qe_join_indices": (I, [P, C.c_void_p, U64, C.c_void_p, U64, C.POINTER(List), C.POINTER(List)]),
+        "qe_sync_stream_ptr": (I, [P, C.POINTER(C.c_void_p)]),
         "qe_list_alloc": (I, [P, U64, C.POINTER(List)]),
         "qe_list_from_host": (I, [P, VP, U64, C.c_uint32, C.POINTER(List)]),
         "qe_list_to_host": (I, [P, C.POINTER(List), VP]),
@@ -272,6 +279,36 @@ class Ctx:
         s = C.c_uint64()
         self._chk(self.lib.qe_checksum(self.h, col, C.byref(rows) if rows is not None else None, C.byref(s)))
         return s.value
+
+    # ---- multi-GPU plan primitives ----
+    def partition(self, keys_ptr: int, n: int, col_ptrs: list[int], nparts: int, out_keys_ptr: int,
+                  out_col_ptrs: list[int]) -> list[int]:
+        counts = (C.c_uint64 * nparts)()
+        cols = (C.c_void_p * max(1, len(col_ptrs)))(*col_ptrs)
+        ocols = (C.c_void_p * max(1, len(out_col_ptrs)))(*out_col_ptrs)
+        self._chk(self.lib.qe_partition(self.h, keys_ptr, n, cols, len(col_ptrs), nparts, counts, out_keys_ptr,
+                                        ocols))
+        return list(counts)
+
+    def filter_scan_range(self, col: Col, start: int, end: int, op: str, v: int) -> List:
+        l = List()
+        self._chk(self.lib.qe_filter_scan_range(self.h, col, start, end, op.encode(), v, C.byref(l)))
+        return l
+
+    def iota(self, start: int, n: int) -> List:
+        l = List()
+        self._chk(self.lib.qe_iota(self.h, start, n, C.byref(l)))
+        return l
+
+    def take_u32(self, src_ptr: int, idx: List) -> List:
+        l = List()
+        self._chk(self.lib.qe_take_u32(self.h, src_ptr, C.byref(idx), C.byref(l)))
+        return l
+
+    def join_indices(self, a_ptr: int, na: int, b_ptr: int, nb: int) -> tuple[List, List]:
+        ia, ib = List(), List()
+        self._chk(self.lib.qe_join_indices(self.h, a_ptr, na, b_ptr, nb, C.byref(ia), C.byref(ib)))
+        return ia, ib
 
     def sync(self):
         self._chk(self.lib.qe_sync(self.h))

@@ -1,0 +1,97 @@
+"""GPU tests of the multi-GPU plan's primitives and of qe.dist.GPUEngine end to end."""
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import dist_cpu_engine as dce
+import gpu_dist_worker
+from qe import datagen as dg
+from qe.dist import DistExecutor, GPUEngine
+
+pytestmark = pytest.mark.gpu
+
+C3 = "0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>1000000000&3.2<3000000000|1.2 2.2 3.2"
+
+
+@pytest.mark.parametrize("n,parts,ncols", [(0, 2, 1), (1, 8, 2), (100_000, 8, 3), (3_000_001, 5, 1), (4096, 64, 4)])
+def test_partition_is_stable_grouping(ctx, n, parts, ncols):
+    import torch
+    rng = np.random.default_rng(n)
+    keys = rng.integers(0, 1 << 40, n, dtype=np.uint64)
+    cols = [rng.integers(0, 1 << 31, n).astype(np.uint32) for _ in range(ncols)]
+    dk = torch.from_numpy(keys.view(np.int64)).cuda()
+    dc = [torch.from_numpy(c.view(np.int32)).cuda() for c in cols]
+    ok = torch.empty(max(1, n), dtype=torch.int64, device="cuda")
+    oc = [torch.empty(max(1, n), dtype=torch.int32, device="cuda") for _ in cols]
+    torch.cuda.synchronize()
+    counts = ctx.partition(dk.data_ptr(), n, [t.data_ptr() for t in dc], parts, ok.data_ptr(),
+                           [t.data_ptr() for t in oc])
+    dest = (dce.fmix64(keys) % np.uint64(parts)).astype(np.int64)
+    order = np.argsort(dest, kind="stable")
+    assert counts == np.bincount(dest, minlength=parts).tolist()
+    np.testing.assert_array_equal(ok.cpu().numpy()[:n].view(np.uint64), keys[order])
+    for c, o in zip(cols, oc):
+        np.testing.assert_array_equal(o.cpu().numpy()[:n].view(np.uint32), c[order])
+
+
+def test_filter_scan_range_and_iota(ctx):
+    a = dg.column(3, 1, 2, 50_000, ("hi32",))
+    rel = ctx.load_relation([a])
+    l = ctx.filter_scan_range(ctx.column(rel, 0), 12_345, 40_000, ">", 1 << 31)
+    want = np.nonzero(a[12_345:40_000] > np.uint64(1 << 31))[0] + 12_345
+    np.testing.assert_array_equal(ctx.list_to_host(l), want.astype(np.uint32))
+    i = ctx.iota(7, 1000)
+    np.testing.assert_array_equal(ctx.list_to_host(i), np.arange(7, 1007, dtype=np.uint32))
+
+
+def test_join_indices_and_take(ctx):
+    rng = np.random.default_rng(1)
+    ka = rng.integers(0, 500, 20_000, dtype=np.uint64)
+    kb = rng.integers(0, 500, 30_000, dtype=np.uint64)
+    import torch
+    ta, tb = torch.from_numpy(ka.view(np.int64)).cuda(), torch.from_numpy(kb.view(np.int64)).cuda()
+    torch.cuda.synchronize()
+    ia, ib = ctx.join_indices(ta.data_ptr(), len(ka), tb.data_ptr(), len(kb))
+    ha, hb = ctx.list_to_host(ia), ctx.list_to_host(ib)
+    assert np.all(ka[ha] == kb[hb])
+    got = sorted(zip(ha.tolist(), hb.tolist()))
+    want = dce.NumpyEngine(None, 0, 1).join_local(ka, kb)
+    assert got == sorted(zip(want[0].tolist(), want[1].tolist()))
+    src = ctx.list_from_host(np.arange(20_000, dtype=np.uint32) * 3)
+    t = ctx.take_u32(src.d, ia)
+    np.testing.assert_array_equal(ctx.list_to_host(t), ha * 3)
+
+
+def test_gpu_plan_single_rank_equals_faithful_executor(ctx):
+    rows = 2_000_000
+    ctx.drop_relations()
+    kinds = [("mod", rows), ("mod", rows), ("hi32",)]
+    for r in range(4):
+        ctx.gen_relation(rows, kinds, seed=1, gen_rel=r)
+    faithful, rc = ctx.run(C3 + "\n")
+    out, nrows = DistExecutor(GPUEngine(ctx, 0, 1), [rows] * 4).run(C3)
+    assert rc == 0 and out == faithful
+    assert nrows == ctx.last_result_rows()
+    ctx.drop_relations()
+
+
+def test_gpu_plan_two_ranks_share_one_gpu(ctx):
+    rows = 1_000_000
+    ctx.drop_relations()
+    kinds = [("mod", rows), ("mod", rows), ("hi32",)]
+    for r in range(4):
+        ctx.gen_relation(rows, kinds, seed=1, gen_rel=r)
+    want, _ = ctx.run(C3 + "\n0 1|0.1=1.0|0.2 1.2\n")
+    ctx.drop_relations()
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = dce.free_port()
+    procs = [mpc.Process(target=gpu_dist_worker.worker, args=(r, 2, port, rows, [C3, "0 1|0.1=1.0|0.2 1.2"], q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert res[0][0] + res[1][0] == want
