@@ -362,10 +362,17 @@ def bench_main(args, metric, query, cpu_baseline_fn=None, roofline_fn=None, traf
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # QE_DIST_BACKEND=gloo rehearses the multi-rank path on fewer GPUs than ranks (host-staged
+    # exchange); production is nccl = RCCL, one rank per GPU
+    backend = os.environ.get("QE_DIST_BACKEND", "nccl")
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     if not dist.is_initialized():
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    ctx = lib.Ctx(local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
+        else:
+            dist.init_process_group(backend)
+    ctx = lib.Ctx(dev)
     eng = GPUEngine(ctx, rank, world)
     total_rows = args.rows * world                 # weak scaling: every rank owns args.rows per relation
     kinds = [("mod", total_rows), ("mod", total_rows), ("hi32",)]
@@ -387,7 +394,7 @@ def bench_main(args, metric, query, cpu_baseline_fn=None, roofline_fn=None, traf
     torch.cuda.synchronize()
     dist.barrier()
     dt = time.perf_counter() - t0
-    tmax = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+    tmax = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}" if backend == "nccl" else "cpu")
     dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     dt = float(tmax.item())
     stats = ctx.kernel_stats()
