@@ -51,11 +51,23 @@ typedef struct { uint32_t* d; uint64_t n; uint64_t cap; uint32_t flags; } qe_lis
 
 /* Join input: (key, rowid) pairs in SoA -- the reference's `relation` of `tuple`s
  * (src/structs.h:7-15).  `val == NULL` means rowid i for every i (a base column).
- * flags: QE_PAIRS_DISTINCT (no rowid twice), QE_PAIRS_SORTED (ascending by key).
- * owns: bit 0 key buffer, bit 1 val buffer belong to the pairs (freed by qe_pairs_free). */
-typedef struct { uint64_t* key; uint32_t* val; uint64_t n; uint32_t flags; uint32_t owns; } qe_pairs;
+ * match: per-row count of partner rows, filled by qe_merge_join on its sorted path (NULL
+ * before), used by qe_driver_counts.  kor/kand: OR / AND of all keys when QE_PAIRS_BITS is set
+ * (the sort then skips its own reduction).
+ * flags: QE_PAIRS_DISTINCT (no rowid twice), QE_PAIRS_SORTED (ascending by key), QE_PAIRS_BITS.
+ * owns: bit 0 key, bit 1 val, bit 2 match buffer belong to the pairs (qe_pairs_free). */
+typedef struct {
+    uint64_t* key;
+    uint32_t* val;
+    uint32_t* match;
+    uint64_t n;
+    uint64_t kor, kand;
+    uint32_t flags;
+    uint32_t owns;
+} qe_pairs;
 #define QE_PAIRS_DISTINCT 1u
 #define QE_PAIRS_SORTED 2u
+#define QE_PAIRS_BITS 4u
 
 /* Per-kernel statistics (profiling, qe_set_profiling). */
 typedef struct {
@@ -82,6 +94,9 @@ int qe_gen_relation(qe_ctx*, uint64_t rows, uint64_t ncols, const int* kinds, co
                     uint64_t seed, uint32_t gen_rel, uint64_t row_start);
 int qe_relation_count(qe_ctx*);
 int qe_relation_column(qe_ctx*, int rel, int col, qe_col* out);
+/* Column statistics computed once when the relation is loaded/generated (OR and AND of every
+ * value: the bits that vary, which is all an LSD radix sort needs to plan its passes). */
+int qe_relation_column_bits(qe_ctx*, int rel, int col, uint64_t* kor, uint64_t* kand);
 int qe_relation_rows(qe_ctx*, int rel, uint64_t* rows);
 int qe_drop_relations(qe_ctx*);
 
@@ -112,21 +127,27 @@ int qe_sort_pairs(qe_ctx*, qe_pairs* inout);
 int qe_is_sorted(qe_ctx*, const qe_pairs*, int* sorted);
 /* a8: join_relations (src/join.c:325-392): aligned payload lists in key, R, S order.  Runs the
  * merge-path kernel when both inputs are sorted and the exact two-pointer semantics otherwise. */
-int qe_merge_join(qe_ctx*, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS);
+int qe_merge_join(qe_ctx*, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS);
 /* a9: scan_join (src/join.c:395-423). */
 int qe_scan_join(qe_ctx*, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS);
 /* a8 dedup: the multiset non_duplicates[mode] of a join (src/join.c:358-367) as a dense count
  * array over rowids [0, rows): counts[x] = #distinct (pR,pS) pairs whose mode-side rowid is x.
  * R/S (nullable) are the join's inputs: when both are QE_PAIRS_SORTED and the other side is
- * QE_PAIRS_DISTINCT the counts come from one annotated merge pass; otherwise from an exact
- * sort + unique of the packed pairs (outR[i], outS[i]).  join_payloads only ever uses the
- * driver as a sorted multiset (src/join.c:436-445), so counts are all it needs. */
+ * QE_PAIRS_DISTINCT the counts come from the merge's per-row match counts (mode 0) or one
+ * annotated merge pass (mode 1); otherwise from an exact sort + unique of the packed pairs
+ * (outR[i], outS[i]).  join_payloads only ever uses the driver as a sorted multiset
+ * (src/join.c:436-445), so counts are all it needs. */
 int qe_driver_counts(qe_ctx*, const qe_pairs* R, const qe_pairs* S, const qe_list* outR, const qe_list* outS,
                      int mode, uint64_t rows, uint32_t** d_counts);
 /* a10: join_payloads (src/join.c:426-484): edit[i] repeated counts[last[i]] times, ordered by
  * last[i] (stable).  |edit| < |last| is undefined in the reference -> QE_EINVAL. */
 int qe_join_payloads(qe_ctx*, const uint32_t* d_counts, uint64_t rows, const qe_list* last,
                      const qe_list* edit, qe_list* out);
+/* The same for every entry fix_all_mid_results updates with one (driver, last) pair
+ * (src/join.c:493-500): the pruning, the sort by `last` and the counts are shared, only the
+ * expansion runs per edit list.  outs[k] receives join_payloads(driver, last, edits[k]). */
+int qe_join_payloads_multi(qe_ctx*, const uint32_t* d_counts, uint64_t rows, const qe_list* last,
+                           const qe_list* const* edits, int nedits, qe_list* outs);
 /* a12: print_sums' inner loop (src/utilities.c:216-219): sum of col[rowid] mod 2^64. */
 int qe_checksum(qe_ctx*, qe_col col, const qe_list* rows, uint64_t* sum);
 

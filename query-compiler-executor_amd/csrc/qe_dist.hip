@@ -237,8 +237,8 @@ int qe_take_u32(qe_ctx* c, const uint32_t* src, const qe_list* idx, qe_list* out
 int qe_join_indices(qe_ctx* c, const uint64_t* keysA, uint64_t nA, const uint64_t* keysB, uint64_t nB, qe_list* ia,
                     qe_list* ib) {
     QE_API_BEGIN(c)
-    qe_pairs A{const_cast<uint64_t*>(keysA), nullptr, nA, QE_PAIRS_DISTINCT, 0};
-    qe_pairs B{const_cast<uint64_t*>(keysB), nullptr, nB, QE_PAIRS_DISTINCT, 0};
+    qe_pairs A{const_cast<uint64_t*>(keysA), nullptr, nullptr, nA, 0, 0, QE_PAIRS_DISTINCT, 0};
+    qe_pairs B{const_cast<uint64_t*>(keysB), nullptr, nullptr, nB, 0, 0, QE_PAIRS_DISTINCT, 0};
     int rc = qe_sort_pairs(c, &A);
     if (rc == 0) rc = qe_sort_pairs(c, &B);
     if (rc == 0) rc = qe_merge_join(c, &A, &B, ia, ib);

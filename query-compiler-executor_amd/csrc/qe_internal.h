@@ -30,6 +30,7 @@ struct Error : std::runtime_error {
 struct Relation {
     uint64_t rows = 0;
     std::vector<uint64_t*> cols;
+    std::vector<uint64_t> kor, kand;   // column statistics: OR / AND of all values (at load)
 };
 
 struct PendingEvent {
@@ -136,9 +137,13 @@ struct SortOut {
     uint32_t* vals;
     bool keys_new, vals_new;
 };
+// bits (nullable): host {OR, AND} of the keys when already known; otherwise one reduction pass
 SortOut radix_sort_u64(qe_ctx* c, const uint64_t* keys, const uint32_t* vals /*nullable: iota*/, uint64_t n,
-                       bool with_vals);
-SortOut radix_sort_u32(qe_ctx* c, const uint32_t* keys, const uint32_t* vals, uint64_t n);
+                       bool with_vals, const uint64_t* bits = nullptr);
+SortOut radix_sort_u32(qe_ctx* c, const uint32_t* keys, const uint32_t* vals, uint64_t n,
+                       const uint64_t* bits = nullptr);
+// OR / AND of n keys -> host out[2] (synchronises)
+void key_bits_u64(qe_ctx* c, const uint64_t* keys, uint64_t n, uint64_t* out);
 
 }  // namespace qe
 

@@ -79,7 +79,11 @@ __global__ void __launch_bounds__(1024) tile_scan_kernel(uint64_t* __restrict__ 
     if (threadIdx.x == 0) *total = carry;
 }
 
-// WRITE = 0: per-tile counts + flags (+ optional driver-count annotation)
+// R keys live in LDS with one pad slot per 8: thread t walks elements 8t..8t+7, and without the
+// pad the 32 lanes of a ds_read_b64 group would hit 4 banks (8-way conflict)
+__device__ __forceinline__ uint32_t rpad(uint32_t e) { return e + (e >> 3); }
+
+// WRITE = 0: per-tile counts + flags (+ optional per-row match counts / driver annotation)
 // WRITE = 1: expansion into outR / outS at tile offsets
 template <int WRITE>
 __global__ void __launch_bounds__(MJB) mj_tile(const uint64_t* __restrict__ rk, const uint32_t* __restrict__ rv,
@@ -87,8 +91,9 @@ __global__ void __launch_bounds__(MJB) mj_tile(const uint64_t* __restrict__ rk, 
                                                const uint32_t* __restrict__ sv, uint64_t nS,
                                                const uint64_t* __restrict__ win, uint64_t* __restrict__ tile_counts,
                                                uint32_t* __restrict__ outR, uint32_t* __restrict__ outS,
-                                               uint32_t* __restrict__ flags, uint32_t* __restrict__ annot) {
-    __shared__ uint64_t s_r[MJ_TILE];
+                                               uint32_t* __restrict__ flags, uint32_t* __restrict__ annot,
+                                               uint32_t* __restrict__ match) {
+    __shared__ uint64_t s_r[MJ_TILE + MJ_TILE / 8];
     __shared__ uint64_t s_s[MJ_WIN];
     __shared__ uint32_t s_lo[WRITE ? MJ_TILE : 1];    // window-relative S start per R element
     __shared__ uint32_t s_off[WRITE ? MJ_TILE : 1];   // tile-relative output offset per R element
@@ -102,7 +107,7 @@ __global__ void __launch_bounds__(MJB) mj_tile(const uint64_t* __restrict__ rk, 
     const uint64_t wn = whi - wlo;
     const bool in_lds = wn <= MJ_WIN;
     if (threadIdx.x == 0) s_flag = 0;
-    for (uint32_t i = threadIdx.x; i < tn; i += MJB) s_r[i] = rk[base + i];
+    for (uint32_t i = threadIdx.x; i < tn; i += MJB) s_r[rpad(i)] = rk[base + i];
     if (in_lds)
         for (uint32_t i = threadIdx.x; i < wn; i += MJB) s_s[i] = sk[wlo + i];
     __syncthreads();
@@ -123,7 +128,7 @@ __global__ void __launch_bounds__(MJB) mj_tile(const uint64_t* __restrict__ rk, 
         cnt[j] = 0;
         lo_rel[j] = 0;
         if (e >= tn) continue;
-        uint64_t key = s_r[e];
+        uint64_t key = s_r[rpad(e)];
         uint64_t lo, hi;
         if (have_p && key == prev_key) {
             lo = prev_lo;
@@ -159,8 +164,9 @@ __global__ void __launch_bounds__(MJB) mj_tile(const uint64_t* __restrict__ rk, 
         tsum += c;
         if (!WRITE) {
             if (c > 1) myflag |= MJF_R_FANOUT;
+            if (match) match[base + e] = c;
             if (c > 0) {
-                uint64_t nxt = e + 1 < tn ? s_r[e + 1] : (base + e + 1 < nR ? rk[base + e + 1] : ~key);
+                uint64_t nxt = e + 1 < tn ? s_r[rpad(e + 1)] : (base + e + 1 < nR ? rk[base + e + 1] : ~key);
                 if (nxt == key) myflag |= MJF_S_DUP;
                 if (annot) annot[rv ? rv[base + e] : (uint32_t)(base + e)] = c;
             }
@@ -258,28 +264,62 @@ __global__ void __launch_bounds__(256) is_sorted_kernel(const uint64_t* __restri
     if (__any(b) && lane_id() == 0) atomicOr(bad, 1u);
 }
 
+// keys = col[rows] in list order, plus the OR / AND of the gathered keys (the radix sort's
+// pass plan) so the sort needs no reduction pass of its own
 __global__ void __launch_bounds__(256) gather_keys_kernel(const uint64_t* __restrict__ col,
                                                           const uint32_t* __restrict__ rows, uint64_t n,
-                                                          uint64_t* __restrict__ out) {
+                                                          uint64_t* __restrict__ out,
+                                                          unsigned long long* __restrict__ bits) {
+    uint64_t o = 0, a = ~0ull;
     uint64_t i4 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
     if (i4 + 3 < n) {
         uint4 r = *reinterpret_cast<const uint4*>(rows + i4);
-        ulonglong2 a, b;
-        a.x = col[r.x];
-        a.y = col[r.y];
-        b.x = col[r.z];
-        b.y = col[r.w];
-        *reinterpret_cast<ulonglong2*>(out + i4) = a;
-        *reinterpret_cast<ulonglong2*>(out + i4 + 2) = b;
+        ulonglong2 x, y;
+        x.x = col[r.x];
+        x.y = col[r.y];
+        y.x = col[r.z];
+        y.y = col[r.w];
+        *reinterpret_cast<ulonglong2*>(out + i4) = x;
+        *reinterpret_cast<ulonglong2*>(out + i4 + 2) = y;
+        o = x.x | x.y | y.x | y.y;
+        a = x.x & x.y & y.x & y.y;
     } else {
-        for (uint64_t i = i4; i < n; i++) out[i] = col[rows[i]];
+        for (uint64_t i = i4; i < n; i++) {
+            uint64_t k = col[rows[i]];
+            out[i] = k;
+            o |= k;
+            a &= k;
+        }
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        o |= shfl_xor_u64(o, m);
+        a &= shfl_xor_u64(a, m);
+    }
+    __shared__ uint64_t so[4], sa[4];
+    if (lane_id() == 0) {
+        so[wave_id()] = o;
+        sa[wave_id()] = a;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        o = so[0] | so[1] | so[2] | so[3];
+        a = sa[0] & sa[1] & sa[2] & sa[3];
+        atomicOr(&bits[0], (unsigned long long)o);
+        atomicAnd(&bits[1], (unsigned long long)a);
     }
 }
 
-__global__ void __launch_bounds__(256) widen_u32_kernel(const uint32_t* __restrict__ in, uint64_t n,
-                                                        uint64_t* __restrict__ out) {
+// driver counts from the merge's per-row match counts: counts[rowid] = matches (every row of a
+// rowid carries the same key, hence the same count: plain stores, no atomics)
+__global__ void __launch_bounds__(256) scatter_match_kernel(const uint32_t* __restrict__ val,
+                                                            const uint32_t* __restrict__ match, uint64_t n,
+                                                            uint32_t* __restrict__ counts) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = in[i];
+    if (i < n) {
+        uint32_t m = match[i];
+        if (m) counts[val ? val[i] : (uint32_t)i] = m;
+    }
 }
 
 // sum of col[rowid] mod 2^64 (print_sums, src/utilities.c:216-219); rows == null: whole column
@@ -313,11 +353,12 @@ __global__ void __launch_bounds__(256) checksum_kernel(const uint64_t* __restric
 // element i (sorted by last) is emitted counts[last[i]] times
 constexpr int XB = 256, X_ITEMS = 8, X_TILE = XB * X_ITEMS;
 
+// WRITE = 1 emits vals[idx[i]] (idx != null) or vals[i]
 template <int WRITE>
 __global__ void __launch_bounds__(XB) expand_kernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
                                                     uint64_t n, const uint32_t* __restrict__ counts,
                                                     uint64_t* __restrict__ tile_counts, uint32_t* __restrict__ out,
-                                                    uint32_t* __restrict__ flags) {
+                                                    uint32_t* __restrict__ flags, const uint32_t* __restrict__ idx) {
     __shared__ uint32_t s_off[WRITE ? X_TILE : 1];
     __shared__ uint64_t s_red[XB / 64];
     const uint32_t tile = blockIdx.x;
@@ -327,10 +368,20 @@ __global__ void __launch_bounds__(XB) expand_kernel(const uint32_t* __restrict__
     uint64_t tsum = 0;
     uint32_t mx = 0;
     const uint32_t e0 = threadIdx.x * X_ITEMS;
+    uint32_t k[X_ITEMS];
+    if (e0 + X_ITEMS <= tn) {   // 2 x 16-B loads of this thread's 8 keys
+        uint4 a = *reinterpret_cast<const uint4*>(keys + base + e0);
+        uint4 b = *reinterpret_cast<const uint4*>(keys + base + e0 + 4);
+        k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w;
+        k[4] = b.x; k[5] = b.y; k[6] = b.z; k[7] = b.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < X_ITEMS; j++) k[j] = e0 + j < tn ? keys[base + e0 + j] : 0;
+    }
 #pragma unroll
     for (int j = 0; j < X_ITEMS; j++) {
         uint32_t e = e0 + j;
-        c[j] = e < tn ? counts[keys[base + e]] : 0;
+        c[j] = e < tn ? counts[k[j]] : 0;
         tsum += c[j];
         mx = c[j] > mx ? c[j] : mx;
     }
@@ -369,7 +420,7 @@ __global__ void __launch_bounds__(XB) expand_kernel(const uint32_t* __restrict__
             if (s_off[m] <= o) a = m;
             else b = m;
         }
-        out[gofs + o] = vals[base + a];
+        out[gofs + o] = idx ? vals[idx[base + a]] : vals[base + a];
     }
 }
 
@@ -404,12 +455,18 @@ enum : uint32_t { PF_DISTINCT = 1u, PF_SORTED = 2u };
 
 const char* op_ok(char op) { return (op == '=' || op == '<' || op == '>') ? nullptr : "Wrong operator"; }
 
-// merge join on sorted inputs; returns pair count and flags
-void merge_sorted(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS, uint32_t* oflags) {
+// merge join on sorted inputs; returns pair count and flags.  R->match receives each R row's
+// number of S partners (the mode-0 driver counts come from it for free)
+void merge_sorted(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS, uint32_t* oflags) {
     const uint64_t nR = R->n, nS = S->n;
     outR->n = outS->n = 0;
     *oflags = 0;
+    if (!R->match && nR) {
+        R->match = dalloc_t<uint32_t>(c, nR);
+        R->owns |= 4;
+    }
     if (nR == 0 || nS == 0) {
+        if (nR) QE_HIP(hipMemsetAsync(R->match, 0, nR * 4, c->stream));
         outR->d = dalloc_t<uint32_t>(c, 1);
         outS->d = dalloc_t<uint32_t>(c, 1);
         outR->cap = outS->cap = 0;
@@ -427,9 +484,9 @@ void merge_sorted(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR
         QE_HIP(hipGetLastError());
     }
     {
-        Timed t(c, "mj_count", 8.0 * nR + 8.0 * nS);
+        Timed t(c, "mj_count", 8.0 * nR + 8.0 * nS + 4.0 * nR);
         hipLaunchKernelGGL(mj_tile<0>, dim3(nt), dim3(MJB), 0, c->stream, R->key, R->val, nR, S->key, S->val, nS, win,
-                           tc, nullptr, nullptr, d_flags, nullptr);
+                           tc, nullptr, nullptr, d_flags, nullptr, R->match);
         QE_HIP(hipGetLastError());
         hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, c->stream, tc, (uint64_t)nt, c->d_scratch + 17);
         QE_HIP(hipGetLastError());
@@ -445,7 +502,7 @@ void merge_sorted(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR
     if (P) {
         Timed t(c, "mj_write", 12.0 * nR + 12.0 * nS + 8.0 * P);
         hipLaunchKernelGGL(mj_tile<1>, dim3(nt), dim3(MJB), 0, c->stream, R->key, R->val, nR, S->key, S->val, nS, win,
-                           tc, outR->d, outS->d, nullptr, nullptr);
+                           tc, outR->d, outS->d, nullptr, nullptr, nullptr);
         QE_HIP(hipGetLastError());
     }
     dfree(c, win);
@@ -521,6 +578,13 @@ uint32_t* driver_counts_sorted(qe_ctx* c, const qe_pairs* A, const qe_pairs* B, 
     uint32_t* cnt = dalloc_t<uint32_t>(c, std::max<uint64_t>(rows, 1));
     QE_HIP(hipMemsetAsync(cnt, 0, std::max<uint64_t>(rows, 1) * 4, c->stream));
     if (A->n == 0 || B->n == 0) return cnt;
+    if (A->match) {   // A was the merge's R side: its per-row match counts are the answer
+        Timed t(c, "driver_scatter", 12.0 * A->n);
+        hipLaunchKernelGGL(scatter_match_kernel, dim3(grid_for(A->n, 256)), dim3(256), 0, c->stream, A->val, A->match,
+                           A->n, cnt);
+        QE_HIP(hipGetLastError());
+        return cnt;
+    }
     const uint32_t nt = (uint32_t)((A->n + MJ_TILE - 1) / MJ_TILE);
     uint64_t* win = dalloc_t<uint64_t>(c, 2 * (uint64_t)nt);
     uint64_t* tc = dalloc_t<uint64_t>(c, nt);
@@ -531,7 +595,7 @@ uint32_t* driver_counts_sorted(qe_ctx* c, const qe_pairs* A, const qe_pairs* B, 
                            nt, win);
         QE_HIP(hipGetLastError());
         hipLaunchKernelGGL(mj_tile<0>, dim3(nt), dim3(MJB), 0, c->stream, A->key, A->val, A->n, B->key, B->val, B->n,
-                           win, tc, nullptr, nullptr, d_flags, cnt);
+                           win, tc, nullptr, nullptr, d_flags, cnt, nullptr);
         QE_HIP(hipGetLastError());
     }
     dfree(c, win);
@@ -570,12 +634,21 @@ int qe_filter_refine(qe_ctx* c, qe_col col, char op, uint64_t v, qe_list* inout)
 
 int qe_gather_pairs(qe_ctx* c, qe_col col, const qe_list* rows, qe_pairs* out) {
     QE_API_BEGIN(c)
+    out->match = nullptr;
     if (!rows) {
         out->key = const_cast<uint64_t*>(col.d);
         out->val = nullptr;
         out->n = col.n;
         out->flags = PF_DISTINCT;
         out->owns = 0;
+        // a base column: its OR / AND were computed when the relation was loaded
+        for (auto& r : c->rels)
+            for (size_t j = 0; j < r.cols.size(); j++)
+                if (r.cols[j] == col.d && r.rows == col.n && j < r.kor.size()) {
+                    out->kor = r.kor[j];
+                    out->kand = r.kand[j];
+                    out->flags |= QE_PAIRS_BITS;
+                }
         return 0;
     }
     const uint64_t n = rows->n;
@@ -584,12 +657,20 @@ int qe_gather_pairs(qe_ctx* c, qe_col col, const qe_list* rows, qe_pairs* out) {
     out->n = n;
     out->flags = (rows->flags & QE_LIST_DISTINCT) ? PF_DISTINCT : 0;
     out->owns = 1;
+    uint64_t* d_bits = c->d_scratch + 44;
+    uint64_t init[2] = {0ull, ~0ull};
+    QE_HIP(hipMemcpyAsync(d_bits, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
     if (n) {
         Timed t(c, "gather_keys", 12.0 * n + 8.0 * n);
         hipLaunchKernelGGL(gather_keys_kernel, dim3(grid_for((n + 3) / 4, 256)), dim3(256), 0, c->stream, col.d,
-                           rows->d, n, out->key);
+                           rows->d, n, out->key, (unsigned long long*)d_bits);
         QE_HIP(hipGetLastError());
     }
+    uint64_t kb[2];
+    read_words(c, d_bits, kb, 2);
+    out->kor = kb[0];
+    out->kand = kb[1];
+    out->flags |= QE_PAIRS_BITS;
     return 0;
     QE_API_END(c)
 }
@@ -597,7 +678,8 @@ int qe_gather_pairs(qe_ctx* c, qe_col col, const qe_list* rows, qe_pairs* out) {
 int qe_sort_pairs(qe_ctx* c, qe_pairs* p) {
     QE_API_BEGIN(c)
     if (p->flags & PF_SORTED) return 0;
-    SortOut so = radix_sort_u64(c, p->key, p->val, p->n, true);
+    uint64_t bits[2] = {p->kor, p->kand};
+    SortOut so = radix_sort_u64(c, p->key, p->val, p->n, true, (p->flags & QE_PAIRS_BITS) ? bits : nullptr);
     if (so.keys_new) {
         if (p->owns & 1) dfree(c, p->key);
         p->key = (uint64_t*)so.keys;
@@ -620,7 +702,7 @@ int qe_is_sorted(qe_ctx* c, const qe_pairs* p, int* sorted) {
     QE_API_END(c)
 }
 
-int qe_merge_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS) {
+int qe_merge_join(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS) {
     QE_API_BEGIN(c)
     const bool sorted = pairs_sorted(c, R) && pairs_sorted(c, S);
     uint32_t fl = MJF_R_FANOUT | MJF_S_DUP;
@@ -658,40 +740,44 @@ int qe_driver_counts(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const qe_l
     QE_API_END(c)
 }
 
-int qe_join_payloads(qe_ctx* c, const uint32_t* d_counts, uint64_t rows, const qe_list* last, const qe_list* edit,
-                     qe_list* out) {
+int qe_join_payloads_multi(qe_ctx* c, const uint32_t* d_counts, uint64_t rows, const qe_list* last,
+                           const qe_list* const* edits, int nedits, qe_list* outs) {
     QE_API_BEGIN(c)
-    (void)rows;
-    if (edit->n < last->n) throw Error(QE_EINVAL, "join_payloads: |edit| < |last| (reference-undefined)");
+    for (int k = 0; k < nedits; k++)
+        if (edits[k]->n < last->n) throw Error(QE_EINVAL, "join_payloads: |edit| < |last| (reference-undefined)");
     const uint64_t n = last->n;
-    out->n = 0;
-    out->flags = 0;
-    if (n == 0) {
-        out->d = dalloc_t<uint32_t>(c, 1);
-        out->cap = 0;
-        out->flags = QE_LIST_DISTINCT;
-        return 0;
+    for (int k = 0; k < nedits; k++) {
+        outs[k].n = outs[k].cap = 0;
+        outs[k].flags = 0;
+        outs[k].d = nullptr;
     }
-    // 1. drop (last, edit) whose driver count is 0 -- they emit nothing
-    uint32_t* pl = dalloc_t<uint32_t>(c, n);
-    uint32_t* pe = dalloc_t<uint32_t>(c, n);
-    uint64_t m = compact_nonzero_pairs(c, d_counts, last->d, edit->d, n, pl, pe);
-    // 2. stable sort by `last` (the reference sorts R = (last, edit) by key, src/join.c:444)
-    SortOut so = radix_sort_u32(c, pl, pe, m);
+    // 1. positions whose driver count is 0 emit nothing: keep (last[i], i) for the others
+    uint32_t* pl = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
+    uint32_t* pi = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
+    uint64_t m = n ? compact_nonzero_pairs(c, d_counts, last->d, nullptr, n, pl, pi) : 0;
+    // 2. one stable sort by `last` for every edit list (the reference sorts R = (last, edit)
+    //    by key per entry, src/join.c:444; the permutation is the same for all of them).
+    //    Rowids are < rows, which bounds the bits the sort has to look at.
+    uint64_t hb = 0;
+    while (hb < 64 && (rows - 1) >> hb) hb++;
+    uint64_t bits[2] = {hb >= 64 ? ~0ull : ((1ull << hb) - 1), 0};
+    SortOut so = radix_sort_u32(c, pl, pi, m, rows > 1 ? bits : nullptr);
     const uint32_t* sk = (const uint32_t*)so.keys;
-    const uint32_t* sv = so.vals;
-    // 3. emit edit x driver multiplicity, in sorted order
+    const uint32_t* sidx = so.vals;
+    // 3. per sorted position: driver multiplicity -> output offsets (shared)
     uint64_t P = 0;
     uint32_t mflag = 0;
+    uint64_t* tc = nullptr;
+    uint32_t nt = 0;
     if (m) {
-        const uint32_t nt = (uint32_t)((m + X_TILE - 1) / X_TILE);
-        uint64_t* tc = dalloc_t<uint64_t>(c, nt);
+        nt = (uint32_t)((m + X_TILE - 1) / X_TILE);
+        tc = dalloc_t<uint64_t>(c, nt);
         uint32_t* d_flags = (uint32_t*)(c->d_scratch + 30);
         QE_HIP(hipMemsetAsync(d_flags, 0, 4, c->stream));
         {
             Timed t(c, "payload_count", 8.0 * m);
-            hipLaunchKernelGGL(expand_kernel<0>, dim3(nt), dim3(XB), 0, c->stream, sk, sv, m, d_counts, tc, nullptr,
-                               d_flags);
+            hipLaunchKernelGGL(expand_kernel<0>, dim3(nt), dim3(XB), 0, c->stream, sk, sidx, m, d_counts, tc, nullptr,
+                               d_flags, nullptr);
             QE_HIP(hipGetLastError());
             hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, c->stream, tc, (uint64_t)nt,
                                c->d_scratch + 31);
@@ -701,26 +787,32 @@ int qe_join_payloads(qe_ctx* c, const uint32_t* d_counts, uint64_t rows, const q
         read_words(c, c->d_scratch + 30, h, 2);
         mflag = (uint32_t)h[0];
         P = h[1];
-        out->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(P, 1));
+    }
+    // 4. per edit list: edit[perm[i]] x multiplicity, in sorted order
+    for (int k = 0; k < nedits; k++) {
+        outs[k].d = dalloc_t<uint32_t>(c, std::max<uint64_t>(P, 1));
+        outs[k].n = outs[k].cap = P;
+        outs[k].flags = ((edits[k]->flags & QE_LIST_DISTINCT) && !(mflag & 1u)) ? QE_LIST_DISTINCT : 0;
         if (P) {
             Timed t(c, "payload_expand", 12.0 * m + 4.0 * P);
-            hipLaunchKernelGGL(expand_kernel<1>, dim3(nt), dim3(XB), 0, c->stream, sk, sv, m, d_counts, tc, out->d,
-                               nullptr);
+            hipLaunchKernelGGL(expand_kernel<1>, dim3(nt), dim3(XB), 0, c->stream, sk, edits[k]->d, m, d_counts, tc,
+                               outs[k].d, nullptr, sidx);
             QE_HIP(hipGetLastError());
         }
-        dfree(c, tc);
-    } else {
-        out->d = dalloc_t<uint32_t>(c, 1);
     }
-    out->n = P;
-    out->cap = P;
-    out->flags = ((edit->flags & QE_LIST_DISTINCT) && !(mflag & 1u)) ? QE_LIST_DISTINCT : 0;
+    if (tc) dfree(c, tc);
     if (so.keys_new) dfree(c, so.keys);
     if (so.vals_new) dfree(c, so.vals);
     dfree(c, pl);
-    dfree(c, pe);
+    dfree(c, pi);
     return 0;
     QE_API_END(c)
+}
+
+int qe_join_payloads(qe_ctx* c, const uint32_t* d_counts, uint64_t rows, const qe_list* last, const qe_list* edit,
+                     qe_list* out) {
+    const qe_list* e[1] = {edit};
+    return qe_join_payloads_multi(c, d_counts, rows, last, e, 1, out);
 }
 
 int qe_checksum(qe_ctx* c, qe_col col, const qe_list* rows, uint64_t* sum) {

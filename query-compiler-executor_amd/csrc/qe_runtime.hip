@@ -186,6 +186,19 @@ __global__ void __launch_bounds__(256) gen_column_kernel(uint64_t* out, uint64_t
 
 using namespace qe;
 
+// column statistics: OR / AND of every column, one read at load time (zone-map style metadata
+// that lets the radix sort plan its passes without a reduction pass per query)
+static void column_stats(qe_ctx* c, Relation& r) {
+    r.kor.resize(r.cols.size());
+    r.kand.resize(r.cols.size());
+    for (size_t j = 0; j < r.cols.size(); j++) {
+        uint64_t b[2];
+        key_bits_u64(c, r.cols[j], r.rows, b);
+        r.kor[j] = b[0];
+        r.kand[j] = b[1];
+    }
+}
+
 // =============================================================================================
 // C ABI: lifecycle, relations, buffers, profiling
 // =============================================================================================
@@ -263,6 +276,7 @@ int qe_load_relation(qe_ctx* c, uint64_t rows, uint64_t ncols, const uint64_t* c
         r.cols.push_back(d);
     }
     QE_HIP(hipStreamSynchronize(c->stream));
+    column_stats(c, r);
     c->rels.push_back(std::move(r));
     return (int)c->rels.size() - 1;
     QE_API_END(c)
@@ -286,6 +300,7 @@ int qe_gen_relation(qe_ctx* c, uint64_t rows, uint64_t ncols, const int* kinds, 
         r.cols.push_back(d);
     }
     QE_HIP(hipStreamSynchronize(c->stream));
+    column_stats(c, r);
     c->rels.push_back(std::move(r));
     return (int)c->rels.size() - 1;
     QE_API_END(c)
@@ -310,6 +325,14 @@ int qe_relation_column(qe_ctx* c, int rel, int col, qe_col* out) {
         return QE_EINVAL;
     out->d = c->rels[rel].cols[col];
     out->n = c->rels[rel].rows;
+    return 0;
+}
+
+int qe_relation_column_bits(qe_ctx* c, int rel, int col, uint64_t* kor, uint64_t* kand) {
+    if (!c || rel < 0 || rel >= (int)c->rels.size() || col < 0 || col >= (int)c->rels[rel].cols.size())
+        return QE_EINVAL;
+    *kor = c->rels[rel].kor[col];
+    *kand = c->rels[rel].kand[col];
     return 0;
 }
 
@@ -377,7 +400,9 @@ int qe_pairs_from_host(qe_ctx* c, const uint64_t* key, const uint32_t* val, uint
         QE_HIP(hipMemcpyAsync(out->val, val, n * 4, hipMemcpyHostToDevice, c->stream));
     }
     QE_HIP(hipStreamSynchronize(c->stream));
+    out->match = nullptr;
     out->n = n;
+    out->kor = out->kand = 0;
     out->flags = 0;
     out->owns = 3;
     return 0;
@@ -406,6 +431,8 @@ void qe_pairs_free(qe_ctx* c, qe_pairs* p) {
     if (!c || !p) return;
     if (p->owns & 1) dfree(c, p->key);
     if (p->owns & 2) dfree(c, p->val);
+    if (p->owns & 4) dfree(c, p->match);
+    p->match = nullptr;
     p->key = nullptr;
     p->val = nullptr;
     p->n = 0;

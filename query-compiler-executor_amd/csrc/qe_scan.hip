@@ -93,18 +93,25 @@ struct ScanJoinOp {            // scan_join: positional key equality, both paylo
     }
 };
 
-struct NonzeroPairsOp {        // join_payloads: keep (last[i], edit[i]) whose driver count > 0
+struct NonzeroPairsOp {        // join_payloads: keep (last[i], edit[i] or i) whose driver count > 0
     static constexpr int VEC = 4;
-    const uint32_t *counts, *last, *edit;
+    const uint32_t *counts, *last, *edit;   // edit == null: emit the position i
     __device__ __forceinline__ void load(uint64_t base, uint64_t n, bool* f, uint32_t* v0, uint32_t* v1) const {
+        uint32_t l[4];
+        if (base + 3 < n) {
+            uint4 x = *reinterpret_cast<const uint4*>(last + base);
+            l[0] = x.x; l[1] = x.y; l[2] = x.z; l[3] = x.w;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++) l[k] = base + k < n ? last[base + k] : 0;
+        }
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             uint64_t i = base + k;
             bool ok = i < n;
-            uint32_t l = ok ? last[i] : 0;
-            f[k] = ok && counts[l] != 0;
-            v0[k] = l;
-            v1[k] = ok ? edit[i] : 0;
+            f[k] = ok && counts[l[k]] != 0;
+            v0[k] = l[k];
+            v1[k] = ok ? (edit ? edit[i] : (uint32_t)i) : 0;
         }
     }
 };

@@ -240,22 +240,34 @@ static PassDesc plan_passes(uint64_t kor, uint64_t kand) {
 }
 
 template <typename K>
-static SortOut radix_sort_impl(qe_ctx* c, const K* keys, const uint32_t* vals, uint64_t n, bool with_vals,
-                               const char* name) {
-    SortOut so{(void*)keys, (uint32_t*)vals, false, false};
-    if (n < 2) return so;
-    if (n >= 0xFFFFFFFFull) throw Error(QE_EINVAL, "sort input too large");
+static void key_bits_impl(qe_ctx* c, const K* keys, uint64_t n, uint64_t* out) {
     uint64_t* d_bits = c->d_scratch + 8;   // [or, and]
     uint64_t init[2] = {0ull, ~0ull};
     QE_HIP(hipMemcpyAsync(d_bits, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
-    {
+    if (n) {
         Timed t(c, "sort_keybits", (double)sizeof(K) * n);
         hipLaunchKernelGGL(key_bits_kernel<K>, dim3(grid_for(n, 256 * 16, 4096)), dim3(256), 0, c->stream, keys,
                            n, d_bits);
         QE_HIP(hipGetLastError());
     }
+    read_words(c, d_bits, out, 2);
+}
+
+void key_bits_u64(qe_ctx* c, const uint64_t* keys, uint64_t n, uint64_t* out) { key_bits_impl(c, keys, n, out); }
+
+template <typename K>
+static SortOut radix_sort_impl(qe_ctx* c, const K* keys, const uint32_t* vals, uint64_t n, bool with_vals,
+                               const char* name, const uint64_t* bits) {
+    SortOut so{(void*)keys, (uint32_t*)vals, false, false};
+    if (n < 2) return so;
+    if (n >= 0xFFFFFFFFull) throw Error(QE_EINVAL, "sort input too large");
     uint64_t kb[2];
-    read_words(c, d_bits, kb, 2);
+    if (bits) {
+        kb[0] = bits[0];
+        kb[1] = bits[1];
+    } else {
+        key_bits_impl(c, keys, n, kb);
+    }
     PassDesc pd = plan_passes(kb[0], kb[1]);
     if (pd.npass == 0) return so;   // every key equal: already sorted (and stable)
 
@@ -313,12 +325,14 @@ static SortOut radix_sort_impl(qe_ctx* c, const K* keys, const uint32_t* vals, u
     return so;
 }
 
-SortOut radix_sort_u64(qe_ctx* c, const uint64_t* keys, const uint32_t* vals, uint64_t n, bool with_vals) {
-    return radix_sort_impl<uint64_t>(c, keys, vals, n, with_vals, with_vals ? "sort_pass_k64v32" : "sort_pass_k64");
+SortOut radix_sort_u64(qe_ctx* c, const uint64_t* keys, const uint32_t* vals, uint64_t n, bool with_vals,
+                       const uint64_t* bits) {
+    return radix_sort_impl<uint64_t>(c, keys, vals, n, with_vals, with_vals ? "sort_pass_k64v32" : "sort_pass_k64",
+                                     bits);
 }
 
-SortOut radix_sort_u32(qe_ctx* c, const uint32_t* keys, const uint32_t* vals, uint64_t n) {
-    return radix_sort_impl<uint32_t>(c, keys, vals, n, true, "sort_pass_k32v32");
+SortOut radix_sort_u32(qe_ctx* c, const uint32_t* keys, const uint32_t* vals, uint64_t n, const uint64_t* bits) {
+    return radix_sort_impl<uint32_t>(c, keys, vals, n, true, "sort_pass_k32v32", bits);
 }
 
 }  // namespace qe

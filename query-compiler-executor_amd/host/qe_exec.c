@@ -175,27 +175,37 @@ static void fix_all(exec_t* x, const jres_t* jr, exists_t ex, mra_t* M, uint32_t
                     int mode) {
     entity_t* E = M->v[ex.ent];
     qe_list* update = E->e[ex.idx].list;
-    int needed = 0;
+    size_t nedit = 0;
     for (size_t i = 0; i < E->n; i++)
-        if (E->e[i].relation != relR && E->e[i].relation != relS) needed = 1;
-    if (needed) {
+        if (E->e[i].relation != relR && E->e[i].relation != relS) nedit++;
+    if (nedit) {
+        /* every entry shares (driver, last): one pruning + sort, one expansion per entry */
         uint64_t rows = rows_of(x, E->e[ex.idx].relation);
         uint32_t* counts = NULL;
         chk(x, qe_driver_counts(x->q, jr->R, jr->S, jr->res[0], jr->res[1], mode, rows, &counts));
+        const qe_list** edits = (const qe_list**)malloc(nedit * sizeof(qe_list*));
+        qe_list* outs = (qe_list*)calloc(nedit, sizeof(qe_list));
+        size_t k = 0;
+        for (size_t i = 0; i < E->n; i++)
+            if (E->e[i].relation != relR && E->e[i].relation != relS) edits[k++] = E->e[i].list;
+        int rc = qe_join_payloads_multi(x->q, counts, rows, update, edits, (int)nedit, outs);
+        qe_counts_free(x->q, counts);
+        free(edits);
+        if (rc != 0) {
+            free(outs);
+            if (rc == QE_EINVAL) fail(x, QE_EINVAL, "join_payloads on lists of different lengths (reference-undefined)");
+            chk(x, rc);
+        }
+        k = 0;
         for (size_t i = 0; i < E->n; i++) {
             mid_t* ed = &E->e[i];
             if (ed->relation != relR && ed->relation != relS) {
                 qe_list* nl = new_list(x);
-                int rc = qe_join_payloads(x->q, counts, rows, update, ed->list, nl);
-                if (rc == QE_EINVAL) {
-                    qe_counts_free(x->q, counts);
-                    fail(x, QE_EINVAL, "join_payloads on lists of different lengths (reference-undefined)");
-                }
-                chk(x, rc);
+                *nl = outs[k++];
                 ed->list = nl;
             }
         }
-        qe_counts_free(x->q, counts);
+        free(outs);
     }
     E->e[ex.idx] = tmp;
 }

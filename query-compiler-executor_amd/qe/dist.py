@@ -187,8 +187,8 @@ class GPUEngine:
     def keep_equal(self, ka: DArr, kb: DArr) -> DArr:
         P = self.lib.Pairs
         A, B = P(), P()
-        A.key, A.val, A.n, A.flags, A.owns = ka.ptr, None, ka.n, 1, 0
-        B.key, B.val, B.n, B.flags, B.owns = kb.ptr, None, kb.n, 1, 0
+        A.key, A.n, A.flags = ka.ptr, ka.n, 1
+        B.key, B.n, B.flags = kb.ptr, kb.n, 1
         a, b = self.ctx.scan_join(A, B)
         self.ctx.list_free(b)
         return self._list(a)

@@ -29,8 +29,8 @@ class List(C.Structure):
 
 
 class Pairs(C.Structure):
-    _fields_ = [("key", C.c_void_p), ("val", C.c_void_p), ("n", C.c_uint64), ("flags", C.c_uint32),
-                ("owns", C.c_uint32)]
+    _fields_ = [("key", C.c_void_p), ("val", C.c_void_p), ("match", C.c_void_p), ("n", C.c_uint64),
+                ("kor", C.c_uint64), ("kand", C.c_uint64), ("flags", C.c_uint32), ("owns", C.c_uint32)]
 
 
 class KStat(C.Structure):
@@ -84,6 +84,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "qe_driver_counts": (I, [P, C.POINTER(Pairs), C.POINTER(Pairs), C.POINTER(List), C.POINTER(List), I, U64,
                                  C.POINTER(C.c_void_p)]),
         "qe_join_payloads": (I, [P, C.c_void_p, U64, C.POINTER(List), C.POINTER(List), C.POINTER(List)]),
+        "qe_join_payloads_multi": (I, [P, C.c_void_p, U64, C.POINTER(List), C.POINTER(C.POINTER(List)), I,
+                                       C.POINTER(List)]),
+        "qe_relation_column_bits": (I, [P, I, I, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "qe_checksum": (I, [P, Col, C.POINTER(List), C.POINTER(C.c_uint64)]),
         "qe_partition": (I, [P, C.c_void_p, U64, C.POINTER(C.c_void_p), I, C.c_uint32, C.POINTER(C.c_uint64),
                              C.c_void_p, C.POINTER(C.c_void_p)]),
@@ -274,6 +277,17 @@ class Ctx:
         out = List()
         self._chk(self.lib.qe_join_payloads(self.h, counts, rows, C.byref(last), C.byref(edit), C.byref(out)))
         return out
+
+    def join_payloads_multi(self, counts, rows: int, last: List, edits: list[List]) -> list[List]:
+        arr = (C.POINTER(List) * len(edits))(*[C.pointer(e) for e in edits])
+        outs = (List * len(edits))()
+        self._chk(self.lib.qe_join_payloads_multi(self.h, counts, rows, C.byref(last), arr, len(edits), outs))
+        return list(outs)
+
+    def column_bits(self, rel: int, col: int) -> tuple[int, int]:
+        a, b = C.c_uint64(), C.c_uint64()
+        self._chk(self.lib.qe_relation_column_bits(self.h, rel, col, C.byref(a), C.byref(b)))
+        return a.value, b.value
 
     def checksum(self, col: Col, rows: List | None) -> int:
         s = C.c_uint64()

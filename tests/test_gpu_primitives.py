@@ -261,3 +261,43 @@ def test_checksum_wraps_mod_2_64(ctx, n):
     rows = np.random.default_rng(n).integers(0, len(a), n).astype(np.uint32)
     l = ctx.list_from_host(rows)
     assert ctx.checksum(col, l) == int(np.sum(a[rows], dtype=np.uint64))
+
+
+def test_join_payloads_multi_shares_the_permutation(ctx):
+    rng = np.random.default_rng(5)
+    rows, n = 5000, 20_000
+    counts = rng.integers(0, 3, rows).astype(np.uint32)
+    last = rng.integers(0, rows, n).astype(np.uint32)
+    edits = [rng.integers(0, 1 << 31, n + k).astype(np.uint32) for k in range(3)]
+    L = ctx.list_from_host(last)
+    E = [ctx.list_from_host(e) for e in edits]
+    dc = ctx.list_from_host(counts)
+    outs = ctx.join_payloads_multi(dc.d, rows, L, E)
+    for e, o in zip(edits, outs):
+        np.testing.assert_array_equal(ctx.list_to_host(o), _ref_join_payloads(counts, last, e[:n]))
+
+
+def test_column_bits_at_load(ctx):
+    a = np.array([0b1010, 0b1110, 0b1011], dtype=np.uint64)
+    rel = ctx.load_relation([a, a * 0 + 7])
+    assert ctx.column_bits(rel, 0) == (0b1111, 0b1010)
+    assert ctx.column_bits(rel, 1) == (7, 7)
+
+
+def test_merge_fills_match_counts_and_driver_counts_use_them(ctx):
+    rng = np.random.default_rng(8)
+    colR = rng.integers(0, 300, 4000, dtype=np.uint64)
+    colS = rng.integers(0, 300, 3000, dtype=np.uint64)
+    cR, cS = _col(ctx, colR), _col(ctx, colS)
+    lr = rng.integers(0, 4000, 6000).astype(np.uint32)          # R side with duplicate rowids
+    LR = ctx.list_from_host(lr)
+    R = ctx.gather_pairs(cR, LR)
+    S = ctx.gather_pairs(cS, None)                               # base column: distinct
+    assert S.flags & lib.PAIRS_DISTINCT and S.flags & 4          # stats known from load
+    ctx.sort_pairs(R)
+    ctx.sort_pairs(S)
+    a, b = ctx.merge_join(R, S)
+    assert R.match
+    d = ctx.driver_counts(R, S, a, b, 0, 4000)
+    want = _ref_nondup_counts(ctx.list_to_host(a), ctx.list_to_host(b), 0, 4000)
+    np.testing.assert_array_equal(ctx.counts_to_host(d, 4000), want)
