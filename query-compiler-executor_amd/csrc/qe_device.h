@@ -147,22 +147,40 @@ __device__ __forceinline__ uint64_t lookback_wave(uint64_t* status, uint32_t epo
 
 // Thread-serial lookback for one of many per-tile totals (radix digits): `stride` words per
 // tile, this thread owns column `col`.  The aggregate must already be published.
+// Each step reads the next LB_WIN predecessors' words at once (independent loads in flight), so
+// a walk over k aggregate-only tiles costs ~k/LB_WIN load latencies instead of k.
+constexpr int LB_WIN = 8;
 __device__ __forceinline__ uint64_t lookback_serial(uint64_t* status, uint32_t epoch, uint32_t tile,
                                                     uint32_t stride, uint32_t col) {
     uint64_t excl = 0;
     int64_t idx = (int64_t)tile - 1;
     uint32_t spins = 0;
     while (idx >= 0) {
-        uint64_t w = ld_agent(&status[(uint64_t)idx * stride + col]);
-        uint32_t f = lb_flag(w, epoch);
-        if (f == 0) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 24)) break;
-            continue;
+        uint64_t w[LB_WIN];
+#pragma unroll
+        for (int q = 0; q < LB_WIN; q++)
+            w[q] = idx - q >= 0 ? ld_agent(&status[(uint64_t)(idx - q) * stride + col])
+                                : lb_word(epoch, LB_FLAG_INC, 0);
+        int used = 0;
+        bool done = false, stall = false;
+#pragma unroll
+        for (int q = 0; q < LB_WIN; q++) {
+            if (done || stall) continue;
+            uint32_t f = lb_flag(w[q], epoch);
+            if (f == 0) {
+                stall = true;       // predecessor idx - q has not published yet: re-poll from there
+                continue;
+            }
+            excl += w[q] & LB_VAL_MASK;
+            used++;
+            if (f == LB_FLAG_INC) done = true;
         }
-        excl += w & LB_VAL_MASK;
-        if (f == LB_FLAG_INC) break;
-        --idx;
+        if (done) break;
+        idx -= used;
+        if (stall) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 24)) break;   // bounded spin: never hang the GPU
+        }
     }
     return excl;
 }

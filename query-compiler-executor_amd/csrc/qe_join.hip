@@ -83,43 +83,45 @@ __global__ void __launch_bounds__(1024) tile_scan_kernel(uint64_t* __restrict__ 
 // pad the 32 lanes of a ds_read_b64 group would hit 4 banks (8-way conflict)
 __device__ __forceinline__ uint32_t rpad(uint32_t e) { return e + (e >> 3); }
 
-// WRITE = 0: per-tile counts + flags (+ optional per-row match counts / driver annotation)
-// WRITE = 1: expansion into outR / outS at tile offsets
-template <int WRITE>
-__global__ void __launch_bounds__(MJB) mj_tile(const uint64_t* __restrict__ rk, const uint32_t* __restrict__ rv,
-                                               uint64_t nR, const uint64_t* __restrict__ sk,
-                                               const uint32_t* __restrict__ sv, uint64_t nS,
-                                               const uint64_t* __restrict__ win, uint64_t* __restrict__ tile_counts,
-                                               uint32_t* __restrict__ outR, uint32_t* __restrict__ outS,
-                                               uint32_t* __restrict__ flags, uint32_t* __restrict__ annot,
-                                               uint32_t* __restrict__ match) {
-    __shared__ uint64_t s_r[MJ_TILE + MJ_TILE / 8];
-    __shared__ uint64_t s_s[MJ_WIN];
-    __shared__ uint32_t s_lo[WRITE ? MJ_TILE : 1];    // window-relative S start per R element
-    __shared__ uint32_t s_off[WRITE ? MJ_TILE : 1];   // tile-relative output offset per R element
-    __shared__ uint64_t s_red[MJB / 64];
-    __shared__ uint32_t s_flag;
+struct MJShared {
+    uint64_t r[MJ_TILE + MJ_TILE / 8];
+    union {                       // the S window is dead once every thread has walked (a barrier
+        uint64_t s[MJ_WIN];       // separates the walk from the emission's use of the space)
+        struct {
+            uint32_t lo[MJ_TILE];     // window-relative S start per R element
+            uint32_t off[MJ_TILE];    // tile-relative output offset per R element
+        };
+        struct {
+            uint32_t oR[2 * MJ_TILE];   // a balanced tile's pairs, staged for coalesced stores
+            uint32_t oS[2 * MJ_TILE];
+        };
+    };
+    uint64_t red[MJB / 64];
+    uint64_t excl;
+    uint32_t flag;
+    uint32_t ticket;
+};
 
-    const uint32_t tile = blockIdx.x;
-    const uint64_t base = (uint64_t)tile * MJ_TILE;
-    const uint32_t tn = (uint32_t)std::min<uint64_t>(MJ_TILE, nR - base);
-    const uint64_t wlo = win[2 * tile], whi = win[2 * tile + 1];
-    const uint64_t wn = whi - wlo;
-    const bool in_lds = wn <= MJ_WIN;
-    if (threadIdx.x == 0) s_flag = 0;
-    for (uint32_t i = threadIdx.x; i < tn; i += MJB) s_r[rpad(i)] = rk[base + i];
-    if (in_lds)
-        for (uint32_t i = threadIdx.x; i < wn; i += MJB) s_s[i] = sk[wlo + i];
+// stage the tile's R keys and (when it fits) its S window in LDS
+__device__ __forceinline__ void mj_stage(MJShared& sh, const uint64_t* rk, uint64_t base, uint32_t tn,
+                                         const uint64_t* sk, uint64_t wlo, uint64_t wn) {
+    if (threadIdx.x == 0) sh.flag = 0;
+    for (uint32_t i = threadIdx.x; i < tn; i += MJB) sh.r[rpad(i)] = rk[base + i];
+    if (wn <= MJ_WIN)
+        for (uint32_t i = threadIdx.x; i < wn; i += MJB) sh.s[i] = sk[wlo + i];
     __syncthreads();
+}
 
-    auto S = [&](uint64_t i) -> uint64_t { return in_lds ? s_s[i] : sk[wlo + i]; };
-
-    uint32_t cnt[MJ_ITEMS];
-    uint32_t lo_rel[MJ_ITEMS];
+// each thread walks its MJ_ITEMS consecutive R keys through the S window: [lo, hi) per key
+// (merge walk; binary search when a gap or a run is longer than MJ_WALK)
+__device__ __forceinline__ uint64_t mj_walk(const MJShared& sh, const uint64_t* sk, uint64_t wlo, uint64_t wn,
+                                            uint32_t tn, uint32_t (&cnt)[MJ_ITEMS],
+                                            uint32_t (&lo_rel)[MJ_ITEMS]) {
+    const bool in_lds = wn <= MJ_WIN;
+    auto S = [&](uint64_t i) -> uint64_t { return in_lds ? sh.s[i] : sk[wlo + i]; };
     uint64_t tsum = 0;
-    uint32_t myflag = 0;
     const uint32_t e0 = threadIdx.x * MJ_ITEMS;
-    uint64_t p = 0;   // walk pointer (window-relative)
+    uint64_t p = 0;
     bool have_p = false;
     uint64_t prev_key = 0, prev_lo = 0, prev_hi = 0;
 #pragma unroll
@@ -128,7 +130,7 @@ __global__ void __launch_bounds__(MJB) mj_tile(const uint64_t* __restrict__ rk, 
         cnt[j] = 0;
         lo_rel[j] = 0;
         if (e >= tn) continue;
-        uint64_t key = s_r[rpad(e)];
+        uint64_t key = sh.r[rpad(e)];
         uint64_t lo, hi;
         if (have_p && key == prev_key) {
             lo = prev_lo;
@@ -158,68 +160,189 @@ __global__ void __launch_bounds__(MJB) mj_tile(const uint64_t* __restrict__ rk, 
             prev_lo = lo;
             prev_hi = hi;
         }
-        uint32_t c = (uint32_t)(hi - lo);
-        cnt[j] = c;
+        cnt[j] = (uint32_t)(hi - lo);
         lo_rel[j] = (uint32_t)lo;
-        tsum += c;
-        if (!WRITE) {
-            if (c > 1) myflag |= MJF_R_FANOUT;
-            if (match) match[base + e] = c;
-            if (c > 0) {
-                uint64_t nxt = e + 1 < tn ? s_r[rpad(e + 1)] : (base + e + 1 < nR ? rk[base + e + 1] : ~key);
-                if (nxt == key) myflag |= MJF_S_DUP;
-                if (annot) annot[rv ? rv[base + e] : (uint32_t)(base + e)] = c;
-            }
+        tsum += cnt[j];
+    }
+    return tsum;
+}
+
+// per-row match counts, output-distinctness flags, optional driver-count annotation
+__device__ __forceinline__ uint32_t mj_annotate_rows(const MJShared& sh, const uint64_t* rk, const uint32_t* rv,
+                                                     uint64_t nR, uint64_t base, uint32_t tn,
+                                                     const uint32_t (&cnt)[MJ_ITEMS], uint32_t* match,
+                                                     uint32_t* annot) {
+    uint32_t myflag = 0;
+    const uint32_t e0 = threadIdx.x * MJ_ITEMS;
+    const bool full = e0 + MJ_ITEMS <= tn;
+    if (match && full) {   // this thread's 8 counts: two 16-B stores
+        *reinterpret_cast<uint4*>(match + base + e0) = make_uint4(cnt[0], cnt[1], cnt[2], cnt[3]);
+        *reinterpret_cast<uint4*>(match + base + e0 + 4) = make_uint4(cnt[4], cnt[5], cnt[6], cnt[7]);
+    }
+#pragma unroll
+    for (int j = 0; j < MJ_ITEMS; j++) {
+        uint32_t e = e0 + j;
+        if (e >= tn) continue;
+        uint32_t c = cnt[j];
+        if (c > 1) myflag |= MJF_R_FANOUT;
+        if (match && !full) match[base + e] = c;
+        if (c > 0) {
+            uint64_t key = sh.r[rpad(e)];
+            uint64_t nxt = e + 1 < tn ? sh.r[rpad(e + 1)] : (base + e + 1 < nR ? rk[base + e + 1] : ~key);
+            if (nxt == key) myflag |= MJF_S_DUP;
+            if (annot) annot[rv ? rv[base + e] : (uint32_t)(base + e)] = c;
         }
     }
+    return myflag;
+}
 
-    if (!WRITE) {
-        uint64_t s = wave_sum_u64(tsum);
-        if (lane_id() == 0) s_red[wave_id()] = s;
-        if (myflag) atomicOr(&s_flag, myflag);
+__device__ __forceinline__ void mj_publish_flags(MJShared& sh, uint32_t myflag, uint32_t* flags) {
+    if (myflag) atomicOr(&sh.flag, myflag);
+    __syncthreads();
+    if (threadIdx.x == 0 && sh.flag) {
+        uint32_t seen = __hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (sh.flag & ~seen) atomicOr(flags, sh.flag);   // one word for the grid: no hot-spot
+    }
+}
+
+// block-exclusive offsets of the per-thread sums; returns this thread's start, sets *btotal
+__device__ __forceinline__ uint64_t mj_block_scan(MJShared& sh, uint64_t tsum, uint64_t* btotal) {
+    uint64_t inc = wave_incl_scan_u64(tsum);
+    if (lane_id() == 63) sh.red[wave_id()] = inc;
+    __syncthreads();
+    uint64_t add = 0, tot = 0;
+    for (int w = 0; w < MJB / 64; w++) {
+        if (w < wave_id()) add += sh.red[w];
+        tot += sh.red[w];
+    }
+    *btotal = tot;
+    return inc - tsum + add;
+}
+
+// write the tile's pairs at [gofs, gofs + btotal): a balanced tile (<= 2 pairs per R row) is
+// built in LDS by its threads and stored as one coalesced run; a heavy tile uses a
+// load-balanced expansion (every output slot finds its R row by binary search)
+__device__ __forceinline__ void mj_emit(MJShared& sh, const uint32_t* rv, const uint32_t* sv, uint64_t base,
+                                        uint32_t tn, uint64_t wlo, uint64_t run, uint64_t btotal, uint64_t gofs,
+                                        const uint32_t (&cnt)[MJ_ITEMS], const uint32_t (&lo_rel)[MJ_ITEMS],
+                                        uint32_t* outR, uint32_t* outS) {
+    const uint32_t e0 = threadIdx.x * MJ_ITEMS;
+    if (btotal <= 2 * (uint64_t)MJ_TILE) {
+        uint32_t r[MJ_ITEMS];
+        if (rv && e0 + MJ_ITEMS <= tn) {
+            uint4 a = *reinterpret_cast<const uint4*>(rv + base + e0);
+            uint4 b = *reinterpret_cast<const uint4*>(rv + base + e0 + 4);
+            r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = a.w;
+            r[4] = b.x; r[5] = b.y; r[6] = b.z; r[7] = b.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < MJ_ITEMS; j++)
+                r[j] = e0 + j < tn ? (rv ? rv[base + e0 + j] : (uint32_t)(base + e0 + j)) : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < MJ_ITEMS; j++) {
+            if (e0 + j >= tn) continue;
+            for (uint32_t k = 0; k < cnt[j]; k++) {
+                uint64_t sidx = wlo + lo_rel[j] + k;
+                sh.oR[run + k] = r[j];
+                sh.oS[run + k] = sv ? sv[sidx] : (uint32_t)sidx;
+            }
+            run += cnt[j];
+        }
         __syncthreads();
-        if (threadIdx.x == 0) {
-            uint64_t t = 0;
-            for (int w = 0; w < MJB / 64; w++) t += s_red[w];
-            tile_counts[tile] = t;
-            if (s_flag) atomicOr(flags, s_flag);
+        for (uint32_t i = threadIdx.x; i < (uint32_t)btotal; i += MJB) {
+            outR[gofs + i] = sh.oR[i];
+            outS[gofs + i] = sh.oS[i];
         }
         return;
     }
-
-    // block exclusive scan of per-thread sums
-    uint64_t inc = wave_incl_scan_u64(tsum);
-    if (lane_id() == 63) s_red[wave_id()] = inc;
-    __syncthreads();
-    uint64_t add = 0;
-    for (int w = 0; w < wave_id(); w++) add += s_red[w];
-    uint64_t run = inc - tsum + add;
-    uint64_t btotal = 0;
-    for (int w = 0; w < MJB / 64; w++) btotal += s_red[w];
 #pragma unroll
     for (int j = 0; j < MJ_ITEMS; j++) {
         uint32_t e = e0 + j;
         if (e < tn) {
-            s_off[e] = (uint32_t)run;
-            s_lo[e] = lo_rel[j];
+            sh.off[e] = (uint32_t)run;
+            sh.lo[e] = lo_rel[j];
             run += cnt[j];
         }
     }
     __syncthreads();
-    const uint64_t gofs = tile_counts[tile];
     for (uint64_t o = threadIdx.x; o < btotal; o += MJB) {
-        // last element with s_off[e] <= o
-        uint32_t a = 0, b = tn;
+        uint32_t a = 0, b = tn;   // last element with off[e] <= o
         while (b - a > 1) {
             uint32_t m = (a + b) >> 1;
-            if (s_off[m] <= o) a = m;
+            if (sh.off[m] <= o) a = m;
             else b = m;
         }
-        uint64_t k = o - s_off[a];
-        uint64_t sidx = wlo + s_lo[a] + k;
+        uint64_t sidx = wlo + sh.lo[a] + (o - sh.off[a]);
         outR[gofs + o] = rv ? rv[base + a] : (uint32_t)(base + a);
         outS[gofs + o] = sv ? sv[sidx] : (uint32_t)sidx;
     }
+}
+
+// Two-pass form.  WRITE = 0: per-tile counts + flags (+ match counts / driver annotation);
+// WRITE = 1: pairs at the scanned tile offsets.
+template <int WRITE>
+__global__ void __launch_bounds__(MJB) mj_tile(const uint64_t* __restrict__ rk, const uint32_t* __restrict__ rv,
+                                               uint64_t nR, const uint64_t* __restrict__ sk,
+                                               const uint32_t* __restrict__ sv, uint64_t nS,
+                                               const uint64_t* __restrict__ win, uint64_t* __restrict__ tile_counts,
+                                               uint32_t* __restrict__ outR, uint32_t* __restrict__ outS,
+                                               uint32_t* __restrict__ flags, uint32_t* __restrict__ annot,
+                                               uint32_t* __restrict__ match) {
+    __shared__ MJShared sh;
+    const uint32_t tile = blockIdx.x;
+    const uint64_t base = (uint64_t)tile * MJ_TILE;
+    const uint32_t tn = (uint32_t)std::min<uint64_t>(MJ_TILE, nR - base);
+    const uint64_t wlo = win[2 * tile], wn = win[2 * tile + 1] - wlo;
+    mj_stage(sh, rk, base, tn, sk, wlo, wn);
+    uint32_t cnt[MJ_ITEMS], lo_rel[MJ_ITEMS];
+    uint64_t tsum = mj_walk(sh, sk, wlo, wn, tn, cnt, lo_rel);
+    if (!WRITE) {
+        uint32_t f = mj_annotate_rows(sh, rk, rv, nR, base, tn, cnt, match, annot);
+        uint64_t s = wave_sum_u64(tsum);
+        if (lane_id() == 0) sh.red[wave_id()] = s;
+        mj_publish_flags(sh, f, flags);   // contains the barrier
+        if (threadIdx.x == 0) tile_counts[tile] = sh.red[0] + sh.red[1] + sh.red[2] + sh.red[3];
+        return;
+    }
+    uint64_t btotal;
+    uint64_t run = mj_block_scan(sh, tsum, &btotal);
+    mj_emit(sh, rv, sv, base, tn, wlo, run, btotal, tile_counts[tile], cnt, lo_rel, outR, outS);
+}
+
+// Single-pass form: count, decoupled lookback for the tile's output offset, write -- the keys
+// are read once.  Outputs have room for `cap` pairs; a tile that would overflow writes nothing
+// and the host re-runs the exact two-pass form (tile_counts is filled for it).
+__global__ void __launch_bounds__(MJB) mj_fused(const uint64_t* __restrict__ rk, const uint32_t* __restrict__ rv,
+                                                uint64_t nR, const uint64_t* __restrict__ sk,
+                                                const uint32_t* __restrict__ sv, uint64_t nS,
+                                                const uint64_t* __restrict__ win, uint64_t* __restrict__ tile_counts,
+                                                uint32_t* __restrict__ match, uint32_t* __restrict__ outR,
+                                                uint32_t* __restrict__ outS, uint64_t cap, uint32_t* __restrict__ flags,
+                                                uint64_t* status, uint32_t* ticket, uint32_t epoch, uint32_t ntiles,
+                                                uint64_t* total_out) {
+    __shared__ MJShared sh;
+    const uint32_t tile = take_ticket(ticket, &sh.ticket);
+    const uint64_t base = (uint64_t)tile * MJ_TILE;
+    const uint32_t tn = (uint32_t)std::min<uint64_t>(MJ_TILE, nR - base);
+    const uint64_t wlo = win[2 * tile], wn = win[2 * tile + 1] - wlo;
+    mj_stage(sh, rk, base, tn, sk, wlo, wn);
+    uint32_t cnt[MJ_ITEMS], lo_rel[MJ_ITEMS];
+    uint64_t tsum = mj_walk(sh, sk, wlo, wn, tn, cnt, lo_rel);
+    uint32_t f = mj_annotate_rows(sh, rk, rv, nR, base, tn, cnt, match, nullptr);
+    uint64_t btotal;
+    uint64_t run = mj_block_scan(sh, tsum, &btotal);
+    if (wave_id() == 0) {
+        uint64_t ex = lookback_wave(status, epoch, tile, btotal);
+        if (lane_id() == 0) {
+            sh.excl = ex;
+            tile_counts[tile] = btotal;
+            if (tile == ntiles - 1) *total_out = ex + btotal;
+        }
+    }
+    mj_publish_flags(sh, f, flags);   // contains the barrier that publishes sh.excl
+    const uint64_t gofs = sh.excl;
+    if (gofs + btotal <= cap) mj_emit(sh, rv, sv, base, tn, wlo, run, btotal, gofs, cnt, lo_rel, outR, outS);
 }
 
 // The reference's two-pointer loop verbatim (src/join.c:342-377) for inputs that are not
@@ -271,24 +394,26 @@ __global__ void __launch_bounds__(256) gather_keys_kernel(const uint64_t* __rest
                                                           uint64_t* __restrict__ out,
                                                           unsigned long long* __restrict__ bits) {
     uint64_t o = 0, a = ~0ull;
-    uint64_t i4 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-    if (i4 + 3 < n) {
-        uint4 r = *reinterpret_cast<const uint4*>(rows + i4);
-        ulonglong2 x, y;
-        x.x = col[r.x];
-        x.y = col[r.y];
-        y.x = col[r.z];
-        y.y = col[r.w];
-        *reinterpret_cast<ulonglong2*>(out + i4) = x;
-        *reinterpret_cast<ulonglong2*>(out + i4 + 2) = y;
-        o = x.x | x.y | y.x | y.y;
-        a = x.x & x.y & y.x & y.y;
-    } else {
-        for (uint64_t i = i4; i < n; i++) {
-            uint64_t k = col[rows[i]];
-            out[i] = k;
-            o |= k;
-            a &= k;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 4;   // bounded grid: few atomics
+    for (uint64_t i4 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i4 < n; i4 += stride) {
+        if (i4 + 3 < n) {
+            uint4 r = *reinterpret_cast<const uint4*>(rows + i4);
+            ulonglong2 x, y;
+            x.x = col[r.x];
+            x.y = col[r.y];
+            y.x = col[r.z];
+            y.y = col[r.w];
+            *reinterpret_cast<ulonglong2*>(out + i4) = x;
+            *reinterpret_cast<ulonglong2*>(out + i4 + 2) = y;
+            o |= x.x | x.y | y.x | y.y;
+            a &= x.x & x.y & y.x & y.y;
+        } else {
+            for (uint64_t i = i4; i < n; i++) {
+                uint64_t k = col[rows[i]];
+                out[i] = k;
+                o |= k;
+                a &= k;
+            }
         }
     }
 #pragma unroll
@@ -390,7 +515,9 @@ __global__ void __launch_bounds__(XB) expand_kernel(const uint32_t* __restrict__
         mx = wave_max_u32(mx);
         if (lane_id() == 0) {
             s_red[wave_id()] = s;
-            if (mx > 1) atomicOr(flags, 1u);
+            // one flag word for the whole grid: skip the atomic once it is set (no hot-spot)
+            if (mx > 1 && !(__hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u))
+                atomicOr(flags, 1u);
         }
         __syncthreads();
         if (threadIdx.x == 0) tile_counts[tile] = s_red[0] + s_red[1] + s_red[2] + s_red[3];
@@ -483,24 +610,37 @@ void merge_sorted(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_l
                            win);
         QE_HIP(hipGetLastError());
     }
+    // single pass with room for nR + nS pairs (every fan-out <= 1 + |S|/|R| case); the exact
+    // two-pass form only when the join turns out larger
+    const uint64_t cap = nR + nS;
+    uint32_t* oR = dalloc_t<uint32_t>(c, cap);
+    uint32_t* oS = dalloc_t<uint32_t>(c, cap);
     {
-        Timed t(c, "mj_count", 8.0 * nR + 8.0 * nS + 4.0 * nR);
-        hipLaunchKernelGGL(mj_tile<0>, dim3(nt), dim3(MJB), 0, c->stream, R->key, R->val, nR, S->key, S->val, nS, win,
-                           tc, nullptr, nullptr, d_flags, nullptr, R->match);
-        QE_HIP(hipGetLastError());
-        hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, c->stream, tc, (uint64_t)nt, c->d_scratch + 17);
+        LBSlot s = lb_acquire(c, nt);
+        Timed t(c, "mj_fused", 12.0 * nR + 12.0 * nS + 4.0 * nR);   // + 8 B per pair, added below
+        hipLaunchKernelGGL(mj_fused, dim3(nt), dim3(MJB), 0, c->stream, R->key, R->val, nR, S->key, S->val, nS, win, tc,
+                           R->match, oR, oS, cap, d_flags, s.status, s.ticket, s.epoch, nt, c->d_scratch + 17);
         QE_HIP(hipGetLastError());
     }
     uint64_t h[2];
     read_words(c, c->d_scratch + 16, h, 2);
     const uint64_t P = h[1];
     *oflags = (uint32_t)h[0];
-    outR->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(P, 1));
-    outS->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(P, 1));
-    outR->cap = outS->cap = P;
+    if (c->prof && !c->pending.empty() && P <= cap) c->pending.back().bytes += 8.0 * P;
     outR->n = outS->n = P;
-    if (P) {
+    if (P <= cap) {
+        outR->d = oR;
+        outS->d = oS;
+        outR->cap = outS->cap = cap;
+    } else {
+        dfree(c, oR);
+        dfree(c, oS);
+        outR->d = dalloc_t<uint32_t>(c, P);
+        outS->d = dalloc_t<uint32_t>(c, P);
+        outR->cap = outS->cap = P;
         Timed t(c, "mj_write", 12.0 * nR + 12.0 * nS + 8.0 * P);
+        hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, c->stream, tc, (uint64_t)nt, c->d_scratch + 18);
+        QE_HIP(hipGetLastError());
         hipLaunchKernelGGL(mj_tile<1>, dim3(nt), dim3(MJB), 0, c->stream, R->key, R->val, nR, S->key, S->val, nS, win,
                            tc, outR->d, outS->d, nullptr, nullptr, nullptr);
         QE_HIP(hipGetLastError());
@@ -662,7 +802,7 @@ int qe_gather_pairs(qe_ctx* c, qe_col col, const qe_list* rows, qe_pairs* out) {
     QE_HIP(hipMemcpyAsync(d_bits, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
     if (n) {
         Timed t(c, "gather_keys", 12.0 * n + 8.0 * n);
-        hipLaunchKernelGGL(gather_keys_kernel, dim3(grid_for((n + 3) / 4, 256)), dim3(256), 0, c->stream, col.d,
+        hipLaunchKernelGGL(gather_keys_kernel, dim3(grid_for((n + 3) / 4, 256, 4096)), dim3(256), 0, c->stream, col.d,
                            rows->d, n, out->key, (unsigned long long*)d_bits);
         QE_HIP(hipGetLastError());
     }

@@ -6,17 +6,24 @@
 // reference can produce and unobservable on the rand-invariant domain.
 //
 // Pipeline for n pairs:
-//   1. key_bits     -- OR / AND reduction: only bits that vary across keys are sorted
-//                      (keys < 2^27 at 100 M rows: 27 bits, 4 passes of <= 8 bits, not 8).
-//   2. digit_hist   -- one read of the keys builds the 256-bin histograms of every pass in LDS.
-//   3. digit_scan   -- exclusive scan per pass -> global base offset of each digit.
-//   4. radix_pass   -- per digit pass, ONE read + ONE write of the pairs: a tile of 256 x ITEMS
-//                      pairs is ranked in registers (8 ballots per element = wave match-any,
-//                      per-wave LDS counters), per-digit tile totals go through a decoupled
-//                      lookback (thread d owns digit d), and the tile is re-ordered by digit
-//                      in LDS so the global scatter writes runs of equal digits.
-// HBM per pass: 12 B read + 12 B write per pair (u64 key + u32 rowid).
+//   1. key bits     -- OR / AND of the keys (known from the producer: column statistics at load
+//                      time, or fused into the gather): only the bit range [lo, hi) that varies is
+//                      sorted -- 27 bits at 100 M rows, i.e. 3 passes of 9 bits, not 8 of 8.
+//   2. packing      -- when hi - lo <= 32 the pair travels as ONE u64 word (field << 32 | rowid):
+//                      the first pass reads key + rowid and writes words, middle passes move 8 B
+//                      in + 8 B out per pair, the last pass writes key + rowid back (the key's
+//                      constant bits are restored from the AND).  Otherwise key and rowid travel
+//                      separately (64-bit keys with > 32 varying bits; the dedup sort of packed
+//                      pairs has no rowid at all).
+//   3. digit_hist   -- one read of the keys builds the histograms of every pass in LDS.
+//   4. digit_scan   -- exclusive scan per pass -> global base offset of each digit.
+//   5. radix_pass   -- per pass: a tile of 256 x ITEMS words is ranked in registers (RBITS
+//                      ballots per element = wave match-any, per-wave LDS counters), staged in
+//                      LDS in digit order, THEN the per-digit decoupled lookback (thread-serial,
+//                      one chain per digit) -- its latency overlaps the staging -- and the tile
+//                      is written as runs of equal digits.
 #include <algorithm>
+#include <cstdlib>
 
 #include "qe_device.h"
 #include "qe_internal.h"
@@ -25,9 +32,9 @@ namespace qe {
 
 constexpr int RB = 256;          // block
 constexpr int RNW = RB / 64;     // waves per block
-constexpr int RBINS = 256;       // 8-bit digits (narrower passes use a mask)
-constexpr int R_ITEMS = 16;      // pairs per thread per tile
+constexpr int R_ITEMS = 16;      // words per thread per tile
 constexpr int RTILE = RB * R_ITEMS;
+constexpr int MAX_PASS = 8;
 
 template <typename K>
 __global__ void __launch_bounds__(256) key_bits_kernel(const K* __restrict__ keys, uint64_t n, uint64_t* out) {
@@ -61,76 +68,233 @@ __global__ void __launch_bounds__(256) key_bits_kernel(const K* __restrict__ key
 
 struct PassDesc {
     int npass;
-    int shift[8];
-    uint32_t mask[8];
+    int shift[MAX_PASS];        // absolute key bit of each digit
+    uint32_t mask[MAX_PASS];
 };
 
-template <typename K>
+template <typename K, int RBITS>
 __global__ void __launch_bounds__(256) digit_hist_kernel(const K* __restrict__ keys, uint64_t n, PassDesc pd,
                                                          uint32_t* __restrict__ hist) {
-    __shared__ uint32_t h[8][RBINS];
-    for (int i = threadIdx.x; i < 8 * RBINS; i += blockDim.x) (&h[0][0])[i] = 0;
+    constexpr int BINS = 1 << RBITS;
+    constexpr int HP = RBITS <= 8 ? 8 : (64 + RBITS - 1) / RBITS;   // passes that fit
+    __shared__ uint32_t h[HP * BINS];
+    for (int i = threadIdx.x; i < HP * BINS; i += blockDim.x) h[i] = 0;
     __syncthreads();
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         uint64_t k = (uint64_t)keys[i];
-        for (int p = 0; p < pd.npass; p++) atomicAdd(&h[p][(uint32_t)(k >> pd.shift[p]) & pd.mask[p]], 1u);
+        for (int p = 0; p < pd.npass; p++) atomicAdd(&h[p * BINS + ((uint32_t)(k >> pd.shift[p]) & pd.mask[p])], 1u);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < pd.npass * RBINS; i += blockDim.x) {
-        uint32_t v = (&h[0][0])[i];
+    for (int i = threadIdx.x; i < pd.npass * BINS; i += blockDim.x) {
+        uint32_t v = h[i];
         if (v) atomicAdd(&hist[i], v);
     }
 }
 
-// one block per pass: exclusive scan of 256 counts
+// block of 256 threads per pass: exclusive scan of BINS counts (thread owns BINS/256 digits)
+template <int RBITS>
 __global__ void __launch_bounds__(256) digit_scan_kernel(uint32_t* hist) {
+    constexpr int BINS = 1 << RBITS, DPT = BINS / RB;
     __shared__ uint32_t wsum[RNW];
-    uint32_t* h = hist + blockIdx.x * RBINS;
-    uint32_t v = h[threadIdx.x];
-    uint32_t inc = wave_incl_scan_u32(v);
+    uint32_t* h = hist + blockIdx.x * BINS;
+    uint32_t v[DPT], s = 0;
+#pragma unroll
+    for (int q = 0; q < DPT; q++) {
+        v[q] = h[threadIdx.x * DPT + q];
+        s += v[q];
+    }
+    uint32_t inc = wave_incl_scan_u32(s);
     if (lane_id() == 63) wsum[wave_id()] = inc;
     __syncthreads();
-    uint32_t add = 0;
-    for (int w = 0; w < wave_id(); w++) add += wsum[w];
-    h[threadIdx.x] = inc - v + add;
+    uint32_t run = inc - s;
+    for (int w = 0; w < wave_id(); w++) run += wsum[w];
+#pragma unroll
+    for (int q = 0; q < DPT; q++) {
+        h[threadIdx.x * DPT + q] = run;
+        run += v[q];
+    }
 }
 
-template <typename K, bool VIN, bool VOUT>
-__global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                                        K* __restrict__ kout, uint32_t* __restrict__ vout, uint64_t n,
-                                                        int shift, uint32_t mask,
+// input / output formats of a pass
+enum { IN_WORD = 0, IN_KV = 1, IN_KIOTA = 2 };
+enum { OUT_WORD = 0, OUT_KV = 1 };
+
+// word <-> (key, rowid).  PACK: word = ((key >> lo) & fmask) << 32 | rowid, key restored as
+// kconst | (field << lo).  !PACK: word = key (no rowid; key-only sorts of 64-bit words).
+struct Field {
+    int lo;
+    uint64_t fmask;
+    uint64_t kconst;
+};
+
+template <typename K, int IN, int OUT, bool PACK, int RBITS>
+__global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ kin, const uint64_t* __restrict__ win,
+                                                        const uint32_t* __restrict__ vin, K* __restrict__ kout,
+                                                        uint64_t* __restrict__ wout, uint32_t* __restrict__ vout,
+                                                        uint64_t n, int dsh, uint32_t mask, Field f,
                                                         const uint32_t* __restrict__ digit_base, uint64_t* status,
                                                         uint32_t* ticket, uint32_t epoch) {
-    constexpr int WT = 64 * R_ITEMS;   // pairs per wave
-    __shared__ union {
-        K keys[RTILE];
-        uint32_t vals[RTILE];
-    } stage;
-    __shared__ uint32_t whist[RNW][RBINS];   // per-wave digit counts -> exclusive over waves
-    __shared__ uint32_t bexcl[RBINS];        // tile-local exclusive offset of each digit
-    __shared__ uint32_t gofs[RBINS];         // global position of digit run start - bexcl
+    constexpr int BINS = 1 << RBITS, DPT = BINS / RB;
+    constexpr int WT = 64 * R_ITEMS;
+    __shared__ uint64_t stage[RTILE];
+    __shared__ uint32_t whist[RNW][BINS];   // per-wave digit counts -> exclusive over waves
+    __shared__ uint32_t bexcl[BINS];        // tile-local exclusive offset of each digit
+    __shared__ uint32_t gofs[BINS];         // global position of the digit's run - bexcl
     __shared__ uint32_t wsum[RNW];
     __shared__ uint32_t s_ticket;
 
     const uint32_t tile = take_ticket(ticket, &s_ticket);
     const int w = wave_id(), l = lane_id();
     const uint64_t lt = lanemask_lt();
-    for (int i = threadIdx.x; i < RNW * RBINS; i += RB) (&whist[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < RNW * BINS; i += RB) (&whist[0][0])[i] = 0;
     __syncthreads();
 
     const uint64_t wave_base = (uint64_t)tile * RTILE + (uint64_t)w * WT;
-    K key[R_ITEMS];
-    uint32_t val[R_ITEMS];
+    uint64_t word[R_ITEMS];
     uint32_t pos[R_ITEMS];
 #pragma unroll
     for (int j = 0; j < R_ITEMS; j++) {
         uint64_t i = wave_base + (uint64_t)j * 64 + l;
         bool ok = i < n;
-        key[j] = ok ? kin[i] : (K)0;
-        if (VOUT) val[j] = VIN ? (ok ? vin[i] : 0u) : (uint32_t)i;
+        if (IN == IN_WORD) {
+            word[j] = ok ? win[i] : 0;
+        } else {
+            uint64_t k = ok ? (uint64_t)kin[i] : 0;
+            if (PACK) {
+                uint32_t v = IN == IN_KV ? (ok ? vin[i] : 0u) : (uint32_t)i;
+                word[j] = (((k >> f.lo) & f.fmask) << 32) | v;
+            } else {
+                word[j] = k;
+            }
+        }
     }
-    // rank inside the wave, stable: element order is (j, lane)
+    // stable rank inside the wave: element order is (j, lane)
+#pragma unroll
+    for (int j = 0; j < R_ITEMS; j++) {
+        uint64_t i = wave_base + (uint64_t)j * 64 + l;
+        bool ok = i < n;
+        uint32_t d = (uint32_t)(word[j] >> dsh) & mask;
+        uint64_t peers = __ballot(ok);
+#pragma unroll
+        for (int b = 0; b < RBITS; b++) {
+            bool bit = (d >> b) & 1u;
+            uint64_t m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        int leader = peers ? (__ffsll((unsigned long long)peers) - 1) : 0;
+        uint32_t old = 0;
+        if (ok && l == leader) {
+            old = whist[w][d];
+            whist[w][d] = old + (uint32_t)__popcll(peers);
+        }
+        old = (uint32_t)__shfl((int)old, leader, 64);
+        pos[j] = old + (uint32_t)__popcll(peers & lt);
+    }
+    __syncthreads();
+    // thread t owns digits t*DPT .. t*DPT+DPT-1: totals, exclusive over waves, publish aggregate
+    uint32_t tot[DPT], tsum = 0;
+#pragma unroll
+    for (int q = 0; q < DPT; q++) {
+        const uint32_t d = threadIdx.x * DPT + q;
+        uint32_t t = 0;
+#pragma unroll
+        for (int ww = 0; ww < RNW; ww++) {
+            uint32_t c = whist[ww][d];
+            whist[ww][d] = t;
+            t += c;
+        }
+        tot[q] = t;
+        tsum += t;
+        st_agent(&status[(uint64_t)tile * BINS + d], lb_word(epoch, tile == 0 ? LB_FLAG_INC : LB_FLAG_AGG, t));
+    }
+    uint32_t inc = wave_incl_scan_u32(tsum);
+    if (l == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t run = inc - tsum;
+    for (int ww = 0; ww < w; ww++) run += wsum[ww];
+#pragma unroll
+    for (int q = 0; q < DPT; q++) {
+        bexcl[threadIdx.x * DPT + q] = run;
+        run += tot[q];
+    }
+    __syncthreads();
+    // stage the tile in digit order (tile-local offsets only)
+#pragma unroll
+    for (int j = 0; j < R_ITEMS; j++) {
+        uint64_t i = wave_base + (uint64_t)j * 64 + l;
+        if (i < n) {
+            uint32_t dd = (uint32_t)(word[j] >> dsh) & mask;
+            stage[bexcl[dd] + whist[w][dd] + pos[j]] = word[j];
+        }
+    }
+    // now the predecessors' counts: by this time most have published their inclusive prefix
+#pragma unroll
+    for (int q = 0; q < DPT; q++) {
+        const uint32_t d = threadIdx.x * DPT + q;
+        uint64_t ex = 0;
+        if (tile > 0) {
+            ex = lookback_serial(status, epoch, tile, BINS, d);
+            st_agent(&status[(uint64_t)tile * BINS + d], lb_word(epoch, LB_FLAG_INC, ex + tot[q]));
+        }
+        gofs[d] = digit_base[d] + (uint32_t)ex - bexcl[d];
+    }
+    __syncthreads();
+    const uint64_t tbase = (uint64_t)tile * RTILE;
+    const uint32_t tn = (uint32_t)((n - tbase) < (uint64_t)RTILE ? (n - tbase) : (uint64_t)RTILE);
+#pragma unroll
+    for (int k = 0; k < R_ITEMS; k++) {
+        uint32_t i = (uint32_t)k * RB + threadIdx.x;
+        if (i < tn) {
+            uint64_t wd = stage[i];
+            uint32_t p = gofs[(uint32_t)(wd >> dsh) & mask] + i;
+            if (OUT == OUT_WORD) {
+                wout[p] = wd;
+            } else if (PACK) {
+                kout[p] = (K)(f.kconst | ((wd >> 32) << f.lo));
+                vout[p] = (uint32_t)wd;
+            } else {
+                kout[p] = (K)wd;
+            }
+        }
+    }
+}
+
+// Non-packable pairs (64-bit keys with > 32 varying bits AND a rowid): key and rowid staged
+// separately.  Kept simple: rare in this workload (never in the measured configs).
+template <typename K, bool VIN>
+__global__ void __launch_bounds__(RB) radix_pass_kv_kernel(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                           K* __restrict__ kout, uint32_t* __restrict__ vout, uint64_t n,
+                                                           int shift, uint32_t mask,
+                                                           const uint32_t* __restrict__ digit_base, uint64_t* status,
+                                                           uint32_t* ticket, uint32_t epoch) {
+    constexpr int BINS = 256;
+    constexpr int WT = 64 * R_ITEMS;
+    __shared__ union {
+        K keys[RTILE];
+        uint32_t vals[RTILE];
+    } stage;
+    __shared__ uint32_t whist[RNW][BINS];
+    __shared__ uint32_t bexcl[BINS];
+    __shared__ uint32_t gofs[BINS];
+    __shared__ uint32_t wsum[RNW];
+    __shared__ uint32_t s_ticket;
+
+    const uint32_t tile = take_ticket(ticket, &s_ticket);
+    const int w = wave_id(), l = lane_id();
+    const uint64_t lt = lanemask_lt();
+    for (int i = threadIdx.x; i < RNW * BINS; i += RB) (&whist[0][0])[i] = 0;
+    __syncthreads();
+    const uint64_t wave_base = (uint64_t)tile * RTILE + (uint64_t)w * WT;
+    K key[R_ITEMS];
+    uint32_t val[R_ITEMS], pos[R_ITEMS];
+#pragma unroll
+    for (int j = 0; j < R_ITEMS; j++) {
+        uint64_t i = wave_base + (uint64_t)j * 64 + l;
+        bool ok = i < n;
+        key[j] = ok ? kin[i] : (K)0;
+        val[j] = VIN ? (ok ? vin[i] : 0u) : (uint32_t)i;
+    }
 #pragma unroll
     for (int j = 0; j < R_ITEMS; j++) {
         uint64_t i = wave_base + (uint64_t)j * 64 + l;
@@ -150,10 +314,9 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
             whist[w][d] = old + (uint32_t)__popcll(peers);
         }
         old = (uint32_t)__shfl((int)old, leader, 64);
-        pos[j] = old + (uint32_t)__popcll(peers & lt);   // rank within (wave, digit)
+        pos[j] = old + (uint32_t)__popcll(peers & lt);
     }
     __syncthreads();
-    // thread d owns digit d
     const uint32_t d = threadIdx.x;
     uint32_t tot = 0;
 #pragma unroll
@@ -162,26 +325,16 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
         whist[ww][d] = tot;
         tot += c;
     }
-    // publish this tile's count of digit d, then look back for the predecessors'
-    const uint64_t sidx = (uint64_t)tile * RBINS + d;
-    if (tile == 0) st_agent(&status[sidx], lb_word(epoch, LB_FLAG_INC, tot));
-    else st_agent(&status[sidx], lb_word(epoch, LB_FLAG_AGG, tot));
-    // tile-local exclusive scan over digits
+    const uint64_t sidx = (uint64_t)tile * BINS + d;
+    st_agent(&status[sidx], lb_word(epoch, tile == 0 ? LB_FLAG_INC : LB_FLAG_AGG, tot));
     uint32_t inc = wave_incl_scan_u32(tot);
     if (l == 63) wsum[w] = inc;
-    uint64_t excl = 0;
-    if (tile > 0) {
-        excl = lookback_serial(status, epoch, tile, RBINS, d);
-        st_agent(&status[sidx], lb_word(epoch, LB_FLAG_INC, excl + tot));
-    }
     __syncthreads();
     uint32_t add = 0;
     for (int ww = 0; ww < w; ww++) add += wsum[ww];
     const uint32_t be = inc - tot + add;
     bexcl[d] = be;
-    gofs[d] = digit_base[d] + (uint32_t)excl - be;
     __syncthreads();
-    // stage keys in digit order
 #pragma unroll
     for (int j = 0; j < R_ITEMS; j++) {
         uint64_t i = wave_base + (uint64_t)j * 64 + l;
@@ -191,6 +344,12 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
             stage.keys[pos[j]] = key[j];
         }
     }
+    uint64_t excl = 0;
+    if (tile > 0) {
+        excl = lookback_serial(status, epoch, tile, BINS, d);
+        st_agent(&status[sidx], lb_word(epoch, LB_FLAG_INC, excl + tot));
+    }
+    gofs[d] = digit_base[d] + (uint32_t)excl - be;
     __syncthreads();
     const uint64_t tbase = (uint64_t)tile * RTILE;
     const uint32_t tn = (uint32_t)((n - tbase) < (uint64_t)RTILE ? (n - tbase) : (uint64_t)RTILE);
@@ -200,35 +359,46 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
         uint32_t i = (uint32_t)k * RB + threadIdx.x;
         if (i < tn) {
             K kk = stage.keys[i];
-            uint32_t dd = (uint32_t)((uint64_t)kk >> shift) & mask;
-            gp[k] = gofs[dd] + i;
+            gp[k] = gofs[(uint32_t)((uint64_t)kk >> shift) & mask] + i;
             kout[gp[k]] = kk;
         }
     }
-    if (VOUT) {
-        __syncthreads();
+    __syncthreads();
 #pragma unroll
-        for (int j = 0; j < R_ITEMS; j++) {
-            uint64_t i = wave_base + (uint64_t)j * 64 + l;
-            if (i < n) stage.vals[pos[j]] = val[j];
-        }
-        __syncthreads();
+    for (int j = 0; j < R_ITEMS; j++) {
+        uint64_t i = wave_base + (uint64_t)j * 64 + l;
+        if (i < n) stage.vals[pos[j]] = val[j];
+    }
+    __syncthreads();
 #pragma unroll
-        for (int k = 0; k < R_ITEMS; k++) {
-            uint32_t i = (uint32_t)k * RB + threadIdx.x;
-            if (i < tn) vout[gp[k]] = stage.vals[i];
-        }
+    for (int k = 0; k < R_ITEMS; k++) {
+        uint32_t i = (uint32_t)k * RB + threadIdx.x;
+        if (i < tn) vout[gp[k]] = stage.vals[i];
     }
 }
 
-static PassDesc plan_passes(uint64_t kor, uint64_t kand) {
+// ---- host side -------------------------------------------------------------------------------
+
+static int sort_maxbits() {
+    static int mb = [] {
+        // tuning knob (8..11).  Measured on MI355X at 1e8 pairs, 27 key bits: 4 passes of 7 bits
+        // 2.72 ms vs 3 passes of 9 bits 3.26 ms -- wider digits cost more per pass than they save.
+        const char* s = getenv("QE_SORT_MAXBITS");
+        int v = s ? atoi(s) : 8;
+        return v < 8 ? 8 : (v > 11 ? 11 : v);
+    }();
+    return mb;
+}
+
+static PassDesc plan_passes(uint64_t kor, uint64_t kand, int maxbits, int* width_out) {
     PassDesc pd{};
     uint64_t vary = kor & ~kand;
+    *width_out = 0;
     if (!vary) return pd;
     int lo = __builtin_ctzll(vary);
     int hi = 64 - __builtin_clzll(vary);
     int nbits = hi - lo;
-    int np = (nbits + 7) / 8;
+    int np = (nbits + maxbits - 1) / maxbits;
     int width = (nbits + np - 1) / np;
     pd.npass = np;
     for (int p = 0; p < np; p++) {
@@ -236,6 +406,7 @@ static PassDesc plan_passes(uint64_t kor, uint64_t kand) {
         int wbits = std::min(width, hi - pd.shift[p]);
         pd.mask[p] = (1u << wbits) - 1u;
     }
+    *width_out = width;
     return pd;
 }
 
@@ -255,6 +426,122 @@ static void key_bits_impl(qe_ctx* c, const K* keys, uint64_t n, uint64_t* out) {
 
 void key_bits_u64(qe_ctx* c, const uint64_t* keys, uint64_t n, uint64_t* out) { key_bits_impl(c, keys, n, out); }
 
+template <typename K, int RBITS>
+static void hist_and_scan(qe_ctx* c, const K* keys, uint64_t n, const PassDesc& pd, uint32_t* hist) {
+    QE_HIP(hipMemsetAsync(hist, 0, (size_t)pd.npass * (1u << RBITS) * sizeof(uint32_t), c->stream));
+    Timed t(c, "sort_hist", (double)sizeof(K) * n);
+    hipLaunchKernelGGL((digit_hist_kernel<K, RBITS>), dim3(grid_for(n, 256 * 32, 2048)), dim3(256), 0, c->stream, keys,
+                       n, pd, hist);
+    QE_HIP(hipGetLastError());
+    hipLaunchKernelGGL((digit_scan_kernel<RBITS>), dim3(pd.npass), dim3(256), 0, c->stream, hist);
+    QE_HIP(hipGetLastError());
+}
+
+// packed sort: every pass on u64 words; first pass from (key, rowid or iota), last pass back to it
+template <typename K, int RBITS>
+static SortOut sort_packed(qe_ctx* c, const K* keys, const uint32_t* vals, uint64_t n, const PassDesc& pd, Field f,
+                           const char* name) {
+    constexpr int BINS = 1 << RBITS;
+    uint32_t* hist = dalloc_t<uint32_t>(c, (size_t)MAX_PASS * BINS);
+    hist_and_scan<K, RBITS>(c, keys, n, pd, hist);
+    const uint64_t nt = (n + RTILE - 1) / RTILE;
+    const int P = pd.npass;
+    uint64_t* wbuf[2] = {P > 1 ? dalloc_t<uint64_t>(c, n) : nullptr, P > 2 ? dalloc_t<uint64_t>(c, n) : nullptr};
+    K* kout = dalloc_t<K>(c, n);
+    uint32_t* vout = dalloc_t<uint32_t>(c, n);
+    const uint64_t* win = nullptr;
+    for (int p = 0; p < P; p++) {
+        const bool first = p == 0, last = p == P - 1;
+        const int dsh = 32 + pd.shift[p] - f.lo;
+        uint64_t* wo = last ? nullptr : wbuf[p & 1];
+        LBSlot s = lb_acquire(c, nt * BINS);
+        double bytes = (first ? (double)sizeof(K) + 4 : 8.0) * n + (last ? (double)sizeof(K) + 4 : 8.0) * n;
+        Timed t(c, name, bytes);
+#define QE_RP(IN, OUT)                                                                                             \
+    hipLaunchKernelGGL((radix_pass_kernel<K, IN, OUT, true, RBITS>), dim3((unsigned)nt), dim3(RB), 0, c->stream,   \
+                       keys, win, vals, kout, wo, vout, n, dsh, pd.mask[p], f, hist + p * BINS, s.status, s.ticket, \
+                       s.epoch)
+        if (first && last) {
+            if (vals) QE_RP(IN_KV, OUT_KV);
+            else QE_RP(IN_KIOTA, OUT_KV);
+        } else if (first) {
+            if (vals) QE_RP(IN_KV, OUT_WORD);
+            else QE_RP(IN_KIOTA, OUT_WORD);
+        } else if (last) {
+            QE_RP(IN_WORD, OUT_KV);
+        } else {
+            QE_RP(IN_WORD, OUT_WORD);
+        }
+#undef QE_RP
+        QE_HIP(hipGetLastError());
+        win = wo;
+    }
+    dfree(c, hist);
+    if (wbuf[0]) dfree(c, wbuf[0]);
+    if (wbuf[1]) dfree(c, wbuf[1]);
+    return SortOut{kout, vout, true, true};
+}
+
+// key-only sort of 64-bit words (dedup of packed pairs): the word is the key
+template <int RBITS>
+static SortOut sort_keys_only(qe_ctx* c, const uint64_t* keys, uint64_t n, const PassDesc& pd, const char* name) {
+    constexpr int BINS = 1 << RBITS;
+    uint32_t* hist = dalloc_t<uint32_t>(c, (size_t)MAX_PASS * BINS);
+    hist_and_scan<uint64_t, RBITS>(c, keys, n, pd, hist);
+    const uint64_t nt = (n + RTILE - 1) / RTILE;
+    uint64_t* buf[2] = {dalloc_t<uint64_t>(c, n), pd.npass > 1 ? dalloc_t<uint64_t>(c, n) : nullptr};
+    const uint64_t* in = keys;
+    Field f{0, 0, 0};
+    for (int p = 0; p < pd.npass; p++) {
+        uint64_t* out = buf[p & 1];
+        LBSlot s = lb_acquire(c, nt * BINS);
+        Timed t(c, name, 16.0 * n);
+        hipLaunchKernelGGL((radix_pass_kernel<uint64_t, IN_WORD, OUT_WORD, false, RBITS>), dim3((unsigned)nt), dim3(RB),
+                           0, c->stream, nullptr, in, nullptr, nullptr, out, nullptr, n, pd.shift[p], pd.mask[p], f,
+                           hist + p * BINS, s.status, s.ticket, s.epoch);
+        QE_HIP(hipGetLastError());
+        in = out;
+    }
+    dfree(c, hist);
+    int last = (pd.npass - 1) & 1;
+    if (pd.npass > 1) dfree(c, buf[last ^ 1]);
+    return SortOut{buf[last], nullptr, true, false};
+}
+
+template <typename K>
+static SortOut sort_kv_unpacked(qe_ctx* c, const K* keys, const uint32_t* vals, uint64_t n, const PassDesc& pd,
+                                const char* name) {
+    uint32_t* hist = dalloc_t<uint32_t>(c, (size_t)MAX_PASS * 256);
+    hist_and_scan<K, 8>(c, keys, n, pd, hist);
+    const uint64_t nt = (n + RTILE - 1) / RTILE;
+    K* kbuf[2] = {dalloc_t<K>(c, n), pd.npass > 1 ? dalloc_t<K>(c, n) : nullptr};
+    uint32_t* vbuf[2] = {dalloc_t<uint32_t>(c, n), pd.npass > 1 ? dalloc_t<uint32_t>(c, n) : nullptr};
+    const K* kin = keys;
+    const uint32_t* vin = vals;
+    for (int p = 0; p < pd.npass; p++) {
+        LBSlot s = lb_acquire(c, nt * 256);
+        Timed t(c, name, 2.0 * n * (sizeof(K) + 4));
+        if (vin)
+            hipLaunchKernelGGL((radix_pass_kv_kernel<K, true>), dim3((unsigned)nt), dim3(RB), 0, c->stream, kin, vin,
+                               kbuf[p & 1], vbuf[p & 1], n, pd.shift[p], pd.mask[p], hist + p * 256, s.status,
+                               s.ticket, s.epoch);
+        else
+            hipLaunchKernelGGL((radix_pass_kv_kernel<K, false>), dim3((unsigned)nt), dim3(RB), 0, c->stream, kin,
+                               nullptr, kbuf[p & 1], vbuf[p & 1], n, pd.shift[p], pd.mask[p], hist + p * 256,
+                               s.status, s.ticket, s.epoch);
+        QE_HIP(hipGetLastError());
+        kin = kbuf[p & 1];
+        vin = vbuf[p & 1];
+    }
+    dfree(c, hist);
+    int last = (pd.npass - 1) & 1;
+    if (pd.npass > 1) {
+        dfree(c, kbuf[last ^ 1]);
+        dfree(c, vbuf[last ^ 1]);
+    }
+    return SortOut{kbuf[last], vbuf[last], true, true};
+}
+
 template <typename K>
 static SortOut radix_sort_impl(qe_ctx* c, const K* keys, const uint32_t* vals, uint64_t n, bool with_vals,
                                const char* name, const uint64_t* bits) {
@@ -268,61 +555,29 @@ static SortOut radix_sort_impl(qe_ctx* c, const K* keys, const uint32_t* vals, u
     } else {
         key_bits_impl(c, keys, n, kb);
     }
-    PassDesc pd = plan_passes(kb[0], kb[1]);
-    if (pd.npass == 0) return so;   // every key equal: already sorted (and stable)
-
-    uint32_t* hist = dalloc_t<uint32_t>(c, 8 * RBINS);
-    QE_HIP(hipMemsetAsync(hist, 0, 8 * RBINS * sizeof(uint32_t), c->stream));
-    {
-        Timed t(c, "sort_hist", (double)sizeof(K) * n);
-        hipLaunchKernelGGL(digit_hist_kernel<K>, dim3(grid_for(n, 256 * 32, 2048)), dim3(256), 0, c->stream, keys,
-                           n, pd, hist);
-        QE_HIP(hipGetLastError());
-        hipLaunchKernelGGL(digit_scan_kernel, dim3(pd.npass), dim3(256), 0, c->stream, hist);
-        QE_HIP(hipGetLastError());
+    const uint64_t vary = kb[0] & ~kb[1];
+    if (!vary) return so;   // every key equal: already sorted (and stable)
+    const int lo = __builtin_ctzll(vary), hi = 64 - __builtin_clzll(vary);
+    const bool pack = with_vals && hi - lo <= 32;
+    int width = 0;
+    if (pack) {
+        const int mb = sort_maxbits();
+        PassDesc pd = plan_passes(kb[0], kb[1], mb, &width);
+        const uint64_t fmask = (1ull << (hi - lo)) - 1;   // hi - lo <= 32 here
+        Field f{lo, fmask, kb[1] & ~(fmask << lo)};         // constant key bits come back from the AND
+        switch (width <= 8 ? 8 : width) {
+        case 8: return sort_packed<K, 8>(c, keys, vals, n, pd, f, name);
+        case 9: return sort_packed<K, 9>(c, keys, vals, n, pd, f, name);
+        case 10: return sort_packed<K, 10>(c, keys, vals, n, pd, f, name);
+        default: return sort_packed<K, 11>(c, keys, vals, n, pd, f, name);
+        }
     }
-    const uint64_t nt = (n + RTILE - 1) / RTILE;
-    K* kbuf[2] = {dalloc_t<K>(c, n), pd.npass > 1 ? dalloc_t<K>(c, n) : nullptr};
-    uint32_t* vbuf[2] = {nullptr, nullptr};
-    if (with_vals) {
-        vbuf[0] = dalloc_t<uint32_t>(c, n);
-        if (pd.npass > 1) vbuf[1] = dalloc_t<uint32_t>(c, n);
+    PassDesc pd = plan_passes(kb[0], kb[1], 8, &width);
+    if (!with_vals) {
+        if constexpr (sizeof(K) == 8) return sort_keys_only<8>(c, (const uint64_t*)keys, n, pd, name);
+        throw Error(QE_EINVAL, "key-only sort needs 64-bit keys");
     }
-    const K* kin = keys;
-    const uint32_t* vin = vals;
-    const double pass_bytes = 2.0 * n * (sizeof(K) + (with_vals ? 4 : 0));
-    for (int p = 0; p < pd.npass; p++) {
-        K* kout = kbuf[p & 1];
-        uint32_t* vout = vbuf[p & 1];
-        LBSlot s = lb_acquire(c, nt * RBINS);
-        Timed t(c, name, pass_bytes);
-        if (!with_vals)
-            hipLaunchKernelGGL((radix_pass_kernel<K, false, false>), dim3((unsigned)nt), dim3(RB), 0, c->stream, kin,
-                               nullptr, kout, nullptr, n, pd.shift[p], pd.mask[p], hist + p * RBINS, s.status,
-                               s.ticket, s.epoch);
-        else if (vin)
-            hipLaunchKernelGGL((radix_pass_kernel<K, true, true>), dim3((unsigned)nt), dim3(RB), 0, c->stream, kin,
-                               vin, kout, vout, n, pd.shift[p], pd.mask[p], hist + p * RBINS, s.status, s.ticket,
-                               s.epoch);
-        else
-            hipLaunchKernelGGL((radix_pass_kernel<K, false, true>), dim3((unsigned)nt), dim3(RB), 0, c->stream, kin,
-                               nullptr, kout, vout, n, pd.shift[p], pd.mask[p], hist + p * RBINS, s.status,
-                               s.ticket, s.epoch);
-        QE_HIP(hipGetLastError());
-        kin = kout;
-        vin = vout;
-    }
-    dfree(c, hist);
-    int last = (pd.npass - 1) & 1;
-    if (pd.npass > 1) {
-        dfree(c, kbuf[last ^ 1]);
-        if (with_vals) dfree(c, vbuf[last ^ 1]);
-    }
-    so.keys = kbuf[last];
-    so.vals = with_vals ? vbuf[last] : nullptr;
-    so.keys_new = true;
-    so.vals_new = with_vals;
-    return so;
+    return sort_kv_unpacked<K>(c, keys, vals, n, pd, name);
 }
 
 SortOut radix_sort_u64(qe_ctx* c, const uint64_t* keys, const uint32_t* vals, uint64_t n, bool with_vals,

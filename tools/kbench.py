@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Kernel-level timing of libqe primitives at full size (tuning aid, not the headline bench).
+
+    python tools/kbench.py [sort|merge|payloads|all] [--n 100000000] [--reps 5]
+Prints per-kernel ms (HIP events on the libqe stream) and algorithmic GB/s.
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "query-compiler-executor_amd"))
+
+from qe import lib  # noqa: E402
+
+
+def report(ctx, label, reps):
+    st = ctx.kernel_stats()
+    tot = 0.0
+    for k, s in sorted(st.items(), key=lambda kv: -kv[1]["ms"]):
+        if not s["launches"]:
+            continue
+        ms = s["ms"] / reps
+        tot += ms
+        gbs = s["alg_bytes"] / (s["ms"] * 1e-3) / 1e9 if s["ms"] else 0
+        print(f"  {label:10s} {k:22s} {ms:8.3f} ms/rep  {s['launches'] / reps:5.1f} launches  {gbs:8.1f} GB/s")
+    print(f"  {label:10s} {'TOTAL':22s} {tot:8.3f} ms/rep", flush=True)
+    ctx.reset_stats()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("what", nargs="?", default="all")
+    ap.add_argument("--n", type=int, default=100_000_000)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    ctx = lib.Ctx(0)
+    n = a.n
+    kinds = [("mod", n), ("mod", n), ("hi32",)]
+    r0 = ctx.gen_relation(n, kinds, seed=1, gen_rel=0)
+    r1 = ctx.gen_relation(n, kinds, seed=1, gen_rel=1)
+    ctx.sync()
+    ctx.set_profiling(True)
+    if a.what in ("sort", "all"):
+        for rep in range(a.reps + 1):
+            p = ctx.gather_pairs(ctx.column(r0, 1), None)
+            ctx.sort_pairs(p)
+            ctx.pairs_free(p)
+            if rep == 0:
+                ctx.reset_stats()
+        report(ctx, f"sort{os.environ.get('QE_SORT_MAXBITS', '')}", a.reps)
+    if a.what in ("merge", "all"):
+        R = ctx.gather_pairs(ctx.column(r0, 1), None)
+        S = ctx.gather_pairs(ctx.column(r1, 0), None)
+        ctx.sort_pairs(R)
+        ctx.sort_pairs(S)
+        ctx.reset_stats()
+        for rep in range(a.reps):
+            x, y = ctx.merge_join(R, S)
+            ctx.list_free(x)
+            ctx.list_free(y)
+        report(ctx, "merge", a.reps)
+    if a.what in ("gather", "all"):
+        R = ctx.gather_pairs(ctx.column(r0, 1), None)
+        ctx.sort_pairs(R)
+        rows = lib.List()
+        rows.d, rows.n, rows.cap = R.val, R.n, R.n
+        for rep in range(a.reps):
+            p = ctx.gather_pairs(ctx.column(r1, 1), rows)
+            ctx.pairs_free(p)
+        report(ctx, "gather", a.reps)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
