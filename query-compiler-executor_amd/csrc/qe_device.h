@@ -149,7 +149,10 @@ __device__ __forceinline__ uint64_t lookback_wave(uint64_t* status, uint32_t epo
 // tile, this thread owns column `col`.  The aggregate must already be published.
 // Each step reads the next LB_WIN predecessors' words at once (independent loads in flight), so
 // a walk over k aggregate-only tiles costs ~k/LB_WIN load latencies instead of k.
-constexpr int LB_WIN = 8;
+#ifndef QE_LB_WIN
+#define QE_LB_WIN 8
+#endif
+constexpr int LB_WIN = QE_LB_WIN;
 __device__ __forceinline__ uint64_t lookback_serial(uint64_t* status, uint32_t epoch, uint32_t tile,
                                                     uint32_t stride, uint32_t col) {
     uint64_t excl = 0;

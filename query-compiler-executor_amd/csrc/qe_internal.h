@@ -128,7 +128,7 @@ uint64_t filter_refine(qe_ctx* c, const uint64_t* col, const uint32_t* in, uint6
                        uint32_t* out);
 uint64_t scan_join_k(qe_ctx* c, const uint64_t* rk, const uint32_t* rv, const uint64_t* sk, const uint32_t* sv,
                      uint64_t n, uint32_t* outR, uint32_t* outS);
-uint64_t compact_nonzero_pairs(qe_ctx* c, const uint32_t* counts, const uint32_t* last, const uint32_t* edit,
+uint64_t compact_nonzero_pairs(qe_ctx* c, const uint32_t* nz, uint64_t nzw, const uint32_t* last, const uint32_t* edit,
                                uint64_t n, uint32_t* out_last, uint32_t* out_edit);
 
 // sort (qe_sort.hip): stable LSD radix; returns buffers (may alias inputs when 0 passes needed)

@@ -102,13 +102,52 @@ struct MJShared {
     uint32_t ticket;
 };
 
-// stage the tile's R keys and (when it fits) its S window in LDS
+// stage the tile's R keys and (when it fits) its S window in LDS.  Every load of the tile is
+// issued before the first LDS store: 24 independent loads in flight per thread instead of one
+// (a load -> store loop leaves ~6 KB in flight per CU, a quarter of what HBM needs).
 __device__ __forceinline__ void mj_stage(MJShared& sh, const uint64_t* rk, uint64_t base, uint32_t tn,
                                          const uint64_t* sk, uint64_t wlo, uint64_t wn) {
     if (threadIdx.x == 0) sh.flag = 0;
-    for (uint32_t i = threadIdx.x; i < tn; i += MJB) sh.r[rpad(i)] = rk[base + i];
-    if (wn <= MJ_WIN)
-        for (uint32_t i = threadIdx.x; i < wn; i += MJB) sh.s[i] = sk[wlo + i];
+    constexpr int RS = MJ_TILE / MJB, SS = MJ_WIN / MJB;
+    uint64_t rr[RS], ss[SS];
+    const uint32_t t = threadIdx.x;
+    if (tn == MJ_TILE) {   // base is a multiple of MJ_TILE: 16-B aligned pairs
+        const uint4* r4 = reinterpret_cast<const uint4*>(rk + base);
+#pragma unroll
+        for (int k = 0; k < RS / 2; k++) {
+            uint4 v = r4[t + k * MJB];
+            rr[2 * k] = ((uint64_t)v.y << 32) | v.x;
+            rr[2 * k + 1] = ((uint64_t)v.w << 32) | v.z;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < RS / 2; k++) {
+            uint32_t i = 2 * (t + k * MJB);
+            rr[2 * k] = i < tn ? rk[base + i] : 0;
+            rr[2 * k + 1] = i + 1 < tn ? rk[base + i + 1] : 0;
+        }
+    }
+    const bool sw = wn <= MJ_WIN;
+    if (sw) {
+#pragma unroll
+        for (int k = 0; k < SS; k++) {
+            uint32_t i = t + k * MJB;
+            ss[k] = i < wn ? sk[wlo + i] : 0;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < RS / 2; k++) {
+        uint32_t i = 2 * (t + k * MJB);
+        if (i < tn) sh.r[rpad(i)] = rr[2 * k];
+        if (i + 1 < tn) sh.r[rpad(i + 1)] = rr[2 * k + 1];
+    }
+    if (sw) {
+#pragma unroll
+        for (int k = 0; k < SS; k++) {
+            uint32_t i = t + k * MJB;
+            if (i < wn) sh.s[i] = ss[k];
+        }
+    }
     __syncthreads();
 }
 
@@ -243,16 +282,31 @@ __device__ __forceinline__ void mj_emit(MJShared& sh, const uint32_t* rv, const 
         for (int j = 0; j < MJ_ITEMS; j++) {
             if (e0 + j >= tn) continue;
             for (uint32_t k = 0; k < cnt[j]; k++) {
-                uint64_t sidx = wlo + lo_rel[j] + k;
                 sh.oR[run + k] = r[j];
-                sh.oS[run + k] = sv ? sv[sidx] : (uint32_t)sidx;
+                sh.oS[run + k] = lo_rel[j] + k;   // window-relative; S payloads gathered below
             }
             run += cnt[j];
         }
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < (uint32_t)btotal; i += MJB) {
-            outR[gofs + i] = sh.oR[i];
-            outS[gofs + i] = sh.oS[i];
+        // four independent S-payload loads in flight per thread per round (the window is read
+        // in order, so each round's loads coalesce)
+        const uint32_t bt = (uint32_t)btotal;
+        for (uint32_t i0 = threadIdx.x; i0 < bt; i0 += 4 * MJB) {
+            uint32_t v[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                uint32_t i = i0 + q * MJB;
+                uint64_t sidx = wlo + (i < bt ? sh.oS[i] : 0);
+                v[q] = i < bt ? (sv ? sv[sidx] : (uint32_t)sidx) : 0;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                uint32_t i = i0 + q * MJB;
+                if (i < bt) {
+                    outR[gofs + i] = sh.oR[i];
+                    outS[gofs + i] = v[q];
+                }
+            }
         }
         return;
     }
@@ -333,7 +387,11 @@ __global__ void __launch_bounds__(MJB) mj_fused(const uint64_t* __restrict__ rk,
     uint64_t btotal;
     uint64_t run = mj_block_scan(sh, tsum, &btotal);
     if (wave_id() == 0) {
+#ifdef QE_DIAG_MJ_NOLB   // ablation only: tile offset = its first R row (in range, wrong when fan-out != 1)
+        uint64_t ex = base;
+#else
         uint64_t ex = lookback_wave(status, epoch, tile, btotal);
+#endif
         if (lane_id() == 0) {
             sh.excl = ex;
             tile_counts[tile] = btotal;
@@ -342,7 +400,11 @@ __global__ void __launch_bounds__(MJB) mj_fused(const uint64_t* __restrict__ rk,
     }
     mj_publish_flags(sh, f, flags);   // contains the barrier that publishes sh.excl
     const uint64_t gofs = sh.excl;
+#ifdef QE_DIAG_MJ_NOEMIT
+    if (gofs + btotal > cap + 1) outR[0] = (uint32_t)run;   // keep the walk alive, store nothing
+#else
     if (gofs + btotal <= cap) mj_emit(sh, rv, sv, base, tn, wlo, run, btotal, gofs, cnt, lo_rel, outR, outS);
+#endif
 }
 
 // The reference's two-pointer loop verbatim (src/join.c:342-377) for inputs that are not
@@ -474,9 +536,51 @@ __global__ void __launch_bounds__(256) checksum_kernel(const uint64_t* __restric
     if (threadIdx.x == 0) atomicAdd(out, (unsigned long long)(red[0] + red[1] + red[2] + red[3]));
 }
 
+// nonzero bitmap of the driver counts: one sequential pass over the (rows x 4 B) counts array
+// leaves rows/8 bytes that stay cache-resident for the pruning pass's random tests, which
+// would otherwise fetch a 64-B line of the counts array per 4-B test
+__global__ void __launch_bounds__(256) nonzero_bitmap_kernel(const uint32_t* __restrict__ counts, uint64_t rows,
+                                                             uint32_t* __restrict__ bm) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;   // one 32-row word per thread
+    const uint64_t r0 = w * 32;
+    if (r0 >= rows) return;
+    uint32_t bits = 0;
+    if (r0 + 32 <= rows) {
+        uint4 q[8];
+        const uint4* p = reinterpret_cast<const uint4*>(counts + r0);
+#pragma unroll
+        for (int k = 0; k < 8; k++) q[k] = p[k];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            bits |= (q[k].x ? 1u : 0u) << (4 * k);
+            bits |= (q[k].y ? 1u : 0u) << (4 * k + 1);
+            bits |= (q[k].z ? 1u : 0u) << (4 * k + 2);
+            bits |= (q[k].w ? 1u : 0u) << (4 * k + 3);
+        }
+    } else {
+        for (uint64_t r = r0; r < rows; r++) bits |= (counts[r] ? 1u : 0u) << (r - r0);
+    }
+    bm[w] = bits;
+}
+
 // ---- join_payloads expansion (src/join.c:452-476 on sorted inputs) -------------------------------
 // element i (sorted by last) is emitted counts[last[i]] times
 constexpr int XB = 256, X_ITEMS = 8, X_TILE = XB * X_ITEMS;
+
+constexpr int X_OUT = 2 * X_TILE;   // outputs a tile stages in LDS (mean multiplicity <= 2)
+
+template <int WRITE>
+union XShared {
+    uint32_t out[X_OUT];
+    struct {
+        uint64_t off[X_TILE];   // run start per element (~0 past the tile end)
+        uint32_t val[X_TILE];
+    };
+};
+template <>
+union XShared<0> {
+    uint32_t out[1];
+};
 
 // WRITE = 1 emits vals[idx[i]] (idx != null) or vals[i]
 template <int WRITE>
@@ -484,7 +588,7 @@ __global__ void __launch_bounds__(XB) expand_kernel(const uint32_t* __restrict__
                                                     uint64_t n, const uint32_t* __restrict__ counts,
                                                     uint64_t* __restrict__ tile_counts, uint32_t* __restrict__ out,
                                                     uint32_t* __restrict__ flags, const uint32_t* __restrict__ idx) {
-    __shared__ uint32_t s_off[WRITE ? X_TILE : 1];
+    __shared__ XShared<WRITE> sx;
     __shared__ uint64_t s_red[XB / 64];
     const uint32_t tile = blockIdx.x;
     const uint64_t base = (uint64_t)tile * X_TILE;
@@ -510,7 +614,7 @@ __global__ void __launch_bounds__(XB) expand_kernel(const uint32_t* __restrict__
         tsum += c[j];
         mx = c[j] > mx ? c[j] : mx;
     }
-    if (!WRITE) {
+    if constexpr (!WRITE) {
         uint64_t s = wave_sum_u64(tsum);
         mx = wave_max_u32(mx);
         if (lane_id() == 0) {
@@ -522,6 +626,22 @@ __global__ void __launch_bounds__(XB) expand_kernel(const uint32_t* __restrict__
         __syncthreads();
         if (threadIdx.x == 0) tile_counts[tile] = s_red[0] + s_red[1] + s_red[2] + s_red[3];
         return;
+    } else {   // (if constexpr: XShared<0> has no staging space)
+    // this thread's 8 payloads, all loads in flight at once (idx is read in order, vals[idx] is
+    // the random gather)
+    uint32_t v[X_ITEMS];
+    if (idx && e0 + X_ITEMS <= tn) {
+        uint4 a = *reinterpret_cast<const uint4*>(idx + base + e0);
+        uint4 b = *reinterpret_cast<const uint4*>(idx + base + e0 + 4);
+        uint32_t p[X_ITEMS] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int j = 0; j < X_ITEMS; j++) v[j] = c[j] ? vals[p[j]] : 0;
+    } else {
+#pragma unroll
+        for (int j = 0; j < X_ITEMS; j++) {
+            uint64_t e = base + e0 + j;
+            v[j] = (e0 + j < tn && c[j]) ? vals[idx ? idx[e] : e] : 0;
+        }
     }
     uint64_t inc = wave_incl_scan_u64(tsum);
     if (lane_id() == 63) s_red[wave_id()] = inc;
@@ -529,25 +649,41 @@ __global__ void __launch_bounds__(XB) expand_kernel(const uint32_t* __restrict__
     uint64_t add = 0;
     for (int w = 0; w < wave_id(); w++) add += s_red[w];
     uint64_t run = inc - tsum + add;
-    uint64_t btotal = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+    const uint64_t btotal = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+    const uint64_t gofs = tile_counts[tile];
+    if (btotal <= (uint64_t)X_OUT) {   // typical: the tile's output built in LDS, one coalesced run
+#pragma unroll
+        for (int j = 0; j < X_ITEMS; j++) {
+            for (uint32_t q = 0; q < c[j]; q++) sx.out[run + q] = v[j];
+            run += c[j];
+        }
+        __syncthreads();
+        for (uint32_t o = threadIdx.x; o < (uint32_t)btotal; o += XB) out[gofs + o] = sx.out[o];
+        return;
+    }
+    // heavy tile: run starts + payloads in LDS; output slot o finds its element by a fixed-step
+    // binary search (last e with off[e] <= o), four slots interleaved per thread
 #pragma unroll
     for (int j = 0; j < X_ITEMS; j++) {
         uint32_t e = e0 + j;
-        if (e < tn) {
-            s_off[e] = (uint32_t)run;
-            run += c[j];
-        }
+        sx.off[e] = e < tn ? run : ~0ull;
+        sx.val[e] = v[j];
+        run += c[j];
     }
     __syncthreads();
-    const uint64_t gofs = tile_counts[tile];
-    for (uint64_t o = threadIdx.x; o < btotal; o += XB) {
-        uint32_t a = 0, b = tn;
-        while (b - a > 1) {
-            uint32_t m = (a + b) >> 1;
-            if (s_off[m] <= o) a = m;
-            else b = m;
+    for (uint64_t o0 = threadIdx.x; o0 < btotal; o0 += 4 * XB) {
+        uint32_t a[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (uint32_t step = X_TILE / 2; step; step >>= 1)
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (sx.off[a[q] + step] <= o0 + (uint64_t)q * XB) a[q] += step;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            uint64_t o = o0 + (uint64_t)q * XB;
+            if (o < btotal) out[gofs + o] = sx.val[a[q]];
         }
-        out[gofs + o] = idx ? vals[idx[base + a]] : vals[base + a];
+    }
     }
 }
 
@@ -894,7 +1030,19 @@ int qe_join_payloads_multi(qe_ctx* c, const uint32_t* d_counts, uint64_t rows, c
     // 1. positions whose driver count is 0 emit nothing: keep (last[i], i) for the others
     uint32_t* pl = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
     uint32_t* pi = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
-    uint64_t m = n ? compact_nonzero_pairs(c, d_counts, last->d, nullptr, n, pl, pi) : 0;
+    uint64_t m = 0;
+    if (n) {
+        const uint64_t nw = (rows + 31) / 32;
+        uint32_t* nz = dalloc_t<uint32_t>(c, std::max<uint64_t>(nw, 1));
+        {
+            Timed t(c, "payload_bitmap", 4.0 * rows + nw * 4.0);
+            hipLaunchKernelGGL(nonzero_bitmap_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, c->stream,
+                               d_counts, rows, nz);
+            QE_HIP(hipGetLastError());
+        }
+        m = compact_nonzero_pairs(c, nz, nw, last->d, nullptr, n, pl, pi);
+        dfree(c, nz);
+    }
     // 2. one stable sort by `last` for every edit list (the reference sorts R = (last, edit)
     //    by key per entry, src/join.c:444; the permutation is the same for all of them).
     //    Rowids are < rows, which bounds the bits the sort has to look at.

@@ -95,7 +95,8 @@ struct ScanJoinOp {            // scan_join: positional key equality, both paylo
 
 struct NonzeroPairsOp {        // join_payloads: keep (last[i], edit[i] or i) whose driver count > 0
     static constexpr int VEC = 4;
-    const uint32_t *counts, *last, *edit;   // edit == null: emit the position i
+    const uint32_t *nz, *last, *edit;   // nz: bit r set <=> count[r] > 0; edit == null: emit i
+    uint64_t nzw;                        // words in nz (a rowid past the driver's rows never matches)
     __device__ __forceinline__ void load(uint64_t base, uint64_t n, bool* f, uint32_t* v0, uint32_t* v1) const {
         uint32_t l[4];
         if (base + 3 < n) {
@@ -109,7 +110,7 @@ struct NonzeroPairsOp {        // join_payloads: keep (last[i], edit[i] or i) wh
         for (int k = 0; k < 4; k++) {
             uint64_t i = base + k;
             bool ok = i < n;
-            f[k] = ok && counts[l[k]] != 0;
+            f[k] = ok && (l[k] >> 5) < nzw && ((nz[l[k] >> 5] >> (l[k] & 31)) & 1u);
             v0[k] = l[k];
             v1[k] = ok ? (edit ? edit[i] : (uint32_t)i) : 0;
         }
@@ -245,9 +246,9 @@ uint64_t scan_join_k(qe_ctx* c, const uint64_t* rk, const uint32_t* rv, const ui
     return run_compact<8, 2>(c, "scan_join", 24.0 * n, ScanJoinOp{rk, sk, rv, sv}, n, outR, outS);
 }
 
-uint64_t compact_nonzero_pairs(qe_ctx* c, const uint32_t* counts, const uint32_t* last, const uint32_t* edit,
-                               uint64_t n, uint32_t* out_last, uint32_t* out_edit) {
-    return run_compact<4, 2>(c, "payload_prune", 12.0 * n, NonzeroPairsOp{counts, last, edit}, n, out_last,
+uint64_t compact_nonzero_pairs(qe_ctx* c, const uint32_t* nz, uint64_t nzw, const uint32_t* last,
+                               const uint32_t* edit, uint64_t n, uint32_t* out_last, uint32_t* out_edit) {
+    return run_compact<4, 2>(c, "payload_prune", 8.0 * n, NonzeroPairsOp{nz, last, edit, nzw}, n, out_last,
                              out_edit);
 }
 

@@ -32,7 +32,10 @@ namespace qe {
 
 constexpr int RB = 256;          // block
 constexpr int RNW = RB / 64;     // waves per block
-constexpr int R_ITEMS = 16;      // words per thread per tile
+#ifndef QE_R_ITEMS
+#define QE_R_ITEMS 32
+#endif
+constexpr int R_ITEMS = QE_R_ITEMS;   // words per thread per tile
 constexpr int RTILE = RB * R_ITEMS;
 constexpr int MAX_PASS = 8;
 
@@ -175,6 +178,10 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
         uint64_t i = wave_base + (uint64_t)j * 64 + l;
         bool ok = i < n;
         uint32_t d = (uint32_t)(word[j] >> dsh) & mask;
+#ifdef QE_DIAG_SORT_NORANK   // ablation only: LDS-atomic ranks instead of match-any (unstable, in range)
+        (void)lt;
+        pos[j] = ok ? atomicAdd(&whist[w][d], 1u) : 0u;
+#else
         uint64_t peers = __ballot(ok);
 #pragma unroll
         for (int b = 0; b < RBITS; b++) {
@@ -190,6 +197,7 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
         }
         old = (uint32_t)__shfl((int)old, leader, 64);
         pos[j] = old + (uint32_t)__popcll(peers & lt);
+#endif
     }
     __syncthreads();
     // thread t owns digits t*DPT .. t*DPT+DPT-1: totals, exclusive over waves, publish aggregate
@@ -233,10 +241,12 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
     for (int q = 0; q < DPT; q++) {
         const uint32_t d = threadIdx.x * DPT + q;
         uint64_t ex = 0;
+#ifndef QE_DIAG_SORT_NOLB   // ablation only: skip the lookback (output positions are wrong)
         if (tile > 0) {
             ex = lookback_serial(status, epoch, tile, BINS, d);
             st_agent(&status[(uint64_t)tile * BINS + d], lb_word(epoch, LB_FLAG_INC, ex + tot[q]));
         }
+#endif
         gofs[d] = digit_base[d] + (uint32_t)ex - bexcl[d];
     }
     __syncthreads();
@@ -247,7 +257,11 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
         uint32_t i = (uint32_t)k * RB + threadIdx.x;
         if (i < tn) {
             uint64_t wd = stage[i];
+#ifdef QE_DIAG_SORT_LINEAR   // ablation only: contiguous output instead of the digit scatter
+            uint32_t p = (uint32_t)(tbase + i);
+#else
             uint32_t p = gofs[(uint32_t)(wd >> dsh) & mask] + i;
+#endif
             if (OUT == OUT_WORD) {
                 wout[p] = wd;
             } else if (PACK) {

@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG, "build", "libqe.so")
+LIB_PATH = os.environ.get("QE_LIB_PATH") or os.path.join(PKG, "build", "libqe.so")   # override: ablation builds (tools/)
 HEADER = os.path.join(os.path.dirname(PKG), "include", "qe.h")
 
 QE_EINVAL, QE_EHIP, QE_ENOMEM, QE_EEXIT = -1, -2, -3, -4
