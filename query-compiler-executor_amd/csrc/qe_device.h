@@ -105,23 +105,27 @@ __device__ __forceinline__ uint32_t take_ticket(uint32_t* ticket, uint32_t* lds_
     return t;
 }
 
-// Wave-parallel lookback for ONE running total per tile.  Called by a whole wave; returns the
-// exclusive prefix (same in every lane) and publishes the inclusive one.
-__device__ __forceinline__ uint64_t lookback_wave(uint64_t* status, uint32_t epoch, uint32_t tile,
-                                                  uint64_t agg) {
+// Wave-parallel lookback for ONE running total per tile, in two halves so a tile can publish its
+// aggregate early and do independent work (e.g. stage its output in LDS) before it waits.
+__device__ __forceinline__ void lookback_publish(uint64_t* status, uint32_t epoch, uint32_t tile, uint64_t agg) {
+    if (lane_id() == 0) st_agent(&status[tile], lb_word(epoch, tile == 0 ? LB_FLAG_INC : LB_FLAG_AGG, agg));
+}
+
+// called by a whole wave after lookback_publish; returns the exclusive prefix (same in every
+// lane) and publishes the inclusive one
+__device__ __forceinline__ uint64_t lookback_wait(uint64_t* status, uint32_t epoch, uint32_t tile, uint64_t agg) {
     const int l = lane_id();
-    if (tile == 0) {
-        if (l == 0) st_agent(&status[0], lb_word(epoch, LB_FLAG_INC, agg));
-        return 0;
-    }
-    if (l == 0) st_agent(&status[tile], lb_word(epoch, LB_FLAG_AGG, agg));
+    if (tile == 0) return 0;
     uint64_t excl = 0;
     int64_t base = (int64_t)tile - 1;
     for (;;) {
+        // lane l looks at tile base - l; only the lanes up to the nearest inclusive prefix matter,
+        // so a slow tile further back than that never holds this one up
         int64_t idx = base - l;
         uint64_t w = 0;
         uint32_t f;
         uint32_t spins = 0;
+        int first;
         for (;;) {
             if (idx >= 0) {
                 w = ld_agent(&status[idx]);
@@ -130,12 +134,13 @@ __device__ __forceinline__ uint64_t lookback_wave(uint64_t* status, uint32_t epo
                 w = 0;
                 f = (uint32_t)LB_FLAG_INC;
             }
-            if (!__any(f == 0)) break;
+            const uint64_t inc = __ballot(f == LB_FLAG_INC);
+            first = inc ? (__ffsll((unsigned long long)inc) - 1) : 64;
+            const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);   // lanes 0..first
+            if (!(__ballot(f == 0) & need)) break;
             __builtin_amdgcn_s_sleep(1);
             if (++spins > (1u << 24)) break;   // bounded spin: never hang the GPU
         }
-        uint64_t inc = __ballot(f == LB_FLAG_INC);
-        int first = inc ? (__ffsll((unsigned long long)inc) - 1) : 64;
         uint64_t v = (l <= first && idx >= 0) ? (w & LB_VAL_MASK) : 0;
         excl += wave_sum_u64(v);
         if (first < 64) break;
@@ -143,6 +148,12 @@ __device__ __forceinline__ uint64_t lookback_wave(uint64_t* status, uint32_t epo
     }
     if (l == 0) st_agent(&status[tile], lb_word(epoch, LB_FLAG_INC, excl + agg));
     return excl;
+}
+
+__device__ __forceinline__ uint64_t lookback_wave(uint64_t* status, uint32_t epoch, uint32_t tile,
+                                                  uint64_t agg) {
+    lookback_publish(status, epoch, tile, agg);
+    return lookback_wait(status, epoch, tile, agg);
 }
 
 // Thread-serial lookback for one of many per-tile totals (radix digits): `stride` words per
@@ -187,5 +198,18 @@ __device__ __forceinline__ uint64_t lookback_serial(uint64_t* status, uint32_t e
     }
     return excl;
 }
+
+// Phase timestamps for tuning builds only (tools/build_variant.sh NAME -DQE_DIAG_STAMPS):
+// thread 0 of a tile records s_memrealtime (100 MHz) after each barrier-separated phase.
+#ifdef QE_DIAG_STAMPS
+constexpr uint32_t STAMP_TILES = 1u << 16, STAMP_SLOTS = 8;
+#define QE_STAMP(arr, tile, k)                                                        \
+    do {                                                                              \
+        if (threadIdx.x == 0 && (tile) < STAMP_TILES)                                 \
+            (arr)[(uint64_t)(tile) * STAMP_SLOTS + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define QE_STAMP(arr, tile, k) ((void)0)
+#endif
 
 }  // namespace qe

@@ -71,12 +71,18 @@ __global__ void __launch_bounds__(1024) part_scan_kernel(uint32_t* __restrict__ 
     }
 }
 
+// rowid columns travel by value in the kernel arguments: pointers loaded from a device array
+// would be generic (FLAT loads / stores)
+struct PartCols {
+    const uint32_t* in[4];
+    uint32_t* out[4];
+};
+
 // stable scatter: element order is kept inside every destination segment
 template <int NC>
 __global__ void __launch_bounds__(PB) part_scatter_kernel(const uint64_t* __restrict__ keys, uint64_t n,
                                                           uint32_t nparts, const uint32_t* __restrict__ table,
-                                                          const uint32_t* const* __restrict__ cols,
-                                                          uint64_t* __restrict__ okeys, uint32_t* const* __restrict__ ocols) {
+                                                          PartCols pc, uint64_t* __restrict__ okeys) {
     __shared__ uint32_t cnt[P_ITEMS][PNW][PMAX];   // (step, wave, dest) counts -> exclusive prefix
     const int w = wave_id(), l = lane_id();
     const uint64_t lt = lanemask_lt();
@@ -116,7 +122,7 @@ __global__ void __launch_bounds__(PB) part_scatter_kernel(const uint64_t* __rest
             uint32_t o = cnt[j][w][dest[j]] + rank[j];
             okeys[o] = key[j];
 #pragma unroll
-            for (int c = 0; c < NC; c++) ocols[c][o] = cols[c][i];
+            for (int c = 0; c < NC; c++) pc.out[c][o] = pc.in[c][i];
         }
     }
 }
@@ -154,14 +160,11 @@ int qe_partition(qe_ctx* c, const uint64_t* keys, uint64_t n, const uint32_t* co
     const uint32_t nb = (uint32_t)((n + PTILE - 1) / PTILE);
     uint32_t* table = dalloc_t<uint32_t>(c, (uint64_t)nb * nparts);
     uint64_t* d_tot = dalloc_t<uint64_t>(c, nparts);
-    const uint32_t** d_cols = (const uint32_t**)dalloc(c, 8 * sizeof(void*));
-    uint32_t** d_ocols = (uint32_t**)(d_cols + 4);
-    const void* hp[8] = {};
+    PartCols pc{};
     for (int i = 0; i < ncols; i++) {
-        hp[i] = cols[i];
-        hp[4 + i] = out_cols[i];
+        pc.in[i] = cols[i];
+        pc.out[i] = out_cols[i];
     }
-    QE_HIP(hipMemcpyAsync(d_cols, hp, sizeof(hp), hipMemcpyHostToDevice, c->stream));
     {
         Timed t(c, "partition", (8.0 + 4.0 * ncols) * 2.0 * n + 8.0 * n);
         hipLaunchKernelGGL(part_count_kernel, dim3(nb), dim3(PB), 0, c->stream, keys, n, nparts, table);
@@ -172,7 +175,7 @@ int qe_partition(qe_ctx* c, const uint64_t* keys, uint64_t n, const uint32_t* co
 #define QE_PS(NC)                                                                                              \
     case NC:                                                                                                   \
         hipLaunchKernelGGL(part_scatter_kernel<NC>, dim3(nb), dim3(PB), 0, c->stream, keys, n, nparts, table, \
-                           d_cols, out_keys, d_ocols);                                                         \
+                           pc, out_keys);                                                                      \
         break;
             QE_PS(0) QE_PS(1) QE_PS(2) QE_PS(3) QE_PS(4)
 #undef QE_PS
@@ -183,7 +186,6 @@ int qe_partition(qe_ctx* c, const uint64_t* keys, uint64_t n, const uint32_t* co
     QE_HIP(hipStreamSynchronize(c->stream));
     dfree(c, table);
     dfree(c, d_tot);
-    dfree(c, (void*)d_cols);
     return 0;
     QE_API_END(c)
 }

@@ -2,9 +2,12 @@
 //
 // merge join (reference join_relations, src/join.c:325-392) on sorted inputs:
 //   mj_partition -- one binary search pair per R tile: the S window [lo, hi) the tile can match
-//   mj_tile<0>   -- per tile: R keys + the S window staged in LDS, each thread walks its 8
-//                   consecutive R keys through the window (merge walk, binary search past 16
-//                   steps), tile match count -> global exclusive scan (tile_scan)
+//   mj_fused     -- per tile: R keys + the S window staged in LDS, each thread bounds its 8
+//                   consecutive R keys' matches with interleaved branchless binary searches,
+//                   block scan, decoupled lookback for the tile's output offset (published
+//                   before the pairs are staged in LDS), one coalesced store of the tile's pairs
+//   mj_tile<0>   -- the same walk, tile match count -> global exclusive scan (tile_scan): the
+//                   exact two-pass form when the output outgrows the single pass's buffers
 //   mj_tile<1>   -- recompute, block scan, then a load-balanced expansion: output slot o of the
 //                   tile finds its R element by binary search over the tile's prefix sums, so
 //                   every write of outR/outS is coalesced whatever the fan-out
@@ -12,6 +15,7 @@
 // Unsorted inputs (possible in the reference's state machine) take
 // seq_merge_kernel, the literal two-pointer loop, so results stay identical there too.
 #include <algorithm>
+#include <cstring>
 
 #include "qe_device.h"
 #include "qe_internal.h"
@@ -22,7 +26,6 @@ constexpr int MJB = 256;
 constexpr int MJ_ITEMS = 8;
 constexpr int MJ_TILE = MJB * MJ_ITEMS;   // 2048 R elements per tile
 constexpr int MJ_WIN = 4096;              // S keys staged in LDS (32 KiB)
-constexpr int MJ_WALK = 16;               // linear steps before falling back to binary search
 
 enum : uint32_t { MJF_R_FANOUT = 1u, MJF_S_DUP = 2u, MJF_ERR = 4u };
 
@@ -78,6 +81,12 @@ __global__ void __launch_bounds__(1024) tile_scan_kernel(uint64_t* __restrict__ 
     }
     if (threadIdx.x == 0) *total = carry;
 }
+
+// S window and output staging are XOR-swizzled: thread t's walk reads S near 8t and its emitted
+// run starts near 8t, so unswizzled the lanes of a wave would hit 4 (u64) / 8 (u32) banks.
+// Both swizzles permute within aligned groups of 8, so linear sweeps stay conflict-free.
+__device__ __forceinline__ uint32_t sw64(uint32_t i) { return i ^ ((i >> 5) & 7u); }
+__device__ __forceinline__ uint32_t sw32(uint32_t o) { return o ^ ((o >> 6) & 7u); }
 
 // R keys live in LDS with one pad slot per 8: thread t walks elements 8t..8t+7, and without the
 // pad the 32 lanes of a ds_read_b64 group would hit 4 banks (8-way conflict)
@@ -145,65 +154,135 @@ __device__ __forceinline__ void mj_stage(MJShared& sh, const uint64_t* rk, uint6
 #pragma unroll
         for (int k = 0; k < SS; k++) {
             uint32_t i = t + k * MJB;
-            if (i < wn) sh.s[i] = ss[k];
+            if (i < wn) sh.s[sw64(i)] = ss[k];
         }
     }
     __syncthreads();
 }
 
-// each thread walks its MJ_ITEMS consecutive R keys through the S window: [lo, hi) per key
-// (merge walk; binary search when a gap or a run is longer than MJ_WALK)
+// each thread finds [lo, hi) in the S window for its MJ_ITEMS consecutive R keys:
+//   1. the thread's range [a, b) = [lower_bound(first key), upper_bound(last key)): two
+//      interleaved binary searches over the window;
+//   2. MJ_ITEMS independent branchless lower-bound searches inside [a, b) -- a few elements for
+//      a balanced join -- all in flight together;
+//   3. upper bounds by MJ_PROBE independent equality probes past each lower bound (a binary
+//      search only for a run of equal S keys longer than that).
+// The walk is VALU-bound (64-bit compares), so the work per key is what this minimises; no
+// divergent walk loop, ~log2(window) + log2(b - a) dependent LDS round trips.
+// IN_LDS is a template parameter on purpose: a run-time choice between sh.s and sk inside the
+// accessor compiles to a pointer select and FLAT loads (global-path latency for LDS data).
+constexpr uint32_t MJ_PROBE = 2;
+template <bool IN_LDS>
+__device__ __forceinline__ uint64_t mj_walk_t(const MJShared& sh, const uint64_t* sk, uint64_t wlo, uint64_t wn64,
+                                              uint32_t tn, uint32_t (&cnt)[MJ_ITEMS],
+                                              uint32_t (&lo_rel)[MJ_ITEMS]) {
+    const uint32_t wn = (uint32_t)wn64;   // window-relative positions: nS < 2^32
+    auto S = [&](uint32_t i) -> uint64_t {
+        if constexpr (IN_LDS) return sh.s[sw64(i)];
+        else return sk[wlo + i];
+    };
+    const uint32_t e0 = threadIdx.x * MJ_ITEMS;
+    const uint32_t nv = tn > e0 ? (tn - e0 < (uint32_t)MJ_ITEMS ? tn - e0 : (uint32_t)MJ_ITEMS) : 0u;
+#pragma unroll
+    for (int j = 0; j < MJ_ITEMS; j++) {
+        cnt[j] = 0;
+        lo_rel[j] = 0;
+    }
+    if (nv == 0) return 0;
+    uint64_t key[MJ_ITEMS];
+#pragma unroll
+    for (int j = 0; j < MJ_ITEMS; j++) key[j] = sh.r[rpad(e0 + ((uint32_t)j < nv ? (uint32_t)j : nv - 1))];
+    const uint64_t klast = key[MJ_ITEMS - 1];   // = the last valid key (padded above)
+    uint32_t a = 0, an = wn, b = 0, bn = wn;
+    while (an | bn) {
+        if (an) {
+            const uint32_t h = an >> 1;
+            if (S(a + h) < key[0]) {
+                a += h + 1;
+                an -= h + 1;
+            } else {
+                an = h;
+            }
+        }
+        if (bn) {
+            const uint32_t h = bn >> 1;
+            if (S(b + h) <= klast) {
+                b += h + 1;
+                bn -= h + 1;
+            } else {
+                bn = h;
+            }
+        }
+    }
+    uint32_t lo[MJ_ITEMS], ln[MJ_ITEMS];
+#pragma unroll
+    for (int j = 0; j < MJ_ITEMS; j++) {
+        lo[j] = a;
+        ln[j] = b - a;
+    }
+    for (uint32_t rem = b - a; rem; rem >>= 1) {   // ceil(log2(b - a + 1)) rounds
+#pragma unroll
+        for (int j = 0; j < MJ_ITEMS; j++) {
+            if (ln[j]) {
+                const uint32_t h = ln[j] >> 1;
+                if (S(lo[j] + h) < key[j]) {
+                    lo[j] += h + 1;
+                    ln[j] -= h + 1;
+                } else {
+                    ln[j] = h;
+                }
+            }
+        }
+    }
+    uint32_t hi[MJ_ITEMS];
+    bool open[MJ_ITEMS];
+#pragma unroll
+    for (int j = 0; j < MJ_ITEMS; j++) {
+        hi[j] = lo[j];
+        open[j] = true;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < MJ_PROBE; q++) {
+#pragma unroll
+        for (int j = 0; j < MJ_ITEMS; j++) {
+            if (open[j]) {
+                if (hi[j] < b && S(hi[j]) == key[j]) hi[j]++;
+                else open[j] = false;
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < MJ_ITEMS; j++) {   // a run longer than the probes: binary search
+        if (open[j] && hi[j] < b && S(hi[j]) == key[j]) {
+            uint32_t hn = b - hi[j];
+            while (hn) {
+                const uint32_t h = hn >> 1;
+                if (S(hi[j] + h) <= key[j]) {
+                    hi[j] += h + 1;
+                    hn -= h + 1;
+                } else {
+                    hn = h;
+                }
+            }
+        }
+    }
+    uint64_t tsum = 0;
+#pragma unroll
+    for (int j = 0; j < MJ_ITEMS; j++) {
+        if ((uint32_t)j < nv) {
+            cnt[j] = hi[j] - lo[j];
+            lo_rel[j] = lo[j];
+            tsum += cnt[j];
+        }
+    }
+    return tsum;
+}
+
 __device__ __forceinline__ uint64_t mj_walk(const MJShared& sh, const uint64_t* sk, uint64_t wlo, uint64_t wn,
                                             uint32_t tn, uint32_t (&cnt)[MJ_ITEMS],
                                             uint32_t (&lo_rel)[MJ_ITEMS]) {
-    const bool in_lds = wn <= MJ_WIN;
-    auto S = [&](uint64_t i) -> uint64_t { return in_lds ? sh.s[i] : sk[wlo + i]; };
-    uint64_t tsum = 0;
-    const uint32_t e0 = threadIdx.x * MJ_ITEMS;
-    uint64_t p = 0;
-    bool have_p = false;
-    uint64_t prev_key = 0, prev_lo = 0, prev_hi = 0;
-#pragma unroll
-    for (int j = 0; j < MJ_ITEMS; j++) {
-        uint32_t e = e0 + j;
-        cnt[j] = 0;
-        lo_rel[j] = 0;
-        if (e >= tn) continue;
-        uint64_t key = sh.r[rpad(e)];
-        uint64_t lo, hi;
-        if (have_p && key == prev_key) {
-            lo = prev_lo;
-            hi = prev_hi;
-        } else {
-            if (!have_p) {
-                lo = lower_bound_f(0, wn, key, S);
-            } else {
-                lo = p;
-                int steps = 0;
-                while (lo < wn && S(lo) < key && steps < MJ_WALK) {
-                    lo++;
-                    steps++;
-                }
-                if (lo < wn && S(lo) < key) lo = lower_bound_f(lo, wn, key, S);
-            }
-            hi = lo;
-            int steps = 0;
-            while (hi < wn && S(hi) == key && steps < MJ_WALK) {
-                hi++;
-                steps++;
-            }
-            if (hi < wn && S(hi) == key) hi = upper_bound_f(hi, wn, key, S);
-            have_p = true;
-            p = hi;
-            prev_key = key;
-            prev_lo = lo;
-            prev_hi = hi;
-        }
-        cnt[j] = (uint32_t)(hi - lo);
-        lo_rel[j] = (uint32_t)lo;
-        tsum += cnt[j];
-    }
-    return tsum;
+    return wn <= MJ_WIN ? mj_walk_t<true>(sh, sk, wlo, wn, tn, cnt, lo_rel)
+                        : mj_walk_t<false>(sh, sk, wlo, wn, tn, cnt, lo_rel);
 }
 
 // per-row match counts, output-distinctness flags, optional driver-count annotation
@@ -258,58 +337,67 @@ __device__ __forceinline__ uint64_t mj_block_scan(MJShared& sh, uint64_t tsum, u
     return inc - tsum + add;
 }
 
-// write the tile's pairs at [gofs, gofs + btotal): a balanced tile (<= 2 pairs per R row) is
-// built in LDS by its threads and stored as one coalesced run; a heavy tile uses a
-// load-balanced expansion (every output slot finds its R row by binary search)
-__device__ __forceinline__ void mj_emit(MJShared& sh, const uint32_t* rv, const uint32_t* sv, uint64_t base,
-                                        uint32_t tn, uint64_t wlo, uint64_t run, uint64_t btotal, uint64_t gofs,
-                                        const uint32_t (&cnt)[MJ_ITEMS], const uint32_t (&lo_rel)[MJ_ITEMS],
-                                        uint32_t* outR, uint32_t* outS) {
+// A balanced tile (<= 2 pairs per R row) builds its pairs in LDS -- tile-local offsets only, so
+// this runs while the tile's lookback is in flight -- and stores them as one coalesced run.
+__device__ __forceinline__ bool mj_balanced(uint64_t btotal) { return btotal <= 2 * (uint64_t)MJ_TILE; }
+
+__device__ __forceinline__ void mj_stage_out(MJShared& sh, const uint32_t* rv, uint64_t base, uint32_t tn,
+                                             uint64_t run, const uint32_t (&cnt)[MJ_ITEMS],
+                                             const uint32_t (&lo_rel)[MJ_ITEMS]) {
     const uint32_t e0 = threadIdx.x * MJ_ITEMS;
-    if (btotal <= 2 * (uint64_t)MJ_TILE) {
-        uint32_t r[MJ_ITEMS];
-        if (rv && e0 + MJ_ITEMS <= tn) {
-            uint4 a = *reinterpret_cast<const uint4*>(rv + base + e0);
-            uint4 b = *reinterpret_cast<const uint4*>(rv + base + e0 + 4);
-            r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = a.w;
-            r[4] = b.x; r[5] = b.y; r[6] = b.z; r[7] = b.w;
-        } else {
+    uint32_t r[MJ_ITEMS];
+    if (rv && e0 + MJ_ITEMS <= tn) {
+        uint4 a = *reinterpret_cast<const uint4*>(rv + base + e0);
+        uint4 b = *reinterpret_cast<const uint4*>(rv + base + e0 + 4);
+        r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = a.w;
+        r[4] = b.x; r[5] = b.y; r[6] = b.z; r[7] = b.w;
+    } else {
 #pragma unroll
-            for (int j = 0; j < MJ_ITEMS; j++)
-                r[j] = e0 + j < tn ? (rv ? rv[base + e0 + j] : (uint32_t)(base + e0 + j)) : 0;
-        }
-#pragma unroll
-        for (int j = 0; j < MJ_ITEMS; j++) {
-            if (e0 + j >= tn) continue;
-            for (uint32_t k = 0; k < cnt[j]; k++) {
-                sh.oR[run + k] = r[j];
-                sh.oS[run + k] = lo_rel[j] + k;   // window-relative; S payloads gathered below
-            }
-            run += cnt[j];
-        }
-        __syncthreads();
-        // four independent S-payload loads in flight per thread per round (the window is read
-        // in order, so each round's loads coalesce)
-        const uint32_t bt = (uint32_t)btotal;
-        for (uint32_t i0 = threadIdx.x; i0 < bt; i0 += 4 * MJB) {
-            uint32_t v[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                uint32_t i = i0 + q * MJB;
-                uint64_t sidx = wlo + (i < bt ? sh.oS[i] : 0);
-                v[q] = i < bt ? (sv ? sv[sidx] : (uint32_t)sidx) : 0;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                uint32_t i = i0 + q * MJB;
-                if (i < bt) {
-                    outR[gofs + i] = sh.oR[i];
-                    outS[gofs + i] = v[q];
-                }
-            }
-        }
-        return;
+        for (int j = 0; j < MJ_ITEMS; j++)
+            r[j] = e0 + j < tn ? (rv ? rv[base + e0 + j] : (uint32_t)(base + e0 + j)) : 0;
     }
+#pragma unroll
+    for (int j = 0; j < MJ_ITEMS; j++) {
+        if (e0 + j >= tn) continue;
+        for (uint32_t k = 0; k < cnt[j]; k++) {
+            const uint32_t o = sw32((uint32_t)run + k);
+            sh.oR[o] = r[j];
+            sh.oS[o] = lo_rel[j] + k;   // window-relative; S payloads gathered at store time
+        }
+        run += cnt[j];
+    }
+}
+
+// after a barrier: [gofs, gofs + btotal) <- the staged pairs, four independent S-payload loads in
+// flight per thread per round (the window is read in order, so each round's loads coalesce)
+__device__ __forceinline__ void mj_store_out(const MJShared& sh, const uint32_t* sv, uint64_t wlo, uint64_t btotal,
+                                             uint64_t gofs, uint32_t* outR, uint32_t* outS) {
+    const uint32_t bt = (uint32_t)btotal;
+    for (uint32_t i0 = threadIdx.x; i0 < bt; i0 += 4 * MJB) {
+        uint32_t v[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            uint32_t i = i0 + q * MJB;
+            uint64_t sidx = wlo + (i < bt ? sh.oS[sw32(i)] : 0);
+            v[q] = i < bt ? (sv ? sv[sidx] : (uint32_t)sidx) : 0;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            uint32_t i = i0 + q * MJB;
+            if (i < bt) {
+                outR[gofs + i] = sh.oR[sw32(i)];
+                outS[gofs + i] = v[q];
+            }
+        }
+    }
+}
+
+// a heavy tile: load-balanced expansion (every output slot finds its R row by binary search)
+__device__ __forceinline__ void mj_emit_heavy(MJShared& sh, const uint32_t* rv, const uint32_t* sv, uint64_t base,
+                                              uint32_t tn, uint64_t wlo, uint64_t run, uint64_t btotal, uint64_t gofs,
+                                              const uint32_t (&cnt)[MJ_ITEMS], const uint32_t (&lo_rel)[MJ_ITEMS],
+                                              uint32_t* outR, uint32_t* outS) {
+    const uint32_t e0 = threadIdx.x * MJ_ITEMS;
 #pragma unroll
     for (int j = 0; j < MJ_ITEMS; j++) {
         uint32_t e = e0 + j;
@@ -360,13 +448,24 @@ __global__ void __launch_bounds__(MJB) mj_tile(const uint64_t* __restrict__ rk, 
         return;
     }
     uint64_t btotal;
-    uint64_t run = mj_block_scan(sh, tsum, &btotal);
-    mj_emit(sh, rv, sv, base, tn, wlo, run, btotal, tile_counts[tile], cnt, lo_rel, outR, outS);
+    uint64_t run = mj_block_scan(sh, tsum, &btotal);   // barrier: the S window is dead
+    const uint64_t gofs = tile_counts[tile];
+    if (mj_balanced(btotal)) {
+        mj_stage_out(sh, rv, base, tn, run, cnt, lo_rel);
+        __syncthreads();
+        mj_store_out(sh, sv, wlo, btotal, gofs, outR, outS);
+    } else {
+        mj_emit_heavy(sh, rv, sv, base, tn, wlo, run, btotal, gofs, cnt, lo_rel, outR, outS);
+    }
 }
 
 // Single-pass form: count, decoupled lookback for the tile's output offset, write -- the keys
 // are read once.  Outputs have room for `cap` pairs; a tile that would overflow writes nothing
 // and the host re-runs the exact two-pass form (tile_counts is filled for it).
+#ifdef QE_DIAG_STAMPS
+__device__ uint64_t g_mj_stamps[STAMP_TILES * STAMP_SLOTS];
+#endif
+
 __global__ void __launch_bounds__(MJB) mj_fused(const uint64_t* __restrict__ rk, const uint32_t* __restrict__ rv,
                                                 uint64_t nR, const uint64_t* __restrict__ sk,
                                                 const uint32_t* __restrict__ sv, uint64_t nS,
@@ -376,21 +475,37 @@ __global__ void __launch_bounds__(MJB) mj_fused(const uint64_t* __restrict__ rk,
                                                 uint64_t* status, uint32_t* ticket, uint32_t epoch, uint32_t ntiles,
                                                 uint64_t* total_out) {
     __shared__ MJShared sh;
+#ifdef QE_DIAG_STAMPS
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint32_t tile = take_ticket(ticket, &sh.ticket);
+#ifdef QE_DIAG_STAMPS
+    if (threadIdx.x == 0 && tile < STAMP_TILES) g_mj_stamps[(uint64_t)tile * STAMP_SLOTS] = t_start;
+#endif
     const uint64_t base = (uint64_t)tile * MJ_TILE;
     const uint32_t tn = (uint32_t)std::min<uint64_t>(MJ_TILE, nR - base);
     const uint64_t wlo = win[2 * tile], wn = win[2 * tile + 1] - wlo;
+    QE_STAMP(g_mj_stamps, tile, 1);
     mj_stage(sh, rk, base, tn, sk, wlo, wn);
+    QE_STAMP(g_mj_stamps, tile, 2);
     uint32_t cnt[MJ_ITEMS], lo_rel[MJ_ITEMS];
     uint64_t tsum = mj_walk(sh, sk, wlo, wn, tn, cnt, lo_rel);
+    QE_STAMP(g_mj_stamps, tile, 6);
     uint32_t f = mj_annotate_rows(sh, rk, rv, nR, base, tn, cnt, match, nullptr);
+    QE_STAMP(g_mj_stamps, tile, 7);
     uint64_t btotal;
-    uint64_t run = mj_block_scan(sh, tsum, &btotal);
+    uint64_t run = mj_block_scan(sh, tsum, &btotal);   // barrier: the S window is dead
+    QE_STAMP(g_mj_stamps, tile, 3);
+    const bool balanced = mj_balanced(btotal);
+#ifndef QE_DIAG_MJ_NOLB
+    if (wave_id() == 0) lookback_publish(status, epoch, tile, btotal);
+#endif
+    if (balanced) mj_stage_out(sh, rv, base, tn, run, cnt, lo_rel);   // overlaps the predecessors
     if (wave_id() == 0) {
 #ifdef QE_DIAG_MJ_NOLB   // ablation only: tile offset = its first R row (in range, wrong when fan-out != 1)
         uint64_t ex = base;
 #else
-        uint64_t ex = lookback_wave(status, epoch, tile, btotal);
+        uint64_t ex = lookback_wait(status, epoch, tile, btotal);
 #endif
         if (lane_id() == 0) {
             sh.excl = ex;
@@ -398,13 +513,18 @@ __global__ void __launch_bounds__(MJB) mj_fused(const uint64_t* __restrict__ rk,
             if (tile == ntiles - 1) *total_out = ex + btotal;
         }
     }
-    mj_publish_flags(sh, f, flags);   // contains the barrier that publishes sh.excl
+    mj_publish_flags(sh, f, flags);   // contains the barrier that publishes sh.excl (and the staging)
+    QE_STAMP(g_mj_stamps, tile, 4);
     const uint64_t gofs = sh.excl;
 #ifdef QE_DIAG_MJ_NOEMIT
     if (gofs + btotal > cap + 1) outR[0] = (uint32_t)run;   // keep the walk alive, store nothing
 #else
-    if (gofs + btotal <= cap) mj_emit(sh, rv, sv, base, tn, wlo, run, btotal, gofs, cnt, lo_rel, outR, outS);
+    if (gofs + btotal <= cap) {
+        if (balanced) mj_store_out(sh, sv, wlo, btotal, gofs, outR, outS);
+        else mj_emit_heavy(sh, rv, sv, base, tn, wlo, run, btotal, gofs, cnt, lo_rel, outR, outS);
+    }
 #endif
+    QE_STAMP(g_mj_stamps, tile, 5);
 }
 
 // The reference's two-pointer loop verbatim (src/join.c:342-377) for inputs that are not
@@ -654,11 +774,11 @@ __global__ void __launch_bounds__(XB) expand_kernel(const uint32_t* __restrict__
     if (btotal <= (uint64_t)X_OUT) {   // typical: the tile's output built in LDS, one coalesced run
 #pragma unroll
         for (int j = 0; j < X_ITEMS; j++) {
-            for (uint32_t q = 0; q < c[j]; q++) sx.out[run + q] = v[j];
+            for (uint32_t q = 0; q < c[j]; q++) sx.out[sw32((uint32_t)run + q)] = v[j];
             run += c[j];
         }
         __syncthreads();
-        for (uint32_t o = threadIdx.x; o < (uint32_t)btotal; o += XB) out[gofs + o] = sx.out[o];
+        for (uint32_t o = threadIdx.x; o < (uint32_t)btotal; o += XB) out[gofs + o] = sx.out[sw32(o)];
         return;
     }
     // heavy tile: run starts + payloads in LDS; output slot o finds its element by a fixed-step
@@ -1120,3 +1240,13 @@ int qe_checksum(qe_ctx* c, qe_col col, const qe_list* rows, uint64_t* sum) {
 }
 
 }  // extern "C"
+
+#ifdef QE_DIAG_STAMPS
+extern "C" int qe_diag_stamps_sort(const char* which, uint64_t* out, uint64_t n);
+// tuning builds only (not part of qe.h): copy the last launch's phase stamps out
+extern "C" int qe_diag_stamps(const char* which, uint64_t* out, uint64_t n) {
+    (void)hipDeviceSynchronize();
+    if (!strcmp(which, "mj")) return hipMemcpyFromSymbol(out, HIP_SYMBOL(qe::g_mj_stamps), n * 8) == hipSuccess ? 0 : -2;
+    return qe_diag_stamps_sort(which, out, n);
+}
+#endif

@@ -131,6 +131,10 @@ struct Field {
     uint64_t kconst;
 };
 
+#ifdef QE_DIAG_STAMPS
+__device__ uint64_t g_sort_stamps[STAMP_TILES * STAMP_SLOTS];
+#endif
+
 template <typename K, int IN, int OUT, bool PACK, int RBITS>
 __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ kin, const uint64_t* __restrict__ win,
                                                         const uint32_t* __restrict__ vin, K* __restrict__ kout,
@@ -147,11 +151,18 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
     __shared__ uint32_t wsum[RNW];
     __shared__ uint32_t s_ticket;
 
+#ifdef QE_DIAG_STAMPS
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint32_t tile = take_ticket(ticket, &s_ticket);
+#ifdef QE_DIAG_STAMPS
+    if (threadIdx.x == 0 && tile < STAMP_TILES) g_sort_stamps[(uint64_t)tile * STAMP_SLOTS] = t_start;
+#endif
     const int w = wave_id(), l = lane_id();
     const uint64_t lt = lanemask_lt();
     for (int i = threadIdx.x; i < RNW * BINS; i += RB) (&whist[0][0])[i] = 0;
     __syncthreads();
+    QE_STAMP(g_sort_stamps, tile, 1);
 
     const uint64_t wave_base = (uint64_t)tile * RTILE + (uint64_t)w * WT;
     uint64_t word[R_ITEMS];
@@ -200,6 +211,7 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
 #endif
     }
     __syncthreads();
+    QE_STAMP(g_sort_stamps, tile, 2);
     // thread t owns digits t*DPT .. t*DPT+DPT-1: totals, exclusive over waves, publish aggregate
     uint32_t tot[DPT], tsum = 0;
 #pragma unroll
@@ -227,6 +239,7 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
         run += tot[q];
     }
     __syncthreads();
+    QE_STAMP(g_sort_stamps, tile, 3);
     // stage the tile in digit order (tile-local offsets only)
 #pragma unroll
     for (int j = 0; j < R_ITEMS; j++) {
@@ -249,7 +262,9 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
 #endif
         gofs[d] = digit_base[d] + (uint32_t)ex - bexcl[d];
     }
+    QE_STAMP(g_sort_stamps, tile, 4);   // thread 0's own digits' lookback done
     __syncthreads();
+    QE_STAMP(g_sort_stamps, tile, 5);   // every digit's lookback done
     const uint64_t tbase = (uint64_t)tile * RTILE;
     const uint32_t tn = (uint32_t)((n - tbase) < (uint64_t)RTILE ? (n - tbase) : (uint64_t)RTILE);
 #pragma unroll
@@ -272,6 +287,7 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
             }
         }
     }
+    QE_STAMP(g_sort_stamps, tile, 6);
 }
 
 // Non-packable pairs (64-bit keys with > 32 varying bits AND a rowid): key and rowid staged
@@ -605,3 +621,10 @@ SortOut radix_sort_u32(qe_ctx* c, const uint32_t* keys, const uint32_t* vals, ui
 }
 
 }  // namespace qe
+
+#ifdef QE_DIAG_STAMPS
+extern "C" int qe_diag_stamps_sort(const char* which, uint64_t* out, uint64_t n) {
+    (void)which;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(qe::g_sort_stamps), n * 8) == hipSuccess ? 0 : -2;
+}
+#endif

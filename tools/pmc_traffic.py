@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""HBM bytes per launch per bench stage from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
+
+    python tools/pmc_traffic.py --fetch DIR --write DIR --out profiles/r01_traffic.json \
+        --command "<the rocprofv3 commands>"
+
+Counters (MI355X_MICROARCH.md, HBM section): FETCH_SIZE / WRITE_SIZE are in KiB and count the
+L2's memory-side requests; on gfx950 FETCH_SIZE reports 1/2 of the bytes of a wide coalesced
+streaming read, so it is doubled here (`fetch_corrected`); WRITE_SIZE is taken as is.  The two
+counters cannot share a pass, hence two runs of the same command.
+
+Kernels are mapped to the stage names libqe's own timers use (bench.py "stages"), so the
+roofline's `traffic` lines up with its `achieved` (same launches, per launch).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import re
+from collections import defaultdict
+
+# demangled kernel name -> bench stage (first match wins)
+STAGES = [
+    (r"radix_pass_kernel<unsigned long, \d, \d, true", "sort_pass_k64v32"),
+    (r"radix_pass_kernel<unsigned int, \d, \d, true", "sort_pass_k32v32"),
+    (r"radix_pass_kernel<unsigned long, \d, \d, false", "sort_pass_k64"),
+    (r"radix_pass_kv_kernel<unsigned long", "sort_pass_k64v32"),
+    (r"radix_pass_kv_kernel<unsigned int", "sort_pass_k32v32"),
+    (r"digit_hist_kernel|digit_scan_kernel", "sort_hist"),
+    (r"key_bits_kernel", "sort_keybits"),
+    (r"mj_fused", "mj_fused"),
+    (r"mj_partition", "mj_partition"),
+    (r"mj_tile<1>", "mj_write"),
+    (r"gather_keys_kernel", "gather_keys"),
+    (r"expand_kernel<1>", "payload_expand"),
+    (r"expand_kernel<0>|tile_scan_kernel", "payload_count"),
+    (r"NonzeroPairsOp", "payload_prune"),
+    (r"nonzero_bitmap_kernel", "payload_bitmap"),
+    (r"FilterScanOp", "filter_scan"),
+    (r"FilterRefineOp", "filter_refine"),
+    (r"ScanJoinOp", "scan_join"),
+    (r"scatter_match_kernel", "driver_scatter"),
+    (r"checksum_kernel", "checksum"),
+    (r"gen_column_kernel", "gen_column"),
+]
+
+
+def stage_of(kname: str):
+    for pat, st in STAGES:
+        if re.search(pat, kname):
+            return st
+    return None
+
+
+def read_counter(d: str, counter: str):
+    """{dispatch_id: (kernel_name, value)} from a rocprofv3 counter_collection csv under d."""
+    files = glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection csv under {d}")
+    out = {}
+    for fn in files:
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                if row.get("Counter_Name") != counter:
+                    continue
+                did = (fn, row.get("Dispatch_Id") or row.get("Correlation_Id"))
+                name = row.get("Kernel_Name", "")
+                v = float(row["Counter_Value"])
+                prev = out.get(did)
+                out[did] = (name, v + (prev[1] if prev else 0.0))   # summed over dimensions
+    return out
+
+
+def per_stage(disp):
+    acc = defaultdict(lambda: [0.0, 0, set()])
+    for name, v in disp.values():
+        st = stage_of(name)
+        if st is None:
+            continue
+        a = acc[st]
+        a[0] += v
+        a[1] += 1
+        a[2].add(re.sub(r"\(.*", "", name)[:120])
+    return acc
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--command", default="")
+    a = ap.parse_args()
+    f = per_stage(read_counter(a.fetch, "FETCH_SIZE"))
+    w = per_stage(read_counter(a.write, "WRITE_SIZE"))
+    kern = {}
+    for st in sorted(set(f) | set(w)):
+        fk, fn, names = f.get(st, [0.0, 0, set()])
+        wk, wn, names2 = w.get(st, [0.0, 0, set()])
+        fpl = fk * 1024.0 / fn if fn else None
+        wpl = wk * 1024.0 / wn if wn else None
+        hbm = (2.0 * fpl if fpl is not None else 0.0) + (wpl or 0.0)
+        kern[st] = {"hbm_bytes_per_launch": round(hbm), "fetch_raw_bytes_per_launch": round(fpl) if fpl else None,
+                    "fetch_corrected_bytes_per_launch": round(2 * fpl) if fpl else None,
+                    "write_bytes_per_launch": round(wpl) if wpl else None, "launches_fetch_pass": fn,
+                    "launches_write_pass": wn, "kernels": sorted(names | names2)}
+    doc = {"command": a.command,
+           "units": "bytes per launch; FETCH_SIZE/WRITE_SIZE KiB x 1024",
+           "correction": "gfx950: FETCH_SIZE x2 (MI355X_MICROARCH.md HBM section); WRITE_SIZE as is",
+           "kernels": kern}
+    with open(a.out, "w") as fo:
+        json.dump(doc, fo, indent=1)
+    for st, k in sorted(kern.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"]):
+        print(f"{st:20s} {k['hbm_bytes_per_launch'] / 1e9:8.3f} GB/launch  (fetch x2 {k['fetch_corrected_bytes_per_launch']}, "
+              f"write {k['write_bytes_per_launch']}, n={k['launches_fetch_pass']})")
+
+
+if __name__ == "__main__":
+    main()

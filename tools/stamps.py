@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""Phase timing of mj_fused / radix_pass_kernel tiles from a -DQE_DIAG_STAMPS build (tuning aid).
+
+    QE_LIB_PATH=.../build/diag/libqe_STAMPS.so python tools/stamps.py [--n 100000000]
+Each tile's thread 0 stamps s_memrealtime (100 MHz) after every barrier-separated phase; this
+prints the mean duration of each phase, the launch span and the mean number of tiles in flight.
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "query-compiler-executor_amd"))
+
+from qe import lib  # noqa: E402
+
+SLOTS = 8
+PHASES = {
+    "mj": ["ticket+win", "stage", "walk+annot+scan", "lookback+flags", "emit"],
+    "sort": ["ticket+zero", "load+rank", "totals+publish+scan", "stage+lookback(t0)", "lookback wait", "write"],
+}
+
+
+def report(ctx, which, ntiles):
+    buf = np.zeros(ntiles * SLOTS, dtype=np.uint64)
+    fn = ctx.lib.qe_diag_stamps
+    fn.argtypes = [C.c_char_p, C.c_void_p, C.c_uint64]
+    rc = fn(which.encode(), buf.ctypes.data, buf.size)
+    assert rc == 0, rc
+    st = buf.reshape(ntiles, SLOTS).astype(np.int64)
+    names = PHASES[which]
+    k = len(names) + 1
+    st = st[:, :k]
+    ok = (st > 0).all(axis=1)
+    st = st[ok]
+    d = np.diff(st, axis=1) * 10.0 / 1000.0   # ticks of 10 ns -> us
+    span = (st[:, -1].max() - st[:, 0].min()) * 10.0 / 1000.0
+    busy = (st[:, -1] - st[:, 0]).sum() * 10.0 / 1000.0
+    print(f"== {which}: {ok.sum()} tiles, span {span:.1f} us, mean tiles in flight {busy / span:.1f}, "
+          f"mean tile {(st[:, -1] - st[:, 0]).mean() * 0.01:.2f} us")
+    for i, nm in enumerate(names):
+        col = d[:, i]
+        print(f"   {nm:24s} mean {col.mean():8.3f} us  p50 {np.median(col):8.3f}  p99 {np.percentile(col, 99):8.3f}")
+
+
+def report_split(ctx, ntiles):
+    """mj only: thread 0's walk end (slot 6) and annotate end (slot 7) inside phase 2->3"""
+    buf = np.zeros(ntiles * SLOTS, dtype=np.uint64)
+    ctx.lib.qe_diag_stamps(b"mj", buf.ctypes.data, buf.size)
+    st = buf.reshape(ntiles, SLOTS).astype(np.int64)
+    ok = (st[:, [2, 6, 7, 3]] > 0).all(axis=1)
+    st = st[ok]
+    for nm, x, y in (("walk (t0)", 2, 6), ("annotate (t0)", 6, 7), ("block scan barrier", 7, 3)):
+        d = (st[:, y] - st[:, x]) * 0.01
+        print(f"   {nm:24s} mean {d.mean():8.3f} us  p50 {np.median(d):8.3f}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=100_000_000)
+    a = ap.parse_args()
+    ctx = lib.Ctx(0)
+    n = a.n
+    kinds = [("mod", n), ("mod", n), ("hi32",)]
+    r0 = ctx.gen_relation(n, kinds, seed=1, gen_rel=0)
+    r1 = ctx.gen_relation(n, kinds, seed=1, gen_rel=1)
+    R = ctx.gather_pairs(ctx.column(r0, 1), None)
+    S = ctx.gather_pairs(ctx.column(r1, 0), None)
+    ctx.sort_pairs(R)
+    ctx.sort_pairs(S)
+    ctx.sync()
+    report(ctx, "sort", (n + 8191) // 8192)   # last pass of S's sort
+    for _ in range(2):
+        x, y = ctx.merge_join(R, S)
+        ctx.sync()
+        ctx.list_free(x)
+        ctx.list_free(y)
+    report(ctx, "mj", (n + 2047) // 2048)
+    report_split(ctx, (n + 2047) // 2048)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
