@@ -165,11 +165,12 @@ __device__ __forceinline__ uint64_t lookback_wave(uint64_t* status, uint32_t epo
 #endif
 constexpr int LB_WIN = QE_LB_WIN;
 __device__ __forceinline__ uint64_t lookback_serial(uint64_t* status, uint32_t epoch, uint32_t tile,
-                                                    uint32_t stride, uint32_t col) {
+                                                    uint32_t stride, uint32_t col, uint32_t* diag = nullptr) {
     uint64_t excl = 0;
     int64_t idx = (int64_t)tile - 1;
-    uint32_t spins = 0;
+    uint32_t spins = 0, rounds = 0;
     while (idx >= 0) {
+        rounds++;
         uint64_t w[LB_WIN];
 #pragma unroll
         for (int q = 0; q < LB_WIN; q++)
@@ -195,6 +196,11 @@ __device__ __forceinline__ uint64_t lookback_serial(uint64_t* status, uint32_t e
             __builtin_amdgcn_s_sleep(1);
             if (++spins > (1u << 24)) break;   // bounded spin: never hang the GPU
         }
+    }
+    if (diag) {   // tuning builds: load rounds, stalled rounds, tiles walked
+        diag[0] = rounds;
+        diag[1] = spins;
+        diag[2] = (uint32_t)((int64_t)tile - 1 - idx);
     }
     return excl;
 }

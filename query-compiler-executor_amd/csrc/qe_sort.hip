@@ -17,7 +17,7 @@
 //                      pairs has no rowid at all).
 //   3. digit_hist   -- one read of the keys builds the histograms of every pass in LDS.
 //   4. digit_scan   -- exclusive scan per pass -> global base offset of each digit.
-//   5. radix_pass   -- per pass: a tile of 256 x ITEMS words is ranked in registers (RBITS
+//   5. radix_pass   -- per pass: a tile of 512 x 16 words is ranked in registers (RBITS
 //                      ballots per element = wave match-any, per-wave LDS counters), staged in
 //                      LDS in digit order, THEN the per-digit decoupled lookback (thread-serial,
 //                      one chain per digit) -- its latency overlaps the staging -- and the tile
@@ -33,10 +33,15 @@ namespace qe {
 constexpr int RB = 256;          // block
 constexpr int RNW = RB / 64;     // waves per block
 #ifndef QE_R_ITEMS
-#define QE_R_ITEMS 32
+#define QE_R_ITEMS 16
 #endif
+#ifndef QE_R_THREADS
+#define QE_R_THREADS 512
+#endif
+constexpr int R_NT = QE_R_THREADS;    // threads per onesweep tile
 constexpr int R_ITEMS = QE_R_ITEMS;   // words per thread per tile
-constexpr int RTILE = RB * R_ITEMS;
+constexpr int RTILE = R_NT * R_ITEMS;
+constexpr int KV_TILE = RB * R_ITEMS;   // radix_pass_kv_kernel: always RB threads
 constexpr int MAX_PASS = 8;
 
 template <typename K>
@@ -135,20 +140,31 @@ struct Field {
 __device__ uint64_t g_sort_stamps[STAMP_TILES * STAMP_SLOTS];
 #endif
 
-template <typename K, int IN, int OUT, bool PACK, int RBITS>
-__global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ kin, const uint64_t* __restrict__ win,
+// One pass over a tile of NT x ITEMS words: rank in registers (RBITS ballots per element = wave
+// match-any, per-wave LDS counters), stage the tile in LDS in digit order, then write it as runs
+// of equal digits.  The tile's global digit offsets come from a per-digit decoupled lookback
+// (thread-serial, one chain per digit; the tile aggregate is published before staging so the
+// chain overlaps it).  `offs` = the pass's digit bases.
+// Measured on MI355X (1e8 pairs, 4 passes): tile size sets the length of each digit's output run
+// (tile / bins words) -- 8192-word tiles beat 4096 by 15 %; 512 threads x 16 beat 256 x 32 by
+// 10 % (twice the waves per CU at the same LDS); a reduce-then-scan variant without lookback
+// (per-tile count pass + scan + scatter) measured equal: its extra read cancels the saving.
+template <typename K, int IN, int OUT, bool PACK, int RBITS, int ITEMS, int NT>
+__global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ kin, const uint64_t* __restrict__ win,
                                                         const uint32_t* __restrict__ vin, K* __restrict__ kout,
                                                         uint64_t* __restrict__ wout, uint32_t* __restrict__ vout,
                                                         uint64_t n, int dsh, uint32_t mask, Field f,
-                                                        const uint32_t* __restrict__ digit_base, uint64_t* status,
+                                                        const uint32_t* __restrict__ offs, uint64_t* status,
                                                         uint32_t* ticket, uint32_t epoch) {
-    constexpr int BINS = 1 << RBITS, DPT = BINS / RB;
-    constexpr int WT = 64 * R_ITEMS;
-    __shared__ uint64_t stage[RTILE];
-    __shared__ uint32_t whist[RNW][BINS];   // per-wave digit counts -> exclusive over waves
+    constexpr int BINS = 1 << RBITS, DPT = BINS >= NT ? BINS / NT : 1;   // digits per thread
+    constexpr int NW = NT / 64;
+    constexpr int TILE = NT * ITEMS, WT = 64 * ITEMS;
+    const bool owner = DPT > 1 || (int)threadIdx.x < BINS;   // this thread owns digits
+    __shared__ uint64_t stage[TILE];
+    __shared__ uint32_t whist[NW][BINS];   // per-wave digit counts -> exclusive over waves
     __shared__ uint32_t bexcl[BINS];        // tile-local exclusive offset of each digit
     __shared__ uint32_t gofs[BINS];         // global position of the digit's run - bexcl
-    __shared__ uint32_t wsum[RNW];
+    __shared__ uint32_t wsum[NW];
     __shared__ uint32_t s_ticket;
 
 #ifdef QE_DIAG_STAMPS
@@ -160,15 +176,15 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
 #endif
     const int w = wave_id(), l = lane_id();
     const uint64_t lt = lanemask_lt();
-    for (int i = threadIdx.x; i < RNW * BINS; i += RB) (&whist[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < NW * BINS; i += NT) (&whist[0][0])[i] = 0;
     __syncthreads();
     QE_STAMP(g_sort_stamps, tile, 1);
 
-    const uint64_t wave_base = (uint64_t)tile * RTILE + (uint64_t)w * WT;
-    uint64_t word[R_ITEMS];
-    uint32_t pos[R_ITEMS];
+    const uint64_t wave_base = (uint64_t)tile * TILE + (uint64_t)w * WT;
+    uint64_t word[ITEMS];
+    uint32_t pos[ITEMS];
 #pragma unroll
-    for (int j = 0; j < R_ITEMS; j++) {
+    for (int j = 0; j < ITEMS; j++) {
         uint64_t i = wave_base + (uint64_t)j * 64 + l;
         bool ok = i < n;
         if (IN == IN_WORD) {
@@ -185,7 +201,7 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
     }
     // stable rank inside the wave: element order is (j, lane)
 #pragma unroll
-    for (int j = 0; j < R_ITEMS; j++) {
+    for (int j = 0; j < ITEMS; j++) {
         uint64_t i = wave_base + (uint64_t)j * 64 + l;
         bool ok = i < n;
         uint32_t d = (uint32_t)(word[j] >> dsh) & mask;
@@ -217,9 +233,11 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
 #pragma unroll
     for (int q = 0; q < DPT; q++) {
         const uint32_t d = threadIdx.x * DPT + q;
+        tot[q] = 0;
+        if (!owner) continue;
         uint32_t t = 0;
 #pragma unroll
-        for (int ww = 0; ww < RNW; ww++) {
+        for (int ww = 0; ww < NW; ww++) {
             uint32_t c = whist[ww][d];
             whist[ww][d] = t;
             t += c;
@@ -235,24 +253,25 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
     for (int ww = 0; ww < w; ww++) run += wsum[ww];
 #pragma unroll
     for (int q = 0; q < DPT; q++) {
-        bexcl[threadIdx.x * DPT + q] = run;
+        if (owner) bexcl[threadIdx.x * DPT + q] = run;
         run += tot[q];
     }
     __syncthreads();
     QE_STAMP(g_sort_stamps, tile, 3);
     // stage the tile in digit order (tile-local offsets only)
 #pragma unroll
-    for (int j = 0; j < R_ITEMS; j++) {
+    for (int j = 0; j < ITEMS; j++) {
         uint64_t i = wave_base + (uint64_t)j * 64 + l;
         if (i < n) {
             uint32_t dd = (uint32_t)(word[j] >> dsh) & mask;
             stage[bexcl[dd] + whist[w][dd] + pos[j]] = word[j];
         }
     }
-    // now the predecessors' counts: by this time most have published their inclusive prefix
 #pragma unroll
     for (int q = 0; q < DPT; q++) {
         const uint32_t d = threadIdx.x * DPT + q;
+        if (!owner) continue;
+        // the predecessors' counts: by this time most have published their inclusive prefix
         uint64_t ex = 0;
 #ifndef QE_DIAG_SORT_NOLB   // ablation only: skip the lookback (output positions are wrong)
         if (tile > 0) {
@@ -260,16 +279,16 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
             st_agent(&status[(uint64_t)tile * BINS + d], lb_word(epoch, LB_FLAG_INC, ex + tot[q]));
         }
 #endif
-        gofs[d] = digit_base[d] + (uint32_t)ex - bexcl[d];
+        gofs[d] = offs[d] + (uint32_t)ex - bexcl[d];
     }
-    QE_STAMP(g_sort_stamps, tile, 4);   // thread 0's own digits' lookback done
+    QE_STAMP(g_sort_stamps, tile, 4);
     __syncthreads();
-    QE_STAMP(g_sort_stamps, tile, 5);   // every digit's lookback done
-    const uint64_t tbase = (uint64_t)tile * RTILE;
-    const uint32_t tn = (uint32_t)((n - tbase) < (uint64_t)RTILE ? (n - tbase) : (uint64_t)RTILE);
+    QE_STAMP(g_sort_stamps, tile, 5);
+    const uint64_t tbase = (uint64_t)tile * TILE;
+    const uint32_t tn = (uint32_t)((n - tbase) < (uint64_t)TILE ? (n - tbase) : (uint64_t)TILE);
 #pragma unroll
-    for (int k = 0; k < R_ITEMS; k++) {
-        uint32_t i = (uint32_t)k * RB + threadIdx.x;
+    for (int k = 0; k < ITEMS; k++) {
+        uint32_t i = (uint32_t)k * NT + threadIdx.x;
         if (i < tn) {
             uint64_t wd = stage[i];
 #ifdef QE_DIAG_SORT_LINEAR   // ablation only: contiguous output instead of the digit scatter
@@ -277,6 +296,7 @@ __global__ void __launch_bounds__(RB) radix_pass_kernel(const K* __restrict__ ki
 #else
             uint32_t p = gofs[(uint32_t)(wd >> dsh) & mask] + i;
 #endif
+            if ((uint64_t)p >= n) continue;   // never taken with consistent offsets; keeps stores in bounds
             if (OUT == OUT_WORD) {
                 wout[p] = wd;
             } else if (PACK) {
@@ -301,8 +321,8 @@ __global__ void __launch_bounds__(RB) radix_pass_kv_kernel(const K* __restrict__
     constexpr int BINS = 256;
     constexpr int WT = 64 * R_ITEMS;
     __shared__ union {
-        K keys[RTILE];
-        uint32_t vals[RTILE];
+        K keys[KV_TILE];
+        uint32_t vals[KV_TILE];
     } stage;
     __shared__ uint32_t whist[RNW][BINS];
     __shared__ uint32_t bexcl[BINS];
@@ -315,7 +335,7 @@ __global__ void __launch_bounds__(RB) radix_pass_kv_kernel(const K* __restrict__
     const uint64_t lt = lanemask_lt();
     for (int i = threadIdx.x; i < RNW * BINS; i += RB) (&whist[0][0])[i] = 0;
     __syncthreads();
-    const uint64_t wave_base = (uint64_t)tile * RTILE + (uint64_t)w * WT;
+    const uint64_t wave_base = (uint64_t)tile * KV_TILE + (uint64_t)w * WT;
     K key[R_ITEMS];
     uint32_t val[R_ITEMS], pos[R_ITEMS];
 #pragma unroll
@@ -381,8 +401,8 @@ __global__ void __launch_bounds__(RB) radix_pass_kv_kernel(const K* __restrict__
     }
     gofs[d] = digit_base[d] + (uint32_t)excl - be;
     __syncthreads();
-    const uint64_t tbase = (uint64_t)tile * RTILE;
-    const uint32_t tn = (uint32_t)((n - tbase) < (uint64_t)RTILE ? (n - tbase) : (uint64_t)RTILE);
+    const uint64_t tbase = (uint64_t)tile * KV_TILE;
+    const uint32_t tn = (uint32_t)((n - tbase) < (uint64_t)KV_TILE ? (n - tbase) : (uint64_t)KV_TILE);
     uint32_t gp[R_ITEMS];
 #pragma unroll
     for (int k = 0; k < R_ITEMS; k++) {
@@ -488,7 +508,8 @@ static SortOut sort_packed(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
         double bytes = (first ? (double)sizeof(K) + 4 : 8.0) * n + (last ? (double)sizeof(K) + 4 : 8.0) * n;
         Timed t(c, name, bytes);
 #define QE_RP(IN, OUT)                                                                                             \
-    hipLaunchKernelGGL((radix_pass_kernel<K, IN, OUT, true, RBITS>), dim3((unsigned)nt), dim3(RB), 0, c->stream,   \
+    hipLaunchKernelGGL((radix_pass_kernel<K, IN, OUT, true, RBITS, R_ITEMS, R_NT>), dim3((unsigned)nt), dim3(R_NT), 0, \
+                       c->stream,                                                                                  \
                        keys, win, vals, kout, wo, vout, n, dsh, pd.mask[p], f, hist + p * BINS, s.status, s.ticket, \
                        s.epoch)
         if (first && last) {
@@ -526,7 +547,7 @@ static SortOut sort_keys_only(qe_ctx* c, const uint64_t* keys, uint64_t n, const
         uint64_t* out = buf[p & 1];
         LBSlot s = lb_acquire(c, nt * BINS);
         Timed t(c, name, 16.0 * n);
-        hipLaunchKernelGGL((radix_pass_kernel<uint64_t, IN_WORD, OUT_WORD, false, RBITS>), dim3((unsigned)nt), dim3(RB),
+        hipLaunchKernelGGL((radix_pass_kernel<uint64_t, IN_WORD, OUT_WORD, false, RBITS, R_ITEMS, R_NT>), dim3((unsigned)nt), dim3(R_NT),
                            0, c->stream, nullptr, in, nullptr, nullptr, out, nullptr, n, pd.shift[p], pd.mask[p], f,
                            hist + p * BINS, s.status, s.ticket, s.epoch);
         QE_HIP(hipGetLastError());
@@ -543,7 +564,7 @@ static SortOut sort_kv_unpacked(qe_ctx* c, const K* keys, const uint32_t* vals, 
                                 const char* name) {
     uint32_t* hist = dalloc_t<uint32_t>(c, (size_t)MAX_PASS * 256);
     hist_and_scan<K, 8>(c, keys, n, pd, hist);
-    const uint64_t nt = (n + RTILE - 1) / RTILE;
+    const uint64_t nt = (n + KV_TILE - 1) / KV_TILE;
     K* kbuf[2] = {dalloc_t<K>(c, n), pd.npass > 1 ? dalloc_t<K>(c, n) : nullptr};
     uint32_t* vbuf[2] = {dalloc_t<uint32_t>(c, n), pd.npass > 1 ? dalloc_t<uint32_t>(c, n) : nullptr};
     const K* kin = keys;

@@ -58,6 +58,20 @@ def report_split(ctx, ntiles):
         print(f"   {nm:24s} mean {d.mean():8.3f} us  p50 {np.median(d):8.3f}")
 
 
+def report_sort_walk(ctx, ntiles):
+    """sort: thread 0 staging vs lookback split, and its lookback walk (rounds, stalls, tiles)"""
+    buf = np.zeros(ntiles * SLOTS, dtype=np.uint64)
+    ctx.lib.qe_diag_stamps(b"sort", buf.ctypes.data, buf.size)
+    st = buf.reshape(ntiles, SLOTS)
+    t = st[1:, :7].astype(np.int64)
+    print(f"   {'staging (t0)':24s} mean {((t[:, 6] - t[:, 3]) * 0.01).mean():8.3f} us")
+    print(f"   {'lookback (t0)':24s} mean {((t[:, 4] - t[:, 6]) * 0.01).mean():8.3f} us")
+    dg = st[1:, 7]
+    rounds, spins, walked = dg >> 40, (dg >> 20) & 0xFFFFF, dg & 0xFFFFF
+    for nm, v in (("rounds", rounds), ("stalled rounds", spins), ("tiles walked", walked)):
+        print(f"   {nm:24s} mean {v.mean():8.2f}  p50 {np.median(v):6.0f}  p99 {np.percentile(v, 99):6.0f}  max {v.max()}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=100_000_000)
@@ -73,6 +87,7 @@ def main():
     ctx.sort_pairs(S)
     ctx.sync()
     report(ctx, "sort", (n + 8191) // 8192)   # last pass of S's sort
+    report_sort_walk(ctx, (n + 8191) // 8192)
     for _ in range(2):
         x, y = ctx.merge_join(R, S)
         ctx.sync()
