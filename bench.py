@@ -159,6 +159,20 @@ def run_single(args):
     rows = ctx.last_result_rows()
     ms = dt / args.steps * 1e3
     value = rows * args.steps / dt
+    # the same query with every intermediate rowid list materialised (QE_DLE=0), for the record
+    dle_env = os.environ.get("QE_DLE")
+    os.environ["QE_DLE"] = "0"
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        out_all, _ = ctx.run(QUERY)
+    ctx.sync()
+    torch.cuda.synchronize()
+    dt_all = time.perf_counter() - t1
+    if dle_env is None:
+        del os.environ["QE_DLE"]
+    else:
+        os.environ["QE_DLE"] = dle_env
     kern = sorted(stats.items(), key=lambda kv: -kv[1]["ms"])
     total_kernel_ms = sum(s["ms"] for _, s in kern) / args.steps
     res = {
@@ -169,7 +183,11 @@ def run_single(args):
         "config": {"workload": "C3: 4-relation chain join R0-R1-R2-R3, 2 filters on R3, %d rows/rel" % args.rows,
                    "query": QUERY.strip(), "rows_per_relation": args.rows, "result_rows": rows,
                    "stdout": out, "executor": "libqe faithful state machine (qe_run_queries)",
+                   "dead_list_elimination": os.environ.get("QE_DLE", "1") != "0",
                    "parallelism": "single GPU"},
+        "all_lists_materialised": {"ms_per_step": round(dt_all / args.steps * 1e3, 3),
+                                   "value": round(rows * args.steps / dt_all, 1),
+                                   "stdout_identical": out_all == out},
         "roofline": roofline(stats, load_traffic()),
         "kernel_ms_per_step": round(total_kernel_ms, 3),
         "stages": {k: {"ms_per_step": round(s["ms"] / args.steps, 3), "launches_per_step": s["launches"] / args.steps,

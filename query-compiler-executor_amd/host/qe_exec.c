@@ -54,7 +54,18 @@ typedef struct {
     int jb_code;
     qe_list** lists;             /* every list made for the current query (freed at its end) */
     size_t nlists, caplists;
+    int dle;                     /* dead-list elimination on (QE_DLE=0 turns it off) */
+    const uint8_t* live;         /* live[b]: binding b is read by a later predicate or a select */
 } exec_t;
+
+/* Dead-list elimination.  fix_all re-materialises every other entry of the entity
+ * (join_payloads, src/join.c:486-505), but an entry whose binding no later predicate and no select
+ * reads is never observed again: its CONTENT is skipped, its LENGTH -- the only thing a later
+ * join_payloads looks at (the |edit| < |last| guard) -- is kept exactly.  Such a list carries
+ * QE_LIST_DEAD (host-only) and no data; reading one is an internal error, not a fallback. */
+#define QE_LIST_DEAD 0x40000000u
+
+static void need_data(exec_t* x, const qe_list* l);
 
 static void fail(exec_t* x, int code, const char* msg) {
     if (msg) fprintf(stderr, "[ERROR] %s\n", msg);
@@ -67,6 +78,10 @@ static void chk(exec_t* x, int rc) {
         fprintf(stderr, "[ERROR] libqe: %s\n", qe_last_error(x->q));
         fail(x, rc, NULL);
     }
+}
+
+static void need_data(exec_t* x, const qe_list* l) {
+    if (l && (l->flags & QE_LIST_DEAD)) fail(x, QE_EINVAL, "internal: a dead-eliminated list was read");
 }
 
 static qe_list* new_list(exec_t* x) {
@@ -155,10 +170,12 @@ typedef struct {
     qe_list* res[2];             /* join_result.results[0/1] */
     qe_pairs* R;                 /* the join inputs, kept for the driver-count fast path */
     qe_pairs* S;
+    const qe_list* src[2];       /* the lists R / S were gathered from (NULL: a base column) */
 } jres_t;
 
 /* allocate_relation (src/join.c:122-142) / allocate_relation_mid_results (src/join.c:96-120) */
 static void gather(exec_t* x, qe_pairs* out, uint64_t relation, uint64_t col, const qe_list* rows) {
+    if (rows) need_data(x, rows);
     chk(x, qe_gather_pairs(x->q, column(x, relation, col), rows, out));
 }
 
@@ -175,38 +192,78 @@ static void fix_all(exec_t* x, const jres_t* jr, exists_t ex, mra_t* M, uint32_t
                     int mode) {
     entity_t* E = M->v[ex.ent];
     qe_list* update = E->e[ex.idx].list;
-    size_t nedit = 0;
+    /* which entries get join_payloads: every other one; with DLE only those still read later */
+    uint8_t* pick = (uint8_t*)calloc(E->n ? E->n : 1, 1);
+    size_t nedit = 0, npick = 0;
+    ptrdiff_t first_edit = -1;
     for (size_t i = 0; i < E->n; i++)
-        if (E->e[i].relation != relR && E->e[i].relation != relS) nedit++;
-    if (nedit) {
-        /* every entry shares (driver, last): one pruning + sort, one expansion per entry */
-        uint64_t rows = rows_of(x, E->e[ex.idx].relation);
-        uint32_t* counts = NULL;
-        chk(x, qe_driver_counts(x->q, jr->R, jr->S, jr->res[0], jr->res[1], mode, rows, &counts));
-        const qe_list** edits = (const qe_list**)malloc(nedit * sizeof(qe_list*));
-        qe_list* outs = (qe_list*)calloc(nedit, sizeof(qe_list));
-        size_t k = 0;
-        for (size_t i = 0; i < E->n; i++)
-            if (E->e[i].relation != relR && E->e[i].relation != relS) edits[k++] = E->e[i].list;
-        int rc = qe_join_payloads_multi(x->q, counts, rows, update, edits, (int)nedit, outs);
-        qe_counts_free(x->q, counts);
-        free(edits);
-        if (rc != 0) {
-            free(outs);
-            if (rc == QE_EINVAL) fail(x, QE_EINVAL, "join_payloads on lists of different lengths (reference-undefined)");
-            chk(x, rc);
+        if (E->e[i].relation != relR && E->e[i].relation != relS) {
+            nedit++;
+            if (first_edit < 0) first_edit = (ptrdiff_t)i;
+            if (!x->dle || x->live[E->e[i].pid]) {
+                pick[i] = 1;
+                npick++;
+            }
         }
-        k = 0;
+    if (nedit) {
+        for (size_t i = 0; i < E->n; i++)   /* join_payloads' guard, on every entry, dead or not */
+            if (E->e[i].relation != relR && E->e[i].relation != relS && E->e[i].list->n < update->n) {
+                free(pick);
+                fail(x, QE_EINVAL, "join_payloads on lists of different lengths (reference-undefined)");
+            }
+        /* join_payloads' output length is the sum over `update` of the driver count.  When the
+         * counts come from the sorted fast path (the other side's rowids distinct) and `update` is
+         * the list this side was gathered from, that sum IS the join's pair count. */
+        const qe_pairs* me = mode == 0 ? jr->R : jr->S;
+        const qe_pairs* other = mode == 0 ? jr->S : jr->R;
+        const int p_known = (me->flags & QE_PAIRS_SORTED) && (other->flags & QE_PAIRS_SORTED) &&
+                            (other->flags & QE_PAIRS_DISTINCT) && jr->src[mode] == update;
+        if (npick == 0 && !p_known) {       /* materialise one entry to learn the length */
+            pick[first_edit] = 1;
+            npick = 1;
+        }
+        uint64_t P = jr->res[0]->n;
+        qe_list* outs = NULL;
+        if (npick) {
+            need_data(x, update);
+            uint64_t rows = rows_of(x, E->e[ex.idx].relation);
+            uint32_t* counts = NULL;
+            chk(x, qe_driver_counts(x->q, jr->R, jr->S, jr->res[0], jr->res[1], mode, rows, &counts));
+            const qe_list** edits = (const qe_list**)malloc(npick * sizeof(qe_list*));
+            outs = (qe_list*)calloc(npick, sizeof(qe_list));
+            size_t k = 0;
+            for (size_t i = 0; i < E->n; i++)
+                if (pick[i]) {
+                    need_data(x, E->e[i].list);
+                    edits[k++] = E->e[i].list;
+                }
+            int rc = qe_join_payloads_multi(x->q, counts, rows, update, edits, (int)npick, outs);
+            qe_counts_free(x->q, counts);
+            free(edits);
+            if (rc != 0) {
+                free(outs);
+                free(pick);
+                if (rc == QE_EINVAL) fail(x, QE_EINVAL, "join_payloads on lists of different lengths (reference-undefined)");
+                chk(x, rc);
+            }
+            P = outs[0].n;
+        }
+        size_t k = 0;
         for (size_t i = 0; i < E->n; i++) {
             mid_t* ed = &E->e[i];
-            if (ed->relation != relR && ed->relation != relS) {
-                qe_list* nl = new_list(x);
+            if (ed->relation == relR || ed->relation == relS) continue;
+            qe_list* nl = new_list(x);
+            if (pick[i]) {
                 *nl = outs[k++];
-                ed->list = nl;
+            } else {
+                nl->n = P;
+                nl->flags = QE_LIST_DEAD;
             }
+            ed->list = nl;
         }
         free(outs);
     }
+    free(pick);
     E->e[ex.idx] = tmp;
 }
 
@@ -253,7 +310,8 @@ static void update_mid_results(exec_t* x, const jres_t* jr, mra_t* M, uint64_t r
 }
 
 /* build_relations (src/join.c:152-292): pick the variant, gather both inputs */
-static int build_relations(exec_t* x, const query_t* q, const pred_t* p, mra_t* M, qe_pairs rel[2]) {
+static int build_relations(exec_t* x, const query_t* q, const pred_t* p, mra_t* M, qe_pairs rel[2],
+                           const qe_list* src[2]) {
     uint64_t lhs_rel = q->rels[p->frel], lhs_col = p->fcol;
     uint64_t rhs_rel = q->rels[p->srel], rhs_col = p->scol;
     if (lhs_rel == rhs_rel && lhs_col == rhs_col) return DO_NOTHING;
@@ -261,14 +319,15 @@ static int build_relations(exec_t* x, const query_t* q, const pred_t* p, mra_t* 
     ptrdiff_t li = relation_exists_current(E, lhs_rel, p->frel);
     ptrdiff_t ri = relation_exists_current(E, rhs_rel, p->srel);
     if (li != -1 && ri == -1) {
-        gather(x, &rel[0], lhs_rel, lhs_col, E->e[li].list);
+        src[0] = E->e[li].list;
+        gather(x, &rel[0], lhs_rel, lhs_col, src[0]);
         exists_t ex = relation_exists(M, rhs_rel, p->srel);
         mid_t* T = NULL;
-        if (ex.idx == -1) gather(x, &rel[1], rhs_rel, rhs_col, NULL);
-        else {
+        if (ex.idx != -1) {
             T = &M->v[ex.ent]->e[ex.idx];
-            gather(x, &rel[1], rhs_rel, rhs_col, T->list);
+            src[1] = T->list;
         }
+        gather(x, &rel[1], rhs_rel, rhs_col, src[1]);
         mid_t* mid = &E->e[li];
         if (!T) {
             if (mid->lcs == (int32_t)lhs_col) return JOIN_SORT_RHS;
@@ -281,19 +340,22 @@ static int build_relations(exec_t* x, const query_t* q, const pred_t* p, mra_t* 
         return CLASSIC_JOIN;
     }
     if (li != -1 && ri != -1) {
-        gather(x, &rel[0], lhs_rel, lhs_col, E->e[li].list);
-        gather(x, &rel[1], rhs_rel, rhs_col, E->e[ri].list);
+        src[0] = E->e[li].list;
+        gather(x, &rel[0], lhs_rel, lhs_col, src[0]);
+        src[1] = E->e[ri].list;
+        gather(x, &rel[1], rhs_rel, rhs_col, src[1]);
         return SCAN_JOIN;
     }
     if (li == -1 && ri != -1) {
-        gather(x, &rel[1], rhs_rel, rhs_col, E->e[ri].list);
+        src[1] = E->e[ri].list;
+        gather(x, &rel[1], rhs_rel, rhs_col, src[1]);
         exists_t ex = relation_exists(M, lhs_rel, p->frel);
         mid_t* T = NULL;
-        if (ex.idx == -1) gather(x, &rel[0], lhs_rel, lhs_col, NULL);
-        else {
+        if (ex.idx != -1) {
             T = &M->v[ex.ent]->e[ex.idx];
-            gather(x, &rel[0], lhs_rel, lhs_col, T->list);
+            src[0] = T->list;
         }
+        gather(x, &rel[0], lhs_rel, lhs_col, src[0]);
         mid_t* mid = &E->e[ri];
         if (!T) {
             if (mid->lcs == (int32_t)rhs_col) return JOIN_SORT_LHS;
@@ -316,11 +378,14 @@ static int build_relations(exec_t* x, const query_t* q, const pred_t* p, mra_t* 
 static int execute_join(exec_t* x, const query_t* q, const pred_t* p, mra_t* M) {
     qe_pairs rel[2];
     memset(rel, 0, sizeof(rel));
-    int v = build_relations(x, q, p, M, rel);
+    const qe_list* src[2] = {NULL, NULL};
+    int v = build_relations(x, q, p, M, rel, src);
     if (v == DO_NOTHING) return 0;
     jres_t jr;
     jr.res[0] = new_list(x);
     jr.res[1] = new_list(x);
+    jr.src[0] = src[0];
+    jr.src[1] = src[1];
     jr.R = &rel[0];
     jr.S = &rel[1];
     switch (v) {
@@ -361,6 +426,7 @@ static int execute_filter(exec_t* x, const query_t* q, const pred_t* p, mra_t* M
     exists_t ex = relation_exists(M, relation, p->frel);
     if (ex.idx != -1) {                                           /* exec_filter_rel_exists */
         qe_list* l = M->v[ex.ent]->e[ex.idx].list;
+        need_data(x, l);
         if (!op_valid(p->op)) {
             if (l->n != 0) {
                 fprintf(stderr, "[ERROR] Wrong operator\n");
@@ -403,6 +469,7 @@ static void print_sums(exec_t* x, const query_t* q, const mra_t* M) {
             fputs("NULL ", x->out);
         } else {
             uint64_t s = 0;
+            need_data(x, l);
             chk(x, qe_checksum(x->q, column(x, relation, colno), l, &s));
             fprintf(x->out, "%lu ", (unsigned long)s);
         }
@@ -549,11 +616,22 @@ static void execute_query(exec_t* x, query_t* q) {
     mra_t M;
     memset(&M, 0, sizeof(M));
     int ok = query_valid(x, q);   /* out-of-range ids are undefined in the reference: no line */
+    uint8_t* live = (uint8_t*)calloc(q->nrels ? q->nrels : 1, 1);
     for (size_t i = 0; ok && i < q->npreds; i++) {
+        /* bindings read after predicate i: later predicates and the selects */
+        memset(live, 0, q->nrels ? q->nrels : 1);
+        for (size_t s = 0; s < q->nsel; s++) live[q->sel[2 * s]] = 1;
+        for (size_t j = i + 1; j < q->npreds; j++) {
+            live[q->preds[j].frel] = 1;
+            if (q->preds[j].type == 0) live[q->preds[j].srel] = 1;
+        }
+        x->live = live;
         const pred_t* p = &q->preds[i];
         int r = p->type == 1 ? execute_filter(x, q, p, &M) : execute_join(x, q, p, &M);
         if (r == -1) ok = 0;
     }
+    x->live = NULL;
+    free(live);
     if (ok) print_sums(x, q, &M);
     mra_free(&M);
     free_lists(x);
@@ -577,6 +655,10 @@ int qe_run_queries(qe_ctx* ctx, const char* text, char** out, size_t* outlen) {
     exec_t x;
     memset(&x, 0, sizeof(x));
     x.q = ctx;
+    {
+        const char* e = getenv("QE_DLE");
+        x.dle = !(e && e[0] == '0');
+    }
     *out = NULL;
     *outlen = 0;
     x.out = open_memstream(out, outlen);

@@ -39,6 +39,16 @@ def test_gpu_executor_matches_reference_golden(ctx, name, idx, ds, case):
     assert rc == case["rc"]
 
 
+def test_gpu_executor_without_dead_list_elimination(ctx, monkeypatch):
+    """QE_DLE=0 materialises every intermediate list, as the reference does: same bytes on every
+    golden (the default run above has dead-list elimination on)."""
+    monkeypatch.setenv("QE_DLE", "0")
+    for name, idx, ds, case in CASES:
+        _load(ctx, ds)
+        out, rc = ctx.run(case["input"])
+        assert (out, rc) == (case["stdout"], case["rc"]), (name, idx, case["input"])
+
+
 @pytest.mark.parametrize("fixture", ["protocol", "known_answers"])
 def test_dropin_binary_matches_reference_golden(fixture):
     doc = goldens.load(os.path.join(goldens.GOLDEN_DIR, f"{fixture}.json"))
