@@ -310,6 +310,210 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
     QE_STAMP(g_sort_stamps, tile, 6);
 }
 
+// ---- two-level sort: 14 high bits by two global passes, the rest inside LDS per bucket ---------
+// For 20..31 varying bits: the top H = 15 bits split the array into 32768 buckets (~4 K words
+// each at 10^8 keys below 10^8 -- keys rarely fill their top bit's range, so H leaves room);
+// two onesweep passes (8 + 7 bits, LSD order) leave it bucket-partitioned and stable; then one
+// workgroup per bucket sorts the bucket's remaining L = bits - 15 bits in LDS (two stable ranking
+// rounds, no lookback: the bucket boundaries come from the histogram) and writes key + rowid
+// coalesced.  64 B per element instead of 80, two lookback passes instead of 4.  A bucket larger
+// than LDS (skew) sends the whole sort back to the plain LSD passes.
+constexpr int TL_H = 15;
+constexpr int TL_BUCKETS = 1 << TL_H;
+#ifndef QE_TL_NT
+#define QE_TL_NT 512
+#endif
+#ifndef QE_TL_ITEMS
+#define QE_TL_ITEMS 10
+#endif
+constexpr int TL_NT = QE_TL_NT, TL_ITEMS = QE_TL_ITEMS, TL_CAP = TL_NT * TL_ITEMS;   // words per bucket in LDS
+
+// histogram of the top TL_H varying bits (bucket id = field >> L)
+template <typename K>
+__global__ void __launch_bounds__(1024) tl_hist_kernel(const K* __restrict__ keys, uint64_t n, Field f, int L,
+                                                       uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[TL_BUCKETS];   // 128 KiB: one block per CU, 16 waves
+    for (int i = threadIdx.x; i < TL_BUCKETS; i += 1024) h[i] = 0;
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * 1024 * 4;
+    for (uint64_t i0 = ((uint64_t)blockIdx.x * 1024 + threadIdx.x) * 4; i0 < n; i0 += stride) {
+        uint64_t k[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) k[q] = i0 + q < n ? (uint64_t)keys[i0 + q] : 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (i0 + q < n) atomicAdd(&h[(uint32_t)((((k[q] >> f.lo) & f.fmask) >> L) & (TL_BUCKETS - 1))], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < TL_BUCKETS; i += 1024)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// one block: bucket starts (exclusive scan, plus the end), the two global passes' digit bases (the
+// histogram's marginals over the low 8 / high 7 bucket bits) and the largest bucket
+__global__ void __launch_bounds__(1024) tl_scan_kernel(const uint32_t* __restrict__ hist, uint32_t* __restrict__ bstart,
+                                                       uint32_t* __restrict__ base1, uint32_t* __restrict__ base2,
+                                                       uint64_t* __restrict__ maxb) {
+    constexpr int PER = TL_BUCKETS / 1024;
+    __shared__ uint32_t h[TL_BUCKETS];
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t c1[256], c2[128];
+    __shared__ uint32_t wmax[16];
+    const int t = threadIdx.x;
+    uint32_t v[PER], mine = 0, mx = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        v[k] = hist[t * PER + k];
+        h[t * PER + k] = v[k];
+        mine += v[k];
+        mx = v[k] > mx ? v[k] : mx;
+    }
+    uint32_t inc = wave_incl_scan_u32(mine);
+    mx = wave_max_u32(mx);
+    if (lane_id() == 63) wsum[wave_id()] = inc;
+    if (lane_id() == 0) wmax[wave_id()] = mx;
+    __syncthreads();
+    uint32_t run = inc - mine;
+    for (int w = 0; w < wave_id(); w++) run += wsum[w];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        bstart[t * PER + k] = run;
+        run += v[k];
+    }
+    if (t == 1023) bstart[TL_BUCKETS] = run;
+    if (t == 0) {
+        uint32_t m = 0;
+        for (int w = 0; w < 16; w++) m = wmax[w] > m ? wmax[w] : m;
+        *maxb = m;
+    }
+    // marginals: pass 1 sorts by the bucket's low 8 bits, pass 2 by its high 7
+    if (t < 256) {
+        uint32_t a = 0;
+        for (int d2 = 0; d2 < 128; d2++) a += h[d2 * 256 + t];
+        c1[t] = a;
+    } else if (t < 384) {
+        const int d2 = t - 256;
+        uint32_t a = 0;
+        for (int d1 = 0; d1 < 256; d1++) a += h[d2 * 256 + d1];
+        c2[d2] = a;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t r1 = 0, r2 = 0;
+        for (int d = 0; d < 256; d++) {
+            base1[d] = r1;
+            r1 += c1[d];
+        }
+        for (int d = 0; d < 256; d++) {
+            base2[d] = r2;
+            r2 += d < 128 ? c2[d] : 0u;
+        }
+    }
+}
+
+// one workgroup per bucket: up to TL_CAP packed words, sorted by the low L bits in LDS.  Each wave
+// owns a contiguous slice of jm x 64 words, jm = ceil(m / (waves x 64)): every wave works and the
+// work is proportional to the bucket, not to TL_CAP.
+template <typename K>
+__global__ void __launch_bounds__(TL_NT) tl_local_kernel(const uint64_t* __restrict__ win, K* __restrict__ kout,
+                                                         uint32_t* __restrict__ vout,
+                                                         const uint32_t* __restrict__ bstart, Field f, int r1,
+                                                         int r2) {
+    constexpr int NW = TL_NT / 64, BINS = 256;
+    __shared__ uint64_t stage[TL_CAP];
+    __shared__ uint32_t whist[NW][BINS];
+    __shared__ uint32_t bexcl[BINS];
+    __shared__ uint32_t wsum[NW];
+    const uint32_t s0 = bstart[blockIdx.x], m = bstart[blockIdx.x + 1] - s0;
+    if (m == 0) return;   // block-uniform
+    const int w = wave_id(), l = lane_id();
+    const uint64_t lt = lanemask_lt();
+    const uint32_t jm = (m + NW * 64 - 1) / (NW * 64);   // <= TL_ITEMS since m <= TL_CAP
+    const uint32_t wbase = (uint32_t)w * jm * 64;
+    uint64_t word[TL_ITEMS];
+#pragma unroll
+    for (int j = 0; j < TL_ITEMS; j++) {
+        const uint32_t i = wbase + (uint32_t)j * 64 + l;
+        word[j] = ((uint32_t)j < jm && i < m) ? win[s0 + i] : 0;
+    }
+    for (int r = 0; r < 2; r++) {
+        const int bits = r == 0 ? r1 : r2;
+        if (bits == 0) break;
+        const int dsh = 32 + (r == 0 ? 0 : r1);
+        const uint32_t mask = (1u << bits) - 1u;
+        for (int i = threadIdx.x; i < NW * BINS; i += TL_NT) (&whist[0][0])[i] = 0;
+        __syncthreads();
+        uint32_t pos[TL_ITEMS];
+#pragma unroll
+        for (int j = 0; j < TL_ITEMS; j++) {   // stable rank inside the wave: (j, lane) order
+            pos[j] = 0;
+            if ((uint32_t)j >= jm) continue;     // wave-uniform
+            const uint32_t i = wbase + (uint32_t)j * 64 + l;
+            const bool ok = i < m;
+            const uint32_t d = (uint32_t)(word[j] >> dsh) & mask;
+            uint64_t peers = __ballot(ok);
+#pragma unroll
+            for (int b = 0; b < 8; b++) {
+                if (b >= bits) break;
+                const bool bit = (d >> b) & 1u;
+                const uint64_t mm = __ballot(bit);
+                peers &= bit ? mm : ~mm;
+            }
+            const int leader = peers ? (__ffsll((unsigned long long)peers) - 1) : 0;
+            uint32_t old = 0;
+            if (ok && l == leader) {
+                old = whist[w][d];
+                whist[w][d] = old + (uint32_t)__popcll(peers);
+            }
+            old = (uint32_t)__shfl((int)old, leader, 64);
+            pos[j] = old + (uint32_t)__popcll(peers & lt);
+        }
+        __syncthreads();
+        uint32_t tot = 0;
+        if (threadIdx.x < BINS) {
+            const uint32_t d = threadIdx.x;
+#pragma unroll
+            for (int ww = 0; ww < NW; ww++) {
+                const uint32_t c = whist[ww][d];
+                whist[ww][d] = tot;
+                tot += c;
+            }
+        }
+        const uint32_t inc = wave_incl_scan_u32(tot);
+        if (l == 63) wsum[w] = inc;
+        __syncthreads();
+        if (threadIdx.x < BINS) {
+            uint32_t ex = inc - tot;
+            for (int ww = 0; ww < w; ww++) ex += wsum[ww];
+            bexcl[threadIdx.x] = ex;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < TL_ITEMS; j++) {
+            const uint32_t i = wbase + (uint32_t)j * 64 + l;
+            if ((uint32_t)j < jm && i < m) {
+                const uint32_t d = (uint32_t)(word[j] >> dsh) & mask;
+                stage[bexcl[d] + whist[w][d] + pos[j]] = word[j];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < TL_ITEMS; j++) {
+            const uint32_t i = wbase + (uint32_t)j * 64 + l;
+            word[j] = ((uint32_t)j < jm && i < m) ? stage[i] : 0;
+        }
+        __syncthreads();   // every read of stage before the next round writes it
+    }
+#pragma unroll
+    for (int j = 0; j < TL_ITEMS; j++) {
+        const uint32_t i = wbase + (uint32_t)j * 64 + l;
+        if ((uint32_t)j < jm && i < m) {
+            kout[s0 + i] = (K)(f.kconst | ((word[j] >> 32) << f.lo));
+            vout[s0 + i] = (uint32_t)word[j];
+        }
+    }
+}
+
 // Non-packable pairs (64-bit keys with > 32 varying bits AND a rowid): key and rowid staged
 // separately.  Kept simple: rare in this workload (never in the measured configs).
 template <typename K, bool VIN>
@@ -533,6 +737,80 @@ static SortOut sort_packed(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
     return SortOut{kout, vout, true, true};
 }
 
+// two-level packed sort (see tl_* kernels); nullopt-style: returns false when a bucket would not
+// fit LDS (skew), after which the caller runs the plain LSD passes
+template <typename K>
+static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint64_t n, int bits, Field f,
+                           const char* name, SortOut* out) {
+    const int L = bits - TL_H;   // 5..16 low bits sorted in LDS
+    const int r1 = L < 8 ? L : 8, r2 = L - r1;
+    uint32_t* hist = dalloc_t<uint32_t>(c, TL_BUCKETS);
+    // digit bases: 256 entries each (the pass kernel reads one per possible 8-bit digit)
+    uint32_t* bstart = dalloc_t<uint32_t>(c, TL_BUCKETS + 1 + 512);
+    uint32_t* base1 = bstart + TL_BUCKETS + 1;
+    uint32_t* base2 = base1 + 256;
+    uint64_t* d_max = c->d_scratch + 34;
+    QE_HIP(hipMemsetAsync(hist, 0, TL_BUCKETS * sizeof(uint32_t), c->stream));
+    {
+        Timed t(c, "sort_hist", (double)sizeof(K) * n);
+        hipLaunchKernelGGL((tl_hist_kernel<K>), dim3(grid_for((n + 3) / 4, 1024, 256)), dim3(1024), 0, c->stream, keys,
+                           n, f, L, hist);
+        QE_HIP(hipGetLastError());
+        hipLaunchKernelGGL(tl_scan_kernel, dim3(1), dim3(1024), 0, c->stream, hist, bstart, base1, base2, d_max);
+        QE_HIP(hipGetLastError());
+    }
+    uint64_t mx = read_u64(c, d_max);
+    if (mx > (uint64_t)TL_CAP) {
+        dfree(c, hist);
+        dfree(c, bstart);
+        return false;
+    }
+    const uint64_t nt = (n + RTILE - 1) / RTILE;
+    uint64_t* w1 = dalloc_t<uint64_t>(c, n);
+    uint64_t* w2 = dalloc_t<uint64_t>(c, n);
+    K* kout = dalloc_t<K>(c, n);
+    uint32_t* vout = dalloc_t<uint32_t>(c, n);
+    for (int p = 0; p < 2; p++) {
+        const int dsh = 32 + L + 8 * p;
+        const uint32_t pmask = p == 0 ? 255u : 127u;
+        LBSlot sl = lb_acquire(c, nt * 256);
+        Timed t(c, name, p == 0 ? ((double)sizeof(K) + 4 + 8) * n : 16.0 * n);
+        if (p == 1)
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_WORD, OUT_WORD, true, 8, R_ITEMS, R_NT>), dim3((unsigned)nt),
+                               dim3(R_NT), 0, c->stream, keys, w1, vals, kout, w2, vout, n, dsh, pmask, f, base2,
+                               sl.status, sl.ticket, sl.epoch);
+        else if (vals)
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV, OUT_WORD, true, 8, R_ITEMS, R_NT>), dim3((unsigned)nt),
+                               dim3(R_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, dsh, pmask, f, base1,
+                               sl.status, sl.ticket, sl.epoch);
+        else
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KIOTA, OUT_WORD, true, 8, R_ITEMS, R_NT>), dim3((unsigned)nt),
+                               dim3(R_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, dsh, pmask, f, base1,
+                               sl.status, sl.ticket, sl.epoch);
+        QE_HIP(hipGetLastError());
+    }
+    {
+        Timed t(c, "sort_local", 8.0 * n + ((double)sizeof(K) + 4) * n);
+        hipLaunchKernelGGL((tl_local_kernel<K>), dim3(TL_BUCKETS), dim3(TL_NT), 0, c->stream, w2, kout, vout, bstart, f,
+                           r1, r2);
+        QE_HIP(hipGetLastError());
+    }
+    dfree(c, w1);
+    dfree(c, w2);
+    dfree(c, hist);
+    dfree(c, bstart);
+    *out = SortOut{kout, vout, true, true};
+    return true;
+}
+
+static bool two_level_on() {
+    static bool on = [] {   // tuning knob: QE_SORT_TWO_LEVEL=0 keeps every pass global
+        const char* s = getenv("QE_SORT_TWO_LEVEL");
+        return !(s && s[0] == '0');
+    }();
+    return on;
+}
+
 // key-only sort of 64-bit words (dedup of packed pairs): the word is the key
 template <int RBITS>
 static SortOut sort_keys_only(qe_ctx* c, const uint64_t* keys, uint64_t n, const PassDesc& pd, const char* name) {
@@ -616,6 +894,13 @@ static SortOut radix_sort_impl(qe_ctx* c, const K* keys, const uint32_t* vals, u
         PassDesc pd = plan_passes(kb[0], kb[1], mb, &width);
         const uint64_t fmask = (1ull << (hi - lo)) - 1;   // hi - lo <= 32 here
         Field f{lo, fmask, kb[1] & ~(fmask << lo)};         // constant key bits come back from the AND
+        // two-level when the buckets can average well under LDS's TL_CAP = 8192 words (the
+        // histogram's maximum decides; a skewed input falls through to the LSD passes)
+        const int nb = hi - lo;
+        if (two_level_on() && nb >= 20 && nb <= TL_H + 16 && n >= (1u << 22) && n <= 4000ull * TL_BUCKETS) {
+            SortOut so2;
+            if (sort_two_level<K>(c, keys, vals, n, nb, f, name, &so2)) return so2;
+        }
         switch (width <= 8 ? 8 : width) {
         case 8: return sort_packed<K, 8>(c, keys, vals, n, pd, f, name);
         case 9: return sort_packed<K, 9>(c, keys, vals, n, pd, f, name);

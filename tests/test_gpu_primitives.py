@@ -110,6 +110,43 @@ def test_sort_pairs_stable(ctx, n, domain):
     ctx.pairs_free(p)
 
 
+def _keys_for(case, n, rng):
+    if case == "27bit":
+        return rng.integers(0, 100_000_000, n, dtype=np.uint64)
+    if case == "20bit":                       # one local ranking round (L = 5)
+        return rng.integers(0, 1 << 20, n, dtype=np.uint64)
+    if case == "31bit":                       # L = 16: two full 8-bit local rounds
+        return rng.integers(0, 1 << 31, n, dtype=np.uint64)
+    if case == "19bit":                       # below the two-level range: plain LSD
+        return rng.integers(0, 1 << 19, n, dtype=np.uint64)
+    if case == "const_hi":                    # constant high bits restored from the AND
+        return (np.uint64(1 << 40) | rng.integers(0, 1 << 25, n, dtype=np.uint64)).astype(np.uint64)
+    if case == "stride8":                     # varying bits start at bit 3
+        return (rng.integers(0, 1 << 24, n, dtype=np.uint64) << np.uint64(3)).astype(np.uint64)
+    if case == "skew":                        # one key holds half the rows: a bucket overflows LDS
+        k = rng.integers(0, 100_000_000, n, dtype=np.uint64)
+        k[rng.random(n) < 0.5] = 77_777_777
+        return k
+    raise ValueError(case)
+
+
+@pytest.mark.parametrize("case", ["27bit", "20bit", "31bit", "19bit", "const_hi", "stride8", "skew"])
+def test_sort_pairs_two_level_sizes(ctx, case):
+    """n >= 2^22 takes the two-level sort (15 high bits by global passes, the rest in LDS per
+    bucket) when 20..31 bits vary; skew or fewer bits fall back to the LSD passes."""
+    n = 5_000_000
+    rng = np.random.default_rng(len(case))
+    k = _keys_for(case, n, rng)
+    v = rng.permutation(n).astype(np.uint32)
+    p = ctx.pairs_from_host(k, v)
+    ctx.sort_pairs(p)
+    gk, gv = ctx.pairs_to_host(p)
+    order = np.argsort(k, kind="stable")
+    np.testing.assert_array_equal(gk, k[order])
+    np.testing.assert_array_equal(gv, v[order])
+    ctx.pairs_free(p)
+
+
 def test_sort_base_column_generates_rowids(ctx):
     a = dg.column(5, 0, 0, 123_457, ("mod", 50_000))
     col = _col(ctx, a)
@@ -233,7 +270,7 @@ def _ref_join_payloads(counts, last, edit):
     return np.repeat(e, counts[l]).astype(np.uint32)
 
 
-@pytest.mark.parametrize("n", [0, 1, 1000, 300_000])
+@pytest.mark.parametrize("n", [0, 1, 1000, 300_000, 6_000_000])
 def test_join_payloads(ctx, n):
     rng = np.random.default_rng(n)
     rows = max(1, n // 2)
