@@ -92,17 +92,24 @@ __device__ __forceinline__ uint32_t sw32(uint32_t o) { return o ^ ((o >> 6) & 7u
 // pad the 32 lanes of a ds_read_b64 group would hit 4 banks (8-way conflict)
 __device__ __forceinline__ uint32_t rpad(uint32_t e) { return e + (e >> 3); }
 
-struct MJShared {
-    uint64_t r[MJ_TILE + MJ_TILE / 8];
+// KT = uint64_t: keys as they are.  KT = uint32_t: key - (the tile's first R key): every key a tile
+// touches lies in [first R key, last R key] (the S window is bounded by those), so when R's
+// varying bits are all below bit 32 the tile works on 32-bit offsets -- one-op compares in the
+// VALU-bound walk, half the LDS bytes, and (with a 1.5x output stage) 4 workgroups per CU.
+template <typename KT, int OUTCAP>
+struct MJSharedG {
+    using Key = KT;
+    static constexpr int kOutCap = OUTCAP;   // pairs a balanced tile stages in LDS
+    KT r[MJ_TILE + MJ_TILE / 8];
     union {                       // the S window is dead once every thread has walked (a barrier
-        uint64_t s[MJ_WIN];       // separates the walk from the emission's use of the space)
+        KT s[MJ_WIN];             // separates the walk from the emission's use of the space)
         struct {
             uint32_t lo[MJ_TILE];     // window-relative S start per R element
             uint32_t off[MJ_TILE];    // tile-relative output offset per R element
         };
         struct {
-            uint32_t oR[2 * MJ_TILE];   // a balanced tile's pairs, staged for coalesced stores
-            uint32_t oS[2 * MJ_TILE];
+            uint32_t oR[OUTCAP];      // a balanced tile's pairs, staged for coalesced stores
+            uint32_t oS[OUTCAP];
         };
     };
     uint64_t red[MJB / 64];
@@ -110,12 +117,23 @@ struct MJShared {
     uint32_t flag;
     uint32_t ticket;
 };
+using MJShared64 = MJSharedG<uint64_t, 2 * MJ_TILE>;
+using MJShared32 = MJSharedG<uint32_t, 3 * MJ_TILE / 2>;
+
+// bank swizzle of the S window for the key width (sw64: u64 slots, sw32: u32 slots)
+template <typename KT>
+__device__ __forceinline__ uint32_t swz(uint32_t i) {
+    if constexpr (sizeof(KT) == 8) return sw64(i);
+    else return sw32(i);
+}
 
 // stage the tile's R keys and (when it fits) its S window in LDS.  Every load of the tile is
 // issued before the first LDS store: 24 independent loads in flight per thread instead of one
 // (a load -> store loop leaves ~6 KB in flight per CU, a quarter of what HBM needs).
-__device__ __forceinline__ void mj_stage(MJShared& sh, const uint64_t* rk, uint64_t base, uint32_t tn,
-                                         const uint64_t* sk, uint64_t wlo, uint64_t wn) {
+template <class SH>
+__device__ __forceinline__ void mj_stage(SH& sh, const uint64_t* rk, uint64_t base, uint32_t tn,
+                                         const uint64_t* sk, uint64_t wlo, uint64_t wn, uint64_t kbase) {
+    using KT = typename SH::Key;
     if (threadIdx.x == 0) sh.flag = 0;
     constexpr int RS = MJ_TILE / MJB, SS = MJ_WIN / MJB;
     uint64_t rr[RS], ss[SS];
@@ -147,14 +165,14 @@ __device__ __forceinline__ void mj_stage(MJShared& sh, const uint64_t* rk, uint6
 #pragma unroll
     for (int k = 0; k < RS / 2; k++) {
         uint32_t i = 2 * (t + k * MJB);
-        if (i < tn) sh.r[rpad(i)] = rr[2 * k];
-        if (i + 1 < tn) sh.r[rpad(i + 1)] = rr[2 * k + 1];
+        if (i < tn) sh.r[rpad(i)] = (KT)(rr[2 * k] - kbase);
+        if (i + 1 < tn) sh.r[rpad(i + 1)] = (KT)(rr[2 * k + 1] - kbase);
     }
     if (sw) {
 #pragma unroll
         for (int k = 0; k < SS; k++) {
             uint32_t i = t + k * MJB;
-            if (i < wn) sh.s[sw64(i)] = ss[k];
+            if (i < wn) sh.s[swz<KT>(i)] = (KT)(ss[k] - kbase);
         }
     }
     __syncthreads();
@@ -172,14 +190,15 @@ __device__ __forceinline__ void mj_stage(MJShared& sh, const uint64_t* rk, uint6
 // IN_LDS is a template parameter on purpose: a run-time choice between sh.s and sk inside the
 // accessor compiles to a pointer select and FLAT loads (global-path latency for LDS data).
 constexpr uint32_t MJ_PROBE = 2;
-template <bool IN_LDS>
-__device__ __forceinline__ uint64_t mj_walk_t(const MJShared& sh, const uint64_t* sk, uint64_t wlo, uint64_t wn64,
-                                              uint32_t tn, uint32_t (&cnt)[MJ_ITEMS],
+template <bool IN_LDS, class SH>
+__device__ __forceinline__ uint64_t mj_walk_t(const SH& sh, const uint64_t* sk, uint64_t wlo, uint64_t wn64,
+                                              uint32_t tn, uint64_t kbase, uint32_t (&cnt)[MJ_ITEMS],
                                               uint32_t (&lo_rel)[MJ_ITEMS]) {
+    using KT = typename SH::Key;
     const uint32_t wn = (uint32_t)wn64;   // window-relative positions: nS < 2^32
-    auto S = [&](uint32_t i) -> uint64_t {
-        if constexpr (IN_LDS) return sh.s[sw64(i)];
-        else return sk[wlo + i];
+    auto S = [&](uint32_t i) -> KT {
+        if constexpr (IN_LDS) return sh.s[swz<KT>(i)];
+        else return (KT)(sk[wlo + i] - kbase);
     };
     const uint32_t e0 = threadIdx.x * MJ_ITEMS;
     const uint32_t nv = tn > e0 ? (tn - e0 < (uint32_t)MJ_ITEMS ? tn - e0 : (uint32_t)MJ_ITEMS) : 0u;
@@ -189,10 +208,10 @@ __device__ __forceinline__ uint64_t mj_walk_t(const MJShared& sh, const uint64_t
         lo_rel[j] = 0;
     }
     if (nv == 0) return 0;
-    uint64_t key[MJ_ITEMS];
+    KT key[MJ_ITEMS];
 #pragma unroll
     for (int j = 0; j < MJ_ITEMS; j++) key[j] = sh.r[rpad(e0 + ((uint32_t)j < nv ? (uint32_t)j : nv - 1))];
-    const uint64_t klast = key[MJ_ITEMS - 1];   // = the last valid key (padded above)
+    const KT klast = key[MJ_ITEMS - 1];   // = the last valid key (padded above)
     uint32_t a = 0, an = wn, b = 0, bn = wn;
     while (an | bn) {
         if (an) {
@@ -278,16 +297,18 @@ __device__ __forceinline__ uint64_t mj_walk_t(const MJShared& sh, const uint64_t
     return tsum;
 }
 
-__device__ __forceinline__ uint64_t mj_walk(const MJShared& sh, const uint64_t* sk, uint64_t wlo, uint64_t wn,
-                                            uint32_t tn, uint32_t (&cnt)[MJ_ITEMS],
+template <class SH>
+__device__ __forceinline__ uint64_t mj_walk(const SH& sh, const uint64_t* sk, uint64_t wlo, uint64_t wn,
+                                            uint32_t tn, uint64_t kbase, uint32_t (&cnt)[MJ_ITEMS],
                                             uint32_t (&lo_rel)[MJ_ITEMS]) {
-    return wn <= MJ_WIN ? mj_walk_t<true>(sh, sk, wlo, wn, tn, cnt, lo_rel)
-                        : mj_walk_t<false>(sh, sk, wlo, wn, tn, cnt, lo_rel);
+    return wn <= MJ_WIN ? mj_walk_t<true>(sh, sk, wlo, wn, tn, kbase, cnt, lo_rel)
+                        : mj_walk_t<false>(sh, sk, wlo, wn, tn, kbase, cnt, lo_rel);
 }
 
 // per-row match counts, output-distinctness flags, optional driver-count annotation
-__device__ __forceinline__ uint32_t mj_annotate_rows(const MJShared& sh, const uint64_t* rk, const uint32_t* rv,
-                                                     uint64_t nR, uint64_t base, uint32_t tn,
+template <class SH>
+__device__ __forceinline__ uint32_t mj_annotate_rows(const SH& sh, const uint64_t* rk, const uint32_t* rv,
+                                                     uint64_t nR, uint64_t base, uint32_t tn, uint64_t kbase,
                                                      const uint32_t (&cnt)[MJ_ITEMS], uint32_t* match,
                                                      uint32_t* annot) {
     uint32_t myflag = 0;
@@ -305,8 +326,8 @@ __device__ __forceinline__ uint32_t mj_annotate_rows(const MJShared& sh, const u
         if (c > 1) myflag |= MJF_R_FANOUT;
         if (match && !full) match[base + e] = c;
         if (c > 0) {
-            uint64_t key = sh.r[rpad(e)];
-            uint64_t nxt = e + 1 < tn ? sh.r[rpad(e + 1)] : (base + e + 1 < nR ? rk[base + e + 1] : ~key);
+            const uint64_t key = kbase + sh.r[rpad(e)];   // back to the full key
+            const uint64_t nxt = e + 1 < tn ? kbase + sh.r[rpad(e + 1)] : (base + e + 1 < nR ? rk[base + e + 1] : ~key);
             if (nxt == key) myflag |= MJF_S_DUP;
             if (annot) annot[rv ? rv[base + e] : (uint32_t)(base + e)] = c;
         }
@@ -314,7 +335,8 @@ __device__ __forceinline__ uint32_t mj_annotate_rows(const MJShared& sh, const u
     return myflag;
 }
 
-__device__ __forceinline__ void mj_publish_flags(MJShared& sh, uint32_t myflag, uint32_t* flags) {
+template <class SH>
+__device__ __forceinline__ void mj_publish_flags(SH& sh, uint32_t myflag, uint32_t* flags) {
     if (myflag) atomicOr(&sh.flag, myflag);
     __syncthreads();
     if (threadIdx.x == 0 && sh.flag) {
@@ -324,7 +346,8 @@ __device__ __forceinline__ void mj_publish_flags(MJShared& sh, uint32_t myflag, 
 }
 
 // block-exclusive offsets of the per-thread sums; returns this thread's start, sets *btotal
-__device__ __forceinline__ uint64_t mj_block_scan(MJShared& sh, uint64_t tsum, uint64_t* btotal) {
+template <class SH>
+__device__ __forceinline__ uint64_t mj_block_scan(SH& sh, uint64_t tsum, uint64_t* btotal) {
     uint64_t inc = wave_incl_scan_u64(tsum);
     if (lane_id() == 63) sh.red[wave_id()] = inc;
     __syncthreads();
@@ -337,11 +360,14 @@ __device__ __forceinline__ uint64_t mj_block_scan(MJShared& sh, uint64_t tsum, u
     return inc - tsum + add;
 }
 
-// A balanced tile (<= 2 pairs per R row) builds its pairs in LDS -- tile-local offsets only, so
-// this runs while the tile's lookback is in flight -- and stores them as one coalesced run.
-__device__ __forceinline__ bool mj_balanced(uint64_t btotal) { return btotal <= 2 * (uint64_t)MJ_TILE; }
+// A balanced tile (pairs fit the LDS output stage: 2 per R row for u64 keys, 1.5 for u32) builds
+// its pairs in LDS -- tile-local offsets only, so this runs while the tile's lookback is in
+// flight -- and stores them as one coalesced run.
+template <class SH>
+__device__ __forceinline__ bool mj_balanced(uint64_t btotal) { return btotal <= (uint64_t)SH::kOutCap; }
 
-__device__ __forceinline__ void mj_stage_out(MJShared& sh, const uint32_t* rv, uint64_t base, uint32_t tn,
+template <class SH>
+__device__ __forceinline__ void mj_stage_out(SH& sh, const uint32_t* rv, uint64_t base, uint32_t tn,
                                              uint64_t run, const uint32_t (&cnt)[MJ_ITEMS],
                                              const uint32_t (&lo_rel)[MJ_ITEMS]) {
     const uint32_t e0 = threadIdx.x * MJ_ITEMS;
@@ -370,7 +396,8 @@ __device__ __forceinline__ void mj_stage_out(MJShared& sh, const uint32_t* rv, u
 
 // after a barrier: [gofs, gofs + btotal) <- the staged pairs, four independent S-payload loads in
 // flight per thread per round (the window is read in order, so each round's loads coalesce)
-__device__ __forceinline__ void mj_store_out(const MJShared& sh, const uint32_t* sv, uint64_t wlo, uint64_t btotal,
+template <class SH>
+__device__ __forceinline__ void mj_store_out(const SH& sh, const uint32_t* sv, uint64_t wlo, uint64_t btotal,
                                              uint64_t gofs, uint32_t* outR, uint32_t* outS) {
     const uint32_t bt = (uint32_t)btotal;
     for (uint32_t i0 = threadIdx.x; i0 < bt; i0 += 4 * MJB) {
@@ -393,7 +420,8 @@ __device__ __forceinline__ void mj_store_out(const MJShared& sh, const uint32_t*
 }
 
 // a heavy tile: load-balanced expansion (every output slot finds its R row by binary search)
-__device__ __forceinline__ void mj_emit_heavy(MJShared& sh, const uint32_t* rv, const uint32_t* sv, uint64_t base,
+template <class SH>
+__device__ __forceinline__ void mj_emit_heavy(SH& sh, const uint32_t* rv, const uint32_t* sv, uint64_t base,
                                               uint32_t tn, uint64_t wlo, uint64_t run, uint64_t btotal, uint64_t gofs,
                                               const uint32_t (&cnt)[MJ_ITEMS], const uint32_t (&lo_rel)[MJ_ITEMS],
                                               uint32_t* outR, uint32_t* outS) {
@@ -431,16 +459,16 @@ __global__ void __launch_bounds__(MJB) mj_tile(const uint64_t* __restrict__ rk, 
                                                uint32_t* __restrict__ outR, uint32_t* __restrict__ outS,
                                                uint32_t* __restrict__ flags, uint32_t* __restrict__ annot,
                                                uint32_t* __restrict__ match) {
-    __shared__ MJShared sh;
+    __shared__ MJShared64 sh;
     const uint32_t tile = blockIdx.x;
     const uint64_t base = (uint64_t)tile * MJ_TILE;
     const uint32_t tn = (uint32_t)std::min<uint64_t>(MJ_TILE, nR - base);
     const uint64_t wlo = win[2 * tile], wn = win[2 * tile + 1] - wlo;
-    mj_stage(sh, rk, base, tn, sk, wlo, wn);
+    mj_stage(sh, rk, base, tn, sk, wlo, wn, 0);
     uint32_t cnt[MJ_ITEMS], lo_rel[MJ_ITEMS];
-    uint64_t tsum = mj_walk(sh, sk, wlo, wn, tn, cnt, lo_rel);
+    uint64_t tsum = mj_walk(sh, sk, wlo, wn, tn, 0, cnt, lo_rel);
     if (!WRITE) {
-        uint32_t f = mj_annotate_rows(sh, rk, rv, nR, base, tn, cnt, match, annot);
+        uint32_t f = mj_annotate_rows(sh, rk, rv, nR, base, tn, 0, cnt, match, annot);
         uint64_t s = wave_sum_u64(tsum);
         if (lane_id() == 0) sh.red[wave_id()] = s;
         mj_publish_flags(sh, f, flags);   // contains the barrier
@@ -450,7 +478,7 @@ __global__ void __launch_bounds__(MJB) mj_tile(const uint64_t* __restrict__ rk, 
     uint64_t btotal;
     uint64_t run = mj_block_scan(sh, tsum, &btotal);   // barrier: the S window is dead
     const uint64_t gofs = tile_counts[tile];
-    if (mj_balanced(btotal)) {
+    if (mj_balanced<MJShared64>(btotal)) {
         mj_stage_out(sh, rv, base, tn, run, cnt, lo_rel);
         __syncthreads();
         mj_store_out(sh, sv, wlo, btotal, gofs, outR, outS);
@@ -466,6 +494,7 @@ __global__ void __launch_bounds__(MJB) mj_tile(const uint64_t* __restrict__ rk, 
 __device__ uint64_t g_mj_stamps[STAMP_TILES * STAMP_SLOTS];
 #endif
 
+template <class SH>
 __global__ void __launch_bounds__(MJB) mj_fused(const uint64_t* __restrict__ rk, const uint32_t* __restrict__ rv,
                                                 uint64_t nR, const uint64_t* __restrict__ sk,
                                                 const uint32_t* __restrict__ sv, uint64_t nS,
@@ -474,7 +503,7 @@ __global__ void __launch_bounds__(MJB) mj_fused(const uint64_t* __restrict__ rk,
                                                 uint32_t* __restrict__ outS, uint64_t cap, uint32_t* __restrict__ flags,
                                                 uint64_t* status, uint32_t* ticket, uint32_t epoch, uint32_t ntiles,
                                                 uint64_t* total_out) {
-    __shared__ MJShared sh;
+    __shared__ SH sh;
 #ifdef QE_DIAG_STAMPS
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -485,18 +514,19 @@ __global__ void __launch_bounds__(MJB) mj_fused(const uint64_t* __restrict__ rk,
     const uint64_t base = (uint64_t)tile * MJ_TILE;
     const uint32_t tn = (uint32_t)std::min<uint64_t>(MJ_TILE, nR - base);
     const uint64_t wlo = win[2 * tile], wn = win[2 * tile + 1] - wlo;
+    const uint64_t kbase = sizeof(typename SH::Key) == 8 ? 0 : rk[base];   // the tile's first key
     QE_STAMP(g_mj_stamps, tile, 1);
-    mj_stage(sh, rk, base, tn, sk, wlo, wn);
+    mj_stage(sh, rk, base, tn, sk, wlo, wn, kbase);
     QE_STAMP(g_mj_stamps, tile, 2);
     uint32_t cnt[MJ_ITEMS], lo_rel[MJ_ITEMS];
-    uint64_t tsum = mj_walk(sh, sk, wlo, wn, tn, cnt, lo_rel);
+    uint64_t tsum = mj_walk(sh, sk, wlo, wn, tn, kbase, cnt, lo_rel);
     QE_STAMP(g_mj_stamps, tile, 6);
-    uint32_t f = mj_annotate_rows(sh, rk, rv, nR, base, tn, cnt, match, nullptr);
+    uint32_t f = mj_annotate_rows(sh, rk, rv, nR, base, tn, kbase, cnt, match, nullptr);
     QE_STAMP(g_mj_stamps, tile, 7);
     uint64_t btotal;
     uint64_t run = mj_block_scan(sh, tsum, &btotal);   // barrier: the S window is dead
     QE_STAMP(g_mj_stamps, tile, 3);
-    const bool balanced = mj_balanced(btotal);
+    const bool balanced = mj_balanced<SH>(btotal);
 #ifndef QE_DIAG_MJ_NOLB
     if (wave_id() == 0) lookback_publish(status, epoch, tile, btotal);
 #endif
@@ -874,8 +904,17 @@ void merge_sorted(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_l
     {
         LBSlot s = lb_acquire(c, nt);
         Timed t(c, "mj_fused", 12.0 * nR + 12.0 * nS + 4.0 * nR);   // + 8 B per pair, added below
-        hipLaunchKernelGGL(mj_fused, dim3(nt), dim3(MJB), 0, c->stream, R->key, R->val, nR, S->key, S->val, nS, win, tc,
-                           R->match, oR, oS, cap, d_flags, s.status, s.ticket, s.epoch, nt, c->d_scratch + 17);
+        // 32-bit tile offsets when R's keys vary only below bit 32 (known from the producer's
+        // OR / AND): every key a tile compares then differs from its first R key by < 2^32
+        const bool key32 = (R->flags & QE_PAIRS_BITS) && ((R->kor & ~R->kand) >> 32) == 0;
+        if (key32)
+            hipLaunchKernelGGL(mj_fused<MJShared32>, dim3(nt), dim3(MJB), 0, c->stream, R->key, R->val, nR, S->key,
+                               S->val, nS, win, tc, R->match, oR, oS, cap, d_flags, s.status, s.ticket, s.epoch, nt,
+                               c->d_scratch + 17);
+        else
+            hipLaunchKernelGGL(mj_fused<MJShared64>, dim3(nt), dim3(MJB), 0, c->stream, R->key, R->val, nR, S->key,
+                               S->val, nS, win, tc, R->match, oR, oS, cap, d_flags, s.status, s.ticket, s.epoch, nt,
+                               c->d_scratch + 17);
         QE_HIP(hipGetLastError());
     }
     uint64_t h[2];
