@@ -15,7 +15,14 @@
 
 namespace qe {
 
-constexpr int CB = 256;   // block
+#ifndef QE_CB
+#define QE_CB 512
+#endif
+#ifndef QE_FS_ITEMS
+#define QE_FS_ITEMS 8
+#endif
+constexpr int CB = QE_CB;   // block
+constexpr int FS_ITEMS = QE_FS_ITEMS;   // filter scan: steps of 2 x CB rows per tile
 constexpr int CNW = CB / 64;
 
 enum { OP_EQ = 0, OP_GT = 1, OP_LT = 2 };
@@ -118,6 +125,10 @@ struct NonzeroPairsOp {        // join_payloads: keep (last[i], edit[i] or i) wh
 };
 
 // ---- the kernel -------------------------------------------------------------------------------
+#ifdef QE_DIAG_STAMPS
+__device__ uint64_t g_cp_stamps[STAMP_TILES * STAMP_SLOTS];
+#endif
+
 template <int ITEMS, int NOUT, class Op>
 __global__ void __launch_bounds__(CB) compact_kernel(Op op, uint64_t n, uint32_t ntiles, uint64_t* status,
                                                      uint32_t* ticket, uint32_t epoch, uint32_t* __restrict__ out0,
@@ -131,7 +142,14 @@ __global__ void __launch_bounds__(CB) compact_kernel(Op op, uint64_t n, uint32_t
     __shared__ uint64_t s_excl;
     __shared__ uint32_t s_total;
 
+#ifdef QE_DIAG_STAMPS
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint32_t tile = take_ticket(ticket, &s_ticket);
+#ifdef QE_DIAG_STAMPS
+    if (threadIdx.x == 0 && tile < STAMP_TILES) g_cp_stamps[(uint64_t)tile * STAMP_SLOTS] = t_start;
+#endif
+    QE_STAMP(g_cp_stamps, tile, 1);
     const uint64_t tile_base = (uint64_t)tile * TILE;
     const int w = wave_id(), l = lane_id();
     const uint64_t lt = lanemask_lt();
@@ -162,6 +180,7 @@ __global__ void __launch_bounds__(CB) compact_kernel(Op op, uint64_t n, uint32_t
         if (l == 0) s_cnt[j * CNW + w] = tot;
     }
     __syncthreads();
+    QE_STAMP(g_cp_stamps, tile, 2);
     if (w == 0) {
         uint32_t c = l < ITEMS * CNW ? s_cnt[l] : 0;
         uint32_t inc = wave_incl_scan_u32(c);
@@ -175,6 +194,7 @@ __global__ void __launch_bounds__(CB) compact_kernel(Op op, uint64_t n, uint32_t
         }
     }
     __syncthreads();
+    QE_STAMP(g_cp_stamps, tile, 3);
 #pragma unroll
     for (int j = 0; j < ITEMS; j++) {
         uint32_t b = s_cnt[j * CNW + w];
@@ -187,13 +207,21 @@ __global__ void __launch_bounds__(CB) compact_kernel(Op op, uint64_t n, uint32_t
         }
     }
     __syncthreads();
+    QE_STAMP(g_cp_stamps, tile, 4);
     const uint32_t total = s_total;
     const uint64_t off = s_excl;
     for (uint32_t i = threadIdx.x; i < total; i += CB) {
         out0[off + i] = s_vals[0][i];
         if (NOUT == 2) out1[off + i] = s_vals[NOUT - 1][i];
     }
+    QE_STAMP(g_cp_stamps, tile, 5);
 }
+
+#ifdef QE_DIAG_STAMPS
+extern "C" int qe_diag_stamps_cp(uint64_t* out, uint64_t n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(qe::g_cp_stamps), n * 8) == hipSuccess ? 0 : -2;
+}
+#endif
 
 // `bytes` = algorithmic input bytes; 4 B per output list per survivor is added once the count
 // is known (SURVEY.md §8(d) byte model).
@@ -222,9 +250,9 @@ uint64_t filter_scan(qe_ctx* c, const uint64_t* col, uint64_t n, char op, uint64
     double b = 8.0 * n;
     uint64_t m;
     switch (op) {
-    case '=': m = run_compact<8, 1>(c, "filter_scan", b, FilterScanOp<OP_EQ>{col, v}, n, out, nullptr); break;
-    case '>': m = run_compact<8, 1>(c, "filter_scan", b, FilterScanOp<OP_GT>{col, v}, n, out, nullptr); break;
-    case '<': m = run_compact<8, 1>(c, "filter_scan", b, FilterScanOp<OP_LT>{col, v}, n, out, nullptr); break;
+    case '=': m = run_compact<FS_ITEMS, 1>(c, "filter_scan", b, FilterScanOp<OP_EQ>{col, v}, n, out, nullptr); break;
+    case '>': m = run_compact<FS_ITEMS, 1>(c, "filter_scan", b, FilterScanOp<OP_GT>{col, v}, n, out, nullptr); break;
+    case '<': m = run_compact<FS_ITEMS, 1>(c, "filter_scan", b, FilterScanOp<OP_LT>{col, v}, n, out, nullptr); break;
     default: throw Error(QE_EINVAL, "Wrong operator");
     }
     return m;

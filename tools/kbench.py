@@ -61,6 +61,13 @@ def main():
             ctx.list_free(x)
             ctx.list_free(y)
         report(ctx, "merge", a.reps)
+    if a.what in ("filter", "all"):
+        col = ctx.column(r0, 2)   # hi32: uniform in [0, 2^32)
+        for rep in range(a.reps):
+            l1 = ctx.filter_scan(col, ">", 1_000_000_000)
+            ctx.filter_refine(col, "<", 3_000_000_000, l1)
+            ctx.list_free(l1)
+        report(ctx, "filter", a.reps)
     if a.what in ("gather", "all"):
         R = ctx.gather_pairs(ctx.column(r0, 1), None)
         ctx.sort_pairs(R)

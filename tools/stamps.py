@@ -21,6 +21,7 @@ SLOTS = 8
 PHASES = {
     "mj": ["ticket+win", "stage", "walk+annot+scan", "lookback+flags", "emit"],
     "sort": ["ticket+zero", "load+rank", "totals+publish+scan", "stage+lookback(t0)", "lookback wait", "write"],
+    "cp": ["ticket", "load+ballots", "scan+lookback", "stage", "write"],
 }
 
 
@@ -58,36 +59,30 @@ def report_split(ctx, ntiles):
         print(f"   {nm:24s} mean {d.mean():8.3f} us  p50 {np.median(d):8.3f}")
 
 
-def report_sort_walk(ctx, ntiles):
-    """sort: thread 0 staging vs lookback split, and its lookback walk (rounds, stalls, tiles)"""
-    buf = np.zeros(ntiles * SLOTS, dtype=np.uint64)
-    ctx.lib.qe_diag_stamps(b"sort", buf.ctypes.data, buf.size)
-    st = buf.reshape(ntiles, SLOTS)
-    t = st[1:, :7].astype(np.int64)
-    print(f"   {'staging (t0)':24s} mean {((t[:, 6] - t[:, 3]) * 0.01).mean():8.3f} us")
-    print(f"   {'lookback (t0)':24s} mean {((t[:, 4] - t[:, 6]) * 0.01).mean():8.3f} us")
-    dg = st[1:, 7]
-    rounds, spins, walked = dg >> 40, (dg >> 20) & 0xFFFFF, dg & 0xFFFFF
-    for nm, v in (("rounds", rounds), ("stalled rounds", spins), ("tiles walked", walked)):
-        print(f"   {nm:24s} mean {v.mean():8.2f}  p50 {np.median(v):6.0f}  p99 {np.percentile(v, 99):6.0f}  max {v.max()}")
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=100_000_000)
+    ap.add_argument("--what", default="sort,mj")
     a = ap.parse_args()
     ctx = lib.Ctx(0)
     n = a.n
     kinds = [("mod", n), ("mod", n), ("hi32",)]
     r0 = ctx.gen_relation(n, kinds, seed=1, gen_rel=0)
     r1 = ctx.gen_relation(n, kinds, seed=1, gen_rel=1)
+    if "cp" in a.what:
+        l1 = ctx.filter_scan(ctx.column(r0, 2), ">", 1_000_000_000)
+        ctx.sync()
+        report(ctx, "cp", (n + 8191) // 8192)
+        ctx.list_free(l1)
+    if "sort" not in a.what and "mj" not in a.what:
+        ctx.close()
+        return
     R = ctx.gather_pairs(ctx.column(r0, 1), None)
     S = ctx.gather_pairs(ctx.column(r1, 0), None)
     ctx.sort_pairs(R)
     ctx.sort_pairs(S)
     ctx.sync()
     report(ctx, "sort", (n + 8191) // 8192)   # last pass of S's sort
-    report_sort_walk(ctx, (n + 8191) // 8192)
     for _ in range(2):
         x, y = ctx.merge_join(R, S)
         ctx.sync()
