@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py -- the headline benchmark: joined tuples/s on the 4-relation chain join (config C3).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--no-cpu]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--no-cpu] [--workload c3|c4]
 
 Workload (BASELINE.json configs[2]): four relations of R = 100 M rows
 (c0 = v % R, c1 = v % R, c2 = v >> 32, splitmix64 seed 1, generated straight into HBM), query
@@ -212,9 +212,17 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-rows", type=int, default=16_000_000)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--workload", choices=["c3", "c4"], default="c3",
+                    help="c3 (default): the headline 4-relation chain join; c4: the SIGMOD-style batch")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1 or args.gpus > 1:
+    if args.workload == "c4":
+        from qe import c4bench
+        if world > 1:
+            res = c4bench.run_dist(args, log)
+        else:
+            res = c4bench.run_single(args, log, roofline_fn=roofline, traffic_fn=load_traffic)
+    elif world > 1 or args.gpus > 1:
         from qe import dist
         res = dist.bench_main(args, METRIC, QUERY, cpu_baseline_fn=cpu_baseline, roofline_fn=roofline,
                               traffic_fn=load_traffic)

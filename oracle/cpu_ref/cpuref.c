@@ -614,6 +614,27 @@ int cpuref_add_relation(cpuref_ctx* c, uint64_t rows, uint64_t ncols, const uint
 }
 
 /* execute_query (src/utilities.c:258-287): a failing predicate silently drops the line */
+/* CPUREF_TRACE=1: after every predicate, every list, in oracle/ref_trace_main.c's format */
+static void trace_mra(const mra_t* M, size_t step) {
+    static int on = -1;
+    if (on < 0) on = getenv("CPUREF_TRACE") != NULL;
+    if (!on) return;
+    for (size_t j = 0; j < M->n; j++)
+        for (size_t i = 0; i < M->v[j]->n; i++) {
+            const mid_t* m = &M->v[j]->e[i];
+            uint64_t n = m->list->n, sum = 0, h = 1469598103934665603ull;
+            for (uint64_t k = 0; k < n; k++) {
+                sum += m->list->v[k];
+                h = (h ^ m->list->v[k]) * 1099511628211ull;
+            }
+            fprintf(stderr, "step %zu ent %zu idx %zu rel %lu pid %lu lcs %d n %lu sum %lu hash %016lx head", step, j, i,
+                    (unsigned long)m->relation, (unsigned long)m->pid, m->lcs, (unsigned long)n,
+                    (unsigned long)sum, (unsigned long)h);
+            for (uint64_t k = 0; k < n && k < 12; k++) fprintf(stderr, " %lu", (unsigned long)m->list->v[k]);
+            fputc('\n', stderr);
+        }
+}
+
 static int execute_query(cpuref_ctx* c, const query_t* q) {
     mra_t M = { 0 };
     int rc = 0;
@@ -625,6 +646,8 @@ static int execute_query(cpuref_ctx* c, const query_t* q) {
         if (p->type == 0 && (p->srel >= q->nrels || q->rels[p->srel] >= c->nrels ||
                              p->scol >= c->rels[q->rels[p->srel]].ncols)) { rc = -1; break; }
         int r = p->type == 1 ? execute_filter(c, q, p, &M) : execute_join(c, q, p, &M);
+        if (getenv("CPUREF_TRACE")) fprintf(stderr, "query 0 pred %zu type %d rc %d\n", i, p->type, r);
+        trace_mra(&M, i);
         if (r == -1) { rc = -1; break; }
     }
     if (rc == 0) {

@@ -1,0 +1,180 @@
+"""C4: the SIGMOD-2018-style batch (BASELINE.json configs[3]) -- §8(f) row f-1.
+
+Workload: the 14 relations of qe.datagen.c4_spec(1.0) (1e5..1e7 rows, 2..6 columns, seed 4)
+generated in HBM, and the C4 queries that pass the reference's rand-invariance gate at N/100
+(tests/golden/c4.json, made by oracle/gen_golden.py with the real reference binary) and finish
+with exit status 0, run as batches of <= 50 separated by F lines -- the reference's protocol.
+One step = the whole batch through libqe's faithful executor.
+
+Multi-GPU: queries are independent, so the batch is scheduled replicas-style:
+query i runs on rank i mod N, every rank holds every relation (1.8 GB), outputs are gathered to
+rank 0 in input order.  Total work is fixed: strong scaling.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+
+from . import datagen as dg
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+GOLDEN = os.path.join(ROOT, "tests", "golden", "c4.json")
+METRIC = "queries/sec, SIGMOD-2018-style batch (C4: 14 relations, gated query set)"
+
+
+def load_queries() -> list[str]:
+    with open(GOLDEN) as f:
+        doc = json.load(f)
+    return [c["input"] for c in doc["cases"] if c["rc"] == 0]
+
+
+def gen_c4(ctx, scale: float = 1.0) -> list:
+    specs = dg.c4_spec(scale)
+    for r, sp in enumerate(specs):
+        ctx.gen_relation(sp.rows, sp.kinds, seed=dg.C4_SEED, gen_rel=r)
+    ctx.sync()
+    return specs
+
+
+def cpu_sample(queries: list[str], gpu_ctx, budget_s: float = 20.0) -> dict:
+    """oracle/cpu_ref, one core, on the first queries of the batch until ~budget_s of CPU time;
+    the GPU runs the same queries one by one for a byte comparison."""
+    import ctypes as C
+
+    so = os.path.join(ROOT, "oracle", "build", "libcpuref.so")
+    lib = C.CDLL(so)
+    lib.cpuref_create.restype = C.c_void_p
+    lib.cpuref_add_relation.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_void_p)]
+    lib.cpuref_run_str.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+    lib.cpuref_destroy.argtypes = [C.c_void_p]
+    specs = dg.c4_spec(1.0)
+    rels = dg.make_relations(specs, dg.C4_SEED)
+    h = lib.cpuref_create()
+    keep = []
+    for sp, cols in zip(specs, rels):
+        arr = (C.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
+        keep.append(arr)
+        lib.cpuref_add_relation(h, sp.rows, len(cols), arr)
+    try:
+        os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
+    except Exception:
+        pass
+    done, cpu_outs, t_cpu = 0, [], 0.0
+    for q in queries:
+        out, n = C.c_void_p(), C.c_size_t()
+        t0 = time.perf_counter()
+        lib.cpuref_run_str(h, q.encode(), C.byref(out), C.byref(n))
+        t_cpu += time.perf_counter() - t0
+        cpu_outs.append(C.string_at(out, n.value).decode("latin-1"))
+        done += 1
+        if t_cpu > budget_s:
+            break
+    lib.cpuref_destroy(h)
+    gpu_outs = [gpu_ctx.run(q)[0] for q in queries[:done]]
+    return {"value": round(done / t_cpu, 3), "unit": "queries/s", "cores": 1, "kind": "port",
+            "sample": f"first {done} of {len(queries)} C4 queries at full size; oracle/cpu_ref single-threaded, "
+                      f"{t_cpu:.1f} s",
+            "seconds": round(t_cpu, 3), "queries": done, "parity_with_gpu": cpu_outs == gpu_outs}
+
+
+def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
+    import torch
+
+    from . import lib
+    torch.cuda.init()
+    ctx = lib.Ctx(0)
+    queries = load_queries()
+    text = dg.c4_batches(queries)
+    t0 = time.time()
+    specs = gen_c4(ctx)
+    log(f"[c4] {len(specs)} relations in HBM in {time.time() - t0:.2f}s; {len(queries)} gated queries")
+    out = None
+    for _ in range(args.warmup):
+        out, rc = ctx.run(text)
+    ctx.set_profiling(True)
+    ctx.reset_stats()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out, rc = ctx.run(text)
+    ctx.sync()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    stats = ctx.kernel_stats()
+    ctx.set_profiling(False)
+    kern = sorted(stats.items(), key=lambda kv: -kv[1]["ms"])
+    res = {
+        "metric": METRIC, "value": round(len(queries) * args.steps / dt, 2), "unit": "queries/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic: qe.datagen.c4_spec(1.0) relations generated in HBM (seed 4)",
+        "config": {"workload": "C4: 14 relations, %d gated SIGMOD-style queries in batches of %d"
+                               % (len(queries), dg.C4_BATCH),
+                   "rows_total": sum(s.rows for s in specs), "output_lines": out.count("\n"),
+                   "executor": "libqe faithful state machine (qe_run_queries)", "parallelism": "single GPU"},
+        "roofline": roofline_fn(stats, traffic_fn() if traffic_fn else None) if roofline_fn else None,
+        "stages": {k: {"ms_per_step": round(s["ms"] / args.steps, 3), "launches_per_step": s["launches"] / args.steps}
+                   for k, s in kern[:10]},
+    }
+    if not args.no_cpu:
+        res["cpu_baseline"] = cpu_sample(queries, ctx)
+    ctx.close()
+    return res
+
+
+def run_dist(args, log) -> dict | None:
+    """replicas-style: rank r runs queries r, r+N, ...; outputs gathered to rank 0 in order"""
+    import torch
+    import torch.distributed as dist
+
+    from . import lib
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("QE_DIST_BACKEND", "nccl")
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    if not dist.is_initialized():
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
+        else:
+            dist.init_process_group(backend)
+    ctx = lib.Ctx(dev)
+    queries = load_queries()
+    mine = [q for i, q in enumerate(queries) if i % world == rank]
+    gen_c4(ctx)
+    outs = None
+    for _ in range(args.warmup):
+        outs = [ctx.run(q)[0] for q in mine]
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        outs = [ctx.run(q)[0] for q in mine]
+    ctx.sync()
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    tmax = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}" if backend == "nccl" else "cpu")
+    dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    dt = float(tmax.item())
+    gathered = [None] * world
+    dist.all_gather_object(gathered, outs)
+    ctx.close()
+    if rank != 0:
+        return None
+    ordered = []
+    for i in range(len(queries)):
+        ordered.append(gathered[i % world][i // world])
+    text = "".join(ordered)
+    return {
+        "metric": METRIC, "value": round(len(queries) * args.steps / dt, 2), "unit": "queries/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic: qe.datagen.c4_spec(1.0) relations generated in HBM (seed 4), replicated on every rank",
+        "config": {"workload": "C4: 14 relations, %d gated SIGMOD-style queries" % len(queries),
+                   "output_lines": text.count("\n"), "executor": "libqe faithful state machine, one query per rank",
+                   "parallelism": f"query-parallel replicas x{world}"},
+        "roofline": None, "cpu_baseline": None,
+    }

@@ -125,3 +125,69 @@ def protocol_input(paths: list[str], queries: str) -> str:
     """stdin for the reference protocol: paths, Done, query lines (main/queries_main.c)."""
     q = queries if queries.endswith("\n") or not queries else queries + "\n"
     return "".join(p + "\n" for p in paths) + "Done\n" + q
+
+
+# ---- C4: SIGMOD-2018-style batch (SURVEY.md §8(d)) ------------------------------------------------
+C4_SEED = 4
+C4_RELS = 14
+C4_QUERIES = 1000
+C4_BATCH = 50
+
+
+def c4_spec(scale: float = 1.0, seed: int = C4_SEED) -> list[RelSpec]:
+    """14 relations, sizes log-uniform in [1e5, 1e7] x scale, 2..6 columns.  Column roles by
+    position: 0, 1, 4 join keys ("mod", D) with D = 1e7 x scale shared by every relation (so any
+    key column joins any other with ~n1*n2/D output rows); 2, 5 uniform u32 payloads ("hi32");
+    3 a coarser key ("mod", D / 10).  scale = 0.01 is the rand-invariance-gate size."""
+    rng = np.random.default_rng(seed)
+    d = max(1, int(round(1e7 * scale)))
+    role = [("mod", d), ("mod", d), ("hi32",), ("mod", max(1, d // 10)), ("mod", d), ("hi32",)]
+    specs = []
+    for _ in range(C4_RELS):
+        rows = int(round(10 ** rng.uniform(5.0, 7.0) * scale))
+        ncols = int(rng.integers(2, 7))
+        specs.append(RelSpec(max(1, rows), role[:ncols]))
+    return specs
+
+
+def c4_queries(specs: list[RelSpec], n: int = C4_QUERIES, seed: int = C4_SEED) -> list[str]:
+    """SIGMOD-style queries: 2-4 bindings, chain or star equi-joins on key columns, 0-2 filters
+    on u32 payload columns (scale-free selectivity), 1-3 selects."""
+    rng = np.random.default_rng(seed + 1000)
+    out = []
+    for _ in range(n):
+        nb = int(rng.integers(2, 5))
+        rels = [int(x) for x in rng.choice(len(specs), nb, replace=False)]
+        keys = [[c for c, k in enumerate(specs[r].kinds) if k[0] == "mod"] for r in rels]
+        pays = [[c for c, k in enumerate(specs[r].kinds) if k[0] == "hi32"] for r in rels]
+        star = rng.random() < 0.35
+        preds = []
+        for b in range(1, nb):
+            a = 0 if star else b - 1
+            preds.append(f"{a}.{int(rng.choice(keys[a]))}={b}.{int(rng.choice(keys[b]))}")
+        nf = int(rng.choice([0, 1, 2], p=[0.3, 0.45, 0.25]))
+        for _ in range(nf):
+            cands = [b for b in range(nb) if pays[b]]
+            if not cands:
+                break
+            b = int(rng.choice(cands))
+            op = ">" if rng.random() < 0.5 else "<"
+            v = int(rng.integers(1 << 28, (1 << 32) - (1 << 28)))
+            preds.append(f"{b}.{int(rng.choice(pays[b]))}{op}{v}")
+        rng.shuffle(preds)
+        ns = int(rng.integers(1, 4))
+        sels = []
+        for _ in range(ns):
+            b = int(rng.integers(0, nb))
+            sels.append(f"{b}.{int(rng.integers(0, len(specs[rels[b]].kinds)))}")
+        out.append(" ".join(map(str, rels)) + "|" + "&".join(preds) + "|" + " ".join(sels) + "\n")
+    return out
+
+
+def c4_batches(queries: list[str], batch: int = C4_BATCH) -> str:
+    """the query lines in batches of <= `batch`, each batch closed by an F line"""
+    text = []
+    for i in range(0, len(queries), batch):
+        text.extend(queries[i:i + batch])
+        text.append("F\n")
+    return "".join(text)
