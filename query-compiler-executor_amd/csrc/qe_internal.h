@@ -128,6 +128,9 @@ uint64_t filter_refine(qe_ctx* c, const uint64_t* col, const uint32_t* in, uint6
                        uint32_t* out);
 uint64_t scan_join_k(qe_ctx* c, const uint64_t* rk, const uint32_t* rv, const uint64_t* sk, const uint32_t* sv,
                      uint64_t n, uint32_t* outR, uint32_t* outS);
+// indices i (ascending) with key[i] == pmax[i] <= limit (pmax = inclusive prefix max of key)
+uint64_t compact_prefix_max_hits(qe_ctx* c, const uint64_t* key, const uint64_t* pmax, uint64_t n, uint64_t limit,
+                                 uint32_t* out);
 uint64_t compact_nonzero_pairs(qe_ctx* c, const uint32_t* nz, uint64_t nzw, const uint32_t* last, const uint32_t* edit,
                                uint64_t n, uint32_t* out_last, uint32_t* out_edit);
 

@@ -13,8 +13,11 @@
 //                   every write of outR/outS is coalesced whatever the fan-out
 // Output order = key, then R order, then S order: exactly the reference's nested loop.
 // Unsorted inputs (possible in the reference's state machine) take
-// seq_merge_kernel, the literal two-pointer loop, so results stay identical there too.
+// merge_sequential, an exact parallel form of the literal two-pointer loop, so results stay
+// identical there too.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "qe_device.h"
@@ -557,38 +560,138 @@ __global__ void __launch_bounds__(MJB) mj_fused(const uint64_t* __restrict__ rk,
     QE_STAMP(g_mj_stamps, tile, 5);
 }
 
-// The reference's two-pointer loop verbatim (src/join.c:342-377) for inputs that are not
-// sorted.  One lane: it is only reached by state-machine paths the reference itself runs on
-// unsorted lists (SURVEY.md A.2 consequences), never on the measured configs.
-// MODE 0 counts, MODE 1 writes (optionally only R, for join_payloads' merge).
-template <int MODE>
-__global__ void seq_merge_kernel(const uint64_t* rk, const uint32_t* rv, uint64_t nR, const uint64_t* sk,
-                                 const uint32_t* sv, uint64_t nS, uint32_t* outR, uint32_t* outS, uint64_t* total) {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    uint64_t pr = 0, s_start = 0, o = 0;
-    while (pr < nR && s_start < nS) {
-        uint64_t ps = s_start;
-        int flag = 0;
-        uint64_t key = rk[pr];
-        while (ps < nS) {
-            uint64_t skey = sk[ps];
-            if (key < skey) break;
-            if (key > skey) {
-                ps++;
-                if (flag == 0) s_start = ps;
-            } else {
-                if (MODE == 1) {
-                    outR[o] = rv ? rv[pr] : (uint32_t)pr;
-                    if (outS) outS[o] = sv ? sv[ps] : (uint32_t)ps;
-                }
-                o++;
-                flag = 1;
-                ps++;
-            }
-        }
-        pr++;
+// ---- the reference's two-pointer loop on UNSORTED inputs (src/join.c:342-377) ---------------------
+// Only state-machine paths reach it (SORT_LHS / SORT_RHS on a list whose "sorted"
+// mark is stale), never the measured configs.  Per R row the loop moves s_start to
+//     f(s, k) = the first p >= s with S[p] >= k        (k = the row's key)
+// and emits the p in [f, first p > f with S[p] > k) with S[p] == k.  Since f(f(s, k1), k2) =
+// f(s, max(k1, k2)), the pointer after rows 0..pr is f(0, M) with M = max(R[0..pr]) -- so:
+//   * a row can emit only if its key IS that running max M (else S[f] >= M > key: the inner
+//     loop breaks at once), and M <= max(S) (else f = |S| and the outer loop has ended);
+//   * it then emits exactly the positions where S equals its own running max and that max is
+//     M ("record" positions of S with value M), in position order.
+// So the loop is two prefix-max scans, two compactions and binary searches -- all parallel and
+// exact (it was one lane walking up to 6e7 rows, ~1 s per call, in the C4 batch).
+constexpr int PM_B = 256, PM_ITEMS = 16, PM_CHUNK = PM_B * PM_ITEMS;
+
+__device__ __forceinline__ uint64_t wave_incl_max_u64(uint64_t v) {
+    const int l = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, d, 64);
+        uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d, 64);
+        const uint64_t o = ((uint64_t)hi << 32) | lo;
+        if (l >= d && o > v) v = o;
     }
-    *total = o;
+    return v;
+}
+
+__global__ void __launch_bounds__(PM_B) pmax_reduce_kernel(const uint64_t* __restrict__ x, uint64_t n,
+                                                           uint64_t* __restrict__ bmax) {
+    __shared__ uint64_t red[PM_B / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * PM_CHUNK;
+    uint64_t m = 0;
+#pragma unroll
+    for (int j = 0; j < PM_ITEMS; j++) {
+        const uint64_t i = base + (uint64_t)j * PM_B + threadIdx.x;
+        const uint64_t v = i < n ? x[i] : 0;
+        m = v > m ? v : m;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t o = shfl_xor_u64(m, d);
+        m = o > m ? o : m;
+    }
+    if (lane_id() == 0) red[wave_id()] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (int w = 0; w < PM_B / 64; w++) t = red[w] > t ? red[w] : t;
+        bmax[blockIdx.x] = t;
+    }
+}
+
+// one block: exclusive prefix max of the block maxima, in place
+__global__ void __launch_bounds__(1024) pmax_top_kernel(uint64_t* __restrict__ bmax, uint64_t nb) {
+    __shared__ uint64_t wmax[16];
+    __shared__ uint64_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint64_t base = 0; base < nb; base += 1024) {
+        const uint64_t i = base + threadIdx.x;
+        const uint64_t x = i < nb ? bmax[i] : 0;
+        const uint64_t inc = wave_incl_max_u64(x);
+        if (lane_id() == 63) wmax[wave_id()] = inc;
+        __syncthreads();
+        uint64_t ex = carry;
+        for (int w = 0; w < wave_id(); w++) ex = wmax[w] > ex ? wmax[w] : ex;
+        const uint64_t prev = shfl_u64(inc, lane_id() == 0 ? 0 : lane_id() - 1);
+        const uint64_t mine_ex = lane_id() == 0 ? ex : (prev > ex ? prev : ex);
+        if (i < nb) bmax[i] = mine_ex;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = mine_ex > x ? mine_ex : x;
+        __syncthreads();
+    }
+}
+
+// out[i] = max(x[0..i]): each thread scans 16 consecutive values, then waves and the block combine
+__global__ void __launch_bounds__(PM_B) pmax_apply_kernel(const uint64_t* __restrict__ x, uint64_t n,
+                                                          const uint64_t* __restrict__ bex, uint64_t* __restrict__ out) {
+    __shared__ uint64_t wmax[PM_B / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * PM_CHUNK + (uint64_t)threadIdx.x * PM_ITEMS;
+    uint64_t v[PM_ITEMS], run = 0;
+#pragma unroll
+    for (int j = 0; j < PM_ITEMS; j++) {
+        const uint64_t i = base + j;
+        v[j] = i < n ? x[i] : 0;
+        run = v[j] > run ? v[j] : run;
+        v[j] = run;
+    }
+    const uint64_t inc = wave_incl_max_u64(run);
+    if (lane_id() == 63) wmax[wave_id()] = inc;
+    __syncthreads();
+    uint64_t ex = bex[blockIdx.x];
+    for (int w = 0; w < wave_id(); w++) ex = wmax[w] > ex ? wmax[w] : ex;
+    const uint64_t prev = shfl_u64(inc, lane_id() == 0 ? 0 : lane_id() - 1);
+    if (lane_id() != 0 && prev > ex) ex = prev;
+#pragma unroll
+    for (int j = 0; j < PM_ITEMS; j++) {
+        const uint64_t i = base + j;
+        if (i < n) out[i] = v[j] > ex ? v[j] : ex;
+    }
+}
+
+// per candidate row: the record positions of S whose value equals its key -> [e0, e0 + cnt)
+__global__ void __launch_bounds__(256) seqm_count_kernel(const uint64_t* __restrict__ rk, const uint32_t* __restrict__ cand,
+                                                         uint64_t nc, const uint64_t* __restrict__ sk,
+                                                         const uint32_t* __restrict__ rec, uint64_t nrec,
+                                                         uint64_t* __restrict__ cnt, uint32_t* __restrict__ e0s) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nc) return;
+    const uint64_t key = rk[cand[i]];
+    auto at = [&](uint64_t e) { return sk[rec[e]]; };   // record values are non-decreasing
+    const uint64_t e0 = lower_bound_f(0, nrec, key, at);
+    const uint64_t e1 = (e0 < nrec && at(e0) == key) ? upper_bound_f(e0, nrec, key, at) : e0;
+    cnt[i] = e1 - e0;
+    e0s[i] = (uint32_t)e0;
+}
+
+__global__ void __launch_bounds__(256) seqm_write_kernel(const uint32_t* __restrict__ rv, const uint32_t* __restrict__ cand,
+                                                         uint64_t nc, const uint32_t* __restrict__ sv,
+                                                         const uint32_t* __restrict__ rec,
+                                                         const uint64_t* __restrict__ off, const uint32_t* __restrict__ e0s,
+                                                         uint64_t total, uint32_t* __restrict__ outR,
+                                                         uint32_t* __restrict__ outS) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nc) return;
+    const uint64_t o = off[i], end = i + 1 < nc ? off[i + 1] : total;
+    const uint32_t pr = cand[i];
+    const uint32_t r = rv ? rv[pr] : pr;
+    for (uint64_t j = 0; o + j < end; j++) {
+        const uint32_t p = rec[e0s[i] + j];
+        outR[o + j] = r;
+        outS[o + j] = sv ? sv[p] : p;
+    }
 }
 
 __global__ void __launch_bounds__(256) is_sorted_kernel(const uint64_t* __restrict__ k, uint64_t n, uint32_t* bad) {
@@ -944,24 +1047,71 @@ void merge_sorted(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_l
     dfree(c, tc);
 }
 
+static void prefix_max(qe_ctx* c, const uint64_t* x, uint64_t n, uint64_t* out) {
+    const uint64_t nb = (n + PM_CHUNK - 1) / PM_CHUNK;
+    uint64_t* bmax = dalloc_t<uint64_t>(c, std::max<uint64_t>(nb, 1));
+    hipLaunchKernelGGL(pmax_reduce_kernel, dim3((unsigned)nb), dim3(PM_B), 0, c->stream, x, n, bmax);
+    QE_HIP(hipGetLastError());
+    hipLaunchKernelGGL(pmax_top_kernel, dim3(1), dim3(1024), 0, c->stream, bmax, nb);
+    QE_HIP(hipGetLastError());
+    hipLaunchKernelGGL(pmax_apply_kernel, dim3((unsigned)nb), dim3(PM_B), 0, c->stream, x, n, bmax, out);
+    QE_HIP(hipGetLastError());
+    dfree(c, bmax);
+}
+
 void merge_sequential(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS) {
-    uint64_t* d_total = c->d_scratch + 20;
-    {
-        Timed t(c, "seq_merge", 0);
-        hipLaunchKernelGGL(seq_merge_kernel<0>, dim3(1), dim3(64), 0, c->stream, R->key, R->val, R->n, S->key, S->val,
-                           S->n, nullptr, nullptr, d_total);
-        QE_HIP(hipGetLastError());
+    const uint64_t nR = R->n, nS = S->n;
+    outR->n = outS->n = outR->cap = outS->cap = 0;
+    if (nR == 0 || nS == 0) {
+        outR->d = dalloc_t<uint32_t>(c, 1);
+        outS->d = dalloc_t<uint32_t>(c, 1);
+        return;
     }
-    uint64_t P = read_u64(c, d_total);
+    uint64_t* pmR = dalloc_t<uint64_t>(c, nR);
+    uint64_t* pmS = dalloc_t<uint64_t>(c, nS);
+    uint32_t* rec = dalloc_t<uint32_t>(c, nS);
+    uint32_t* cand = dalloc_t<uint32_t>(c, nR);
+    uint64_t maxS, nrec, nc;
+    {
+        Timed t(c, "seq_merge", 16.0 * (nR + nS));
+        prefix_max(c, R->key, nR, pmR);
+        prefix_max(c, S->key, nS, pmS);
+    }
+    maxS = read_u64(c, pmS + nS - 1);
+    nrec = compact_prefix_max_hits(c, S->key, pmS, nS, ~0ull, rec);     // S's record positions
+    nc = compact_prefix_max_hits(c, R->key, pmR, nR, maxS, cand);       // rows that can emit
+    uint64_t P = 0;
+    uint64_t* cnt = nullptr;
+    uint32_t* e0s = nullptr;
+    if (nc) {
+        cnt = dalloc_t<uint64_t>(c, nc);
+        e0s = dalloc_t<uint32_t>(c, nc);
+        Timed t(c, "seq_merge", 0);
+        hipLaunchKernelGGL(seqm_count_kernel, dim3(grid_for(nc, 256)), dim3(256), 0, c->stream, R->key, cand, nc,
+                           S->key, rec, nrec, cnt, e0s);
+        QE_HIP(hipGetLastError());
+        hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, c->stream, cnt, nc, c->d_scratch + 20);
+        QE_HIP(hipGetLastError());
+        P = read_u64(c, c->d_scratch + 20);
+    }
+    if (getenv("QE_SEQ_DEBUG"))
+        fprintf(stderr, "[seq_merge] nR %lu nS %lu records %lu candidates %lu pairs %lu\n", (unsigned long)nR,
+                (unsigned long)nS, (unsigned long)nrec, (unsigned long)nc, (unsigned long)P);
     outR->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(P, 1));
     outS->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(P, 1));
     outR->n = outS->n = outR->cap = outS->cap = P;
     if (P) {
-        Timed t(c, "seq_merge", 0);
-        hipLaunchKernelGGL(seq_merge_kernel<1>, dim3(1), dim3(64), 0, c->stream, R->key, R->val, R->n, S->key, S->val,
-                           S->n, outR->d, outS->d, d_total);
+        Timed t(c, "seq_merge", 8.0 * P);
+        hipLaunchKernelGGL(seqm_write_kernel, dim3(grid_for(nc, 256)), dim3(256), 0, c->stream, R->val, cand, nc,
+                           S->val, rec, cnt, e0s, P, outR->d, outS->d);
         QE_HIP(hipGetLastError());
     }
+    if (cnt) dfree(c, cnt);
+    if (e0s) dfree(c, e0s);
+    dfree(c, pmR);
+    dfree(c, pmS);
+    dfree(c, rec);
+    dfree(c, cand);
 }
 
 bool pairs_sorted(qe_ctx* c, const qe_pairs* p) {

@@ -124,6 +124,22 @@ struct NonzeroPairsOp {        // join_payloads: keep (last[i], edit[i] or i) wh
     }
 };
 
+struct PrefixMaxHitOp {         // unsorted merge: index i where key[i] equals the running max at i
+    static constexpr int VEC = 2;   // (and, with `limit`, that max is <= limit)
+    const uint64_t *key, *pmax;
+    uint64_t limit;
+    __device__ __forceinline__ void load(uint64_t base, uint64_t n, bool* f, uint32_t* v0, uint32_t*) const {
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const uint64_t i = base + k;
+            const bool ok = i < n;
+            const uint64_t m = ok ? pmax[i] : 0;
+            f[k] = ok && key[i] == m && m <= limit;
+            v0[k] = (uint32_t)i;
+        }
+    }
+};
+
 // ---- the kernel -------------------------------------------------------------------------------
 #ifdef QE_DIAG_STAMPS
 __device__ uint64_t g_cp_stamps[STAMP_TILES * STAMP_SLOTS];
@@ -278,6 +294,11 @@ uint64_t compact_nonzero_pairs(qe_ctx* c, const uint32_t* nz, uint64_t nzw, cons
                                const uint32_t* edit, uint64_t n, uint32_t* out_last, uint32_t* out_edit) {
     return run_compact<4, 2>(c, "payload_prune", 8.0 * n, NonzeroPairsOp{nz, last, edit, nzw}, n, out_last,
                              out_edit);
+}
+
+uint64_t compact_prefix_max_hits(qe_ctx* c, const uint64_t* key, const uint64_t* pmax, uint64_t n, uint64_t limit,
+                                 uint32_t* out) {
+    return run_compact<4, 1>(c, "seq_merge", 16.0 * n, PrefixMaxHitOp{key, pmax, limit}, n, out, nullptr);
 }
 
 }  // namespace qe

@@ -321,6 +321,43 @@ def test_column_bits_at_load(ctx):
     assert ctx.column_bits(rel, 1) == (7, 7)
 
 
+@pytest.mark.parametrize("shape", ["random_small_domain", "random_large", "r_ascending", "s_descending",
+                                   "all_equal", "r_descending", "s_records_tied", "multi_chunk"])
+def test_merge_join_unsorted_shapes(ctx, shape):
+    """the parallel form of the literal loop on unsorted inputs (prefix maxima + records of S),
+    across chunk boundaries of its scans and the degenerate orders"""
+    rng = np.random.default_rng(len(shape))
+    n = 70_000 if shape in ("random_large", "multi_chunk") else 3000
+    if shape == "random_small_domain":
+        rk, sk = rng.integers(0, 50, n, dtype=np.uint64), rng.integers(0, 50, n + 17, dtype=np.uint64)
+    elif shape == "random_large":
+        rk, sk = rng.integers(0, 1 << 40, n, dtype=np.uint64), rng.integers(0, 1 << 40, n, dtype=np.uint64)
+        sk[::97] = rk[::97][: len(sk[::97])]
+    elif shape == "r_ascending":
+        rk, sk = np.arange(n, dtype=np.uint64), rng.integers(0, n, n, dtype=np.uint64)
+    elif shape == "s_descending":
+        rk, sk = rng.integers(0, n, n, dtype=np.uint64), np.arange(n, 0, -1).astype(np.uint64)
+    elif shape == "all_equal":
+        rk, sk = np.full(n, 7, dtype=np.uint64), np.full(500, 7, dtype=np.uint64)
+    elif shape == "r_descending":
+        rk, sk = np.arange(n, 0, -1).astype(np.uint64), rng.integers(0, n, n, dtype=np.uint64)
+    elif shape == "s_records_tied":   # S's running max repeats (ties with the record value)
+        sk = np.repeat(np.arange(0, 300, 3, dtype=np.uint64), 30)
+        rng.shuffle(sk[:1500])
+        rk = rng.integers(0, 300, n, dtype=np.uint64)
+    else:                              # prefix maxima across many 4096-element chunks
+        rk = np.sort(rng.integers(0, 1000, n, dtype=np.uint64))[::-1].copy()
+        rk[::5000] = 999
+        sk = rng.integers(0, 1000, n, dtype=np.uint64)
+    rv = rng.permutation(len(rk)).astype(np.uint32)
+    sv = rng.permutation(len(sk)).astype(np.uint32)
+    R, S = ctx.pairs_from_host(rk, rv), ctx.pairs_from_host(sk, sv)
+    a, b = ctx.merge_join(R, S)
+    wa, wb = _ref_merge(rk.tolist(), rv.tolist(), sk.tolist(), sv.tolist())
+    np.testing.assert_array_equal(ctx.list_to_host(a), wa)
+    np.testing.assert_array_equal(ctx.list_to_host(b), wb)
+
+
 def test_merge_fills_match_counts_and_driver_counts_use_them(ctx):
     rng = np.random.default_rng(8)
     colR = rng.integers(0, 300, 4000, dtype=np.uint64)
