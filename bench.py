@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py -- the headline benchmark: joined tuples/s on the 4-relation chain join (config C3).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--no-cpu] [--workload c3|c4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--no-cpu] [--workload c3|c4|c5]
 
 Workload (BASELINE.json configs[2]): four relations of R = 100 M rows
 (c0 = v % R, c1 = v % R, c2 = v >> 32, splitmix64 seed 1, generated straight into HBM), query
@@ -208,15 +208,26 @@ def main():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--rows", type=int, default=None,
+                    help="rows per relation (per rank for N > 1); default 1e8 (c3) / 1e9 (c5)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-rows", type=int, default=16_000_000)
+    ap.add_argument("--cpu-rows-c5", type=int, default=1_000_000)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--workload", choices=["c3", "c4"], default="c3",
-                    help="c3 (default): the headline 4-relation chain join; c4: the SIGMOD-style batch")
+    ap.add_argument("--workload", choices=["c3", "c4", "c5"], default="c3",
+                    help="c3 (default): the headline 4-relation chain join; c4: the SIGMOD-style batch; "
+                         "c5: the skewed (Zipf 0.9) 2-relation join at 1e9 rows")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.workload == "c4":
+    if args.rows is None and args.workload != "c5":
+        args.rows = 100_000_000
+    if args.workload == "c5":
+        from qe import c5bench
+        if world > 1:
+            res = c5bench.run_dist(args, log)
+        else:
+            res = c5bench.run_single(args, log, roofline_fn=roofline, traffic_fn=load_traffic)
+    elif args.workload == "c4":
         from qe import c4bench
         if world > 1:
             res = c4bench.run_dist(args, log)

@@ -37,6 +37,7 @@ enum {
     QE_EHIP = -2,        /* HIP runtime error */
     QE_ENOMEM = -3,      /* device allocation failed */
     QE_EEXIT = -4,       /* the reference would have called exit(EXIT_FAILURE) here */
+    QE_ETOOBIG = -5,     /* a join result beyond the materialisation limit (qe_set_materialize_limit) */
 };
 
 typedef struct qe_ctx qe_ctx;
@@ -68,6 +69,9 @@ typedef struct {
 #define QE_PAIRS_DISTINCT 1u
 #define QE_PAIRS_SORTED 2u
 #define QE_PAIRS_BITS 4u
+/* match holds this side's partner counts for the join it last took part in (set by
+ * qe_merge_join on R and by qe_merge_join_counts on both sides, cleared by qe_sort_pairs) */
+#define QE_PAIRS_MATCHED 8u
 
 /* Per-kernel statistics (profiling, qe_set_profiling). */
 typedef struct {
@@ -89,9 +93,19 @@ int         qe_sync(qe_ctx*);
 /* Copy a column-major host relation into HBM; returns the relation id (= load order) or <0. */
 int qe_load_relation(qe_ctx*, uint64_t rows, uint64_t ncols, const uint64_t* const* host_cols);
 /* Generate a relation on the device with the splitmix64 generator of SURVEY.md §9.1.
- * kinds[c]: 0 = v % mod[c], 1 = v >> 32. Returns the relation id or <0. */
+ * kinds[c]: 0 = v % mod[c], 1 = v >> 32, 2 = Zipf key over [0, mod[c]) drawn through the table
+ * of qe_set_zipf_table (mod[c] must equal its domain).  Returns the relation id or <0. */
 int qe_gen_relation(qe_ctx*, uint64_t rows, uint64_t ncols, const int* kinds, const uint64_t* mods,
                     uint64_t seed, uint32_t gen_rel, uint64_t row_start);
+/* Zipf sampling table for kind 2 (the C5 skew workload): d_cdf holds `domain`
+ * nondecreasing doubles in device memory, the last one 1.0 (borrowed until the next call or
+ * qe_fini).  A draw takes the 53-bit uniform u = (v >> 11) * 2^-53, rank = #{r : cdf[r] <= u}
+ * capped at domain-1, and returns the seeded Feistel permutation of rank (qe/datagen.py
+ * feistel_perm).  d_cdf = NULL drops the table. */
+int qe_set_zipf_table(qe_ctx*, const double* d_cdf, uint64_t domain, uint64_t perm_seed);
+/* The same with a table libqe builds and owns: cdf[r] = sum_{q<=r} (q+1)^-theta / total, summed
+ * in a fixed order so every run on the device draws the same keys (C5 bench data). */
+int qe_set_zipf(qe_ctx*, uint64_t domain, double theta, uint64_t perm_seed);
 int qe_relation_count(qe_ctx*);
 int qe_relation_column(qe_ctx*, int rel, int col, qe_col* out);
 /* Column statistics computed once when the relation is loaded/generated (OR and AND of every
@@ -126,8 +140,18 @@ int qe_gather_pairs(qe_ctx*, qe_col col, const qe_list* rows, qe_pairs* out);
 int qe_sort_pairs(qe_ctx*, qe_pairs* inout);
 int qe_is_sorted(qe_ctx*, const qe_pairs*, int* sorted);
 /* a8: join_relations (src/join.c:325-392): aligned payload lists in key, R, S order.  Runs the
- * merge-path kernel when both inputs are sorted and the exact two-pointer semantics otherwise. */
+ * merge-path kernel when both inputs are sorted and the exact two-pointer semantics otherwise.
+ * A sorted join of more pairs than the materialisation limit returns QE_ETOOBIG with
+ * outR->n = outS->n = the exact pair count, no lists, and R->match filled (the reference's
+ * DArray cannot hold such a result either: src/DArray.h:14-15, src/DArray.c:62-65). */
 int qe_merge_join(qe_ctx*, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS);
+/* Pairs above which qe_merge_join returns QE_ETOOBIG (default INT32_MAX; env QE_MAT_LIMIT). */
+int qe_set_materialize_limit(qe_ctx*, uint64_t pairs);
+/* a8, aggregate form (C5, SURVEY.md §0.7 / §8(e) "aggregate push-down"): for sorted R and S,
+ * R->match[i] = #S rows with R's key, S->match[j] = #R rows with S's key, *pairs = the join's
+ * exact pair count.  No pair is materialised.  An R already carrying QE_PAIRS_MATCHED (what
+ * qe_merge_join leaves on R, e.g. after QE_ETOOBIG) is taken as counted against this S. */
+int qe_merge_join_counts(qe_ctx*, qe_pairs* R, qe_pairs* S, uint64_t* pairs);
 /* a9: scan_join (src/join.c:395-423). */
 int qe_scan_join(qe_ctx*, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS);
 /* a8 dedup: the multiset non_duplicates[mode] of a join (src/join.c:358-367) as a dense count
@@ -150,6 +174,10 @@ int qe_join_payloads_multi(qe_ctx*, const uint32_t* d_counts, uint64_t rows, con
                            const qe_list* const* edits, int nedits, qe_list* outs);
 /* a12: print_sums' inner loop (src/utilities.c:216-219): sum of col[rowid] mod 2^64. */
 int qe_checksum(qe_ctx*, qe_col col, const qe_list* rows, uint64_t* sum);
+/* a12 over an unmaterialised join side: sum of col[p->val[i]] * p->match[i] mod 2^64, which is
+ * qe_checksum over the list qe_merge_join would have produced for that side
+ * (sum_pairs col(pR) = sum_k (sum_{r in R_k} col(r)) * |S_k|). */
+int qe_checksum_weighted(qe_ctx*, qe_col col, const qe_pairs* p, uint64_t* sum);
 
 /* ---- multi-GPU plan; the exchange itself is an RCCL all-to-all -------------- */
 /* Hash-partition n rows on their key: dest = fmix64(key) % nparts (murmur3 finaliser).  Rows go

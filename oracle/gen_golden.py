@@ -228,6 +228,30 @@ def main():
         ds = {"seed": dg.C4_SEED, "relations": [{"rows": sp.rows, "kinds": [list(k) for k in sp.kinds]}
                                                for sp in specs]}
         process_cases("c4", ds, dg.c4_queries(dg.c4_spec(1.0)), 120, args.workers)
+    if on("c5"):   # C5 skew shape at the gate scale: Zipf keys, shared permutation
+        sp = dg.c5_spec(8000)
+        z = list(sp[1].kinds[0])
+        ds = {"seed": dg.C5_SEED, "relations": [{"rows": r.rows, "kinds": [list(k) for k in r.kinds]} for r in sp]
+              + [{"rows": 6000, "kinds": [z, ["mod", 6000], ["hi32"]]}]}
+        inputs = [
+            dg.C5_QUERY,                                                   # the C5 query
+            "0 1|0.1=1.0|1.2 0.2 0.0 1.1 0.1\n",                         # every column, both sides
+            "1 0|0.0=1.1|0.2 1.2\n",                                     # roles swapped
+            "0 1|0.1=1.0&0.2>2147483648|0.2 1.2\n",                      # filter, then the join (fix_all, nothing to redo)
+            "0 1|0.1=1.0&1.2<1073741824|1.2 0.2\n",
+            "0 1|0.1=1.0&0.2>2147483648&1.2<1073741824|0.2 1.2\n",       # filters on both -> scan_join (K1 quirk)
+            "0 1|0.1=1.0&0.2=5|0.2 1.2\n",                               # empty -> NULL NULL
+            "0 2|0.1=1.0|0.2 1.2\n",                                     # the third (smaller) Zipf relation
+            "2 1|0.0=1.0|0.2 1.2\n",                                     # Zipf x Zipf, different sizes
+            "0 1 2|0.1=1.0&1.1=2.1|0.2 1.2 2.2\n",                       # skewed join, then a uniform one
+            "0 1 2|0.0=2.1&0.1=1.0|0.2 1.2\n",                           # uniform join, then the skewed one
+            "0 1|0.1=1.0|0.2 1.2\nF\n1 0|0.0=1.1|0.2\nF\n",               # batch
+        ]
+        process_cases("c5", ds, inputs, 600, args.workers)
+        sp = dg.c5_spec(3000, theta=1.2)
+        ds = {"seed": dg.C5_SEED + 1, "relations": [{"rows": r.rows, "kinds": [list(k) for k in r.kinds]} for r in sp]}
+        inputs = [dg.C5_QUERY, "1 0|0.0=1.1|1.2 0.2 1.0\n", "0 1|0.1=1.0&1.2>3000000000|0.2 1.2\n"]
+        process_cases("c5_theta12", ds, inputs, 600, args.workers)
     if on("headline"):   # G1-G3 at N = 1M; G3 takes ~1 min per seed
         ds = {"seed": 1, "relations": [{"rows": 1000000, "kinds": [["mod", 1000000], ["mod", 1000000], ["hi32"]]}
                                        for _ in range(4)]}

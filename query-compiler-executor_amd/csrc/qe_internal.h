@@ -66,6 +66,14 @@ struct qe_ctx {
 
     std::vector<qe::Relation> rels;
     uint64_t last_result_rows = 0;
+    // joins larger than this many pairs are not materialised (QE_ETOOBIG): the reference's
+    // DArray holds at most INT32_MAX elements (src/DArray.h:14-15).  QE_MAT_LIMIT overrides.
+    uint64_t mat_limit = 0x7FFFFFFFull;
+    // Zipf sampling table (qe_set_zipf_table): CDF borrowed from the caller, guide owned
+    const double* zipf_cdf = nullptr;
+    uint64_t* zipf_guide = nullptr;
+    double* zipf_owned = nullptr;     // the CDF when qe_set_zipf built it
+    uint64_t zipf_domain = 0, zipf_perm_seed = 0;
 
     // decoupled-lookback state: status words + per-launch tile tickets, epoch-tagged so that
     // nothing is cleared between launches (cleared when the 16-bit epoch wraps)

@@ -29,8 +29,13 @@ constexpr int MJB = 256;
 constexpr int MJ_ITEMS = 8;
 constexpr int MJ_TILE = MJB * MJ_ITEMS;   // 2048 R elements per tile
 constexpr int MJ_WIN = 4096;              // S keys staged in LDS (32 KiB)
+// a tile with more pairs than this is not emitted by its own workgroup: it is listed and
+// expanded afterwards by mj_heavy_prep + mj_heavy_emit, MJ_HEAVY_CHUNK pairs per workgroup
+// (a skewed key can put 1e8 pairs in one tile)
+constexpr uint64_t MJ_HEAVY_DEFER = 1ull << 20;
+constexpr uint64_t MJ_HEAVY_CHUNK = 1ull << 16;
 
-enum : uint32_t { MJF_R_FANOUT = 1u, MJF_S_DUP = 2u, MJF_ERR = 4u };
+enum : uint32_t { MJF_R_FANOUT = 1u, MJF_S_DUP = 2u, MJF_ERR = 4u, MJF_OVF = 8u };   // OVF: the 46-bit lookback sum wrapped
 
 template <class F>
 __device__ __forceinline__ uint64_t lower_bound_f(uint64_t lo, uint64_t hi, uint64_t key, F at) {
@@ -235,6 +240,18 @@ __device__ __forceinline__ uint64_t mj_walk_t(const SH& sh, const uint64_t* sk, 
                 bn = h;
             }
         }
+    }
+    if (key[0] == klast) {   // one key for all of the thread's rows (inside a skewed key's run):
+        uint64_t tsum = 0;    // [a, b) is already its S run
+#pragma unroll
+        for (int j = 0; j < MJ_ITEMS; j++) {
+            if ((uint32_t)j < nv) {
+                cnt[j] = b - a;
+                lo_rel[j] = a;
+                tsum += b - a;
+            }
+        }
+        return tsum;
     }
     uint32_t lo[MJ_ITEMS], ln[MJ_ITEMS];
 #pragma unroll
@@ -481,6 +498,7 @@ __global__ void __launch_bounds__(MJB) mj_tile(const uint64_t* __restrict__ rk, 
     uint64_t btotal;
     uint64_t run = mj_block_scan(sh, tsum, &btotal);   // barrier: the S window is dead
     const uint64_t gofs = tile_counts[tile];
+    if (btotal > MJ_HEAVY_DEFER) return;               // mj_heavy_emit's
     if (mj_balanced<MJShared64>(btotal)) {
         mj_stage_out(sh, rv, base, tn, run, cnt, lo_rel);
         __syncthreads();
@@ -505,7 +523,8 @@ __global__ void __launch_bounds__(MJB) mj_fused(const uint64_t* __restrict__ rk,
                                                 uint32_t* __restrict__ match, uint32_t* __restrict__ outR,
                                                 uint32_t* __restrict__ outS, uint64_t cap, uint32_t* __restrict__ flags,
                                                 uint64_t* status, uint32_t* ticket, uint32_t epoch, uint32_t ntiles,
-                                                uint64_t* total_out) {
+                                                uint64_t* total_out, uint32_t* __restrict__ heavy,
+                                                uint32_t* __restrict__ nheavy) {
     __shared__ SH sh;
 #ifdef QE_DIAG_STAMPS
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
@@ -544,6 +563,7 @@ __global__ void __launch_bounds__(MJB) mj_fused(const uint64_t* __restrict__ rk,
             sh.excl = ex;
             tile_counts[tile] = btotal;
             if (tile == ntiles - 1) *total_out = ex + btotal;
+            if (btotal > LB_VAL_MASK || ex + btotal > LB_VAL_MASK) atomicOr(flags, MJF_OVF);
         }
     }
     mj_publish_flags(sh, f, flags);   // contains the barrier that publishes sh.excl (and the staging)
@@ -552,12 +572,83 @@ __global__ void __launch_bounds__(MJB) mj_fused(const uint64_t* __restrict__ rk,
 #ifdef QE_DIAG_MJ_NOEMIT
     if (gofs + btotal > cap + 1) outR[0] = (uint32_t)run;   // keep the walk alive, store nothing
 #else
-    if (gofs + btotal <= cap) {
+    if (btotal > MJ_HEAVY_DEFER) {
+        if (heavy && threadIdx.x == 0) heavy[atomicAdd(nheavy, 1u)] = tile;
+    } else if (gofs + btotal <= cap) {
         if (balanced) mj_store_out(sh, sv, wlo, btotal, gofs, outR, outS);
         else mj_emit_heavy(sh, rv, sv, base, tn, wlo, run, btotal, gofs, cnt, lo_rel, outR, outS);
     }
 #endif
     QE_STAMP(g_mj_stamps, tile, 5);
+}
+
+// ---- deferred heavy tiles ------------------------------------------------------------------------
+// prep: one workgroup per listed tile re-walks it and leaves, per R row, its absolute S start
+// and its u64 output offset inside the tile (plus the tile's total)
+__global__ void __launch_bounds__(MJB) mj_heavy_prep(const uint64_t* __restrict__ rk, uint64_t nR,
+                                                     const uint64_t* __restrict__ sk, const uint64_t* __restrict__ win,
+                                                     const uint32_t* __restrict__ heavy, uint32_t* __restrict__ hp_lo,
+                                                     uint64_t* __restrict__ hp_off, uint64_t* __restrict__ hp_tot) {
+    __shared__ MJShared64 sh;
+    const uint32_t k = blockIdx.x;
+    const uint32_t tile = heavy[k];
+    const uint64_t base = (uint64_t)tile * MJ_TILE;
+    const uint32_t tn = (uint32_t)std::min<uint64_t>(MJ_TILE, nR - base);
+    const uint64_t wlo = win[2 * tile], wn = win[2 * tile + 1] - wlo;
+    mj_stage(sh, rk, base, tn, sk, wlo, wn, 0);
+    uint32_t cnt[MJ_ITEMS], lo_rel[MJ_ITEMS];
+    const uint64_t tsum = mj_walk(sh, sk, wlo, wn, tn, 0, cnt, lo_rel);
+    uint64_t btotal;
+    uint64_t run = mj_block_scan(sh, tsum, &btotal);
+    const uint32_t e0 = threadIdx.x * MJ_ITEMS;
+#pragma unroll
+    for (int j = 0; j < MJ_ITEMS; j++) {
+        const uint32_t e = e0 + j;
+        if (e < tn) {
+            hp_lo[(uint64_t)k * MJ_TILE + e] = (uint32_t)(wlo + lo_rel[j]);
+            hp_off[(uint64_t)k * MJ_TILE + e] = run;
+            run += cnt[j];
+        }
+    }
+    if (threadIdx.x == 0) hp_tot[k] = btotal;
+}
+
+// emit: one workgroup per MJ_HEAVY_CHUNK output slots of one listed tile; every slot finds its
+// R row by binary search over the tile's offsets (staged in LDS); stores are coalesced
+__global__ void __launch_bounds__(MJB) mj_heavy_emit(const uint32_t* __restrict__ rv, const uint32_t* __restrict__ sv,
+                                                     uint64_t nR, const uint32_t* __restrict__ heavy,
+                                                     const uint32_t* __restrict__ hp_lo,
+                                                     const uint64_t* __restrict__ hp_off,
+                                                     const uint64_t* __restrict__ hp_tot,
+                                                     const uint32_t* __restrict__ chunk_k,
+                                                     const uint64_t* __restrict__ chunk_start,
+                                                     const uint64_t* __restrict__ tile_ofs, uint32_t* __restrict__ outR,
+                                                     uint32_t* __restrict__ outS) {
+    __shared__ uint64_t off[MJ_TILE];
+    __shared__ uint32_t lo[MJ_TILE];
+    const uint32_t k = chunk_k[blockIdx.x];
+    const uint32_t tile = heavy[k];
+    const uint64_t base = (uint64_t)tile * MJ_TILE;
+    const uint32_t tn = (uint32_t)std::min<uint64_t>(MJ_TILE, nR - base);
+    for (uint32_t e = threadIdx.x; e < tn; e += MJB) {
+        off[e] = hp_off[(uint64_t)k * MJ_TILE + e];
+        lo[e] = hp_lo[(uint64_t)k * MJ_TILE + e];
+    }
+    __syncthreads();
+    const uint64_t c0 = chunk_start[blockIdx.x];
+    const uint64_t c1 = std::min<uint64_t>(c0 + MJ_HEAVY_CHUNK, hp_tot[k]);
+    const uint64_t gofs = tile_ofs[tile];
+    for (uint64_t o = c0 + threadIdx.x; o < c1; o += MJB) {
+        uint32_t a = 0, b = tn;   // last row with off <= o
+        while (b - a > 1) {
+            const uint32_t m = (a + b) >> 1;
+            if (off[m] <= o) a = m;
+            else b = m;
+        }
+        const uint64_t sidx = lo[a] + (o - off[a]);
+        outR[gofs + o] = rv ? rv[base + a] : (uint32_t)(base + a);
+        outS[gofs + o] = sv ? sv[sidx] : (uint32_t)sidx;
+    }
 }
 
 // ---- the reference's two-pointer loop on UNSORTED inputs (src/join.c:342-377) ---------------------
@@ -789,6 +880,37 @@ __global__ void __launch_bounds__(256) checksum_kernel(const uint64_t* __restric
     if (threadIdx.x == 0) atomicAdd(out, (unsigned long long)(red[0] + red[1] + red[2] + red[3]));
 }
 
+// sum of col[val[i]] * match[i] mod 2^64 over one side of a sorted merge: the checksum of that
+// side's output list (each row appears match[i] times) without materialising it -- aggregate
+// push-down, SURVEY.md §0.7 / §8(e).  val == null: the rowid is the position.
+__global__ void __launch_bounds__(256) checksum_weighted_kernel(const uint64_t* __restrict__ col,
+                                                                const uint32_t* __restrict__ val,
+                                                                const uint32_t* __restrict__ match, uint64_t n,
+                                                                unsigned long long* __restrict__ out) {
+    uint64_t s = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 4;
+    for (uint64_t i4 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i4 < n; i4 += stride) {
+        if (i4 + 3 < n) {
+            const uint4 m = *reinterpret_cast<const uint4*>(match + i4);
+            uint4 r;
+            if (val) r = *reinterpret_cast<const uint4*>(val + i4);
+            else r = make_uint4((uint32_t)i4, (uint32_t)i4 + 1, (uint32_t)i4 + 2, (uint32_t)i4 + 3);
+            if (m.x) s += col[r.x] * m.x;
+            if (m.y) s += col[r.y] * m.y;
+            if (m.z) s += col[r.z] * m.z;
+            if (m.w) s += col[r.w] * m.w;
+        } else {
+            for (uint64_t i = i4; i < n; i++)
+                if (match[i]) s += col[val ? val[i] : (uint32_t)i] * match[i];
+        }
+    }
+    s = wave_sum_u64(s);
+    __shared__ uint64_t red[4];
+    if (lane_id() == 0) red[wave_id()] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(out, (unsigned long long)(red[0] + red[1] + red[2] + red[3]));
+}
+
 // nonzero bitmap of the driver counts: one sequential pass over the (rows x 4 B) counts array
 // leaves rows/8 bytes that stay cache-resident for the pruning pass's random tests, which
 // would otherwise fetch a 64-B line of the counts array per 4-B test
@@ -971,6 +1093,45 @@ enum : uint32_t { PF_DISTINCT = 1u, PF_SORTED = 2u };
 
 const char* op_ok(char op) { return (op == '=' || op == '<' || op == '>') ? nullptr : "Wrong operator"; }
 
+// the listed heavy tiles' pairs at their exact offsets (tile_ofs: scanned tile counts)
+void emit_deferred(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const uint64_t* win, const uint32_t* heavy,
+                   uint32_t nheavy, const uint64_t* tile_ofs, uint32_t* outR, uint32_t* outS) {
+    uint32_t* hp_lo = dalloc_t<uint32_t>(c, (uint64_t)nheavy * MJ_TILE);
+    uint64_t* hp_off = dalloc_t<uint64_t>(c, (uint64_t)nheavy * MJ_TILE);
+    uint64_t* hp_tot = dalloc_t<uint64_t>(c, nheavy);
+    Timed t(c, "mj_heavy", 0);
+    hipLaunchKernelGGL(mj_heavy_prep, dim3(nheavy), dim3(MJB), 0, c->stream, R->key, R->n, S->key, win, heavy, hp_lo,
+                       hp_off, hp_tot);
+    QE_HIP(hipGetLastError());
+    std::vector<uint64_t> tot(nheavy);
+    QE_HIP(hipMemcpyAsync(tot.data(), hp_tot, nheavy * 8ull, hipMemcpyDeviceToHost, c->stream));
+    QE_HIP(hipStreamSynchronize(c->stream));
+    std::vector<uint32_t> ck;
+    std::vector<uint64_t> cs;
+    double bytes = 0;
+    for (uint32_t k = 0; k < nheavy; k++) {
+        for (uint64_t o = 0; o < tot[k]; o += MJ_HEAVY_CHUNK) {
+            ck.push_back(k);
+            cs.push_back(o);
+        }
+        bytes += 12.0 * tot[k];
+    }
+    if (c->prof && !c->pending.empty()) c->pending.back().bytes += bytes;
+    uint32_t* d_ck = dalloc_t<uint32_t>(c, ck.size());
+    uint64_t* d_cs = dalloc_t<uint64_t>(c, cs.size());
+    QE_HIP(hipMemcpyAsync(d_ck, ck.data(), ck.size() * 4, hipMemcpyHostToDevice, c->stream));
+    QE_HIP(hipMemcpyAsync(d_cs, cs.data(), cs.size() * 8, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(mj_heavy_emit, dim3((unsigned)ck.size()), dim3(MJB), 0, c->stream, R->val, S->val, R->n, heavy,
+                       hp_lo, hp_off, hp_tot, d_ck, d_cs, tile_ofs, outR, outS);
+    QE_HIP(hipGetLastError());
+    QE_HIP(hipStreamSynchronize(c->stream));   // the host vectors above are the copies' sources
+    dfree(c, d_ck);
+    dfree(c, d_cs);
+    dfree(c, hp_lo);
+    dfree(c, hp_off);
+    dfree(c, hp_tot);
+}
+
 // merge join on sorted inputs; returns pair count and flags.  R->match receives each R row's
 // number of S partners (the mode-0 driver counts come from it for free)
 void merge_sorted(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS, uint32_t* oflags) {
@@ -983,6 +1144,7 @@ void merge_sorted(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_l
     }
     if (nR == 0 || nS == 0) {
         if (nR) QE_HIP(hipMemsetAsync(R->match, 0, nR * 4, c->stream));
+        R->flags |= QE_PAIRS_MATCHED;
         outR->d = dalloc_t<uint32_t>(c, 1);
         outS->d = dalloc_t<uint32_t>(c, 1);
         outR->cap = outS->cap = 0;
@@ -1004,6 +1166,8 @@ void merge_sorted(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_l
     const uint64_t cap = nR + nS;
     uint32_t* oR = dalloc_t<uint32_t>(c, cap);
     uint32_t* oS = dalloc_t<uint32_t>(c, cap);
+    uint32_t* heavy = dalloc_t<uint32_t>(c, nt);
+    QE_HIP(hipMemsetAsync(c->d_scratch + 19, 0, 8, c->stream));
     {
         LBSlot s = lb_acquire(c, nt);
         Timed t(c, "mj_fused", 12.0 * nR + 12.0 * nS + 4.0 * nR);   // + 8 B per pair, added below
@@ -1013,20 +1177,41 @@ void merge_sorted(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_l
         if (key32)
             hipLaunchKernelGGL(mj_fused<MJShared32>, dim3(nt), dim3(MJB), 0, c->stream, R->key, R->val, nR, S->key,
                                S->val, nS, win, tc, R->match, oR, oS, cap, d_flags, s.status, s.ticket, s.epoch, nt,
-                               c->d_scratch + 17);
+                               c->d_scratch + 17, heavy, (uint32_t*)(c->d_scratch + 19));
         else
             hipLaunchKernelGGL(mj_fused<MJShared64>, dim3(nt), dim3(MJB), 0, c->stream, R->key, R->val, nR, S->key,
                                S->val, nS, win, tc, R->match, oR, oS, cap, d_flags, s.status, s.ticket, s.epoch, nt,
-                               c->d_scratch + 17);
+                               c->d_scratch + 17, heavy, (uint32_t*)(c->d_scratch + 19));
         QE_HIP(hipGetLastError());
     }
-    uint64_t h[2];
-    read_words(c, c->d_scratch + 16, h, 2);
-    const uint64_t P = h[1];
+    R->flags |= QE_PAIRS_MATCHED;
+    uint64_t h[4];
+    read_words(c, c->d_scratch + 16, h, 4);
+    uint64_t P = h[1];
     *oflags = (uint32_t)h[0];
-    if (c->prof && !c->pending.empty() && P <= cap) c->pending.back().bytes += 8.0 * P;
+    const uint32_t nheavy = (uint32_t)h[3];
+    const bool exact = P <= cap && !(h[0] & MJF_OVF);
+    if (c->prof && !c->pending.empty() && exact) c->pending.back().bytes += 8.0 * P;
+    if (!exact || nheavy) {   // exact u64 offsets (and total) from the per-tile counts
+        hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, c->stream, tc, (uint64_t)nt, c->d_scratch + 18);
+        QE_HIP(hipGetLastError());
+        P = read_u64(c, c->d_scratch + 18);
+    }
     outR->n = outS->n = P;
-    if (P <= cap) {
+    if (P > c->mat_limit) {   // R->match stays valid: the caller may take the aggregate form
+        dfree(c, oR);
+        dfree(c, oS);
+        dfree(c, win);
+        dfree(c, tc);
+        dfree(c, heavy);
+        outR->d = outS->d = nullptr;
+        outR->cap = outS->cap = 0;
+        char msg[160];
+        snprintf(msg, sizeof msg, "merge join of %llu pairs exceeds the materialisation limit %llu",
+                 (unsigned long long)P, (unsigned long long)c->mat_limit);
+        throw Error(QE_ETOOBIG, msg);
+    }
+    if (exact) {
         outR->d = oR;
         outS->d = oS;
         outR->cap = outS->cap = cap;
@@ -1037,14 +1222,59 @@ void merge_sorted(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_l
         outS->d = dalloc_t<uint32_t>(c, P);
         outR->cap = outS->cap = P;
         Timed t(c, "mj_write", 12.0 * nR + 12.0 * nS + 8.0 * P);
-        hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, c->stream, tc, (uint64_t)nt, c->d_scratch + 18);
-        QE_HIP(hipGetLastError());
         hipLaunchKernelGGL(mj_tile<1>, dim3(nt), dim3(MJB), 0, c->stream, R->key, R->val, nR, S->key, S->val, nS, win,
                            tc, outR->d, outS->d, nullptr, nullptr, nullptr);
         QE_HIP(hipGetLastError());
     }
+    if (nheavy) emit_deferred(c, R, S, win, heavy, nheavy, tc, outR->d, outS->d);
+    dfree(c, heavy);
     dfree(c, win);
     dfree(c, tc);
+}
+
+// count-only merge pass: A->match[i] = number of B rows with A's key (both sorted); returns
+// the exact pair count.  The fused kernel runs with no output room, so it stores nothing.
+uint64_t merge_count_side(qe_ctx* c, qe_pairs* A, const qe_pairs* B) {
+    const uint64_t nA = A->n, nB = B->n;
+    if (!A->match && nA) {
+        A->match = dalloc_t<uint32_t>(c, nA);
+        A->owns |= 4;
+    }
+    if (nA == 0) return 0;
+    if (nB == 0) {
+        QE_HIP(hipMemsetAsync(A->match, 0, nA * 4, c->stream));
+        return 0;
+    }
+    const uint32_t nt = (uint32_t)((nA + MJ_TILE - 1) / MJ_TILE);
+    uint64_t* win = dalloc_t<uint64_t>(c, 2 * (uint64_t)nt);
+    uint64_t* tc = dalloc_t<uint64_t>(c, nt);
+    uint32_t* sink = dalloc_t<uint32_t>(c, 1);
+    uint32_t* d_flags = (uint32_t*)(c->d_scratch + 16);
+    QE_HIP(hipMemsetAsync(d_flags, 0, 4, c->stream));
+    {
+        Timed t(c, "mj_count", 12.0 * nA + 12.0 * nB + 4.0 * nA);
+        hipLaunchKernelGGL(mj_partition, dim3((nt + 255) / 256), dim3(256), 0, c->stream, A->key, nA, B->key, nB, nt,
+                           win);
+        QE_HIP(hipGetLastError());
+        LBSlot s = lb_acquire(c, nt);
+        const bool key32 = (A->flags & QE_PAIRS_BITS) && ((A->kor & ~A->kand) >> 32) == 0;
+        if (key32)
+            hipLaunchKernelGGL(mj_fused<MJShared32>, dim3(nt), dim3(MJB), 0, c->stream, A->key, A->val, nA, B->key,
+                               B->val, nB, win, tc, A->match, sink, sink, 0ull, d_flags, s.status, s.ticket, s.epoch,
+                               nt, c->d_scratch + 17, nullptr, nullptr);
+        else
+            hipLaunchKernelGGL(mj_fused<MJShared64>, dim3(nt), dim3(MJB), 0, c->stream, A->key, A->val, nA, B->key,
+                               B->val, nB, win, tc, A->match, sink, sink, 0ull, d_flags, s.status, s.ticket, s.epoch,
+                               nt, c->d_scratch + 17, nullptr, nullptr);
+        QE_HIP(hipGetLastError());
+        hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, c->stream, tc, (uint64_t)nt, c->d_scratch + 18);
+        QE_HIP(hipGetLastError());
+    }
+    const uint64_t P = read_u64(c, c->d_scratch + 18);
+    dfree(c, win);
+    dfree(c, tc);
+    dfree(c, sink);
+    return P;
 }
 
 static void prefix_max(qe_ctx* c, const uint64_t* x, uint64_t n, uint64_t* out) {
@@ -1263,6 +1493,7 @@ int qe_gather_pairs(qe_ctx* c, qe_col col, const qe_list* rows, qe_pairs* out) {
 int qe_sort_pairs(qe_ctx* c, qe_pairs* p) {
     QE_API_BEGIN(c)
     if (p->flags & PF_SORTED) return 0;
+    p->flags &= ~QE_PAIRS_MATCHED;
     uint64_t bits[2] = {p->kor, p->kand};
     SortOut so = radix_sort_u64(c, p->key, p->val, p->n, true, (p->flags & QE_PAIRS_BITS) ? bits : nullptr);
     if (so.keys_new) {
@@ -1295,6 +1526,45 @@ int qe_merge_join(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_l
     else merge_sequential(c, R, S, outR, outS);
     outR->flags = ((R->flags & PF_DISTINCT) && sorted && !(fl & MJF_R_FANOUT)) ? QE_LIST_DISTINCT : 0;
     outS->flags = ((S->flags & PF_DISTINCT) && sorted && !(fl & MJF_S_DUP)) ? QE_LIST_DISTINCT : 0;
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_merge_join_counts(qe_ctx* c, qe_pairs* R, qe_pairs* S, uint64_t* pairs) {
+    QE_API_BEGIN(c)
+    if (!pairs_sorted(c, R) || !pairs_sorted(c, S)) throw Error(QE_EINVAL, "qe_merge_join_counts needs sorted inputs");
+    const bool r_done = (R->flags & QE_PAIRS_MATCHED) && (R->match || R->n == 0);
+    const uint64_t Q = merge_count_side(c, S, R);
+    if (!r_done) {
+        const uint64_t P = merge_count_side(c, R, S);
+        if (P != Q) throw Error(QE_EINVAL, "internal: the two count passes disagree");
+    }
+    R->flags |= QE_PAIRS_MATCHED;
+    S->flags |= QE_PAIRS_MATCHED;
+    *pairs = Q;
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_checksum_weighted(qe_ctx* c, qe_col col, const qe_pairs* p, uint64_t* sum) {
+    QE_API_BEGIN(c)
+    if (p->n && !p->match) throw Error(QE_EINVAL, "qe_checksum_weighted needs match counts");
+    unsigned long long* d = (unsigned long long*)(c->d_scratch + 40);
+    QE_HIP(hipMemsetAsync(d, 0, 8, c->stream));
+    if (p->n) {
+        Timed t(c, "checksum_weighted", (p->val ? 8.0 : 4.0) * p->n);
+        hipLaunchKernelGGL(checksum_weighted_kernel, dim3(grid_for(p->n, 256 * 16, 8192)), dim3(256), 0, c->stream,
+                           col.d, p->val, p->match, p->n, d);
+        QE_HIP(hipGetLastError());
+    }
+    *sum = read_u64(c, (const uint64_t*)d);
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_set_materialize_limit(qe_ctx* c, uint64_t pairs) {
+    QE_API_BEGIN(c)
+    c->mat_limit = pairs;
     return 0;
     QE_API_END(c)
 }

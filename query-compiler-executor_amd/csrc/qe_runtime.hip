@@ -182,6 +182,129 @@ __global__ void __launch_bounds__(256) gen_column_kernel(uint64_t* out, uint64_t
     }
 }
 
+// ---- Zipf keys (C5): inverse CDF through a guide table, then a seeded Feistel permutation ----
+constexpr int ZG_BITS = 24;                       // guide: 2^24 + 1 entries
+constexpr uint64_t ZG_M = 1ull << ZG_BITS;
+
+// guide[j] = #{r : cdf[r] < j / M}: a draw u in [j/M, (j+1)/M) has its rank in [guide[j], guide[j+1]]
+__global__ void __launch_bounds__(256) zipf_guide_kernel(const double* __restrict__ cdf, uint64_t d,
+                                                         uint64_t* __restrict__ guide) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > ZG_M) return;
+    const double t = (double)j * (1.0 / (double)ZG_M);
+    uint64_t lo = 0, hi = d;                      // first r with cdf[r] >= t
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (cdf[mid] < t) lo = mid + 1;
+        else hi = mid;
+    }
+    guide[j] = lo;
+}
+
+// 4 rounds on b-bit words (b even), cycle-walked into [0, d): qe/datagen.py feistel_perm
+__device__ __forceinline__ uint64_t feistel_perm(uint64_t x, uint64_t d, uint32_t half, uint64_t k0, uint64_t k1,
+                                                 uint64_t k2, uint64_t k3) {
+    const uint64_t mask = (1ull << half) - 1;
+    do {
+        uint64_t lo = x & mask, hi = x >> half;
+        uint64_t t;
+        t = hi ^ (splitmix64(lo + k0) & mask); hi = lo; lo = t;
+        t = hi ^ (splitmix64(lo + k1) & mask); hi = lo; lo = t;
+        t = hi ^ (splitmix64(lo + k2) & mask); hi = lo; lo = t;
+        t = hi ^ (splitmix64(lo + k3) & mask); hi = lo; lo = t;
+        x = (hi << half) | lo;
+    } while (x >= d);
+    return x;
+}
+
+// deterministic Zipf CDF: w_r = (r + 1)^-theta summed in a fixed order -- 16 consecutive terms
+// per thread, a fixed shuffle tree per wave and block, one thread per 4096-term block prefix --
+// so every run on the device builds the same table (a library scan with a decoupled look-back
+// adds in a timing-dependent order and changes the low bits run to run)
+constexpr int ZC_ITEMS = 16, ZC_B = 256, ZC_CHUNK = ZC_ITEMS * ZC_B;
+
+__device__ __forceinline__ double zipf_w(uint64_t r, double theta) { return pow((double)(r + 1), -theta); }
+
+__device__ __forceinline__ double wave_incl_scan_f64(double v) {
+    const int l = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const double o = __shfl_up(v, d, 64);
+        if (l >= d) v += o;
+    }
+    return v;
+}
+
+__global__ void __launch_bounds__(ZC_B) zipf_block_sums(uint64_t d, double theta, double* __restrict__ bsum) {
+    __shared__ double red[ZC_B / 64];
+    const uint64_t i0 = (uint64_t)blockIdx.x * ZC_CHUNK + (uint64_t)threadIdx.x * ZC_ITEMS;
+    double s = 0;
+    for (int j = 0; j < ZC_ITEMS; j++)
+        if (i0 + j < d) s += zipf_w(i0 + j, theta);
+    s = wave_incl_scan_f64(s);
+    if ((threadIdx.x & 63) == 63) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) bsum[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+__global__ void __launch_bounds__(1) zipf_block_prefix(double* __restrict__ bsum, uint64_t nb) {
+    double run = 0;   // serial over <= 2.5e5 block sums: fixed order, ~1 ms at D = 1e9
+    for (uint64_t b = 0; b < nb; b++) {
+        const double v = bsum[b];
+        bsum[b] = run;
+        run += v;
+    }
+}
+
+__global__ void __launch_bounds__(ZC_B) zipf_block_scan(uint64_t d, double theta, const double* __restrict__ bpre,
+                                                        double* __restrict__ cdf) {
+    __shared__ double red[ZC_B / 64];
+    const uint64_t i0 = (uint64_t)blockIdx.x * ZC_CHUNK + (uint64_t)threadIdx.x * ZC_ITEMS;
+    double w[ZC_ITEMS], s = 0;
+    for (int j = 0; j < ZC_ITEMS; j++) {
+        w[j] = i0 + j < d ? zipf_w(i0 + j, theta) : 0.0;
+        s += w[j];
+    }
+    const double inc = wave_incl_scan_f64(s);
+    if ((threadIdx.x & 63) == 63) red[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    double run = bpre[blockIdx.x];
+    for (int q = 0; q < (int)(threadIdx.x >> 6); q++) run += red[q];
+    run += inc - s;
+    for (int j = 0; j < ZC_ITEMS; j++) {
+        run += w[j];
+        if (i0 + j < d) cdf[i0 + j] = run;
+    }
+}
+
+// cdf /= total (total: a copy of the last entry, which becomes exactly 1.0)
+__global__ void __launch_bounds__(256) zipf_normalise(uint64_t d, double* __restrict__ cdf,
+                                                      const double* __restrict__ total) {
+    const double last = *total;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < d; i += stride) cdf[i] = cdf[i] / last;
+}
+
+__global__ void __launch_bounds__(256) gen_zipf_kernel(uint64_t* __restrict__ out, uint64_t rows, uint64_t base,
+                                                       uint64_t row_start, const double* __restrict__ cdf,
+                                                       const uint64_t* __restrict__ guide, uint64_t d, uint32_t half,
+                                                       uint64_t k0, uint64_t k1, uint64_t k2, uint64_t k3) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows; i += stride) {
+        const uint64_t v = splitmix64(base + row_start + i);
+        const double u = (double)(v >> 11) * (1.0 / 9007199254740992.0);
+        const uint64_t j = (uint64_t)(u * (double)ZG_M);          // exact: M is a power of two
+        uint64_t lo = guide[j], hi = guide[j + 1];                  // rank in [lo, hi]
+        while (lo < hi) {                                           // first r >= lo with cdf[r] > u
+            const uint64_t mid = (lo + hi) >> 1;
+            if (cdf[mid] <= u) lo = mid + 1;
+            else hi = mid;
+        }
+        const uint64_t rank = lo < d ? lo : d - 1;
+        out[i] = feistel_perm(rank, d, half, k0, k1, k2, k3);
+    }
+}
+
 }  // namespace qe
 
 using namespace qe;
@@ -217,6 +340,7 @@ qe_ctx* qe_init(int device) {
         QE_HIP(hipMalloc(&c->d_scratch, 64 * sizeof(uint64_t)));
         QE_HIP(hipHostMalloc((void**)&c->h_scratch, 64 * sizeof(uint64_t), hipHostMallocDefault));
         QE_HIP(hipStreamSynchronize(c->stream));
+        if (const char* e = getenv("QE_MAT_LIMIT")) c->mat_limit = strtoull(e, nullptr, 0);
     } catch (const Error& e) {
         fprintf(stderr, "qe_init(%d): %s\n", device, e.what());
         delete c;
@@ -293,9 +417,23 @@ int qe_gen_relation(qe_ctx* c, uint64_t rows, uint64_t ncols, const int* kinds, 
         QE_HIP(hipMalloc(&d, std::max<uint64_t>(rows, 1) * sizeof(uint64_t)));
         uint64_t base = (seed << 40) | ((uint64_t)gen_rel << 36) | ((uint64_t)j << 32);
         if (kinds[j] == 0 && mods[j] == 0) throw Error(QE_EINVAL, "mod 0");
-        if (rows)
+        if (kinds[j] == 2) {
+            if (!c->zipf_cdf || mods[j] != c->zipf_domain) throw Error(QE_EINVAL, "no Zipf table for this domain");
+            uint32_t b = 2;
+            while (b < 64 && ((c->zipf_domain - 1) >> b) != 0) b++;
+            b += b & 1;
+            uint64_t k[4];
+            for (int r = 0; r < 4; r++) k[r] = (c->zipf_perm_seed << 40) | (15ull << 36) | ((uint64_t)r << 32);
+            if (rows)
+                hipLaunchKernelGGL(gen_zipf_kernel, dim3(grid_for(rows, 256 * 8, 8192)), dim3(256), 0, c->stream, d,
+                                   rows, base, row_start, c->zipf_cdf, c->zipf_guide, c->zipf_domain, b / 2, k[0],
+                                   k[1], k[2], k[3]);
+        } else if (kinds[j] != 0 && kinds[j] != 1) {
+            throw Error(QE_EINVAL, "unknown column kind");
+        } else if (rows) {
             hipLaunchKernelGGL(gen_column_kernel, dim3(grid_for(rows, 256 * 8, 8192)), dim3(256), 0, c->stream, d,
                                rows, base, row_start, kinds[j], mods[j]);
+        }
         QE_HIP(hipGetLastError());
         r.cols.push_back(d);
     }
@@ -316,6 +454,55 @@ int qe_set_last_result_rows(qe_ctx* c, uint64_t rows) {
     if (!c) return QE_EINVAL;
     c->last_result_rows = rows;
     return 0;
+}
+
+int qe_set_zipf(qe_ctx* c, uint64_t domain, double theta, uint64_t perm_seed) {
+    QE_API_BEGIN(c)
+    if (domain == 0) throw Error(QE_EINVAL, "empty Zipf domain");
+    double* cdf = dalloc_t<double>(c, domain);
+    const uint64_t nb = (domain + ZC_CHUNK - 1) / ZC_CHUNK;
+    double* bsum = dalloc_t<double>(c, nb + 1);
+    hipLaunchKernelGGL(zipf_block_sums, dim3((unsigned)nb), dim3(ZC_B), 0, c->stream, domain, theta, bsum);
+    QE_HIP(hipGetLastError());
+    hipLaunchKernelGGL(zipf_block_prefix, dim3(1), dim3(1), 0, c->stream, bsum, nb);
+    QE_HIP(hipGetLastError());
+    hipLaunchKernelGGL(zipf_block_scan, dim3((unsigned)nb), dim3(ZC_B), 0, c->stream, domain, theta, bsum, cdf);
+    QE_HIP(hipGetLastError());
+    QE_HIP(hipMemcpyAsync(bsum + nb, cdf + domain - 1, 8, hipMemcpyDeviceToDevice, c->stream));
+    hipLaunchKernelGGL(zipf_normalise, dim3(grid_for(domain, 256 * 8, 8192)), dim3(256), 0, c->stream, domain, cdf,
+                       bsum + nb);
+    QE_HIP(hipGetLastError());
+    const int rc = qe_set_zipf_table(c, cdf, domain, perm_seed);
+    dfree(c, bsum);
+    if (rc != 0) {
+        dfree(c, cdf);
+        return rc;
+    }
+    c->zipf_owned = cdf;
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_set_zipf_table(qe_ctx* c, const double* d_cdf, uint64_t domain, uint64_t perm_seed) {
+    QE_API_BEGIN(c)
+    if (c->zipf_guide) dfree(c, c->zipf_guide);
+    if (c->zipf_owned && c->zipf_owned != d_cdf) dfree(c, c->zipf_owned);
+    c->zipf_owned = nullptr;
+    c->zipf_guide = nullptr;
+    c->zipf_cdf = nullptr;
+    c->zipf_domain = 0;
+    if (!d_cdf) return 0;
+    if (domain == 0) throw Error(QE_EINVAL, "empty Zipf domain");
+    c->zipf_guide = dalloc_t<uint64_t>(c, ZG_M + 1);
+    hipLaunchKernelGGL(zipf_guide_kernel, dim3((unsigned)((ZG_M + 1 + 255) / 256)), dim3(256), 0, c->stream, d_cdf,
+                       domain, c->zipf_guide);
+    QE_HIP(hipGetLastError());
+    c->zipf_cdf = d_cdf;
+    c->zipf_domain = domain;
+    c->zipf_perm_seed = perm_seed;
+    sync(c);
+    return 0;
+    QE_API_END(c)
 }
 
 int qe_relation_count(qe_ctx* c) { return c ? (int)c->rels.size() : QE_EINVAL; }

@@ -56,6 +56,9 @@ typedef struct {
     size_t nlists, caplists;
     int dle;                     /* dead-list elimination on (QE_DLE=0 turns it off) */
     const uint8_t* live;         /* live[b]: binding b is read by a later predicate or a select */
+    const uint8_t* pred_live;    /* pred_live[b]: binding b is read by a later predicate */
+    struct agg_side { const qe_list* l; qe_pairs p; } *aggs;   /* unmaterialised join sides */
+    size_t naggs, capaggs;
 } exec_t;
 
 /* Dead-list elimination.  fix_all re-materialises every other entry of the entity
@@ -64,6 +67,13 @@ typedef struct {
  * join_payloads looks at (the |edit| < |last| guard) -- is kept exactly.  Such a list carries
  * QE_LIST_DEAD (host-only) and no data; reading one is an internal error, not a fallback. */
 #define QE_LIST_DEAD 0x40000000u
+
+/* Aggregate join results.  A sorted merge join of more pairs than the materialisation limit
+ * (QE_ETOOBIG; the reference's DArray cannot hold them, src/DArray.h:14-15) whose lists only
+ * print_sums reads afterwards keeps its sorted inputs with per-row partner counts instead: the
+ * list of a side has length P and checksum sum_i col[val[i]] * match[i] (aggregate push-down,
+ * SURVEY.md §0.7).  Such a list carries QE_LIST_AGG and no data. */
+#define QE_LIST_AGG 0x20000000u
 
 static void need_data(exec_t* x, const qe_list* l);
 
@@ -82,6 +92,7 @@ static void chk(exec_t* x, int rc) {
 
 static void need_data(exec_t* x, const qe_list* l) {
     if (l && (l->flags & QE_LIST_DEAD)) fail(x, QE_EINVAL, "internal: a dead-eliminated list was read");
+    if (l && (l->flags & QE_LIST_AGG)) fail(x, QE_EINVAL, "internal: an aggregate join list was read");
 }
 
 static qe_list* new_list(exec_t* x) {
@@ -95,6 +106,8 @@ static qe_list* new_list(exec_t* x) {
 }
 
 static void free_lists(exec_t* x) {
+    for (size_t i = 0; i < x->naggs; i++) qe_pairs_free(x->q, &x->aggs[i].p);
+    x->naggs = 0;
     for (size_t i = 0; i < x->nlists; i++) {
         qe_list_free(x->q, x->lists[i]);
         free(x->lists[i]);
@@ -374,6 +387,59 @@ static int build_relations(exec_t* x, const query_t* q, const pred_t* p, mra_t* 
     return SCAN_JOIN;
 }
 
+/* fix_all on this entity would re-materialise nothing: it holds no other relation's entry */
+static int fix_all_trivial(const mra_t* M, exists_t ex, uint64_t relR, uint64_t relS) {
+    if (ex.idx == -1) return 1;
+    const entity_t* E = M->v[ex.ent];
+    for (size_t i = 0; i < E->n; i++)
+        if (E->e[i].relation != relR && E->e[i].relation != relS) return 0;
+    return 1;
+}
+
+/* the join's lists may stay unmaterialised: no later predicate reads either binding and
+ * update_mid_results only stores them (no join_payloads needs their content) */
+static int aggregate_ok(exec_t* x, const query_t* q, const pred_t* p, const mra_t* M, int v) {
+    if (x->pred_live[p->frel] || x->pred_live[p->srel]) return 0;
+    const uint64_t relR = q->rels[p->frel], relS = q->rels[p->srel];
+    const exists_t exR = relation_exists(M, relR, p->frel), exS = relation_exists(M, relS, p->srel);
+    switch (v) {
+    case CLASSIC_JOIN: return fix_all_trivial(M, exR, relR, relS) && fix_all_trivial(M, exS, relR, relS);
+    case JOIN_SORT_LHS: return fix_all_trivial(M, exS, relR, relS);
+    case JOIN_SORT_RHS: return fix_all_trivial(M, exR, relR, relS);
+    }
+    return 0;
+}
+
+static void keep_agg(exec_t* x, qe_list* l, qe_pairs* p, uint64_t P) {
+    if (x->naggs == x->capaggs) {
+        x->capaggs = x->capaggs ? 2 * x->capaggs : 8;
+        x->aggs = realloc(x->aggs, x->capaggs * sizeof(*x->aggs));
+    }
+    x->aggs[x->naggs].l = l;
+    x->aggs[x->naggs].p = *p;
+    x->naggs++;
+    memset(p, 0, sizeof(*p));        /* ownership moved: execute_join's free is a no-op */
+    l->d = NULL;
+    l->n = P;
+    l->cap = 0;
+    l->flags = QE_LIST_AGG;
+}
+
+/* qe_merge_join, or its aggregate form for a join too large to materialise */
+static void merge(exec_t* x, const query_t* q, const pred_t* p, const mra_t* M, int v, qe_pairs rel[2],
+                  jres_t* jr) {
+    int rc = qe_merge_join(x->q, &rel[0], &rel[1], jr->res[0], jr->res[1]);
+    if (rc != QE_ETOOBIG) {
+        chk(x, rc);
+        return;
+    }
+    if (!aggregate_ok(x, q, p, M, v)) chk(x, rc);
+    uint64_t P = 0;
+    chk(x, qe_merge_join_counts(x->q, &rel[0], &rel[1], &P));
+    keep_agg(x, jr->res[0], &rel[0], P);
+    keep_agg(x, jr->res[1], &rel[1], P);
+}
+
 /* execute_join (src/join.c:630-679) */
 static int execute_join(exec_t* x, const query_t* q, const pred_t* p, mra_t* M) {
     qe_pairs rel[2];
@@ -392,17 +458,17 @@ static int execute_join(exec_t* x, const query_t* q, const pred_t* p, mra_t* M) 
     case CLASSIC_JOIN:
         chk(x, qe_sort_pairs(x->q, &rel[0]));
         chk(x, qe_sort_pairs(x->q, &rel[1]));
-        chk(x, qe_merge_join(x->q, &rel[0], &rel[1], jr.res[0], jr.res[1]));
+        merge(x, q, p, M, v, rel, &jr);
         break;
     case JOIN_SORT_LHS:
         chk(x, qe_sort_pairs(x->q, &rel[0]));
         ensure_sorted_flag(x, &rel[1]);
-        chk(x, qe_merge_join(x->q, &rel[0], &rel[1], jr.res[0], jr.res[1]));
+        merge(x, q, p, M, v, rel, &jr);
         break;
     case JOIN_SORT_RHS:
         chk(x, qe_sort_pairs(x->q, &rel[1]));
         ensure_sorted_flag(x, &rel[0]);
-        chk(x, qe_merge_join(x->q, &rel[0], &rel[1], jr.res[0], jr.res[1]));
+        merge(x, q, p, M, v, rel, &jr);
         break;
     case SCAN_JOIN:
         chk(x, qe_scan_join(x->q, &rel[0], &rel[1], jr.res[0], jr.res[1]));
@@ -469,8 +535,15 @@ static void print_sums(exec_t* x, const query_t* q, const mra_t* M) {
             fputs("NULL ", x->out);
         } else {
             uint64_t s = 0;
-            need_data(x, l);
-            chk(x, qe_checksum(x->q, column(x, relation, colno), l, &s));
+            const qe_pairs* agg = NULL;
+            for (size_t a = 0; a < x->naggs && (l->flags & QE_LIST_AGG); a++)
+                if (x->aggs[a].l == l) agg = &x->aggs[a].p;
+            if (agg) {
+                chk(x, qe_checksum_weighted(x->q, column(x, relation, colno), agg, &s));
+            } else {
+                need_data(x, l);
+                chk(x, qe_checksum(x->q, column(x, relation, colno), l, &s));
+            }
             fprintf(x->out, "%lu ", (unsigned long)s);
         }
     }
@@ -617,21 +690,25 @@ static void execute_query(exec_t* x, query_t* q) {
     memset(&M, 0, sizeof(M));
     int ok = query_valid(x, q);   /* out-of-range ids are undefined in the reference: no line */
     uint8_t* live = (uint8_t*)calloc(q->nrels ? q->nrels : 1, 1);
+    uint8_t* pred_live = (uint8_t*)calloc(q->nrels ? q->nrels : 1, 1);
     for (size_t i = 0; ok && i < q->npreds; i++) {
-        /* bindings read after predicate i: later predicates and the selects */
-        memset(live, 0, q->nrels ? q->nrels : 1);
-        for (size_t s = 0; s < q->nsel; s++) live[q->sel[2 * s]] = 1;
+        /* bindings read after predicate i: later predicates, and those or the selects */
+        memset(pred_live, 0, q->nrels ? q->nrels : 1);
         for (size_t j = i + 1; j < q->npreds; j++) {
-            live[q->preds[j].frel] = 1;
-            if (q->preds[j].type == 0) live[q->preds[j].srel] = 1;
+            pred_live[q->preds[j].frel] = 1;
+            if (q->preds[j].type == 0) pred_live[q->preds[j].srel] = 1;
         }
+        memcpy(live, pred_live, q->nrels ? q->nrels : 1);
+        for (size_t s = 0; s < q->nsel; s++) live[q->sel[2 * s]] = 1;
         x->live = live;
+        x->pred_live = pred_live;
         const pred_t* p = &q->preds[i];
         int r = p->type == 1 ? execute_filter(x, q, p, &M) : execute_join(x, q, p, &M);
         if (r == -1) ok = 0;
     }
-    x->live = NULL;
+    x->live = x->pred_live = NULL;
     free(live);
+    free(pred_live);
     if (ok) print_sums(x, q, &M);
     mra_free(&M);
     free_lists(x);
@@ -706,6 +783,7 @@ int qe_run_queries(qe_ctx* ctx, const char* text, char** out, size_t* outlen) {
     }
     free(qs);
     free(x.lists);
+    free(x.aggs);
     fclose(x.out);
     return rc;
 }

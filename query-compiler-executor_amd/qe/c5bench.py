@@ -1,0 +1,149 @@
+"""C5: the skewed 2-relation join (BASELINE.json configs[4]) -- §8(f) row f-2.
+
+Workload: qe.datagen.c5_spec(N): r0 = (v % N, Zipf key, u32), r1 = (Zipf key, v % N, u32) with
+N = 1e9 rows per side, Zipf(0.9) over D = N through one shared rank->key permutation, generated
+in HBM (libqe builds the Zipf CDF on the device in a fixed summation order, so every run draws
+the same keys, and samples it with its kind-2 generator).  Query `0 1|0.1=1.0|0.2 1.2`.
+
+The join has P ~ 3.8e14 pairs: no machine materialises that, and the reference's DArray caps a
+list at INT32_MAX elements (src/DArray.h:14-15).  libqe's executor therefore takes the aggregate
+form of the merge (qe_merge_join_counts: each row's partner count on both sides) and prints
+sum_i col[rowid_i] * count_i per select, which is exactly the checksum of the list the
+reference would build (proved against the reference at 20 k rows in §9.5 and
+checked here against the C5 goldens and against numpy aggregate truth at 1e8 rows).
+One step = one execution of the query (both sorts, both count passes, both checksums).
+`value` = pairs of the join (joined tuples, counted not materialised) per second.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import time
+
+from . import datagen as dg
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+METRIC = "joined tuples/sec + achieved HBM GB/s, 4-rel chain join, 1/2/4/8 MI355X"
+
+
+def gen_c5(ctx, rows: int, row_start: int = 0, total_rows: int | None = None) -> list:
+    """relations r0, r1 of c5_spec(total_rows) -- rows [row_start, row_start + rows) of each.
+    The Zipf CDF is built by libqe in a fixed summation order: the same keys on every run."""
+    n = total_rows or rows
+    specs = dg.c5_spec(n)
+    ctx.set_zipf(n, dg.C5_THETA, dg.C5_PERM_SEED)
+    try:
+        for r, sp in enumerate(specs):
+            ctx.gen_relation(rows, sp.kinds, seed=dg.C5_SEED, gen_rel=r, row_start=row_start)
+    finally:
+        ctx.set_zipf_table(0, 0, 0)
+    return specs
+
+
+def column_prefix(ctx, rel: int, col: int, m: int):
+    """the first m values of a device column, on the host"""
+    import numpy as np
+    from . import lib
+    c = ctx.column(rel, col)
+    p = lib.Pairs()
+    p.key, p.val, p.match, p.n = c.d, None, None, min(m, c.n)
+    out = np.empty(p.n, dtype=np.uint64)
+    ctx._chk(ctx.lib.qe_pairs_to_host(ctx.h, C.byref(p), out.ctypes.data, None))
+    return out
+
+
+def cpu_sample(ctx, sample_rows: int, budget_note: str = "") -> dict:
+    """oracle/cpu_ref, one core, on the first `sample_rows` rows of both relations (same Zipf
+    columns, so the heavy keys collide as at full size; the join is small enough to
+    materialise).  The GPU runs the same sample through both of its paths for a byte check."""
+    from . import lib
+    cols = [[column_prefix(ctx, r, c, sample_rows) for c in range(3)] for r in range(2)]
+    so = os.path.join(ROOT, "oracle", "build", "libcpuref.so")
+    cl = C.CDLL(so)
+    cl.cpuref_create.restype = C.c_void_p
+    cl.cpuref_add_relation.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_void_p)]
+    cl.cpuref_run_str.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+    cl.cpuref_destroy.argtypes = [C.c_void_p]
+    h = cl.cpuref_create()
+    keep = []
+    for cs in cols:
+        arr = (C.c_void_p * 3)(*[c.ctypes.data for c in cs])
+        keep.append(arr)
+        cl.cpuref_add_relation(h, sample_rows, 3, arr)
+    try:
+        os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
+    except Exception:
+        pass
+    out, n = C.c_void_p(), C.c_size_t()
+    t0 = time.perf_counter()
+    cl.cpuref_run_str(h, dg.C5_QUERY.encode(), C.byref(out), C.byref(n))
+    dt = time.perf_counter() - t0
+    cpu_out = C.string_at(out, n.value).decode("latin-1")
+    cl.cpuref_destroy(h)
+    # the same sample on the GPU: materialised (default limit) and aggregate (limit 0)
+    g = lib.Ctx(ctx.device) if hasattr(ctx, "device") else lib.Ctx(0)
+    for cs in cols:
+        g.load_relation(cs)
+    mat, _ = g.run(dg.C5_QUERY)
+    pairs = g.last_result_rows()
+    g.set_materialize_limit(0)
+    agg, _ = g.run(dg.C5_QUERY)
+    g.close()
+    return {"value": round(pairs / dt, 1), "unit": "joined tuples/s", "cores": 1, "kind": "port",
+            "sample": f"first {sample_rows} rows of both C5 relations (same device-made Zipf columns), "
+                      f"{pairs} pairs materialised by oracle/cpu_ref single-threaded in {dt:.2f} s{budget_note}",
+            "seconds": round(dt, 3), "pairs": pairs,
+            "input_rows_per_s": round(2 * sample_rows / dt, 1),
+            "parity_with_gpu": cpu_out == mat == agg}
+
+
+def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
+    import torch
+
+    from . import lib
+    torch.cuda.init()
+    rows = args.rows or dg.C5_ROWS
+    ctx = lib.Ctx(0)
+    t0 = time.time()
+    gen_c5(ctx, rows)
+    log(f"[c5] 2 x {rows} rows (Zipf {dg.C5_THETA}) in HBM in {time.time() - t0:.1f}s")
+    out = None
+    for _ in range(args.warmup):
+        out, rc = ctx.run(dg.C5_QUERY)
+    ctx.set_profiling(True)
+    ctx.reset_stats()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out, rc = ctx.run(dg.C5_QUERY)
+    ctx.sync()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    pairs = ctx.last_result_rows()
+    stats = ctx.kernel_stats()
+    ctx.set_profiling(False)
+    kern = sorted(stats.items(), key=lambda kv: -kv[1]["ms"])
+    ms = dt / args.steps * 1e3
+    res = {
+        "metric": METRIC, "value": round(pairs * args.steps / dt, 1), "unit": "joined tuples/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic: qe.datagen.c5_spec(%d) generated in HBM (seed %d, Zipf %.1f, shared permutation)"
+                % (rows, dg.C5_SEED, dg.C5_THETA),
+        "config": {"workload": "C5: 2-relation join, %d rows/side, Zipf theta=%.1f keys, query %s"
+                               % (rows, dg.C5_THETA, dg.C5_QUERY.strip()),
+                   "pairs": pairs, "materialised": False,
+                   "path": "libqe faithful executor: sort both sides, qe_merge_join_counts (aggregate form: "
+                           "P > INT32_MAX), qe_checksum_weighted",
+                   "input_rows_per_s": round(2 * rows * args.steps / dt, 1),
+                   "stdout": out, "parallelism": "single GPU"},
+        "roofline": roofline_fn(stats, traffic_fn() if traffic_fn else None) if roofline_fn else None,
+        "stages": {k: {"ms_per_step": round(s["ms"] / args.steps, 3), "launches_per_step": s["launches"] / args.steps}
+                   for k, s in kern[:10]},
+    }
+    if not args.no_cpu:
+        res["cpu_baseline"] = cpu_sample(ctx, args.cpu_rows_c5)
+    else:
+        res["cpu_baseline"] = None
+    ctx.close()
+    return res

@@ -6,7 +6,10 @@ Column kinds:
 * ``("mod", M)``  -> ``v % M``       (join keys; SURVEY uses M = N)
 * ``("hi32",)``   -> ``v >> 32``     (filter / payload column, uniform in [0, 2^32))
 * ``("zipf", D, theta, perm_seed)``  -> Zipf(theta) rank over [0, D) mapped through a shared
-  rank->key permutation (config 5 shape)
+  rank->key permutation (config 5 shape): rank = #{r : cdf[r] <= u} for the 53-bit uniform u of
+  v, capped at D-1, then key = feistel_perm(rank) -- a seeded 4-round Feistel bijection of
+  [0, 2^b) cycle-walked into [0, D).  Given the same CDF table, libqe's device sampler
+  (qe_set_zipf_table + kind 2) draws the same keys bit for bit.
 
 The same generator runs on the GPU inside libqe (``qe_gen_column``); tests check the two agree
 bit for bit.  Files use the reference's binary layout: ``u64 rows, u64 ncols`` then the columns
@@ -60,10 +63,40 @@ def zipf_cdf(domain: int, theta: float) -> np.ndarray:
     return c / c[-1]
 
 
+def feistel_perm(x: np.ndarray, domain: int, perm_seed: int) -> np.ndarray:
+    """Seeded bijection of [0, domain): 4 Feistel rounds (round function splitmix64) on b-bit
+    words, b = bit length of domain-1 rounded up to even (>= 2), cycle-walked until < domain."""
+    b = max(2, int(domain - 1).bit_length())
+    b += b & 1
+    h = np.uint64(b // 2)
+    mask = np.uint64((1 << (b // 2)) - 1)
+    keys = [np.uint64(stream_base(perm_seed, 15, r)) for r in range(4)]
+    x = np.asarray(x, dtype=np.uint64).copy()
+    todo = np.arange(len(x))
+    dom = np.uint64(domain)
+    first = True
+    while first or len(todo):
+        first = False
+        y = x[todo]
+        lo, hi = y & mask, y >> h
+        with np.errstate(over="ignore"):
+            for k in keys:
+                lo, hi = hi ^ (splitmix64(lo + k) & mask), lo
+        y = (hi << h) | lo
+        x[todo] = y
+        todo = todo[y >= dom]
+    return x
+
+
 def zipf_perm(domain: int, perm_seed: int) -> np.ndarray:
     """Rank -> key permutation shared by both sides of a skewed join (seeded)."""
-    keys = splitmix64(np.arange(domain, dtype=np.uint64) + np.uint64(stream_base(perm_seed, 15, 15)))
-    return np.argsort(keys, kind="stable").astype(np.uint64)
+    return feistel_perm(np.arange(domain, dtype=np.uint64), domain, perm_seed)
+
+
+def zipf_ranks(v: np.ndarray, cdf: np.ndarray) -> np.ndarray:
+    u = (v >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)   # 53-bit uniform
+    rank = np.searchsorted(cdf, u, side="right")
+    return np.minimum(rank, len(cdf) - 1).astype(np.uint64)
 
 
 def column(seed: int, rel: int, col: int, rows: int, kind: tuple, start: int = 0) -> np.ndarray:
@@ -74,10 +107,7 @@ def column(seed: int, rel: int, col: int, rows: int, kind: tuple, start: int = 0
         return v >> np.uint64(32)
     if kind[0] == "zipf":
         domain, theta, perm_seed = int(kind[1]), float(kind[2]), int(kind[3])
-        u = (v >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)   # 53-bit uniform
-        rank = np.searchsorted(zipf_cdf(domain, theta), u, side="right")
-        rank = np.minimum(rank, domain - 1)
-        return zipf_perm(domain, perm_seed)[rank]
+        return feistel_perm(zipf_ranks(v, zipf_cdf(domain, theta)), domain, perm_seed)
     raise ValueError(f"unknown column kind {kind!r}")
 
 
@@ -191,3 +221,19 @@ def c4_batches(queries: list[str], batch: int = C4_BATCH) -> str:
         text.extend(queries[i:i + batch])
         text.append("F\n")
     return "".join(text)
+
+
+# ---- C5: skewed 2-relation join --------------------------------------------------
+C5_SEED = 5
+C5_ROWS = 1_000_000_000
+C5_THETA = 0.9
+C5_PERM_SEED = 55
+C5_QUERY = "0 1|0.1=1.0|0.2 1.2\n"
+
+
+def c5_spec(rows: int = C5_ROWS, theta: float = C5_THETA, domain: int | None = None) -> list[RelSpec]:
+    """r0 = (v % N, Zipf key, u32 payload), r1 = (Zipf key, v % N, u32 payload): both Zipf columns
+    over D = N (default) share one rank->key permutation, so the heavy ranks collide."""
+    d = domain if domain is not None else rows
+    z = ("zipf", d, theta, C5_PERM_SEED)
+    return [RelSpec(rows, [("mod", rows), z, ("hi32",)]), RelSpec(rows, [z, ("mod", rows), ("hi32",)])]

@@ -15,7 +15,7 @@ PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("QE_LIB_PATH") or os.path.join(PKG, "build", "libqe.so")   # override: ablation builds (tools/)
 HEADER = os.path.join(os.path.dirname(PKG), "include", "qe.h")
 
-QE_EINVAL, QE_EHIP, QE_ENOMEM, QE_EEXIT = -1, -2, -3, -4
+QE_EINVAL, QE_EHIP, QE_ENOMEM, QE_EEXIT, QE_ETOOBIG = -1, -2, -3, -4, -5
 LIST_DISTINCT = 1
 PAIRS_DISTINCT, PAIRS_SORTED = 1, 2
 
@@ -88,6 +88,11 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
                                        C.POINTER(List)]),
         "qe_relation_column_bits": (I, [P, I, I, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "qe_checksum": (I, [P, Col, C.POINTER(List), C.POINTER(C.c_uint64)]),
+        "qe_checksum_weighted": (I, [P, Col, C.POINTER(Pairs), C.POINTER(C.c_uint64)]),
+        "qe_merge_join_counts": (I, [P, C.POINTER(Pairs), C.POINTER(Pairs), C.POINTER(C.c_uint64)]),
+        "qe_set_materialize_limit": (I, [P, U64]),
+        "qe_set_zipf_table": (I, [P, C.c_void_p, U64, U64]),
+        "qe_set_zipf": (I, [P, U64, C.c_double, U64]),
         "qe_partition": (I, [P, C.c_void_p, U64, C.POINTER(C.c_void_p), I, C.c_uint32, C.POINTER(C.c_uint64),
                              C.c_void_p, C.POINTER(C.c_void_p)]),
         "qe_filter_scan_range": (I, [P, Col, U64, U64, C.c_char, U64, C.POINTER(List)]),
@@ -165,9 +170,20 @@ class Ctx:
         return self._chk(self.lib.qe_load_relation(self.h, rows, len(cols), arr))
 
     def gen_relation(self, rows: int, kinds: list[tuple], seed: int, gen_rel: int, row_start: int = 0) -> int:
-        k = (C.c_int * len(kinds))(*[0 if kd[0] == "mod" else 1 for kd in kinds])
-        m = (C.c_uint64 * len(kinds))(*[int(kd[1]) if kd[0] == "mod" else 0 for kd in kinds])
+        """kinds as qe.datagen: ("mod", M), ("hi32",), ("zipf", D, theta, perm_seed) -- the last
+        needs set_zipf_table(cdf of (D, theta), D, perm_seed) first"""
+        code = {"mod": 0, "hi32": 1, "zipf": 2}
+        k = (C.c_int * len(kinds))(*[code[kd[0]] for kd in kinds])
+        m = (C.c_uint64 * len(kinds))(*[int(kd[1]) if kd[0] in ("mod", "zipf") else 0 for kd in kinds])
         return self._chk(self.lib.qe_gen_relation(self.h, rows, len(kinds), k, m, seed, gen_rel, row_start))
+
+    def set_zipf_table(self, d_cdf_ptr: int, domain: int, perm_seed: int) -> None:
+        """d_cdf_ptr: device address of `domain` float64 CDF values (kept alive by the caller)"""
+        self._chk(self.lib.qe_set_zipf_table(self.h, d_cdf_ptr, domain, perm_seed))
+
+    def set_zipf(self, domain: int, theta: float, perm_seed: int) -> None:
+        """Zipf table built (deterministically) and owned by libqe"""
+        self._chk(self.lib.qe_set_zipf(self.h, domain, theta, perm_seed))
 
     def drop_relations(self):
         self._chk(self.lib.qe_drop_relations(self.h))
@@ -288,6 +304,25 @@ class Ctx:
         a, b = C.c_uint64(), C.c_uint64()
         self._chk(self.lib.qe_relation_column_bits(self.h, rel, col, C.byref(a), C.byref(b)))
         return a.value, b.value
+
+    def column_to_host(self, rel: int, col: int) -> np.ndarray:
+        k = np.empty(self.column(rel, col).n, dtype=np.uint64)
+        p = self.gather_pairs(self.column(rel, col), None)
+        self._chk(self.lib.qe_pairs_to_host(self.h, C.byref(p), k.ctypes.data, None))
+        return k
+
+    def merge_join_counts(self, R: Pairs, S: Pairs) -> int:
+        P = C.c_uint64()
+        self._chk(self.lib.qe_merge_join_counts(self.h, C.byref(R), C.byref(S), C.byref(P)))
+        return P.value
+
+    def checksum_weighted(self, col: Col, p: Pairs) -> int:
+        s = C.c_uint64()
+        self._chk(self.lib.qe_checksum_weighted(self.h, col, C.byref(p), C.byref(s)))
+        return s.value
+
+    def set_materialize_limit(self, pairs: int) -> None:
+        self._chk(self.lib.qe_set_materialize_limit(self.h, pairs))
 
     def checksum(self, col: Col, rows: List | None) -> int:
         s = C.c_uint64()

@@ -18,6 +18,10 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def ctx():
     """One libqe device context for the whole GPU session (native path only, no fallback)."""
+    # torch's bundled HIP runtime must initialise before libqe's (tests use torch for device
+    # buffers; the bench does the same)
+    import torch
+    torch.cuda.init()
     from qe import lib
     c = lib.Ctx(0)
     yield c
