@@ -217,13 +217,16 @@ def main():
     ap.add_argument("--workload", choices=["c3", "c4", "c5"], default="c3",
                     help="c3 (default): the headline 4-relation chain join; c4: the SIGMOD-style batch; "
                          "c5: the skewed (Zipf 0.9) 2-relation join at 1e9 rows")
+    ap.add_argument("--plan", choices=["auto", "dist"], default="auto",
+                    help="auto = faithful executor at N = 1, the partitioned plan (qe.dist) at N > 1; "
+                         "dist = the partitioned plan at every N (its per-rank cost at N = 1); c3 and c5")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.rows is None and args.workload != "c5":
         args.rows = 100_000_000
     if args.workload == "c5":
         from qe import c5bench
-        if world > 1:
+        if world > 1 or args.plan == "dist":
             res = c5bench.run_dist(args, log)
         else:
             res = c5bench.run_single(args, log, roofline_fn=roofline, traffic_fn=load_traffic)
@@ -233,7 +236,7 @@ def main():
             res = c4bench.run_dist(args, log)
         else:
             res = c4bench.run_single(args, log, roofline_fn=roofline, traffic_fn=load_traffic)
-    elif world > 1 or args.gpus > 1:
+    elif world > 1 or args.gpus > 1 or args.plan == "dist":
         from qe import dist
         res = dist.bench_main(args, METRIC, QUERY, cpu_baseline_fn=cpu_baseline, roofline_fn=roofline,
                               traffic_fn=load_traffic)

@@ -195,6 +195,17 @@ int qe_take_u32(qe_ctx*, const uint32_t* src, const qe_list* idx, qe_list* out);
 /* Equi-join of two key arrays (a rank's bucket): sort both, merge, return aligned row indices. */
 int qe_join_indices(qe_ctx*, const uint64_t* keysA, uint64_t nA, const uint64_t* keysB, uint64_t nB, qe_list* ia,
                     qe_list* ib);
+/* Local bucket of a replicated base column: the rows with fmix64(key) % nparts == part, as
+ * (key, rowid) pairs in no particular order (out owns both arrays).  Keys in the sorted list
+ * heavy[0..nheavy) (host memory, <= 1024, the skew path) are left out.  Replaces the exchange
+ * of a join side that is a whole base relation: every rank holds the column. */
+int qe_bucket_select(qe_ctx*, qe_col col, uint32_t nparts, uint32_t part, const uint64_t* heavy, uint32_t nheavy,
+                     qe_pairs* out);
+/* Skew path (C5): over rows [start, end) of `keys`, counts[h] = #rows whose key is heavy[h]
+ * (host arrays, heavy sorted, <= 1024) and, when weights != NULL,
+ * wsum = sum of vals[row] * weights[h] over those rows mod 2^64.  counts/wsum nullable. */
+int qe_heavy_stats(qe_ctx*, qe_col keys, uint64_t start, uint64_t end, const uint64_t* heavy, uint32_t nheavy,
+                   qe_col vals, const uint64_t* weights, uint64_t* counts, uint64_t* wsum);
 /* The ctx's HIP stream (hipStream_t), for callers that order their own work against it. */
 int qe_sync_stream_ptr(qe_ctx*, void** stream);
 

@@ -143,6 +143,141 @@ __global__ void __launch_bounds__(256) add_u32_kernel(uint32_t* __restrict__ a, 
     if (i < n) a[i] += add;
 }
 
+
+// ---- local bucket select: the hash bucket `part` of a replicated base column ----------------------
+// Base columns are replicated on every rank, so a join side that is a whole base
+// relation is bucketed by one scan of the column instead of an exchange: rank g keeps the rows
+// with fmix64(key) % nparts == g -- exactly the rows the exchange would have delivered to it.
+// Unordered compaction (the bucket is sorted next): per (step, wave) survivor runs are ranked with
+// ballots, the block reserves its range with one atomic, every wave writes its runs contiguously.
+// Keys listed in `heavy` (sorted, skew path) are left out of every bucket.
+constexpr int BS_B = 512;
+constexpr int BS_ITEMS = 4;                 // x 2 keys per 16-B load
+constexpr int BS_TILE = BS_B * BS_ITEMS * 2;
+constexpr int BS_NW = BS_B / 64;
+constexpr int HEAVY_MAX = 1024;
+
+__device__ __forceinline__ int heavy_find(const uint64_t* h, uint32_t nh, uint64_t k) {
+    // lower bound over the sorted heavy list (LDS); -1 when absent
+    uint32_t lo = 0, len = nh;
+    while (len > 0) {
+        uint32_t half = len >> 1;
+        bool go = h[lo + half] < k;
+        lo = go ? lo + half + 1 : lo;
+        len = go ? len - half - 1 : half;
+    }
+    return (lo < nh && h[lo] == k) ? (int)lo : -1;
+}
+
+__global__ void __launch_bounds__(BS_B) bucket_select_kernel(const uint64_t* __restrict__ keys, uint64_t n,
+                                                             uint32_t nparts, uint32_t part,
+                                                             const uint64_t* __restrict__ heavy, uint32_t nheavy,
+                                                             uint64_t* __restrict__ okeys, uint32_t* __restrict__ ovals,
+                                                             uint64_t cap, unsigned long long* __restrict__ counter) {
+    __shared__ uint64_t s_heavy[HEAVY_MAX];
+    __shared__ uint32_t s_cnt[BS_ITEMS * 2 * BS_NW];
+    __shared__ uint64_t s_base;
+    for (uint32_t i = threadIdx.x; i < nheavy; i += BS_B) s_heavy[i] = heavy[i];
+    const int w = wave_id(), l = lane_id();
+    const uint64_t lt = lanemask_lt();
+    const uint64_t tile = (uint64_t)blockIdx.x * BS_TILE;
+    uint64_t k[BS_ITEMS][2];
+#pragma unroll
+    for (int j = 0; j < BS_ITEMS; j++) {
+        const uint64_t i = tile + (uint64_t)j * (BS_B * 2) + (uint64_t)threadIdx.x * 2;
+        if (i + 1 < n) {
+            ulonglong2 x = *reinterpret_cast<const ulonglong2*>(keys + i);
+            k[j][0] = x.x;
+            k[j][1] = x.y;
+        } else {
+            k[j][0] = i < n ? keys[i] : 0;
+            k[j][1] = 0;
+        }
+    }
+    __syncthreads();   // s_heavy
+    bool f[BS_ITEMS][2];
+    uint32_t rank[BS_ITEMS][2];
+#pragma unroll
+    for (int j = 0; j < BS_ITEMS; j++) {
+        const uint64_t i = tile + (uint64_t)j * (BS_B * 2) + (uint64_t)threadIdx.x * 2;
+#pragma unroll
+        for (int v = 0; v < 2; v++) {
+            bool ok = i + v < n && (uint32_t)(fmix64(k[j][v]) % nparts) == part;
+            if (ok && nheavy) ok = heavy_find(s_heavy, nheavy, k[j][v]) < 0;
+            f[j][v] = ok;
+            uint64_t m = __ballot(ok);
+            rank[j][v] = (uint32_t)__popcll(m & lt);
+            if (l == 0) s_cnt[(j * 2 + v) * BS_NW + w] = (uint32_t)__popcll(m);
+        }
+    }
+    __syncthreads();
+    if (w == 0) {
+        constexpr int NC = BS_ITEMS * 2 * BS_NW;
+        uint32_t c = l < NC ? s_cnt[l] : 0;
+        uint32_t inc = wave_incl_scan_u32(c);
+        uint32_t total = (uint32_t)__shfl((int)inc, NC - 1, 64);
+        if (l < NC) s_cnt[l] = inc - c;
+        if (l == 0) s_base = total ? atomicAdd(counter, (unsigned long long)total) : 0;
+    }
+    __syncthreads();
+    const uint64_t base = s_base;
+#pragma unroll
+    for (int j = 0; j < BS_ITEMS; j++) {
+        const uint64_t i = tile + (uint64_t)j * (BS_B * 2) + (uint64_t)threadIdx.x * 2;
+#pragma unroll
+        for (int v = 0; v < 2; v++) {
+            const uint64_t o = base + s_cnt[(j * 2 + v) * BS_NW + w] + rank[j][v];
+            if (f[j][v] && o < cap) {   // an overfull bucket is counted, not written, and re-run
+                okeys[o] = k[j][v];
+                ovals[o] = (uint32_t)(i + v);
+            }
+        }
+    }
+}
+
+// ---- heavy-key statistics over a row range (skew path) ---------------------------------------------
+// counts[h] += #rows with key heavy[h]; wsum += sum of vals[row] * weights[h] over those rows (mod 2^64).
+__global__ void __launch_bounds__(BS_B) heavy_stats_kernel(const uint64_t* __restrict__ keys,
+                                                           const uint64_t* __restrict__ vals, uint64_t start,
+                                                           uint64_t end, const uint64_t* __restrict__ heavy,
+                                                           uint32_t nheavy, const uint64_t* __restrict__ weights,
+                                                           unsigned long long* __restrict__ counts,
+                                                           unsigned long long* __restrict__ wsum) {
+    __shared__ uint64_t s_heavy[HEAVY_MAX];
+    __shared__ uint32_t s_cnt[HEAVY_MAX];
+    __shared__ uint64_t s_red[BS_NW];
+    for (uint32_t i = threadIdx.x; i < nheavy; i += BS_B) {
+        s_heavy[i] = heavy[i];
+        s_cnt[i] = 0;
+    }
+    __syncthreads();
+    const uint64_t tile = start + (uint64_t)blockIdx.x * BS_TILE;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < BS_ITEMS * 2; j++) {
+        const uint64_t i = tile + (uint64_t)j * BS_B + threadIdx.x;
+        if (i < end) {
+            const int h = heavy_find(s_heavy, nheavy, keys[i]);
+            if (h >= 0) {
+                atomicAdd(&s_cnt[h], 1u);
+                if (weights) acc += vals[i] * weights[h];
+            }
+        }
+    }
+    if (weights) {
+        acc = wave_sum_u64(acc);
+        if (lane_id() == 0) s_red[wave_id()] = acc;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nheavy; i += BS_B)
+        if (s_cnt[i]) atomicAdd(&counts[i], (unsigned long long)s_cnt[i]);
+    if (weights && threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (int x = 0; x < BS_NW; x++) t += s_red[x];
+        if (t) atomicAdd(wsum, (unsigned long long)t);
+    }
+}
+
 }  // namespace qe
 
 using namespace qe;
@@ -247,6 +382,91 @@ int qe_join_indices(qe_ctx* c, const uint64_t* keysA, uint64_t nA, const uint64_
     qe_pairs_free(c, &A);
     qe_pairs_free(c, &B);
     return rc;
+    QE_API_END(c)
+}
+
+int qe_bucket_select(qe_ctx* c, qe_col col, uint32_t nparts, uint32_t part, const uint64_t* heavy, uint32_t nheavy,
+                     qe_pairs* out) {
+    QE_API_BEGIN(c)
+    if (nparts < 1 || part >= nparts) throw Error(QE_EINVAL, "bad bucket");
+    if (nheavy > (uint32_t)HEAVY_MAX) throw Error(QE_EINVAL, "at most 1024 heavy keys");
+    if (col.n >= 0xFFFFFFFFull) throw Error(QE_EINVAL, "column too large for 32-bit rowids");
+    for (uint32_t i = 1; i < nheavy; i++)
+        if (heavy[i - 1] >= heavy[i]) throw Error(QE_EINVAL, "heavy keys must be sorted and distinct");
+    *out = qe_pairs{};
+    const uint64_t n = col.n;
+    // capacity: the whole column when nparts == 1, else the expected bucket + a generous margin
+    // (the count is checked below; an overfull bucket re-runs with full capacity)
+    uint64_t cap = nparts == 1 ? n : std::min<uint64_t>(n, n / nparts + n / (4 * nparts) + 65536);
+    uint64_t* d_heavy = nullptr;
+    if (nheavy) {
+        d_heavy = dalloc_t<uint64_t>(c, nheavy);
+        QE_HIP(hipMemcpyAsync(d_heavy, heavy, nheavy * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    }
+    unsigned long long* d_cnt = reinterpret_cast<unsigned long long*>(c->d_scratch);
+    const unsigned nb = grid_for(n, BS_TILE);
+    for (int attempt = 0; attempt < 2; attempt++) {
+        out->key = dalloc_t<uint64_t>(c, std::max<uint64_t>(cap, 1));
+        out->val = dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1));
+        QE_HIP(hipMemsetAsync(d_cnt, 0, sizeof(uint64_t), c->stream));
+        if (n) {
+            Timed t(c, "bucket_select", 8.0 * n);
+            hipLaunchKernelGGL(bucket_select_kernel, dim3(nb), dim3(BS_B), 0, c->stream, col.d, n, nparts, part,
+                               d_heavy, nheavy, out->key, out->val, cap, d_cnt);
+            QE_HIP(hipGetLastError());
+        }
+        const uint64_t m = read_u64(c, reinterpret_cast<uint64_t*>(d_cnt));
+        if (m <= cap) {
+            out->n = m;
+            break;
+        }
+        dfree(c, out->key);
+        dfree(c, out->val);
+        if (attempt == 1) throw Error(QE_EINVAL, "internal: bucket larger than its column");
+        cap = n;
+    }
+    if (c->prof && !c->pending.empty()) c->pending.back().bytes += 12.0 * out->n;
+    out->owns = 3;
+    out->flags = QE_PAIRS_DISTINCT;
+    if (d_heavy) dfree(c, d_heavy);
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_heavy_stats(qe_ctx* c, qe_col keys, uint64_t start, uint64_t end, const uint64_t* heavy, uint32_t nheavy,
+                   qe_col vals, const uint64_t* weights, uint64_t* counts, uint64_t* wsum) {
+    QE_API_BEGIN(c)
+    if (end > keys.n || start > end) throw Error(QE_EINVAL, "bad row range");
+    if (nheavy > (uint32_t)HEAVY_MAX) throw Error(QE_EINVAL, "at most 1024 heavy keys");
+    if (weights && (!vals.d || vals.n < end)) throw Error(QE_EINVAL, "weighted sum needs a value column");
+    for (uint32_t i = 1; i < nheavy; i++)
+        if (heavy[i - 1] >= heavy[i]) throw Error(QE_EINVAL, "heavy keys must be sorted and distinct");
+    if (wsum) *wsum = 0;
+    if (counts)
+        for (uint32_t i = 0; i < nheavy; i++) counts[i] = 0;
+    if (nheavy == 0 || end == start) return 0;
+    // device block: [heavy | weights | counts | wsum]
+    uint64_t* d = dalloc_t<uint64_t>(c, 3 * (uint64_t)nheavy + 1);
+    QE_HIP(hipMemcpyAsync(d, heavy, nheavy * 8, hipMemcpyHostToDevice, c->stream));
+    if (weights) QE_HIP(hipMemcpyAsync(d + nheavy, weights, nheavy * 8, hipMemcpyHostToDevice, c->stream));
+    QE_HIP(hipMemsetAsync(d + 2 * nheavy, 0, (nheavy + 1) * 8, c->stream));
+    {
+        const uint64_t n = end - start;
+        Timed t(c, "heavy_stats", 8.0 * n);
+        hipLaunchKernelGGL(heavy_stats_kernel, dim3(grid_for(n, BS_TILE)), dim3(BS_B), 0, c->stream, keys.d,
+                           vals.d, start, end, d, nheavy, weights ? d + nheavy : nullptr,
+                           reinterpret_cast<unsigned long long*>(d + 2 * nheavy),
+                           reinterpret_cast<unsigned long long*>(d + 3 * nheavy));
+        QE_HIP(hipGetLastError());
+    }
+    std::vector<uint64_t> h(nheavy + 1);
+    QE_HIP(hipMemcpyAsync(h.data(), d + 2 * nheavy, (nheavy + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+    QE_HIP(hipStreamSynchronize(c->stream));
+    if (counts)
+        for (uint32_t i = 0; i < nheavy; i++) counts[i] = h[i];
+    if (wsum) *wsum = h[nheavy];
+    dfree(c, d);
+    return 0;
     QE_API_END(c)
 }
 

@@ -184,6 +184,93 @@ class GPUEngine:
         ia, ib = self.ctx.join_indices(ka.ptr, ka.n, kb.ptr, kb.n)
         return self._list(ia), self._list(ib)
 
+    def base_side(self, rel, col):
+        """a whole base relation as a join side: (keys, rowids or None = row i).  One rank: the
+        column itself (zero copy).  N ranks: the local hash bucket of the replicated column
+        (qe_bucket_select) -- the rows the exchange would deliver, without moving them."""
+        c = self.ctx.column(rel, col)
+        if self.world == 1:
+            kor, kand = self.ctx.column_bits(rel, col)
+            return DArr(c.d, c.n, keep=("bits", kor, kand)), None
+        p = self.ctx.bucket_select(c, self.world, self.rank)
+        ctx = self.ctx
+        keys = DArr(p.key, p.n, keep=p, free=lambda: ctx.pairs_free(p))
+        return keys, DArr(p.val, p.n, keep=keys)
+
+    def base_side_light(self, rel, col, heavy):
+        """base_side without the heavy keys (skew path): the local bucket minus heavy keys"""
+        if self.world == 1 and len(heavy) == 0:
+            return self.base_side(rel, col)
+        p = self.ctx.bucket_select(self.ctx.column(rel, col), self.world, self.rank, heavy)
+        ctx = self.ctx
+        keys = DArr(p.key, p.n, keep=p, free=lambda: ctx.pairs_free(p))
+        return keys, DArr(p.val, p.n, keep=keys)
+
+    def join_count_sums(self, ka: DArr, va, kb: DArr, vb, sel_a: list, sel_b: list):
+        """aggregate form of the merge (no pair materialised): (pairs, [sum over pairs of
+        col[rowid_A] for (rel, col) in sel_a], [... sel_b]) mod 2^64 -- qe_merge_join_counts +
+        qe_checksum_weighted"""
+        P = self.lib.Pairs
+        sides = []
+        for k, v in ((ka, va), (kb, vb)):
+            p = P()
+            p.key, p.val, p.n, p.flags, p.owns = k.ptr, (v.ptr if v is not None else None), k.n, 0, 0
+            if isinstance(k.keep, tuple) and k.keep and k.keep[0] == "bits":
+                p.kor, p.kand, p.flags = k.keep[1], k.keep[2], 4
+            sides.append(p)
+        A, B = sides
+        try:
+            self.ctx.sort_pairs(A)
+            self.ctx.sort_pairs(B)
+            pairs = self.ctx.merge_join_counts(A, B)
+            sa = [self.ctx.checksum_weighted(self.ctx.column(r, c), A) for (r, c) in sel_a]
+            sb = [self.ctx.checksum_weighted(self.ctx.column(r, c), B) for (r, c) in sel_b]
+        finally:
+            self.ctx.pairs_free(A)
+            self.ctx.pairs_free(B)
+        return pairs, sa, sb
+
+    def heavy_stats(self, rel, col, start, end, heavy, val=None, weights=None):
+        v = self.ctx.column(*val) if val is not None else None
+        return self.ctx.heavy_stats(self.ctx.column(rel, col), start, end, heavy, v, weights)
+
+    def column_prefix(self, rel, col, m):
+        c = self.ctx.column(rel, col)
+        p = self.lib.Pairs()
+        p.key, p.val, p.match, p.n = c.d, None, None, min(m, c.n)
+        out = np.empty(p.n, dtype=np.uint64)
+        self.ctx._chk(self.ctx.lib.qe_pairs_to_host(self.ctx.h, self.lib.C.byref(p), out.ctypes.data, None))
+        return out
+
+    def allreduce_vec(self, a: np.ndarray) -> np.ndarray:
+        a = np.ascontiguousarray(a, dtype=np.uint64)
+        if self.world == 1 or a.size == 0:
+            return a
+        t = self.torch.from_numpy(a.view(np.int64).copy()).to(self.comm_dev)
+        self.dist.all_reduce(t, group=self.group)
+        return t.cpu().numpy().view(np.uint64)
+
+    def join_pairs(self, ka: DArr, va, kb: DArr, vb):
+        """sort both sides by key (stable LSD radix) and merge: aligned outputs, va[i] (or i when
+        va is None) for side A and likewise for B, in key order"""
+        P = self.lib.Pairs
+        sides = []
+        for k, v in ((ka, va), (kb, vb)):
+            p = P()
+            p.key, p.val, p.n, p.flags, p.owns = k.ptr, (v.ptr if v is not None else None), k.n, 0, 0
+            if isinstance(k.keep, tuple) and k.keep and k.keep[0] == "bits":
+                p.kor, p.kand, p.flags = k.keep[1], k.keep[2], 4          # QE_PAIRS_BITS: column stats
+            sides.append(p)
+        A, B = sides
+        try:
+            self.ctx.sort_pairs(A)
+            self.ctx.sort_pairs(B)
+            oa, ob = self.ctx.merge_join(A, B)
+        finally:
+            self.ctx.pairs_free(A)
+            self.ctx.pairs_free(B)
+        return self._list(oa), self._list(ob)
+
     def keep_equal(self, ka: DArr, kb: DArr) -> DArr:
         P = self.lib.Pairs
         A, B = P(), P()
@@ -237,11 +324,19 @@ class GPUEngine:
 # the plan
 # ---------------------------------------------------------------------------------------------
 class DistExecutor:
-    """Runs one query line with the key-partitioned relational plan on `engine`."""
+    """Runs one query line with the key-partitioned relational plan on `engine`.
 
-    def __init__(self, engine, rel_rows: list[int]):
+    Components: bindings already joined together, each {binding: rowid list}; a whole base
+    relation not touched by any filter or join yet is {binding: None} and is never materialised
+    (as a join side it is the column itself on one rank, the local hash bucket of the
+    replicated column on N ranks).  Consecutive joins are reordered greedily (smallest
+    |A| + |B| first, global sizes) -- relational semantics do not depend on the order, and
+    filters, whose stray count lines do, keep their place between the runs of joins."""
+
+    def __init__(self, engine, rel_rows: list[int], reorder: bool | None = None):
         self.e = engine
         self.rel_rows = rel_rows
+        self.reorder = (os.environ.get("QE_DIST_REORDER", "1") != "0") if reorder is None else reorder
 
     def _base(self, rel):
         s, t = owned_range(self.rel_rows[rel], self.e.rank, self.e.world)
@@ -266,87 +361,226 @@ class DistExecutor:
             if b not in joined:
                 raise NotSupported("selected binding outside the join graph")
         out = []
-        comp_of: dict[int, int] = {}          # binding -> component id
-        comps: dict[int, dict[int, DArr]] = {}  # component -> {binding: rowids}
-        lists: dict[int, DArr] = {}           # filtered, not yet joined bindings
+        comp_of: dict[int, int] = {}            # binding -> component id
+        comps: dict[int, dict] = {}             # component -> {binding: rowids | None (whole base)}
+        size: dict[int, int] = {}               # component -> global rows
+        lists: dict[int, object] = {}           # filtered, not yet joined bindings
+        list_size: dict[int, int] = {}
 
-        def need_after(k):
+        def need_of(pending):
             need = {b for (b, _) in sels}
-            for p in preds[k + 1:]:
-                need.add(p.a[0])
-                if p.b:
-                    need.add(p.b[0])
+            for q in pending:
+                need.add(q.a[0])
+                if q.b:
+                    need.add(q.b[0])
             return need
 
         def component(b):
             if b in comp_of:
                 return comp_of[b]
             cid = len(comps) + 1000 * (b + 1)
-            comps[cid] = {b: lists.pop(b) if b in lists else self._base(rels[b])}
+            if b in lists:
+                comps[cid] = {b: lists.pop(b)}
+                size[cid] = list_size.pop(b)
+            else:
+                comps[cid] = {b: None}
+                size[cid] = self.rel_rows[rels[b]]
             comp_of[b] = cid
             return cid
 
-        for k, p in enumerate(preds):
-            if p.kind == "filter":
-                b, c = p.a
-                rel = rels[b]
-                if b in comp_of:
-                    cid = comp_of[b]
-                    idx = e.filter_idx(rel, c, comps[cid][b], p.op, p.const)
-                    comps[cid] = {bb: e.take(r, idx) for bb, r in comps[cid].items()}
-                    out.append(f"{e.allreduce(e.length(comps[cid][b])) & 0xFFFFFFFF:d}\n")
-                elif b in lists:
-                    lists[b] = e.refine(rel, c, lists[b], p.op, p.const)
-                    out.append(f"{e.allreduce(e.length(lists[b])):d}\n")
-                else:
-                    s, t = owned_range(self.rel_rows[rel], e.rank, e.world)
-                    lists[b] = e.scan(rel, c, s, t, p.op, p.const)
-                continue
+        def rows_of(cid, b):
+            if comps[cid][b] is None:
+                comps[cid][b] = self._base(rels[b])
+            return comps[cid][b]
+
+        def side(cid, b, c, need):
+            """(keys, vals, carried) of one join side; carried = [(binding, rowids-or-'vals')]"""
+            cols = comps[cid]
+            if len(cols) == 1 and b in cols and cols[b] is None:
+                keys, vals = e.base_side(rels[b], c)
+                return keys, vals, ([(b, "vals")] if b in need else [])
+            keys = e.keys(rels[b], c, rows_of(cid, b))
+            keep = [x for x in sorted(cols) if x in need]
+            if e.world > 1:
+                if len(keep) > 4:
+                    raise NotSupported("more than 4 rowid columns in one exchange")
+                keys, rc = e.exchange(keys, [rows_of(cid, x) for x in keep])
+                cur = dict(zip(keep, rc))
+            else:
+                cur = {x: rows_of(cid, x) for x in keep}
+            if len(keep) == 1:
+                return keys, cur[keep[0]], [(keep[0], "vals")]
+            return keys, None, [(x, cur[x]) for x in keep]
+
+        def do_join(p, pending):
             (ba, ca), (bb, cb) = p.a, p.b
             A, B = component(ba), component(bb)
-            need = need_after(k)
+            need = need_of(pending)
             if A == B:
                 cols = comps[A]
-                idx = e.keep_equal(e.keys(rels[ba], ca, cols[ba]), e.keys(rels[bb], cb, cols[bb]))
-                comps[A] = {x: e.take(r, idx) for x, r in cols.items()}
-                continue
-            ka = e.keys(rels[ba], ca, comps[A][ba])
-            kb = e.keys(rels[bb], cb, comps[B][bb])
-            sides = []
-            for cid, kk in ((A, ka), (B, kb)):
-                cols = comps[cid]
-                keep = [x for x in sorted(cols) if x in need] or [sorted(cols)[0]]
-                if e.world > 1:
-                    if len(keep) > 4:
-                        raise NotSupported("more than 4 rowid columns in one exchange")
-                    rk, rc = e.exchange(kk, [cols[x] for x in keep])
-                    sides.append((rk, dict(zip(keep, rc))))
-                else:
-                    sides.append((kk, {x: cols[x] for x in keep}))
-            (rka, ca_cols), (rkb, cb_cols) = sides
-            ia, ib = e.join_local(rka, rkb)
-            merged = {x: e.take(r, ia) for x, r in ca_cols.items()}
-            merged.update({x: e.take(r, ib) for x, r in cb_cols.items()})
+                idx = e.keep_equal(e.keys(rels[ba], ca, rows_of(A, ba)), e.keys(rels[bb], cb, rows_of(A, bb)))
+                comps[A] = {x: e.take(rows_of(A, x), idx) for x in list(cols)}
+                size[A] = e.allreduce(e.length(idx))
+                return
+            ka, va, carry_a = side(A, ba, ca, need)
+            kb, vb, carry_b = side(B, bb, cb, need)
+            oa, ob = e.join_pairs(ka, va, kb, vb)
+            del ka, kb, va, vb
+            merged = {}
+            for carry, o in ((carry_a, oa), (carry_b, ob)):
+                for x, r in carry:
+                    merged[x] = o if isinstance(r, str) else e.take(r, o)
+            if not merged:                       # nothing needed later: keep the row count
+                merged[ba] = oa
             del comps[A], comps[B]
             comps[A] = merged
+            size.pop(B, None)
             for x in list(comp_of):
                 if comp_of[x] in (A, B):
                     comp_of[x] = A
             for x in merged:
                 comp_of[x] = A
+            size[A] = e.allreduce(e.length(next(iter(merged.values()))))
+
+        def cost(p):
+            A = comp_of.get(p.a[0])
+            B = comp_of.get(p.b[0])
+            if A is not None and A == B:
+                return -1
+            def sz(b, cid):
+                if cid is not None:
+                    return size[cid]
+                return list_size[b] if b in lists else self.rel_rows[rels[b]]
+            return sz(p.a[0], A) + sz(p.b[0], B)
+
+        k = 0
+        while k < len(preds):
+            p = preds[k]
+            if p.kind == "filter":
+                b, c = p.a
+                rel = rels[b]
+                if b in comp_of:
+                    cid = comp_of[b]
+                    idx = e.filter_idx(rel, c, rows_of(cid, b), p.op, p.const)
+                    comps[cid] = {bb: e.take(rows_of(cid, bb), idx) for bb in list(comps[cid])}
+                    size[cid] = e.allreduce(e.length(idx))
+                    out.append(f"{size[cid] & 0xFFFFFFFF:d}\n")
+                elif b in lists:
+                    lists[b] = e.refine(rel, c, lists[b], p.op, p.const)
+                    list_size[b] = e.allreduce(e.length(lists[b]))
+                    out.append(f"{list_size[b]:d}\n")
+                else:
+                    s_, t_ = owned_range(self.rel_rows[rel], e.rank, e.world)
+                    lists[b] = e.scan(rel, c, s_, t_, p.op, p.const)
+                    list_size[b] = e.allreduce(e.length(lists[b]))
+                k += 1
+                continue
+            run_end = k
+            while run_end < len(preds) and preds[run_end].kind == "join":
+                run_end += 1
+            run = preds[k:run_end]
+            while run:
+                j = min(range(len(run)), key=lambda i: (cost(run[i]), i)) if self.reorder else 0
+                q = run.pop(j)
+                do_join(q, run + preds[run_end:])
+            k = run_end
         # print_sums
         roots = {comp_of[b] for (b, _) in sels}
         if len(roots) != 1:
             raise NotSupported("disconnected selects")
         cid = roots.pop()
-        anyb = next(iter(comps[cid]))
-        rows = e.allreduce(e.length(comps[cid][anyb]))
+        rows = size[cid]
         line_out = []
         for (b, c) in sels:
-            s = e.allreduce(e.checksum(rels[b], c, comps[cid][b]))
+            s = e.allreduce(e.checksum(rels[b], c, rows_of(cid, b)))
             line_out.append("NULL " if rows == 0 else f"{s} ")
         out.append("".join(line_out) + "\n")
         return "".join(out), rows
+
+
+# ---------------------------------------------------------------------------------------------
+# the skewed 2-relation join in aggregate form (C5, SURVEY.md §8(e) "Skew")
+# ---------------------------------------------------------------------------------------------
+class DistAggJoin:
+    """`r0 r1|0.a=1.b|sel...` (one equi-join, no filters) without materialising pairs, N ranks.
+
+    sum over pairs of col(pR) = sum_k (sum_{r in R_k} col(r)) * |S_k| (and symmetrically), so:
+      heavy keys -- the keys whose sampled frequency exceeds rows / (N * 64) on either side; the
+                    sample is the first `sample` rows of the replicated key columns, identical on
+                    every rank, so every rank derives the same list without communication.  Each
+                    rank counts heavy keys over its own row slice of R and S (qe_heavy_stats),
+                    the counts are all-reduced, and each rank adds
+                    sum_{r in slice, key heavy} col(r) * |S_key| (weighted qe_heavy_stats) --
+                    no heavy row moves and no rank holds a heavy key's whole run;
+      light keys -- hash bucket per rank straight from the replicated columns
+                    (qe_bucket_select, heavy keys left out), sorted, merged in aggregate form
+                    (qe_merge_join_counts) and summed (qe_checksum_weighted);
+    and the sums and pair counts are all-reduced (exact mod 2^64).  The line printed is the
+    reference's print_sums line for the materialised join (SURVEY.md §9.5 proves the aggregate
+    form equal to the reference at 20 k rows)."""
+
+    def __init__(self, engine, rel_rows: list[int], sample: int = 1 << 21, heavy_div: int = 64):
+        self.e, self.rel_rows, self.sample, self.heavy_div = engine, rel_rows, sample, heavy_div
+
+    def heavy_keys(self, rel_a, ca, rel_b, cb) -> np.ndarray:
+        e = self.e
+        if e.world == 1:
+            return np.zeros(0, np.uint64)
+        out = set()
+        for rel, c in ((rel_a, ca), (rel_b, cb)):
+            pre = e.column_prefix(rel, c, self.sample)
+            if pre.size == 0:
+                continue
+            u, cnt = np.unique(pre, return_counts=True)
+            thr = pre.size / (e.world * self.heavy_div)
+            out.update(u[cnt > thr].tolist())
+        h = np.array(sorted(out), dtype=np.uint64)
+        return h[:1024]
+
+    def run(self, line: str):
+        e = self.e
+        rels, preds, sels = parse(line)
+        joins = [p for p in preds if p.kind == "join"]
+        if len(rels) != 2 or len(preds) != 1 or len(joins) != 1 or joins[0].a[0] == joins[0].b[0]:
+            raise NotSupported("aggregate plan: exactly one join between two bindings, no filters")
+        (ba, ca), (bb, cb) = joins[0].a, joins[0].b
+        if rels[ba] == rels[bb] and ca == cb:
+            raise NotSupported("same relation and column on both sides (reference DO_NOTHING)")
+        ra, rb = rels[ba], rels[bb]
+        sel_a = [(ra, c) for (b, c) in sels if b == ba]
+        sel_b = [(rb, c) for (b, c) in sels if b == bb]
+        heavy = self.heavy_keys(ra, ca, rb, cb)
+        # light keys: local buckets, aggregate merge
+        ka, va = e.base_side_light(ra, ca, heavy)
+        kb, vb = e.base_side_light(rb, cb, heavy)
+        pairs, sa, sb = e.join_count_sums(ka, va, kb, vb, sel_a, sel_b)
+        del ka, kb, va, vb
+        # heavy keys: slice counts -> global counts -> weighted slice sums
+        if heavy.size:
+            sa_, ta_ = owned_range(self.rel_rows[ra], e.rank, e.world)
+            sb_, tb_ = owned_range(self.rel_rows[rb], e.rank, e.world)
+            cA, _ = e.heavy_stats(ra, ca, sa_, ta_, heavy)
+            cB, _ = e.heavy_stats(rb, cb, sb_, tb_, heavy)
+            CA, CB = np.split(e.allreduce_vec(np.concatenate([cA, cB])), 2)
+            sa = [(x + e.heavy_stats(ra, ca, sa_, ta_, heavy, val=sc, weights=CB)[1]) & M64
+                  for x, sc in zip(sa, sel_a)]
+            sb = [(x + e.heavy_stats(rb, cb, sb_, tb_, heavy, val=sc, weights=CA)[1]) & M64
+                  for x, sc in zip(sb, sel_b)]
+            heavy_pairs = sum(int(x) * int(y) for x, y in zip(CA.tolist(), CB.tolist()))
+        else:
+            heavy_pairs = 0
+        red = e.allreduce_vec(np.array([pairs & M64] + sa + sb, dtype=np.uint64))
+        total = int(red[0]) + heavy_pairs
+        sums = {}
+        for i, key in enumerate(sel_a):
+            sums[("a", key)] = int(red[1 + i])
+        for i, key in enumerate(sel_b):
+            sums[("b", key)] = int(red[1 + len(sel_a) + i])
+        parts = []
+        for (b, c) in sels:
+            s = sums[("a", (ra, c))] if b == ba else sums[("b", (rb, c))]
+            parts.append("NULL " if total == 0 else f"{s} ")
+        return "".join(parts) + "\n", total, int(heavy.size)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -367,7 +601,8 @@ def bench_main(args, metric, query, cpu_baseline_fn=None, roofline_fn=None, traf
     backend = os.environ.get("QE_DIST_BACKEND", "nccl")
     dev = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev)
-    if not dist.is_initialized():
+    solo = world == 1                  # the plan alone on one GPU (bench.py --plan dist): no group
+    if not solo and not dist.is_initialized():
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
         else:
@@ -385,18 +620,21 @@ def bench_main(args, metric, query, cpu_baseline_fn=None, roofline_fn=None, traf
         out, rows = ex.run(query)
     ctx.set_profiling(True)
     ctx.reset_stats()
-    dist.barrier()
+    if not solo:
+        dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out, rows = ex.run(query)
     ctx.sync()
     torch.cuda.synchronize()
-    dist.barrier()
+    if not solo:
+        dist.barrier()
     dt = time.perf_counter() - t0
-    tmax = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}" if backend == "nccl" else "cpu")
-    dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    dt = float(tmax.item())
+    if not solo:
+        tmax = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}" if backend == "nccl" else "cpu")
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dt = float(tmax.item())
     stats = ctx.kernel_stats()
     ctx.set_profiling(False)
     res = None
@@ -417,9 +655,11 @@ def bench_main(args, metric, query, cpu_baseline_fn=None, roofline_fn=None, traf
             "stages": {k: {"ms_per_step": round(s["ms"] / args.steps, 3)} for k, s in kern[:10]},
             "cpu_baseline": None,
         }
-    dist.barrier()
+    if not solo:
+        dist.barrier()
     ctx.close()
-    dist.destroy_process_group()
+    if not solo:
+        dist.destroy_process_group()
     if rank == 0:
         print(f"[bench] rank 0 done: {out.strip()!r}", file=sys.stderr)
     return res

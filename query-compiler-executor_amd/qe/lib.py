@@ -100,6 +100,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "qe_take_u32": (I, [P, C.c_void_p, C.POINTER(List), C.POINTER(List)]),
         "qe_join_indices": (I, [P, C.c_void_p, U64, C.c_void_p, U64, C.POINTER(List), C.POINTER(List)]),
         "qe_sync_stream_ptr": (I, [P, C.POINTER(C.c_void_p)]),
+        "qe_bucket_select": (I, [P, Col, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.POINTER(Pairs)]),
+        "qe_heavy_stats": (I, [P, Col, U64, U64, C.c_void_p, C.c_uint32, Col, C.c_void_p, C.c_void_p,
+                               C.POINTER(C.c_uint64)]),
         "qe_list_alloc": (I, [P, U64, C.POINTER(List)]),
         "qe_list_from_host": (I, [P, VP, U64, C.c_uint32, C.POINTER(List)]),
         "qe_list_to_host": (I, [P, C.POINTER(List), VP]),
@@ -358,6 +361,25 @@ class Ctx:
         ia, ib = List(), List()
         self._chk(self.lib.qe_join_indices(self.h, a_ptr, na, b_ptr, nb, C.byref(ia), C.byref(ib)))
         return ia, ib
+
+    def bucket_select(self, col: Col, nparts: int, part: int, heavy=None) -> Pairs:
+        """(key, rowid) pairs of the base column's hash bucket `part` (heavy keys left out)"""
+        h = np.ascontiguousarray(heavy if heavy is not None else np.zeros(0, np.uint64), dtype=np.uint64)
+        p = Pairs()
+        self._chk(self.lib.qe_bucket_select(self.h, col, nparts, part, h.ctypes.data if h.size else None, h.size,
+                                            C.byref(p)))
+        return p
+
+    def heavy_stats(self, keys: Col, start: int, end: int, heavy, vals: Col | None = None, weights=None):
+        """-> (counts per heavy key over rows [start, end), weighted value sum mod 2^64 or None)"""
+        h = np.ascontiguousarray(heavy, dtype=np.uint64)
+        counts = np.zeros(h.size, dtype=np.uint64)
+        w = None if weights is None else np.ascontiguousarray(weights, dtype=np.uint64)
+        s = C.c_uint64()
+        self._chk(self.lib.qe_heavy_stats(self.h, keys, start, end, h.ctypes.data if h.size else None, h.size,
+                                          vals if vals is not None else Col(), w.ctypes.data if w is not None else None,
+                                          counts.ctypes.data if h.size else None, C.byref(s)))
+        return counts, (s.value if w is not None else None)
 
     def sync(self):
         self._chk(self.lib.qe_sync(self.h))

@@ -25,3 +25,26 @@ def worker(rank, world, port, rows, queries, outq):
     finally:
         ctx.close()
         dist.destroy_process_group()
+
+
+def agg_worker(rank, world, port, rows, queries, outq):
+    """the aggregate (skew) plan on C5-shaped data, `rows` per side"""
+    import torch
+    import torch.distributed as dist
+
+    from qe import c5bench, lib
+    from qe.dist import DistAggJoin, GPUEngine
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    ctx = lib.Ctx(0)
+    try:
+        c5bench.gen_c5(ctx, rows)
+        ex = DistAggJoin(GPUEngine(ctx, rank, world), [rows, rows])
+        res = [ex.run(q) for q in queries]
+        if rank == 0:
+            outq.put(res)
+    finally:
+        ctx.close()
+        dist.destroy_process_group()

@@ -34,6 +34,44 @@ def test_partition_is_stable_grouping(ctx, n, parts, ncols):
         np.testing.assert_array_equal(o.cpu().numpy()[:n].view(np.uint32), c[order])
 
 
+@pytest.mark.parametrize("n,parts,nheavy", [(0, 2, 0), (1, 1, 0), (5, 3, 1), (100_001, 8, 0), (3_000_001, 8, 5),
+                                            (2_000_000, 1, 0), (777_777, 64, 20)])
+def test_bucket_select_is_the_hash_bucket(ctx, n, parts, nheavy):
+    rng = np.random.default_rng(n + parts)
+    keys = rng.integers(0, max(1, n // 3), n, dtype=np.uint64) * np.uint64(0x9E3779B1)
+    rel = ctx.load_relation([keys])
+    heavy = np.unique(keys[:nheavy]) if nheavy else np.zeros(0, np.uint64)
+    dest = (dce.fmix64(keys) % np.uint64(parts)).astype(np.int64)
+    for part in sorted({0, parts - 1, parts // 2}):
+        p = ctx.bucket_select(ctx.column(rel, 0), parts, part, heavy)
+        k, v = ctx.pairs_to_host(p)
+        ctx.pairs_free(p)
+        want = np.nonzero((dest == part) & ~np.isin(keys, heavy))[0]
+        np.testing.assert_array_equal(np.sort(v), want.astype(np.uint32))   # each row once, no other
+        np.testing.assert_array_equal(k, keys[v])
+    ctx.drop_relations()
+
+
+@pytest.mark.parametrize("n,start,end", [(0, 0, 0), (10, 2, 9), (2_500_000, 123, 2_400_000)])
+def test_heavy_stats_counts_and_weighted_sums(ctx, n, start, end):
+    rng = np.random.default_rng(7 + n)
+    keys = rng.zipf(1.3, n).astype(np.uint64) if n else np.zeros(0, np.uint64)
+    vals = rng.integers(0, 1 << 63, n, dtype=np.uint64)
+    rel = ctx.load_relation([keys, vals])
+    heavy = np.array([1, 2, 3, 5, 1 << 40], dtype=np.uint64)
+    w = np.array([3, 1 << 62, 7, 0, 9], dtype=np.uint64)
+    counts, s = ctx.heavy_stats(ctx.column(rel, 0), start, end, heavy, ctx.column(rel, 1), w)
+    kk, vv = keys[start:end], vals[start:end]
+    want_c = [int(np.sum(kk == h)) for h in heavy]
+    want_s = 0
+    for h, wt in zip(heavy.tolist(), w.tolist()):
+        want_s = (want_s + int(np.sum(vv[kk == h], dtype=np.uint64)) * wt) % (1 << 64)
+    assert counts.tolist() == want_c and s == want_s
+    c2, none = ctx.heavy_stats(ctx.column(rel, 0), start, end, heavy)
+    assert c2.tolist() == want_c and none is None
+    ctx.drop_relations()
+
+
 def test_filter_scan_range_and_iota(ctx):
     a = dg.column(3, 1, 2, 50_000, ("hi32",))
     rel = ctx.load_relation([a])
@@ -95,3 +133,34 @@ def test_gpu_plan_two_ranks_share_one_gpu(ctx):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert res[0][0] + res[1][0] == want
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_gpu_agg_plan_equals_faithful_executor_on_c5(ctx, world):
+    """DistAggJoin (heavy split + local buckets + aggregate merge) on the GPU equals the faithful
+    executor's aggregate path on the same Zipf data; world 2 = two gloo ranks on the one GPU"""
+    from qe import c5bench
+    from qe.dist import DistAggJoin
+    rows = 3_000_000
+    queries = ["0 1|0.1=1.0|0.2 1.2", "0 1|0.1=1.0|1.2 0.2 0.0 1.1 0.1", "1 0|0.0=1.1|0.2 1.2"]
+    ctx.drop_relations()
+    c5bench.gen_c5(ctx, rows)
+    want = [ctx.run(q + "\n")[0] for q in queries]
+    if world == 1:
+        res = [DistAggJoin(GPUEngine(ctx, 0, 1), [rows, rows]).run(q) for q in queries]
+        ctx.drop_relations()
+    else:
+        ctx.drop_relations()
+        mpc = mp.get_context("spawn")
+        q = mpc.Queue()
+        port = dce.free_port()
+        procs = [mpc.Process(target=gpu_dist_worker.agg_worker, args=(r, 2, port, rows, queries, q))
+                 for r in range(2)]
+        for p in procs:
+            p.start()
+        res = q.get(timeout=600)
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+        assert all(nheavy > 0 for _, _, nheavy in res)
+    assert [r[0] for r in res] == want
