@@ -180,8 +180,8 @@ int qe_checksum(qe_ctx*, qe_col col, const qe_list* rows, uint64_t* sum);
 int qe_checksum_weighted(qe_ctx*, qe_col col, const qe_pairs* p, uint64_t* sum);
 
 /* ---- multi-GPU plan; the exchange itself is an RCCL all-to-all -------------- */
-/* Hash-partition n rows on their key: dest = fmix64(key) % nparts (murmur3 finaliser).  Rows go
- * to contiguous per-destination segments (dest order, input order kept inside a segment) of the
+/* Hash-partition n rows on their key: dest = (hi32((key ^ key >> 29) * 0xbf58476d1ce4e5b9) * nparts) >> 32.  Rows go
+ * to contiguous per-destination segments (dest order; order inside a segment unspecified) of the
  * caller's device buffers out_keys / out_cols[c] (capacity n each); counts[p] (host) = rows for
  * destination p.  ncols <= 4 uint32 rowid columns travel with each key. */
 int qe_partition(qe_ctx*, const uint64_t* keys, uint64_t n, const uint32_t* const* cols, int ncols,
@@ -195,7 +195,7 @@ int qe_take_u32(qe_ctx*, const uint32_t* src, const qe_list* idx, qe_list* out);
 /* Equi-join of two key arrays (a rank's bucket): sort both, merge, return aligned row indices. */
 int qe_join_indices(qe_ctx*, const uint64_t* keysA, uint64_t nA, const uint64_t* keysB, uint64_t nB, qe_list* ia,
                     qe_list* ib);
-/* Local bucket of a replicated base column: the rows with fmix64(key) % nparts == part, as
+/* Local bucket of a replicated base column: the rows whose qe_partition dest is `part`, as
  * (key, rowid) pairs in no particular order (out owns both arrays).  Keys in the sorted list
  * heavy[0..nheavy) (host memory, <= 1024, the skew path) are left out.  Replaces the exchange
  * of a join side that is a whole base relation: every rank holds the column. */

@@ -2,7 +2,7 @@
 //
 // Each rank owns a rowid slice of every relation (base columns replicated, so rowid gathers
 // stay local).  Before each join the rows of both sides are hash-partitioned on the join key,
-// dest = fmix64(key) % nparts, into contiguous per-destination segments of caller-provided
+// dest = part_of(key) = (hi32(mix(key)) * nparts) >> 32, into contiguous per-destination segments of caller-provided
 // send buffers; the caller moves them with one RCCL all-to-all per array (torch.distributed,
 // backend "nccl" = RCCL over xGMI), then joins its own bucket locally with the single-GPU
 // sort + merge kernels.  Checksums are added mod 2^64 and all-reduced.
@@ -13,62 +13,82 @@
 
 namespace qe {
 
-__host__ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {   // murmur3 finaliser
-    k ^= k >> 33;
-    k *= 0xff51afd7ed558ccdull;
-    k ^= k >> 33;
-    k *= 0xc4ceb9fe1a85ec53ull;
-    k ^= k >> 33;
-    return k;
+// destination of a key: one xor-shift-multiply mix (splitmix64's first round), its high half
+// scaled to [0, nparts) by a multiply -- a few VALU ops per key.  (murmur3's full finaliser plus
+// a 64-bit modulo -- a software division on gfx950 -- made the 8-way bucket scan ALU-bound.)
+__host__ __device__ __forceinline__ uint32_t part_of(uint64_t k, uint32_t nparts) {
+    const uint64_t h = (k ^ (k >> 29)) * 0xbf58476d1ce4e5b9ull;
+    return (uint32_t)(((h >> 32) * (uint64_t)nparts) >> 32);
 }
 
-constexpr int PB = 256;                 // block
-constexpr int P_ITEMS = 8;
-constexpr int PTILE = PB * P_ITEMS;     // rows per block
 constexpr int PMAX = 64;                // max destinations
+constexpr int PB = 512;                 // block
+constexpr int P_ITEMS = 8;              // rows per thread (strided by PB: coalesced)
+constexpr int PTILE = PB * P_ITEMS;     // rows per tile
 constexpr int PNW = PB / 64;
 
+// lanes of this wave holding the same destination (match-any from log2(nparts) ballots)
+__device__ __forceinline__ uint64_t dest_peers(uint32_t d, bool ok, int dbits) {
+    uint64_t peers = __ballot(ok);
+    for (int b = 0; b < dbits; b++) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t mm = __ballot(bit);
+        peers &= bit ? mm : ~mm;
+    }
+    return peers;
+}
+
+// rows per destination: per-wave match-any, one LDS add per (wave, item, distinct dest), one
+// global add per (block, dest)
 __global__ void __launch_bounds__(PB) part_count_kernel(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nparts,
-                                                        uint32_t* __restrict__ table /*[nblocks][nparts]*/) {
+                                                        int dbits, unsigned long long* __restrict__ counts) {
+    // a capped grid (one global add per (block, dest): ~88 adds per us per word) walking tiles of
+    // PTILE x 2 rows, 16-B loads, the next tile's loads issued before this one is counted
     __shared__ uint32_t h[PMAX];
     for (int i = threadIdx.x; i < PMAX; i += PB) h[i] = 0;
     __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * PTILE;
+    const int l = lane_id();
+    constexpr uint64_t T2 = 2ull * PTILE;
+    const uint64_t stride = (uint64_t)gridDim.x * T2;
+    auto load = [&](uint64_t tile, uint64_t (&k)[P_ITEMS][2]) {
 #pragma unroll
-    for (int j = 0; j < P_ITEMS; j++) {
-        uint64_t i = base + (uint64_t)j * PB + threadIdx.x;
-        if (i < n) atomicAdd(&h[fmix64(keys[i]) % nparts], 1u);
-    }
-    __syncthreads();
-    for (uint32_t p = threadIdx.x; p < nparts; p += PB) table[(uint64_t)blockIdx.x * nparts + p] = h[p];
-}
-
-// column-major exclusive scan of the [nblocks][nparts] table: offset of (block, dest) in the
-// send buffer, destination segments contiguous; totals[p] = rows for dest p.  One block.
-__global__ void __launch_bounds__(1024) part_scan_kernel(uint32_t* __restrict__ table, uint32_t nblocks,
-                                                         uint32_t nparts, uint64_t* __restrict__ totals) {
-    __shared__ uint64_t wsum[16];
-    __shared__ uint64_t carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (uint32_t p = 0; p < nparts; p++) {
-        uint64_t start = carry;
-        for (uint32_t b0 = 0; b0 < nblocks; b0 += 1024) {
-            uint32_t b = b0 + threadIdx.x;
-            uint64_t x = b < nblocks ? table[(uint64_t)b * nparts + p] : 0;
-            uint64_t inc = wave_incl_scan_u64(x);
-            if (lane_id() == 63) wsum[wave_id()] = inc;
-            __syncthreads();
-            uint64_t add = carry;
-            for (int w = 0; w < wave_id(); w++) add += wsum[w];
-            if (b < nblocks) table[(uint64_t)b * nparts + p] = (uint32_t)(inc - x + add);   // rows < 2^32
-            __syncthreads();
-            if (threadIdx.x == 1023) carry = add + inc;
-            __syncthreads();
+        for (int j = 0; j < P_ITEMS; j++) {
+            const uint64_t i = tile + (uint64_t)j * (2 * PB) + 2ull * threadIdx.x;
+            if (i + 1 < n) {
+                ulonglong2 x = *reinterpret_cast<const ulonglong2*>(keys + i);
+                k[j][0] = x.x;
+                k[j][1] = x.y;
+            } else {
+                k[j][0] = i < n ? keys[i] : 0;
+                k[j][1] = 0;
+            }
         }
-        if (threadIdx.x == 0) totals[p] = carry - start;
-        __syncthreads();
+    };
+    uint64_t k[P_ITEMS][2], kn[P_ITEMS][2];
+    uint64_t tile = (uint64_t)blockIdx.x * T2;
+    if (tile < n) load(tile, k);
+    for (; tile < n; tile += stride) {
+        if (tile + stride < n) load(tile + stride, kn);
+#pragma unroll
+        for (int j = 0; j < P_ITEMS; j++) {
+#pragma unroll
+            for (int v = 0; v < 2; v++) {
+                const uint64_t i = tile + (uint64_t)j * (2 * PB) + 2ull * threadIdx.x + v;
+                const bool ok = i < n;
+                const uint32_t d = ok ? part_of(k[j][v], nparts) : 0;
+                const uint64_t peers = dest_peers(d, ok, dbits);
+                if (ok && l == __ffsll((unsigned long long)peers) - 1) atomicAdd(&h[d], (uint32_t)__popcll(peers));
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < P_ITEMS; j++) {
+            k[j][0] = kn[j][0];
+            k[j][1] = kn[j][1];
+        }
     }
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < nparts; p += PB)
+        if (h[p]) atomicAdd(&counts[p], (unsigned long long)h[p]);
 }
 
 // rowid columns travel by value in the kernel arguments: pointers loaded from a device array
@@ -78,52 +98,88 @@ struct PartCols {
     uint32_t* out[4];
 };
 
-// stable scatter: element order is kept inside every destination segment
+// scatter: a tile is ranked by destination in registers (match-any + per-wave LDS counters),
+// staged in LDS in destination order, each destination's range in the send buffer reserved with
+// one atomic on its cursor (cursor[d] starts at d's segment start), and written as runs of
+// ~PTILE / nparts rows.  Order inside a segment is not kept (the receiver sorts).
 template <int NC>
 __global__ void __launch_bounds__(PB) part_scatter_kernel(const uint64_t* __restrict__ keys, uint64_t n,
-                                                          uint32_t nparts, const uint32_t* __restrict__ table,
-                                                          PartCols pc, uint64_t* __restrict__ okeys) {
-    __shared__ uint32_t cnt[P_ITEMS][PNW][PMAX];   // (step, wave, dest) counts -> exclusive prefix
+                                                          uint32_t nparts, int dbits,
+                                                          unsigned long long* __restrict__ cursor, PartCols pc,
+                                                          uint64_t* __restrict__ okeys) {
+    __shared__ uint64_t s_key[PTILE];
+    __shared__ uint32_t s_col[NC > 0 ? NC : 1][PTILE];
+    __shared__ uint8_t s_dest[PTILE];
+    __shared__ uint32_t whist[PNW][PMAX];
+    __shared__ uint32_t toff[PMAX + 1];
+    __shared__ uint64_t gbase[PMAX];
     const int w = wave_id(), l = lane_id();
     const uint64_t lt = lanemask_lt();
-    const uint64_t base = (uint64_t)blockIdx.x * PTILE;
-    uint32_t dest[P_ITEMS], rank[P_ITEMS];
-    uint64_t key[P_ITEMS];
+    const uint64_t tile = (uint64_t)blockIdx.x * PTILE;
+    for (int i = threadIdx.x; i < PNW * PMAX; i += PB) (&whist[0][0])[i] = 0;
+    uint64_t k[P_ITEMS];
+    uint32_t cv[NC > 0 ? NC : 1][P_ITEMS];
 #pragma unroll
     for (int j = 0; j < P_ITEMS; j++) {
-        uint64_t i = base + (uint64_t)j * PB + threadIdx.x;
-        bool ok = i < n;
-        key[j] = ok ? keys[i] : 0;
-        dest[j] = ok ? (uint32_t)(fmix64(key[j]) % nparts) : PMAX;
-        uint32_t r = 0;
-        for (uint32_t p = 0; p < nparts; p++) {
-            uint64_t m = __ballot(dest[j] == p);
-            if (dest[j] == p) r = (uint32_t)__popcll(m & lt);
-            if (l == 0) cnt[j][w][p] = (uint32_t)__popcll(m);
+        const uint64_t i = tile + (uint64_t)j * PB + threadIdx.x;
+        const bool ok = i < n;
+        k[j] = ok ? keys[i] : 0;
+#pragma unroll
+        for (int c = 0; c < NC; c++) cv[c][j] = ok ? pc.in[c][i] : 0;
+    }
+    __syncthreads();   // whist cleared
+    uint32_t dst[P_ITEMS], rank[P_ITEMS];
+#pragma unroll
+    for (int j = 0; j < P_ITEMS; j++) {      // items in order: the wave's LDS counters stay exact
+        const uint64_t i = tile + (uint64_t)j * PB + threadIdx.x;
+        const bool ok = i < n;
+        const uint32_t d = ok ? part_of(k[j], nparts) : 0;
+        const uint64_t peers = dest_peers(d, ok, dbits);
+        const int leader = peers ? __ffsll((unsigned long long)peers) - 1 : 0;
+        uint32_t old = 0;
+        if (ok && l == leader) {
+            old = whist[w][d];
+            whist[w][d] = old + (uint32_t)__popcll(peers);
         }
-        rank[j] = r;
+        old = (uint32_t)__shfl((int)old, leader, 64);
+        dst[j] = ok ? d : PMAX;
+        rank[j] = old + (uint32_t)__popcll(peers & lt);
     }
     __syncthreads();
-    // exclusive prefix over (step, wave) for each destination, starting at the block's offset
-    for (uint32_t p = threadIdx.x; p < nparts; p += PB) {
-        uint32_t run = table[(uint64_t)blockIdx.x * nparts + p];
-        for (int j = 0; j < P_ITEMS; j++)
-            for (int ww = 0; ww < PNW; ww++) {
-                uint32_t c = cnt[j][ww][p];
-                cnt[j][ww][p] = run;
-                run += c;
-            }
+    // per destination: exclusive prefix over waves, tile total; then a scan over destinations
+    uint32_t tot = 0;
+    if (threadIdx.x < PMAX) {
+        const uint32_t d = threadIdx.x;
+#pragma unroll
+        for (int ww = 0; ww < PNW; ww++) {
+            const uint32_t c = whist[ww][d];
+            whist[ww][d] = tot;
+            tot += c;
+        }
+        const uint32_t inc = wave_incl_scan_u32(tot);   // threads 0..63 = wave 0
+        toff[d] = inc - tot;
+        if (d == PMAX - 1) toff[PMAX] = inc;
+        if (tot && d < nparts) gbase[d] = atomicAdd(&cursor[d], (unsigned long long)tot);
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < P_ITEMS; j++) {
-        uint64_t i = base + (uint64_t)j * PB + threadIdx.x;
-        if (i < n) {
-            uint32_t o = cnt[j][w][dest[j]] + rank[j];
-            okeys[o] = key[j];
+        if (dst[j] < PMAX) {
+            const uint32_t pos = toff[dst[j]] + whist[w][dst[j]] + rank[j];
+            s_key[pos] = k[j];
+            s_dest[pos] = (uint8_t)dst[j];
 #pragma unroll
-            for (int c = 0; c < NC; c++) pc.out[c][o] = pc.in[c][i];
+            for (int c = 0; c < NC; c++) s_col[c][pos] = cv[c][j];
         }
+    }
+    __syncthreads();
+    const uint32_t total = toff[PMAX];
+    for (uint32_t i = threadIdx.x; i < total; i += PB) {
+        const uint32_t d = s_dest[i];
+        const uint64_t o = gbase[d] + (i - toff[d]);
+        okeys[o] = s_key[i];
+#pragma unroll
+        for (int c = 0; c < NC; c++) pc.out[c][o] = s_col[c][i];
     }
 }
 
@@ -147,14 +203,24 @@ __global__ void __launch_bounds__(256) add_u32_kernel(uint32_t* __restrict__ a, 
 // ---- local bucket select: the hash bucket `part` of a replicated base column ----------------------
 // Base columns are replicated on every rank, so a join side that is a whole base
 // relation is bucketed by one scan of the column instead of an exchange: rank g keeps the rows
-// with fmix64(key) % nparts == g -- exactly the rows the exchange would have delivered to it.
-// Unordered compaction (the bucket is sorted next): per (step, wave) survivor runs are ranked with
-// ballots, the block reserves its range with one atomic, every wave writes its runs contiguously.
+// with part_of(key, nparts) == g -- exactly the rows the exchange would have delivered to it.
+// Unordered compaction (the bucket is sorted next).  A block walks sub-tiles of 4096 rows
+// (grid-stride, the next sub-tile's loads in flight while this one is ranked), ranks survivors
+// with ballots and appends them to an LDS stage of BS_CAP (key, rowid) pairs; a full stage is
+// flushed as one contiguous run, its range reserved with ONE atomic.  (An atomic per sub-tile
+// serialises on the counter: ~88 per us on one word, 200 k sub-tiles at 8e8 rows = 2.3 ms.)
 // Keys listed in `heavy` (sorted, skew path) are left out of every bucket.
-constexpr int BS_B = 512;
-constexpr int BS_ITEMS = 4;                 // x 2 keys per 16-B load
+#ifndef QE_BS_B
+#define QE_BS_B 256
+#endif
+#ifndef QE_BS_ITEMS
+#define QE_BS_ITEMS 4
+#endif
+constexpr int BS_B = QE_BS_B;
+constexpr int BS_ITEMS = QE_BS_ITEMS;       // x 2 keys per 16-B load
 constexpr int BS_TILE = BS_B * BS_ITEMS * 2;
 constexpr int BS_NW = BS_B / 64;
+constexpr int BS_CAP = BS_TILE;             // staged survivors (a sub-tile's worst case): 12 B each
 constexpr int HEAVY_MAX = 1024;
 
 __device__ __forceinline__ int heavy_find(const uint64_t* h, uint32_t nh, uint64_t k) {
@@ -169,19 +235,8 @@ __device__ __forceinline__ int heavy_find(const uint64_t* h, uint32_t nh, uint64
     return (lo < nh && h[lo] == k) ? (int)lo : -1;
 }
 
-__global__ void __launch_bounds__(BS_B) bucket_select_kernel(const uint64_t* __restrict__ keys, uint64_t n,
-                                                             uint32_t nparts, uint32_t part,
-                                                             const uint64_t* __restrict__ heavy, uint32_t nheavy,
-                                                             uint64_t* __restrict__ okeys, uint32_t* __restrict__ ovals,
-                                                             uint64_t cap, unsigned long long* __restrict__ counter) {
-    __shared__ uint64_t s_heavy[HEAVY_MAX];
-    __shared__ uint32_t s_cnt[BS_ITEMS * 2 * BS_NW];
-    __shared__ uint64_t s_base;
-    for (uint32_t i = threadIdx.x; i < nheavy; i += BS_B) s_heavy[i] = heavy[i];
-    const int w = wave_id(), l = lane_id();
-    const uint64_t lt = lanemask_lt();
-    const uint64_t tile = (uint64_t)blockIdx.x * BS_TILE;
-    uint64_t k[BS_ITEMS][2];
+__device__ __forceinline__ void bs_load(const uint64_t* __restrict__ keys, uint64_t n, uint64_t tile,
+                                        uint64_t (&k)[BS_ITEMS][2]) {
 #pragma unroll
     for (int j = 0; j < BS_ITEMS; j++) {
         const uint64_t i = tile + (uint64_t)j * (BS_B * 2) + (uint64_t)threadIdx.x * 2;
@@ -194,44 +249,98 @@ __global__ void __launch_bounds__(BS_B) bucket_select_kernel(const uint64_t* __r
             k[j][1] = 0;
         }
     }
+}
+
+__global__ void __launch_bounds__(BS_B) bucket_select_kernel(const uint64_t* __restrict__ keys, uint64_t n,
+                                                             uint32_t nparts, uint32_t part,
+                                                             const uint64_t* __restrict__ heavy, uint32_t nheavy,
+                                                             uint64_t* __restrict__ okeys, uint32_t* __restrict__ ovals,
+                                                             uint64_t cap, unsigned long long* __restrict__ counter) {
+    __shared__ uint64_t s_key[BS_CAP];
+    __shared__ uint32_t s_row[BS_CAP];
+    extern __shared__ uint64_t s_heavy[];   // nheavy words (dynamic: no LDS when there are none)
+    __shared__ uint32_t s_cnt[BS_ITEMS * 2 * BS_NW];
+    __shared__ uint32_t s_total;
+    __shared__ uint64_t s_base;
+    constexpr int NC = BS_ITEMS * 2 * BS_NW;
+    static_assert(NC <= 64, "one wave scans the (item, slot, wave) counts");
+    for (uint32_t i = threadIdx.x; i < nheavy; i += BS_B) s_heavy[i] = heavy[i];
+    const int w = wave_id(), l = lane_id();
+    const uint64_t lt = lanemask_lt();
+    const uint64_t nsub = (n + BS_TILE - 1) / BS_TILE;
+    uint32_t fill = 0;   // block-uniform
+    uint64_t k[BS_ITEMS][2], kn[BS_ITEMS][2];
+    uint64_t sub = blockIdx.x;
+    if (sub < nsub) bs_load(keys, n, sub * BS_TILE, k);
     __syncthreads();   // s_heavy
-    bool f[BS_ITEMS][2];
-    uint32_t rank[BS_ITEMS][2];
+    for (; sub < nsub; sub += gridDim.x) {
+        const uint64_t tile = sub * BS_TILE;
+        const uint64_t nxt = sub + gridDim.x;
+        if (nxt < nsub) bs_load(keys, n, nxt * BS_TILE, kn);
+        bool f[BS_ITEMS][2];
+        uint32_t rank[BS_ITEMS][2];
 #pragma unroll
-    for (int j = 0; j < BS_ITEMS; j++) {
-        const uint64_t i = tile + (uint64_t)j * (BS_B * 2) + (uint64_t)threadIdx.x * 2;
+        for (int j = 0; j < BS_ITEMS; j++) {
+            const uint64_t i = tile + (uint64_t)j * (BS_B * 2) + (uint64_t)threadIdx.x * 2;
 #pragma unroll
-        for (int v = 0; v < 2; v++) {
-            bool ok = i + v < n && (uint32_t)(fmix64(k[j][v]) % nparts) == part;
-            if (ok && nheavy) ok = heavy_find(s_heavy, nheavy, k[j][v]) < 0;
-            f[j][v] = ok;
-            uint64_t m = __ballot(ok);
-            rank[j][v] = (uint32_t)__popcll(m & lt);
-            if (l == 0) s_cnt[(j * 2 + v) * BS_NW + w] = (uint32_t)__popcll(m);
-        }
-    }
-    __syncthreads();
-    if (w == 0) {
-        constexpr int NC = BS_ITEMS * 2 * BS_NW;
-        uint32_t c = l < NC ? s_cnt[l] : 0;
-        uint32_t inc = wave_incl_scan_u32(c);
-        uint32_t total = (uint32_t)__shfl((int)inc, NC - 1, 64);
-        if (l < NC) s_cnt[l] = inc - c;
-        if (l == 0) s_base = total ? atomicAdd(counter, (unsigned long long)total) : 0;
-    }
-    __syncthreads();
-    const uint64_t base = s_base;
-#pragma unroll
-    for (int j = 0; j < BS_ITEMS; j++) {
-        const uint64_t i = tile + (uint64_t)j * (BS_B * 2) + (uint64_t)threadIdx.x * 2;
-#pragma unroll
-        for (int v = 0; v < 2; v++) {
-            const uint64_t o = base + s_cnt[(j * 2 + v) * BS_NW + w] + rank[j][v];
-            if (f[j][v] && o < cap) {   // an overfull bucket is counted, not written, and re-run
-                okeys[o] = k[j][v];
-                ovals[o] = (uint32_t)(i + v);
+            for (int v = 0; v < 2; v++) {
+                bool ok = i + v < n && part_of(k[j][v], nparts) == part;
+                if (ok && nheavy) ok = heavy_find(s_heavy, nheavy, k[j][v]) < 0;
+                f[j][v] = ok;
+                const uint64_t m = __ballot(ok);
+                rank[j][v] = (uint32_t)__popcll(m & lt);
+                if (l == 0) s_cnt[(j * 2 + v) * BS_NW + w] = (uint32_t)__popcll(m);
             }
         }
+        __syncthreads();
+        if (w == 0) {
+            const uint32_t c = l < NC ? s_cnt[l] : 0;
+            const uint32_t inc = wave_incl_scan_u32(c);
+            if (l < NC) s_cnt[l] = inc - c;
+            if (l == NC - 1) s_total = inc;
+        }
+        __syncthreads();
+        const uint32_t total = s_total;
+        if (fill + total > (uint32_t)BS_CAP) {          // block-uniform: flush the stage
+            if (threadIdx.x == 0) s_base = atomicAdd(counter, (unsigned long long)fill);
+            __syncthreads();
+            const uint64_t base = s_base;
+            for (uint32_t i = threadIdx.x; i < fill; i += BS_B)
+                if (base + i < cap) {                    // an overfull bucket is counted, not written
+                    okeys[base + i] = s_key[i];
+                    ovals[base + i] = s_row[i];
+                }
+            __syncthreads();
+            fill = 0;
+        }
+#pragma unroll
+        for (int j = 0; j < BS_ITEMS; j++) {
+            const uint64_t i = tile + (uint64_t)j * (BS_B * 2) + (uint64_t)threadIdx.x * 2;
+#pragma unroll
+            for (int v = 0; v < 2; v++)
+                if (f[j][v]) {
+                    const uint32_t o = fill + s_cnt[(j * 2 + v) * BS_NW + w] + rank[j][v];
+                    s_key[o] = k[j][v];
+                    s_row[o] = (uint32_t)(i + v);
+                }
+        }
+        fill += total;
+        __syncthreads();                                 // s_cnt / s_total reused next sub-tile
+#pragma unroll
+        for (int j = 0; j < BS_ITEMS; j++) {
+            k[j][0] = kn[j][0];
+            k[j][1] = kn[j][1];
+        }
+    }
+    if (fill) {
+        if (threadIdx.x == 0) s_base = atomicAdd(counter, (unsigned long long)fill);
+        __syncthreads();
+        const uint64_t base = s_base;
+        for (uint32_t i = threadIdx.x; i < fill; i += BS_B)
+            if (base + i < cap) {
+                okeys[base + i] = s_key[i];
+                ovals[base + i] = s_row[i];
+            }
     }
 }
 
@@ -292,35 +401,46 @@ int qe_partition(qe_ctx* c, const uint64_t* keys, uint64_t n, const uint32_t* co
     if (n >= 0xFFFFFFFFull) throw Error(QE_EINVAL, "partition input too large");
     for (uint32_t p = 0; p < nparts; p++) counts[p] = 0;
     if (n == 0) return 0;
+    int dbits = 0;
+    while ((1u << dbits) < nparts) dbits++;
     const uint32_t nb = (uint32_t)((n + PTILE - 1) / PTILE);
-    uint32_t* table = dalloc_t<uint32_t>(c, (uint64_t)nb * nparts);
-    uint64_t* d_tot = dalloc_t<uint64_t>(c, nparts);
+    unsigned long long* d_cnt = dalloc_t<unsigned long long>(c, 2 * PMAX);   // [counts | cursors]
     PartCols pc{};
     for (int i = 0; i < ncols; i++) {
         pc.in[i] = cols[i];
         pc.out[i] = out_cols[i];
     }
+    QE_HIP(hipMemsetAsync(d_cnt, 0, PMAX * sizeof(uint64_t), c->stream));
     {
-        Timed t(c, "partition", (8.0 + 4.0 * ncols) * 2.0 * n + 8.0 * n);
-        hipLaunchKernelGGL(part_count_kernel, dim3(nb), dim3(PB), 0, c->stream, keys, n, nparts, table);
+        Timed t(c, "partition_count", 8.0 * n);
+        hipLaunchKernelGGL(part_count_kernel, dim3(std::min<uint32_t>(nb, 1024)), dim3(PB), 0, c->stream, keys, n,
+                           nparts, dbits, d_cnt);
         QE_HIP(hipGetLastError());
-        hipLaunchKernelGGL(part_scan_kernel, dim3(1), dim3(1024), 0, c->stream, table, nb, nparts, d_tot);
-        QE_HIP(hipGetLastError());
+    }
+    QE_HIP(hipMemcpyAsync(counts, d_cnt, nparts * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    QE_HIP(hipStreamSynchronize(c->stream));
+    uint64_t start[PMAX], run = 0;
+    for (uint32_t p = 0; p < nparts; p++) {
+        start[p] = run;
+        run += counts[p];
+    }
+    if (run != n) throw Error(QE_EINVAL, "internal: partition counts do not add up");
+    QE_HIP(hipMemcpyAsync(d_cnt + PMAX, start, nparts * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    {
+        Timed t(c, "partition", (8.0 + 4.0 * ncols) * 2.0 * n);
         switch (ncols) {
-#define QE_PS(NC)                                                                                              \
-    case NC:                                                                                                   \
-        hipLaunchKernelGGL(part_scatter_kernel<NC>, dim3(nb), dim3(PB), 0, c->stream, keys, n, nparts, table, \
-                           pc, out_keys);                                                                      \
+#define QE_PS(NC)                                                                                                 \
+    case NC:                                                                                                      \
+        hipLaunchKernelGGL(part_scatter_kernel<NC>, dim3(nb), dim3(PB), 0, c->stream, keys, n, nparts, dbits,    \
+                           d_cnt + PMAX, pc, out_keys);                                                           \
         break;
             QE_PS(0) QE_PS(1) QE_PS(2) QE_PS(3) QE_PS(4)
 #undef QE_PS
         }
         QE_HIP(hipGetLastError());
     }
-    QE_HIP(hipMemcpyAsync(counts, d_tot, nparts * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
-    QE_HIP(hipStreamSynchronize(c->stream));
-    dfree(c, table);
-    dfree(c, d_tot);
+    QE_HIP(hipStreamSynchronize(c->stream));   // the caller hands the buffers to RCCL next
+    dfree(c, d_cnt);
     return 0;
     QE_API_END(c)
 }
@@ -404,14 +524,20 @@ int qe_bucket_select(qe_ctx* c, qe_col col, uint32_t nparts, uint32_t part, cons
         QE_HIP(hipMemcpyAsync(d_heavy, heavy, nheavy * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
     }
     unsigned long long* d_cnt = reinterpret_cast<unsigned long long*>(c->d_scratch);
-    const unsigned nb = grid_for(n, BS_TILE);
+    // grid-stride over sub-tiles with exactly the resident blocks (a second round of blocks would
+    // run behind the first on a fraction of the CUs)
+    static int cus = 0, per_cu = 0;
+    const size_t dyn = (size_t)nheavy * sizeof(uint64_t);
+    if (!cus) QE_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    QE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bucket_select_kernel, BS_B, dyn));
+    const unsigned nb = grid_for(n, BS_TILE, (unsigned)std::max(1, cus * std::max(1, per_cu)));
     for (int attempt = 0; attempt < 2; attempt++) {
         out->key = dalloc_t<uint64_t>(c, std::max<uint64_t>(cap, 1));
         out->val = dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1));
         QE_HIP(hipMemsetAsync(d_cnt, 0, sizeof(uint64_t), c->stream));
         if (n) {
             Timed t(c, "bucket_select", 8.0 * n);
-            hipLaunchKernelGGL(bucket_select_kernel, dim3(nb), dim3(BS_B), 0, c->stream, col.d, n, nparts, part,
+            hipLaunchKernelGGL(bucket_select_kernel, dim3(nb), dim3(BS_B), dyn, c->stream, col.d, n, nparts, part,
                                d_heavy, nheavy, out->key, out->val, cap, d_cnt);
             QE_HIP(hipGetLastError());
         }

@@ -8,7 +8,7 @@ as a relational plan over the device primitives of libqe:
                binding refines it and prints the global count (all-reduce), as the reference's
                exec_filter_rel_exists does (src/filter.c:3-35)
   joins     -- both inputs are gathered to keys (replicated columns, local), hash-partitioned on
-               the key (qe_partition: dest = fmix64(key) % world), exchanged with one RCCL
+               the key (qe_partition: dest = hi32(mix(key)) * world >> 32), exchanged with one RCCL
                all-to-all per array, and joined locally (qe_join_indices: LSD radix sort + merge
                path); rowid columns of the intermediate ride along (qe_take_u32).  Columns no
                later predicate or select needs are dropped before the exchange.
@@ -293,6 +293,12 @@ class GPUEngine:
 
     def exchange(self, keys: DArr, cols: list[DArr]):
         """hash-partition rows on keys and all-to-all them; returns this rank's bucket"""
+        return self.exchange_finish(self.exchange_start(keys, cols))
+
+    def exchange_start(self, keys: DArr, cols: list[DArr]):
+        """partition (libqe stream) + the counts all-to-all, then the data all-to-alls queued
+        asynchronously on the communicator's stream: the caller overlaps its next libqe work
+        (the other join side) with the transfer and calls exchange_finish"""
         torch, dist, W = self.torch, self.dist, self.world
         n = keys.n
         dev = f"cuda:{torch.cuda.current_device()}"
@@ -306,15 +312,23 @@ class GPUEngine:
         dist.all_to_all_single(rcnt, cnt, group=self.group)
         out_splits = [int(v) for v in rcnt.tolist()]
         total = sum(out_splits)
-        outs = []
+        outs, works, keep = [], [], [sk, sc]
         for src, dt in [(sk, torch.int64)] + [(t, torch.int32) for t in sc]:
             s = src[:n].to(self.comm_dev) if self.comm_dev != dev else src[:n]
             r = torch.empty(max(1, total), dtype=dt, device=self.comm_dev)
-            dist.all_to_all_single(r[:total], s, out_splits, counts, group=self.group)
-            if self.comm_dev != dev:
-                r = r.to(dev)
+            works.append(dist.all_to_all_single(r[:total], s, out_splits, counts, group=self.group, async_op=True))
+            keep.append(s)
             outs.append(r)
-        torch.cuda.synchronize()
+        return (outs, works, keep, total, dev)
+
+    def exchange_finish(self, h):
+        outs, works, keep, total, dev = h
+        for w in works:
+            w.wait()
+        if self.comm_dev != dev:
+            outs = [r.to(dev) for r in outs]
+        self.torch.cuda.synchronize()
+        del keep
         rk = DArr(outs[0].data_ptr(), total, keep=outs[0])
         rc = [DArr(t.data_ptr(), total, keep=t) for t in outs[1:]]
         return rk, rc
@@ -394,23 +408,30 @@ class DistExecutor:
             return comps[cid][b]
 
         def side(cid, b, c, need):
-            """(keys, vals, carried) of one join side; carried = [(binding, rowids-or-'vals')]"""
+            """start one join side; returns a function giving (keys, vals, carried), carried =
+            [(binding, rowids | 'vals')].  An exchange is in flight between the two calls."""
             cols = comps[cid]
             if len(cols) == 1 and b in cols and cols[b] is None:
                 keys, vals = e.base_side(rels[b], c)
-                return keys, vals, ([(b, "vals")] if b in need else [])
+                return lambda: (keys, vals, ([(b, "vals")] if b in need else []))
             keys = e.keys(rels[b], c, rows_of(cid, b))
             keep = [x for x in sorted(cols) if x in need]
+
+            def done(keys, cur):
+                if len(keep) == 1:
+                    return keys, cur[keep[0]], [(keep[0], "vals")]
+                return keys, None, [(x, cur[x]) for x in keep]
             if e.world > 1:
                 if len(keep) > 4:
                     raise NotSupported("more than 4 rowid columns in one exchange")
-                keys, rc = e.exchange(keys, [rows_of(cid, x) for x in keep])
-                cur = dict(zip(keep, rc))
-            else:
-                cur = {x: rows_of(cid, x) for x in keep}
-            if len(keep) == 1:
-                return keys, cur[keep[0]], [(keep[0], "vals")]
-            return keys, None, [(x, cur[x]) for x in keep]
+                h = e.exchange_start(keys, [rows_of(cid, x) for x in keep])
+
+                def finish():
+                    rk, rc = e.exchange_finish(h)
+                    return done(rk, dict(zip(keep, rc)))
+                return finish
+            cur = {x: rows_of(cid, x) for x in keep}
+            return lambda: done(keys, cur)
 
         def do_join(p, pending):
             (ba, ca), (bb, cb) = p.a, p.b
@@ -422,8 +443,16 @@ class DistExecutor:
                 comps[A] = {x: e.take(rows_of(A, x), idx) for x in list(cols)}
                 size[A] = e.allreduce(e.length(idx))
                 return
-            ka, va, carry_a = side(A, ba, ca, need)
-            kb, vb, carry_b = side(B, bb, cb, need)
+            # derived sides first, so their exchanges overlap the base side's local bucket scan
+            A_base = len(comps[A]) == 1 and comps[A].get(ba, 0) is None
+            if A_base:
+                fb = side(B, bb, cb, need)
+                fa = side(A, ba, ca, need)
+            else:
+                fa = side(A, ba, ca, need)
+                fb = side(B, bb, cb, need)
+            ka, va, carry_a = fa()
+            kb, vb, carry_b = fb()
             oa, ob = e.join_pairs(ka, va, kb, vb)
             del ka, kb, va, vb
             merged = {}

@@ -11,15 +11,12 @@ from qe.dist import DistExecutor, M64
 _OPS = {"=": np.equal, ">": np.greater, "<": np.less}
 
 
-def fmix64(k: np.ndarray) -> np.ndarray:
-    k = k.astype(np.uint64)
+def part_of(k: np.ndarray, nparts: int) -> np.ndarray:
+    """qe_partition's destination: (hi32((k ^ k >> 29) * 0xbf58476d1ce4e5b9) * nparts) >> 32"""
+    k = np.asarray(k, dtype=np.uint64)
     with np.errstate(over="ignore"):
-        k ^= k >> np.uint64(33)
-        k *= np.uint64(0xff51afd7ed558ccd)
-        k ^= k >> np.uint64(33)
-        k *= np.uint64(0xc4ceb9fe1a85ec53)
-        k ^= k >> np.uint64(33)
-    return k
+        h = (k ^ (k >> np.uint64(29))) * np.uint64(0xbf58476d1ce4e5b9)
+    return ((h >> np.uint64(32)) * np.uint64(nparts)) >> np.uint64(32)
 
 
 class NumpyEngine:
@@ -64,7 +61,7 @@ class NumpyEngine:
         c = self.rels[rel][col]
         if self.world == 1:
             return c, None
-        mask = (fmix64(c) % np.uint64(self.world)) == np.uint64(self.rank)
+        mask = part_of(c, self.world) == np.uint64(self.rank)
         rows = np.nonzero(mask)[0]
         # an unordered bucket, like qe_bucket_select's: shuffle so no test depends on its order
         rows = np.random.default_rng(self.rank + 17).permutation(rows).astype(np.uint32)
@@ -72,7 +69,7 @@ class NumpyEngine:
 
     def base_side_light(self, rel, col, heavy):
         c = self.rels[rel][col]
-        mask = (fmix64(c) % np.uint64(self.world)) == np.uint64(self.rank)
+        mask = part_of(c, self.world) == np.uint64(self.rank)
         mask &= ~np.isin(c, np.asarray(heavy, dtype=np.uint64))
         rows = np.nonzero(mask)[0].astype(np.uint32)
         return c[rows], rows
@@ -139,11 +136,17 @@ class NumpyEngine:
         dist.all_reduce(t, group=self.group)
         return int(t.item()) & M64
 
+    def exchange_start(self, keys, cols):
+        return self.exchange(keys, cols)
+
+    def exchange_finish(self, h):
+        return h
+
     def exchange(self, keys, cols):
         import torch
         import torch.distributed as dist
         self.exchanges += 1
-        dest = (fmix64(keys) % np.uint64(self.world)).astype(np.int64)
+        dest = part_of(keys, self.world).astype(np.int64)
         order = np.argsort(dest, kind="stable")
         counts = np.bincount(dest, minlength=self.world).astype(np.int64)
         cnt = torch.from_numpy(counts)

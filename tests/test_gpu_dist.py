@@ -13,8 +13,11 @@ pytestmark = pytest.mark.gpu
 C3 = "0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>1000000000&3.2<3000000000|1.2 2.2 3.2"
 
 
-@pytest.mark.parametrize("n,parts,ncols", [(0, 2, 1), (1, 8, 2), (100_000, 8, 3), (3_000_001, 5, 1), (4096, 64, 4)])
-def test_partition_is_stable_grouping(ctx, n, parts, ncols):
+@pytest.mark.parametrize("n,parts,ncols", [(0, 2, 1), (1, 8, 2), (100_000, 8, 3), (3_000_001, 5, 1), (4096, 64, 4),
+                                           (2_000_000, 1, 0), (777_777, 7, 4)])
+def test_partition_groups_rows_by_destination(ctx, n, parts, ncols):
+    """every row lands in its destination's segment exactly once, columns riding along (order
+    inside a segment is unspecified: the receiver sorts)"""
     import torch
     rng = np.random.default_rng(n)
     keys = rng.integers(0, 1 << 40, n, dtype=np.uint64)
@@ -26,12 +29,19 @@ def test_partition_is_stable_grouping(ctx, n, parts, ncols):
     torch.cuda.synchronize()
     counts = ctx.partition(dk.data_ptr(), n, [t.data_ptr() for t in dc], parts, ok.data_ptr(),
                            [t.data_ptr() for t in oc])
-    dest = (dce.fmix64(keys) % np.uint64(parts)).astype(np.int64)
-    order = np.argsort(dest, kind="stable")
+    dest = dce.part_of(keys, parts).astype(np.int64)
     assert counts == np.bincount(dest, minlength=parts).tolist()
-    np.testing.assert_array_equal(ok.cpu().numpy()[:n].view(np.uint64), keys[order])
-    for c, o in zip(cols, oc):
-        np.testing.assert_array_equal(o.cpu().numpy()[:n].view(np.uint32), c[order])
+    gk = ok.cpu().numpy()[:n].view(np.uint64)
+    gc = [o.cpu().numpy()[:n].view(np.uint32) for o in oc]
+    # rows are identified by their index in the input (carried in the first column when present)
+    s0 = 0
+    for p, cnt in enumerate(counts):
+        seg = slice(s0, s0 + cnt)
+        s0 += cnt
+        want = np.nonzero(dest == p)[0]
+        got_rows = sorted(zip(gk[seg].tolist(), *[c[seg].tolist() for c in gc]))
+        want_rows = sorted(zip(keys[want].tolist(), *[c[want].tolist() for c in cols]))
+        assert got_rows == want_rows
 
 
 @pytest.mark.parametrize("n,parts,nheavy", [(0, 2, 0), (1, 1, 0), (5, 3, 1), (100_001, 8, 0), (3_000_001, 8, 5),
@@ -41,7 +51,7 @@ def test_bucket_select_is_the_hash_bucket(ctx, n, parts, nheavy):
     keys = rng.integers(0, max(1, n // 3), n, dtype=np.uint64) * np.uint64(0x9E3779B1)
     rel = ctx.load_relation([keys])
     heavy = np.unique(keys[:nheavy]) if nheavy else np.zeros(0, np.uint64)
-    dest = (dce.fmix64(keys) % np.uint64(parts)).astype(np.int64)
+    dest = dce.part_of(keys, parts).astype(np.int64)
     for part in sorted({0, parts - 1, parts // 2}):
         p = ctx.bucket_select(ctx.column(rel, 0), parts, part, heavy)
         k, v = ctx.pairs_to_host(p)

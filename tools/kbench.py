@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--n", type=int, default=100_000_000)
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args()
+    import torch
+    torch.cuda.init()          # torch's HIP runtime first (as bench.py and the tests do)
     ctx = lib.Ctx(0)
     n = a.n
     kinds = [("mod", n), ("mod", n), ("hi32",)]
@@ -68,6 +70,28 @@ def main():
             ctx.filter_refine(col, "<", 3_000_000_000, l1)
             ctx.list_free(l1)
         report(ctx, "filter", a.reps)
+    if a.what in ("bucket", "all"):
+        # the N-rank plan's local bucket of a replicated column: nparts x n rows scanned
+        parts = int(os.environ.get("QE_KB_PARTS", "8"))
+        big = ctx.gen_relation(n * parts, [("mod", n * parts)], seed=1, gen_rel=5)
+        ctx.sync()
+        ctx.reset_stats()
+        for rep in range(a.reps):
+            p = ctx.bucket_select(ctx.column(big, 0), parts, rep % parts)
+            ctx.pairs_free(p)
+        report(ctx, "bucket", a.reps)
+    if a.what in ("partition", "all"):
+        import torch
+        parts = int(os.environ.get("QE_KB_PARTS", "8"))
+        c = ctx.column(r0, 1)
+        cols = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(2)]
+        ok = torch.empty(n, dtype=torch.int64, device="cuda")
+        oc = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(2)]
+        torch.cuda.synchronize()
+        ctx.reset_stats()
+        for rep in range(a.reps):
+            ctx.partition(c.d, n, [t.data_ptr() for t in cols], parts, ok.data_ptr(), [t.data_ptr() for t in oc])
+        report(ctx, "partition", a.reps)
     if a.what in ("gather", "all"):
         R = ctx.gather_pairs(ctx.column(r0, 1), None)
         ctx.sort_pairs(R)
