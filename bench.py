@@ -61,17 +61,19 @@ def roofline(stats: dict, traffic: dict | None):
             "launches": s["launches"]}
 
 
-def load_traffic():
-    """HBM bytes per launch from the rocprofv3 PMC passes committed under profiles/ (or None)."""
-    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))
-    if not fs:
-        return None
-    try:
-        with open(fs[-1]) as f:
-            d = json.load(f)
+def load_traffic(workload: str = "c3"):
+    """HBM bytes per launch from the rocprofv3 PMC passes committed under profiles/ for this
+    workload (files without a "workload" key are C3), or None -- never another workload's."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except Exception:
+            continue
+        if d.get("workload", "c3") != workload:
+            continue
         return {k: v.get("hbm_bytes_per_launch") for k, v in d.get("kernels", {}).items()}
-    except Exception:
-        return None
+    return None
 
 
 def cpu_baseline(sample_rows: int, seed: int, gpu_ctx):
@@ -229,17 +231,17 @@ def main():
         if world > 1 or args.plan == "dist":
             res = c5bench.run_dist(args, log)
         else:
-            res = c5bench.run_single(args, log, roofline_fn=roofline, traffic_fn=load_traffic)
+            res = c5bench.run_single(args, log, roofline_fn=roofline, traffic_fn=lambda: load_traffic("c5"))
     elif args.workload == "c4":
         from qe import c4bench
         if world > 1:
             res = c4bench.run_dist(args, log)
         else:
-            res = c4bench.run_single(args, log, roofline_fn=roofline, traffic_fn=load_traffic)
+            res = c4bench.run_single(args, log, roofline_fn=roofline, traffic_fn=lambda: load_traffic("c4"))
     elif world > 1 or args.gpus > 1 or args.plan == "dist":
         from qe import dist
         res = dist.bench_main(args, METRIC, QUERY, cpu_baseline_fn=cpu_baseline, roofline_fn=roofline,
-                              traffic_fn=load_traffic)
+                              traffic_fn=None)
     else:
         res = run_single(args)
     if res is not None:

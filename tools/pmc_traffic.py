@@ -27,7 +27,13 @@ STAGES = [
     (r"radix_pass_kernel<unsigned long, \d, \d, false", "sort_pass_k64"),
     (r"radix_pass_kv_kernel<unsigned long", "sort_pass_k64v32"),
     (r"radix_pass_kv_kernel<unsigned int", "sort_pass_k32v32"),
-    (r"digit_hist_kernel|digit_scan_kernel", "sort_hist"),
+    (r"digit_hist_kernel|digit_scan_kernel|tl_hist_kernel|tl_scan_kernel", "sort_hist"),
+    (r"tl_local_kernel", "sort_local"),
+    (r"bucket_select_kernel", "bucket_select"),
+    (r"part_count_kernel", "partition_count"),
+    (r"part_scatter_kernel", "partition"),
+    (r"take_u32_kernel", "take_u32"),
+    (r"heavy_stats_kernel", "heavy_stats"),
     (r"key_bits_kernel", "sort_keybits"),
     (r"mj_fused", "mj_fused"),
     (r"mj_partition", "mj_partition"),
@@ -91,6 +97,7 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--out", required=True)
     ap.add_argument("--command", default="")
+    ap.add_argument("--workload", default="c3")
     a = ap.parse_args()
     f = per_stage(read_counter(a.fetch, "FETCH_SIZE"))
     w = per_stage(read_counter(a.write, "WRITE_SIZE"))
@@ -105,7 +112,7 @@ def main():
                     "fetch_corrected_bytes_per_launch": round(2 * fpl) if fpl else None,
                     "write_bytes_per_launch": round(wpl) if wpl else None, "launches_fetch_pass": fn,
                     "launches_write_pass": wn, "kernels": sorted(names | names2)}
-    doc = {"command": a.command,
+    doc = {"command": a.command, "workload": a.workload,
            "units": "bytes per launch; FETCH_SIZE/WRITE_SIZE KiB x 1024",
            "correction": "gfx950: FETCH_SIZE x2 (MI355X_MICROARCH.md HBM section); WRITE_SIZE as is",
            "kernels": kern}
