@@ -321,8 +321,23 @@ template <class SH>
 __device__ __forceinline__ uint64_t mj_walk(const SH& sh, const uint64_t* sk, uint64_t wlo, uint64_t wn,
                                             uint32_t tn, uint64_t kbase, uint32_t (&cnt)[MJ_ITEMS],
                                             uint32_t (&lo_rel)[MJ_ITEMS]) {
-    return wn <= MJ_WIN ? mj_walk_t<true>(sh, sk, wlo, wn, tn, kbase, cnt, lo_rel)
-                        : mj_walk_t<false>(sh, sk, wlo, wn, tn, kbase, cnt, lo_rel);
+    if (wn <= MJ_WIN) return mj_walk_t<true>(sh, sk, wlo, wn, tn, kbase, cnt, lo_rel);
+    // a window beyond LDS: inside a skewed key's run.  When the whole R tile holds one key the
+    // window [lower_bound(first), upper_bound(last)) IS that key's S run -- every row matches all
+    // of it, no search (the per-thread global binary searches cost ~24 dependent HBM round trips)
+    if (tn && sh.r[rpad(0)] == sh.r[rpad(tn - 1)]) {
+        const uint32_t e0 = threadIdx.x * MJ_ITEMS;
+        uint64_t tsum = 0;
+#pragma unroll
+        for (int j = 0; j < MJ_ITEMS; j++) {
+            const bool v = e0 + (uint32_t)j < tn;
+            cnt[j] = v ? (uint32_t)wn : 0u;
+            lo_rel[j] = 0;
+            tsum += v ? wn : 0;
+        }
+        return tsum;
+    }
+    return mj_walk_t<false>(sh, sk, wlo, wn, tn, kbase, cnt, lo_rel);
 }
 
 // per-row match counts, output-distinctness flags, optional driver-count annotation

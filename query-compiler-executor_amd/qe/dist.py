@@ -111,10 +111,12 @@ def owned_range(rows: int, rank: int, world: int) -> tuple[int, int]:
 class DArr:
     """A device array: pointer + length + the object that owns the memory."""
 
-    __slots__ = ("ptr", "n", "keep", "free")
+    __slots__ = ("ptr", "n", "keep", "free", "bits")
 
-    def __init__(self, ptr, n, keep=None, free=None):
-        self.ptr, self.n, self.keep, self.free = ptr, n, keep, free
+    def __init__(self, ptr, n, keep=None, free=None, bits=None):
+        # bits: (OR, AND) bounds of the keys (the source column's statistics: a subset of a
+        # column varies in no bit the column does not), so the sort skips its reduction pass
+        self.ptr, self.n, self.keep, self.free, self.bits = ptr, n, keep, free, bits
 
     def __del__(self):
         if self.free is not None:
@@ -167,7 +169,7 @@ class GPUEngine:
     def keys(self, rel, col, rows: DArr) -> DArr:
         p = self.ctx.gather_pairs(self.ctx.column(rel, col), self._as_list(rows))
         ctx = self.ctx
-        return DArr(p.key, p.n, keep=p, free=lambda: ctx.pairs_free(p))
+        return DArr(p.key, p.n, keep=p, free=lambda: ctx.pairs_free(p), bits=self.ctx.column_bits(rel, col))
 
     def filter_idx(self, rel, col, rows: DArr, op, v) -> DArr:
         k = self.keys(rel, col, rows)
@@ -190,11 +192,10 @@ class GPUEngine:
         (qe_bucket_select) -- the rows the exchange would deliver, without moving them."""
         c = self.ctx.column(rel, col)
         if self.world == 1:
-            kor, kand = self.ctx.column_bits(rel, col)
-            return DArr(c.d, c.n, keep=("bits", kor, kand)), None
+            return DArr(c.d, c.n, bits=self.ctx.column_bits(rel, col)), None
         p = self.ctx.bucket_select(c, self.world, self.rank)
         ctx = self.ctx
-        keys = DArr(p.key, p.n, keep=p, free=lambda: ctx.pairs_free(p))
+        keys = DArr(p.key, p.n, keep=p, free=lambda: ctx.pairs_free(p), bits=self.ctx.column_bits(rel, col))
         return keys, DArr(p.val, p.n, keep=keys)
 
     def base_side_light(self, rel, col, heavy):
@@ -203,7 +204,7 @@ class GPUEngine:
             return self.base_side(rel, col)
         p = self.ctx.bucket_select(self.ctx.column(rel, col), self.world, self.rank, heavy)
         ctx = self.ctx
-        keys = DArr(p.key, p.n, keep=p, free=lambda: ctx.pairs_free(p))
+        keys = DArr(p.key, p.n, keep=p, free=lambda: ctx.pairs_free(p), bits=self.ctx.column_bits(rel, col))
         return keys, DArr(p.val, p.n, keep=keys)
 
     def join_count_sums(self, ka: DArr, va, kb: DArr, vb, sel_a: list, sel_b: list):
@@ -215,8 +216,8 @@ class GPUEngine:
         for k, v in ((ka, va), (kb, vb)):
             p = P()
             p.key, p.val, p.n, p.flags, p.owns = k.ptr, (v.ptr if v is not None else None), k.n, 0, 0
-            if isinstance(k.keep, tuple) and k.keep and k.keep[0] == "bits":
-                p.kor, p.kand, p.flags = k.keep[1], k.keep[2], 4
+            if k.bits is not None:
+                p.kor, p.kand, p.flags = k.bits[0], k.bits[1], 4          # QE_PAIRS_BITS
             sides.append(p)
         A, B = sides
         try:
@@ -258,8 +259,8 @@ class GPUEngine:
         for k, v in ((ka, va), (kb, vb)):
             p = P()
             p.key, p.val, p.n, p.flags, p.owns = k.ptr, (v.ptr if v is not None else None), k.n, 0, 0
-            if isinstance(k.keep, tuple) and k.keep and k.keep[0] == "bits":
-                p.kor, p.kand, p.flags = k.keep[1], k.keep[2], 4          # QE_PAIRS_BITS: column stats
+            if k.bits is not None:
+                p.kor, p.kand, p.flags = k.bits[0], k.bits[1], 4          # QE_PAIRS_BITS: column stats
             sides.append(p)
         A, B = sides
         try:
@@ -319,17 +320,17 @@ class GPUEngine:
             works.append(dist.all_to_all_single(r[:total], s, out_splits, counts, group=self.group, async_op=True))
             keep.append(s)
             outs.append(r)
-        return (outs, works, keep, total, dev)
+        return (outs, works, keep, total, dev, keys.bits)
 
     def exchange_finish(self, h):
-        outs, works, keep, total, dev = h
+        outs, works, keep, total, dev, bits = h
         for w in works:
             w.wait()
         if self.comm_dev != dev:
             outs = [r.to(dev) for r in outs]
         self.torch.cuda.synchronize()
         del keep
-        rk = DArr(outs[0].data_ptr(), total, keep=outs[0])
+        rk = DArr(outs[0].data_ptr(), total, keep=outs[0], bits=bits)
         rc = [DArr(t.data_ptr(), total, keep=t) for t in outs[1:]]
         return rk, rc
 
