@@ -149,7 +149,10 @@ __device__ uint64_t g_sort_stamps[STAMP_TILES * STAMP_SLOTS];
 // (tile / bins words) -- 8192-word tiles beat 4096 by 15 %; 512 threads x 16 beat 256 x 32 by
 // 10 % (twice the waves per CU at the same LDS); a reduce-then-scan variant without lookback
 // (per-tile count pass + scan + scatter) measured equal: its extra read cancels the saving.
-template <typename K, int IN, int OUT, bool PACK, int RBITS, int ITEMS, int NT>
+// PRE = true: the tile's global digit offsets were computed before the launch (the two-level
+// sort's first pass, whose per-tile counts come out of the histogram read it does anyway,
+// tl_hist_tiles_kernel) -- `offs` is a table of BINS offsets per tile; no ticket, no lookback.
+template <typename K, int IN, int OUT, bool PACK, int RBITS, int ITEMS, int NT, bool PRE = false>
 __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ kin, const uint64_t* __restrict__ win,
                                                         const uint32_t* __restrict__ vin, K* __restrict__ kout,
                                                         uint64_t* __restrict__ wout, uint32_t* __restrict__ vout,
@@ -170,7 +173,7 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
 #ifdef QE_DIAG_STAMPS
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-    const uint32_t tile = take_ticket(ticket, &s_ticket);
+    const uint32_t tile = PRE ? blockIdx.x : take_ticket(ticket, &s_ticket);
 #ifdef QE_DIAG_STAMPS
     if (threadIdx.x == 0 && tile < STAMP_TILES) g_sort_stamps[(uint64_t)tile * STAMP_SLOTS] = t_start;
 #endif
@@ -244,7 +247,7 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
         }
         tot[q] = t;
         tsum += t;
-        st_agent(&status[(uint64_t)tile * BINS + d], lb_word(epoch, tile == 0 ? LB_FLAG_INC : LB_FLAG_AGG, t));
+        if (!PRE) st_agent(&status[(uint64_t)tile * BINS + d], lb_word(epoch, tile == 0 ? LB_FLAG_INC : LB_FLAG_AGG, t));
     }
     uint32_t inc = wave_incl_scan_u32(tsum);
     if (l == 63) wsum[w] = inc;
@@ -271,6 +274,10 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
     for (int q = 0; q < DPT; q++) {
         const uint32_t d = threadIdx.x * DPT + q;
         if (!owner) continue;
+        if constexpr (PRE) {
+            gofs[d] = offs[(uint64_t)tile * BINS + d] - bexcl[d];
+            continue;
+        }
         // the predecessors' counts: by this time most have published their inclusive prefix
         uint64_t ex = 0;
 #ifndef QE_DIAG_SORT_NOLB   // ablation only: skip the lookback (output positions are wrong)
@@ -414,17 +421,27 @@ __global__ void __launch_bounds__(1024) tl_scan_kernel(const uint32_t* __restric
 // one workgroup per bucket: up to TL_CAP packed words, sorted by the low L bits in LDS.  Each wave
 // owns a contiguous slice of jm x 64 words, jm = ceil(m / (waves x 64)): every wave works and the
 // work is proportional to the bucket, not to TL_CAP.
-template <typename K>
-__global__ void __launch_bounds__(TL_NT) tl_local_kernel(const uint64_t* __restrict__ win, K* __restrict__ kout,
+// LDS rounds of a local sort: round r sorts field bits [32 + sum(bits[<r]), ... + bits[r])
+struct LocalRounds {
+    int n;
+    int bits[4];
+};
+
+// IN == IN_WORD: packed words of a bucket-partitioned array (bstart); IN_KV / IN_KIOTA: ONE
+// bucket of single_n (key, rowid) pairs packed on load (a small sort: a single launch)
+template <typename K, int IN>
+__global__ void __launch_bounds__(TL_NT) tl_local_kernel(const uint64_t* __restrict__ win, const K* __restrict__ kin,
+                                                         const uint32_t* __restrict__ vin, K* __restrict__ kout,
                                                          uint32_t* __restrict__ vout,
-                                                         const uint32_t* __restrict__ bstart, Field f, int r1,
-                                                         int r2) {
+                                                         const uint32_t* __restrict__ bstart, uint32_t single_n,
+                                                         Field f, LocalRounds lr) {
     constexpr int NW = TL_NT / 64, BINS = 256;
     __shared__ uint64_t stage[TL_CAP];
     __shared__ uint32_t whist[NW][BINS];
     __shared__ uint32_t bexcl[BINS];
     __shared__ uint32_t wsum[NW];
-    const uint32_t s0 = bstart[blockIdx.x], m = bstart[blockIdx.x + 1] - s0;
+    const uint32_t s0 = IN == IN_WORD ? bstart[blockIdx.x] : 0u;
+    const uint32_t m = IN == IN_WORD ? bstart[blockIdx.x + 1] - s0 : single_n;
     if (m == 0) return;   // block-uniform
     const int w = wave_id(), l = lane_id();
     const uint64_t lt = lanemask_lt();
@@ -434,12 +451,19 @@ __global__ void __launch_bounds__(TL_NT) tl_local_kernel(const uint64_t* __restr
 #pragma unroll
     for (int j = 0; j < TL_ITEMS; j++) {
         const uint32_t i = wbase + (uint32_t)j * 64 + l;
-        word[j] = ((uint32_t)j < jm && i < m) ? win[s0 + i] : 0;
+        const bool ok = (uint32_t)j < jm && i < m;
+        if (IN == IN_WORD) {
+            word[j] = ok ? win[s0 + i] : 0;
+        } else {
+            const uint64_t k = ok ? (uint64_t)kin[i] : 0;
+            const uint32_t v = IN == IN_KV ? (ok ? vin[i] : 0u) : i;
+            word[j] = (((k >> f.lo) & f.fmask) << 32) | v;
+        }
     }
-    for (int r = 0; r < 2; r++) {
-        const int bits = r == 0 ? r1 : r2;
-        if (bits == 0) break;
-        const int dsh = 32 + (r == 0 ? 0 : r1);
+    int dsh = 32;
+    for (int r = 0; r < lr.n; r++) {
+        const int bits = lr.bits[r];
+        if (r > 0) dsh += lr.bits[r - 1];
         const uint32_t mask = (1u << bits) - 1u;
         for (int i = threadIdx.x; i < NW * BINS; i += TL_NT) (&whist[0][0])[i] = 0;
         __syncthreads();
@@ -739,11 +763,22 @@ static SortOut sort_packed(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
 
 // two-level packed sort (see tl_* kernels); nullopt-style: returns false when a bucket would not
 // fit LDS (skew), after which the caller runs the plain LSD passes
+static LocalRounds local_rounds(int L) {   // L low bits in rounds of <= 8
+    LocalRounds lr{0, {0, 0, 0, 0}};
+    while (L > 0 && lr.n < 4) {
+        lr.bits[lr.n] = L < 8 ? L : 8;
+        L -= lr.bits[lr.n++];
+    }
+    return lr;
+}
+
+// H = TL_H (15 high bits by two global passes) for large inputs; H = 8 (ONE global pass) for
+// inputs whose 256 buckets fit LDS (<= ~1 M keys)
 template <typename K>
 static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint64_t n, int bits, Field f,
-                           const char* name, SortOut* out) {
-    const int L = bits - TL_H;   // 5..16 low bits sorted in LDS
-    const int r1 = L < 8 ? L : 8, r2 = L - r1;
+                           const char* name, SortOut* out, int H = TL_H) {
+    const int L = bits - H;   // low bits sorted in LDS (<= 24)
+    const LocalRounds lr = local_rounds(L);
     uint32_t* hist = dalloc_t<uint32_t>(c, TL_BUCKETS);
     // digit bases: 256 entries each (the pass kernel reads one per possible 8-bit digit)
     uint32_t* bstart = dalloc_t<uint32_t>(c, TL_BUCKETS + 1 + 512);
@@ -767,10 +802,10 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
     }
     const uint64_t nt = (n + RTILE - 1) / RTILE;
     uint64_t* w1 = dalloc_t<uint64_t>(c, n);
-    uint64_t* w2 = dalloc_t<uint64_t>(c, n);
+    uint64_t* w2 = H == TL_H ? dalloc_t<uint64_t>(c, n) : nullptr;
     K* kout = dalloc_t<K>(c, n);
     uint32_t* vout = dalloc_t<uint32_t>(c, n);
-    for (int p = 0; p < 2; p++) {
+    for (int p = 0; p < (H == TL_H ? 2 : 1); p++) {
         const int dsh = 32 + L + 8 * p;
         const uint32_t pmask = p == 0 ? 255u : 127u;
         LBSlot sl = lb_acquire(c, nt * 256);
@@ -791,12 +826,12 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
     }
     {
         Timed t(c, "sort_local", 8.0 * n + ((double)sizeof(K) + 4) * n);
-        hipLaunchKernelGGL((tl_local_kernel<K>), dim3(TL_BUCKETS), dim3(TL_NT), 0, c->stream, w2, kout, vout, bstart, f,
-                           r1, r2);
+        hipLaunchKernelGGL((tl_local_kernel<K, IN_WORD>), dim3(1u << H), dim3(TL_NT), 0, c->stream,
+                           H == TL_H ? w2 : w1, nullptr, nullptr, kout, vout, bstart, 0u, f, lr);
         QE_HIP(hipGetLastError());
     }
     dfree(c, w1);
-    dfree(c, w2);
+    if (w2) dfree(c, w2);
     dfree(c, hist);
     dfree(c, bstart);
     *out = SortOut{kout, vout, true, true};
@@ -897,7 +932,26 @@ static SortOut radix_sort_impl(qe_ctx* c, const K* keys, const uint32_t* vals, u
         // two-level when the buckets can average well under LDS's TL_CAP = 8192 words (the
         // histogram's maximum decides; a skewed input falls through to the LSD passes)
         const int nb = hi - lo;
-        if (two_level_on() && nb >= 20 && nb <= TL_H + 16 && n >= (1u << 22) && n <= 4000ull * TL_BUCKETS) {
+        if (two_level_on() && n <= (uint64_t)TL_CAP) {
+            // small: one workgroup sorts everything in LDS, rounds of <= 8 bits, one launch
+            K* kout = dalloc_t<K>(c, n);
+            uint32_t* vout = dalloc_t<uint32_t>(c, n);
+            Timed t(c, "sort_small", ((double)sizeof(K) + 4) * 2.0 * n);
+            const LocalRounds lr = local_rounds(nb);
+            if (vals)
+                hipLaunchKernelGGL((tl_local_kernel<K, IN_KV>), dim3(1), dim3(TL_NT), 0, c->stream, nullptr, keys, vals,
+                                   kout, vout, nullptr, (uint32_t)n, f, lr);
+            else
+                hipLaunchKernelGGL((tl_local_kernel<K, IN_KIOTA>), dim3(1), dim3(TL_NT), 0, c->stream, nullptr, keys,
+                                   nullptr, kout, vout, nullptr, (uint32_t)n, f, lr);
+            QE_HIP(hipGetLastError());
+            return SortOut{kout, vout, true, true};
+        }
+        if (two_level_on() && nb >= 12 && nb <= 8 + 24 && n <= 700000) {   // ~2.7 K per bucket: room for unfilled ranges
+            SortOut so2;   // one global pass of 8 bits + LDS buckets (falls through on skew)
+            if (sort_two_level<K>(c, keys, vals, n, nb, f, name, &so2, 8)) return so2;
+        }
+        if (two_level_on() && nb >= 20 && nb <= TL_H + 16 && n >= (1u << 20) && n <= 4000ull * TL_BUCKETS) {
             SortOut so2;
             if (sort_two_level<K>(c, keys, vals, n, nb, f, name, &so2)) return so2;
         }

@@ -147,6 +147,32 @@ def test_sort_pairs_two_level_sizes(ctx, case):
     ctx.pairs_free(p)
 
 
+@pytest.mark.parametrize("n", [2, 64, 1000, 5120, 5121, 70_000, 699_999, 700_001, 1_048_576, 3_000_000])
+@pytest.mark.parametrize("case", ["27bit", "31bit", "12bit", "skew"])
+@pytest.mark.parametrize("with_vals", [True, False])
+def test_sort_pairs_small_and_one_pass_paths(ctx, n, case, with_vals):
+    """n <= 5120: one workgroup sorts in LDS (up to 4 rounds of 8 bits); n <= 700 k: one global
+    8-bit pass + LDS buckets; then the 15-bit two-level sort; skew falls back to LSD passes"""
+    rng = np.random.default_rng(n * 7 + len(case))
+    if case == "12bit":
+        k = rng.integers(0, 1 << 12, n, dtype=np.uint64)
+    else:
+        k = _keys_for(case, n, rng)
+    if with_vals:
+        v = rng.permutation(n).astype(np.uint32)
+        p = ctx.pairs_from_host(k, v)
+    else:                                      # base column: rowids generated (IN_KIOTA)
+        v = np.arange(n, dtype=np.uint32)
+        col = _col(ctx, k)
+        p = ctx.gather_pairs(col, None)
+    ctx.sort_pairs(p)
+    gk, gv = ctx.pairs_to_host(p)
+    order = np.argsort(k, kind="stable")
+    np.testing.assert_array_equal(gk, k[order])
+    np.testing.assert_array_equal(gv, v[order])
+    ctx.pairs_free(p)
+
+
 def test_sort_base_column_generates_rowids(ctx):
     a = dg.column(5, 0, 0, 123_457, ("mod", 50_000))
     col = _col(ctx, a)
