@@ -538,6 +538,274 @@ __global__ void __launch_bounds__(TL_NT) tl_local_kernel(const uint64_t* __restr
     }
 }
 
+// ---- lookback-free global passes of the two-level sort ---------------------------------------
+// The histogram pass reads every key anyway, so it also leaves
+//   * tcnt[t][d1]   -- per first-pass tile t (RTILE keys) the count of each first-pass digit d1
+//                      (the bucket's low 8 bits), and
+//   * gcnt[s][d2]   -- per segment s = d1 * G + g (group g = TL_TPG consecutive tiles) the count
+//                      of each second-pass digit d2 (the bucket's high 7 bits) among group g's
+//                      keys with digit d1.
+// Column-wise exclusive scans (column_scan) turn both into global output offsets.  Pass 1 places
+// tile t's keys of digit d1 from tcnt[t][d1] on -- no ticket, no status words, no lookback.
+// After pass 1 (stable) group g's keys with digit d1 form ONE contiguous run, segment s, which
+// starts at tcnt[g * TL_TPG][d1]; pass 2 gives every segment a workgroup that places its keys of
+// digit d2 from gcnt[s][d2] on -- again without a lookback.  Segments average RTILE keys
+// (TL_TPG tiles x RTILE keys / 256 digits), and a larger one is walked in sub-tiles.
+constexpr uint32_t TL_TPG = 256;
+static_assert(RTILE == 8192, "tl_hist_tiles_kernel counts 8192-key first-pass tiles (1024 threads x 8)");
+
+template <typename K>
+__global__ void __launch_bounds__(1024) tl_hist_tiles_kernel(const K* __restrict__ keys, uint64_t n, Field f, int L,
+                                                             uint32_t nt, uint32_t G, uint32_t Q,
+                                                             uint32_t* __restrict__ tcnt, uint32_t* __restrict__ gcnt) {
+    __shared__ uint32_t h[TL_BUCKETS];   // index d1 * 128 + d2: 128 KiB, one block per CU
+    __shared__ uint32_t th[2][256];      // the tile's d1 counts, double-buffered: one barrier per tile
+    for (int i = threadIdx.x; i < TL_BUCKETS; i += 1024) h[i] = 0;
+    if (threadIdx.x < 512) (&th[0][0])[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t g = blockIdx.x / Q, q = blockIdx.x % Q;   // Q blocks share group g's tiles
+    const uint32_t t_end = (g + 1) * TL_TPG < nt ? (g + 1) * TL_TPG : nt;
+    auto load = [&](uint32_t t, uint64_t (&k)[8]) {
+        const uint64_t base = (uint64_t)t * RTILE;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint64_t i = base + (uint64_t)j * 1024 + threadIdx.x;
+            k[j] = i < n ? (uint64_t)keys[i] : 0;
+        }
+    };
+    uint64_t k[8];
+    uint32_t t = g * TL_TPG + q, prev = 0, par = 0;
+    for (; t < t_end; t += Q, par ^= 1u) {
+        load(t, k);
+        if (t != g * TL_TPG + q && threadIdx.x < 256) {   // the previous tile's counts (its barrier passed)
+            tcnt[(uint64_t)prev * 256 + threadIdx.x] = th[par ^ 1u][threadIdx.x];
+            th[par ^ 1u][threadIdx.x] = 0;
+        }
+        const uint64_t base = (uint64_t)t * RTILE;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint64_t i = base + (uint64_t)j * 1024 + threadIdx.x;
+            if (i < n) {
+                const uint32_t b = (uint32_t)((((k[j] >> f.lo) & f.fmask) >> L) & (TL_BUCKETS - 1));
+                atomicAdd(&h[((b & 255u) << 7) | (b >> 8)], 1u);
+                atomicAdd(&th[par][b & 255u], 1u);
+            }
+        }
+        __syncthreads();
+        prev = t;
+    }
+    if (g * TL_TPG + q < t_end && threadIdx.x < 256) tcnt[(uint64_t)prev * 256 + threadIdx.x] = th[par ^ 1u][threadIdx.x];
+    __syncthreads();
+    for (int i = threadIdx.x; i < TL_BUCKETS; i += 1024)
+        if (h[i]) atomicAdd(&gcnt[((uint64_t)(i >> 7) * G + g) * 128 + (i & 127)], h[i]);
+}
+
+// the bucket histogram in natural order (bucket = d2 << 8 | d1) from the segment counts
+__global__ void __launch_bounds__(128) tl_gsum_kernel(const uint32_t* __restrict__ gcnt, uint32_t G,
+                                                      uint32_t* __restrict__ hist) {
+    const uint32_t d1 = blockIdx.x, d2 = threadIdx.x;
+    const uint32_t* p = gcnt + (uint64_t)d1 * G * 128 + d2;
+    uint32_t s = 0, g = 0;
+    for (; g + 8 <= G; g += 8) {   // 8 independent loads in flight
+        uint32_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = p[(uint64_t)(g + j) * 128];
+#pragma unroll
+        for (int j = 0; j < 8; j++) s += v[j];
+    }
+    for (; g < G; g++) s += p[(uint64_t)g * 128];
+    hist[(d2 << 8) | d1] = s;
+}
+
+// Column-wise exclusive scan of a rows x C matrix of u32 counts, in place: m[r][c] <- base[c] +
+// sum of m[<r][c], with base[c] = sum of all counts of the columns before c (the digit's global
+// start).  Three launches for BOTH matrices of a sort (tile counts, C = 256; segment counts,
+// C = 128): chunk sums, a one-block-per-matrix scan of the chunk sums, apply.
+constexpr uint32_t CS_CH = 64;
+struct CSJob {
+    uint32_t* m;
+    uint32_t* part;
+    uint32_t rows, C, nb;   // nb = chunks of CS_CH rows
+};
+struct CSJobs {
+    CSJob j[2];
+};
+
+__device__ __forceinline__ const CSJob& cs_job(const CSJobs& js, uint32_t& blk) {
+    if (blk < js.j[0].nb) return js.j[0];
+    blk -= js.j[0].nb;
+    return js.j[1];
+}
+
+__global__ void __launch_bounds__(256) cs_reduce_kernel(CSJobs js) {
+    uint32_t blk = blockIdx.x;
+    const CSJob& J = cs_job(js, blk);
+    const uint32_t c = threadIdx.x, r0 = blk * CS_CH;
+    if (c >= J.C) return;
+    uint32_t v[CS_CH];
+#pragma unroll
+    for (uint32_t r = 0; r < CS_CH; r++) v[r] = r0 + r < J.rows ? J.m[(uint64_t)(r0 + r) * J.C + c] : 0u;
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < CS_CH; r++) s += v[r];
+    J.part[(uint64_t)blk * J.C + c] = s;
+}
+
+__global__ void __launch_bounds__(1024) cs_top_kernel(CSJobs js) {
+    const CSJob& J = js.j[blockIdx.x];
+    const uint32_t C = J.C, QN = 1024 / C, nb = J.nb;   // thread (c, q) walks chunk sums q*per .. +per
+    __shared__ uint32_t tot[1024];
+    __shared__ uint32_t colbase[256];
+    __shared__ uint32_t wsum[16];
+    const uint32_t c = threadIdx.x % C, q = threadIdx.x / C;
+    const uint32_t per = (nb + QN - 1) / QN, b0 = q * per < nb ? q * per : nb, b1 = b0 + per < nb ? b0 + per : nb;
+    uint32_t s = 0;
+#pragma unroll 8
+    for (uint32_t b = b0; b < b1; b++) s += J.part[(uint64_t)b * C + c];
+    tot[q * C + c] = s;
+    __syncthreads();
+    uint32_t T = 0;
+    if (threadIdx.x < C)
+        for (uint32_t k = 0; k < QN; k++) T += tot[k * C + threadIdx.x];
+    const uint32_t inc = wave_incl_scan_u32(T);
+    if (lane_id() == 63) wsum[wave_id()] = inc;
+    __syncthreads();
+    if (threadIdx.x < C) {
+        uint32_t ex = inc - T;
+        for (int w = 0; w < wave_id(); w++) ex += wsum[w];
+        colbase[threadIdx.x] = ex;
+    }
+    __syncthreads();
+    uint32_t run = colbase[c];
+    for (uint32_t k = 0; k < q; k++) run += tot[k * C + c];
+#pragma unroll 8
+    for (uint32_t b = b0; b < b1; b++) {
+        const uint32_t v = J.part[(uint64_t)b * C + c];
+        J.part[(uint64_t)b * C + c] = run;
+        run += v;
+    }
+}
+
+__global__ void __launch_bounds__(256) cs_apply_kernel(CSJobs js) {
+    uint32_t blk = blockIdx.x;
+    const CSJob& J = cs_job(js, blk);
+    const uint32_t c = threadIdx.x, r0 = blk * CS_CH;
+    if (c >= J.C) return;
+    uint32_t run = J.part[(uint64_t)blk * J.C + c];
+    uint32_t v[CS_CH];
+#pragma unroll
+    for (uint32_t r = 0; r < CS_CH; r++) v[r] = r0 + r < J.rows ? J.m[(uint64_t)(r0 + r) * J.C + c] : 0u;
+#pragma unroll
+    for (uint32_t r = 0; r < CS_CH; r++) {
+        if (r0 + r < J.rows) J.m[(uint64_t)(r0 + r) * J.C + c] = run;
+        run += v[r];
+    }
+}
+
+// pass 2: one workgroup per segment s = d1 * G + g (the run of group g's keys with first-pass
+// digit d1), stable by the second-pass digit d2 = word bits [dsh, dsh + 7); segment bounds from
+// the scanned tile counts (off1), digit offsets from the scanned segment counts (off2).  A
+// sub-tile of up to TL2_TILE words is ranked in registers, staged in LDS in digit order and
+// written as runs; a segment longer than that is walked in sub-tiles with running offsets.
+// (K only names the instance after the sort it serves; the kernel moves packed words.)
+#ifndef QE_TL2_ITEMS
+#define QE_TL2_ITEMS 18
+#endif
+constexpr int TL2_NT = 512, TL2_ITEMS = QE_TL2_ITEMS, TL2_TILE = TL2_NT * TL2_ITEMS;   // 9216: mean 8192 + 11 sd
+
+template <typename K>
+__global__ void __launch_bounds__(TL2_NT, 4) tl_pass2_kernel(const uint64_t* __restrict__ win, uint64_t* __restrict__ wout,
+                                                         uint64_t n, int dsh, const uint32_t* __restrict__ off1,
+                                                         const uint32_t* __restrict__ off2, uint32_t G) {
+    constexpr int BINS = 128, NW = TL2_NT / 64, WT = 64 * TL2_ITEMS;
+    __shared__ uint64_t stage[TL2_TILE];
+    __shared__ uint32_t whist[NW][BINS];
+    __shared__ uint32_t bexcl[BINS];
+    __shared__ uint32_t gofs[BINS];
+    __shared__ uint32_t wsum[NW];
+    const uint32_t s = blockIdx.x, d1 = s / G, g = s % G;
+    const uint32_t start = off1[(uint64_t)g * TL_TPG * 256 + d1];
+    const uint32_t end = g + 1 < G ? off1[(uint64_t)(g + 1) * TL_TPG * 256 + d1]
+                                   : (d1 < 255 ? off1[d1 + 1] : (uint32_t)n);   // tile 0's row = digit starts
+    const int w = wave_id(), l = lane_id();
+    const uint64_t lt = lanemask_lt();
+    const uint32_t d = threadIdx.x;   // threads 0..127 own one digit each
+    uint32_t run = d < BINS ? off2[(uint64_t)s * BINS + d] : 0u;
+    for (uint32_t base = start; base < end; base += TL2_TILE) {   // block-uniform
+        const uint32_t m = end - base < (uint32_t)TL2_TILE ? end - base : (uint32_t)TL2_TILE;
+        for (int i = threadIdx.x; i < NW * BINS; i += TL2_NT) (&whist[0][0])[i] = 0;
+        uint64_t word[TL2_ITEMS];
+        uint32_t pos2[(TL2_ITEMS + 1) / 2];   // ranks < TL2_TILE: two u16 per register
+        const uint64_t* src = win + base + (uint32_t)w * WT + l;
+        const int lim = (int)m - (int)((uint32_t)w * WT + l);   // element j valid iff j * 64 < lim
+#pragma unroll
+        for (int j = 0; j < TL2_ITEMS; j++) word[j] = j * 64 < lim ? src[j * 64] : 0;
+        __syncthreads();   // whist zeroed
+#pragma unroll
+        for (int j = 0; j < TL2_ITEMS; j++) {   // stable rank inside the wave: (j, lane) order
+            const bool ok = j * 64 < lim;
+            const uint32_t dd = (uint32_t)(word[j] >> dsh) & (BINS - 1);
+            uint64_t peers = __ballot(ok);
+#pragma unroll
+            for (int b = 0; b < 7; b++) {
+                const bool bit = (dd >> b) & 1u;
+                const uint64_t mm = __ballot(bit);
+                peers &= bit ? mm : ~mm;
+            }
+            const int leader = peers ? (__ffsll((unsigned long long)peers) - 1) : 0;
+            uint32_t old = 0;
+            if (ok && l == leader) {
+                old = whist[w][dd];
+                whist[w][dd] = old + (uint32_t)__popcll(peers);
+            }
+            old = (uint32_t)__shfl((int)old, leader, 64);
+            const uint32_t r = old + (uint32_t)__popcll(peers & lt);
+            if (j & 1) pos2[j >> 1] |= r << 16;
+            else pos2[j >> 1] = r;
+        }
+        __syncthreads();
+        uint32_t tot = 0;
+        if (d < BINS) {
+#pragma unroll
+            for (int ww = 0; ww < NW; ww++) {
+                const uint32_t cc = whist[ww][d];
+                whist[ww][d] = tot;
+                tot += cc;
+            }
+        }
+        const uint32_t inc = wave_incl_scan_u32(tot);
+        if (l == 63) wsum[w] = inc;
+        __syncthreads();
+        if (d < BINS) {
+            uint32_t ex = inc - tot;
+            for (int ww = 0; ww < w; ww++) ex += wsum[ww];
+            bexcl[d] = ex;
+            gofs[d] = run - ex;
+            run += tot;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < TL2_ITEMS; j++) {
+            if (j * 64 < lim) {
+                const uint32_t dd = (uint32_t)(word[j] >> dsh) & (BINS - 1);
+                const uint32_t r = (pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                stage[bexcl[dd] + whist[w][dd] + r] = word[j];
+            }
+        }
+        __syncthreads();
+#pragma unroll 6   // (fully unrolled, every LDS read is hoisted and the kernel spills)
+        for (int k = 0; k < TL2_ITEMS; k++) {
+            const uint32_t i = (uint32_t)k * TL2_NT + threadIdx.x;
+            if (i < m) {
+                const uint64_t wd = stage[i];
+                const uint32_t p = gofs[(uint32_t)(wd >> dsh) & (BINS - 1)] + i;
+                if ((uint64_t)p < n) wout[p] = wd;   // never false with consistent offsets
+            }
+        }
+        __syncthreads();   // stage / whist / gofs are rewritten by the next sub-tile
+    }
+}
+
 // Non-packable pairs (64-bit keys with > 32 varying bits AND a rowid): key and rowid staged
 // separately.  Kept simple: rare in this workload (never in the measured configs).
 template <typename K, bool VIN>
@@ -772,11 +1040,130 @@ static LocalRounds local_rounds(int L) {   // L low bits in rounds of <= 8
     return lr;
 }
 
+// both column scans of a two-level sort: m0 (rows0 x 256), m1 (rows1 x 128)
+static void column_scans(qe_ctx* c, uint32_t* m0, uint32_t rows0, uint32_t* m1, uint32_t rows1) {
+    CSJobs js;
+    js.j[0] = CSJob{m0, nullptr, rows0, 256u, (rows0 + CS_CH - 1) / CS_CH};
+    js.j[1] = CSJob{m1, nullptr, rows1, 128u, (rows1 + CS_CH - 1) / CS_CH};
+    uint32_t* part = dalloc_t<uint32_t>(c, (size_t)js.j[0].nb * 256 + (size_t)js.j[1].nb * 128);
+    js.j[0].part = part;
+    js.j[1].part = part + (size_t)js.j[0].nb * 256;
+    const unsigned nblk = js.j[0].nb + js.j[1].nb;
+    hipLaunchKernelGGL(cs_reduce_kernel, dim3(nblk), dim3(256), 0, c->stream, js);
+    QE_HIP(hipGetLastError());
+    hipLaunchKernelGGL(cs_top_kernel, dim3(2), dim3(1024), 0, c->stream, js);
+    QE_HIP(hipGetLastError());
+    hipLaunchKernelGGL(cs_apply_kernel, dim3(nblk), dim3(256), 0, c->stream, js);
+    QE_HIP(hipGetLastError());
+    dfree(c, part);
+}
+
+static bool prof_split() {   // tuning aid: QE_PROF_SPLIT=1 times the second pass under its own name
+    static bool on = [] {
+        const char* s = getenv("QE_PROF_SPLIT");
+        return s && s[0] == '1';
+    }();
+    return on;
+}
+
+static bool sort_pre_on() {
+    static bool on = [] {   // tuning knob: QE_SORT_PRE=0 keeps the lookback form of the two passes
+        const char* s = getenv("QE_SORT_PRE");
+        return !(s && s[0] == '0');
+    }();
+    return on;
+}
+
+// the two-level sort (H = TL_H) with both global passes lookback-free (see tl_hist_tiles_kernel)
+template <typename K>
+static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, uint64_t n, int bits, Field f,
+                               const char* name, SortOut* out) {
+    const int L = bits - TL_H;
+    const LocalRounds lr = local_rounds(L);
+    const uint32_t nt = (uint32_t)((n + RTILE - 1) / RTILE);
+    const uint32_t G = (nt + TL_TPG - 1) / TL_TPG;
+    const uint32_t Q = G >= 256 ? 1u : 256u / G;   // ~one histogram block per CU
+    const uint32_t nseg = 256u * G;
+    uint32_t* tcnt = dalloc_t<uint32_t>(c, (size_t)nt * 256);
+    uint32_t* gcnt = dalloc_t<uint32_t>(c, (size_t)nseg * 128);
+    uint32_t* hist = dalloc_t<uint32_t>(c, TL_BUCKETS);
+    uint32_t* bstart = dalloc_t<uint32_t>(c, TL_BUCKETS + 1 + 512);
+    uint32_t* base1 = bstart + TL_BUCKETS + 1;
+    uint32_t* base2 = base1 + 256;
+    uint64_t* d_max = c->d_scratch + 34;
+    auto release = [&] {
+        dfree(c, tcnt);
+        dfree(c, gcnt);
+        dfree(c, hist);
+        dfree(c, bstart);
+    };
+    QE_HIP(hipMemsetAsync(gcnt, 0, (size_t)nseg * 128 * sizeof(uint32_t), c->stream));
+    {
+        Timed t(c, "sort_hist", (double)sizeof(K) * n);
+        hipLaunchKernelGGL((tl_hist_tiles_kernel<K>), dim3(G * Q), dim3(1024), 0, c->stream, keys, n, f, L, nt, G, Q,
+                           tcnt, gcnt);
+        QE_HIP(hipGetLastError());
+        hipLaunchKernelGGL(tl_gsum_kernel, dim3(256), dim3(128), 0, c->stream, gcnt, G, hist);
+        QE_HIP(hipGetLastError());
+        hipLaunchKernelGGL(tl_scan_kernel, dim3(1), dim3(1024), 0, c->stream, hist, bstart, base1, base2, d_max);
+        QE_HIP(hipGetLastError());
+    }
+    {
+        Timed t(c, "sort_scan", 8.0 * ((double)nt * 256 + (double)nseg * 128));
+        column_scans(c, tcnt, nt, gcnt, nseg);
+    }
+    uint64_t* w1 = dalloc_t<uint64_t>(c, n);
+    uint64_t* w2 = dalloc_t<uint64_t>(c, n);
+    K* kout = dalloc_t<K>(c, n);
+    uint32_t* vout = dalloc_t<uint32_t>(c, n);
+    {
+        // algorithmic bytes: key (+ rowid when given; generated otherwise) in, packed word out
+        Timed t(c, name, ((double)sizeof(K) + (vals ? 4.0 : 0.0) + 8.0) * n);
+        if (vals)
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV, OUT_WORD, true, 8, R_ITEMS, R_NT, true>), dim3(nt),
+                               dim3(R_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, 255u, f, tcnt,
+                               nullptr, nullptr, 0u);
+        else
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KIOTA, OUT_WORD, true, 8, R_ITEMS, R_NT, true>), dim3(nt),
+                               dim3(R_NT), 0, c->stream, keys, nullptr, nullptr, kout, w1, vout, n, 32 + L, 255u, f,
+                               tcnt, nullptr, nullptr, 0u);
+        QE_HIP(hipGetLastError());
+    }
+    {
+        Timed t(c, prof_split() ? "sort_pass2" : name, 16.0 * n);
+        hipLaunchKernelGGL((tl_pass2_kernel<K>), dim3(nseg), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8, tcnt,
+                           gcnt, G);
+        QE_HIP(hipGetLastError());
+    }
+    // the two passes are valid whatever the bucket sizes, so they are queued before the host
+    // reads the largest bucket: the GPU stays busy through that round trip
+    if (read_u64(c, d_max) > (uint64_t)TL_CAP) {   // a bucket beyond LDS (skew): plain LSD passes
+        dfree(c, w1);
+        dfree(c, w2);
+        dfree(c, kout);
+        dfree(c, vout);
+        release();
+        return false;
+    }
+    {
+        Timed t(c, "sort_local", 8.0 * n + ((double)sizeof(K) + 4) * n);
+        hipLaunchKernelGGL((tl_local_kernel<K, IN_WORD>), dim3(TL_BUCKETS), dim3(TL_NT), 0, c->stream, w2, nullptr,
+                           nullptr, kout, vout, bstart, 0u, f, lr);
+        QE_HIP(hipGetLastError());
+    }
+    dfree(c, w1);
+    dfree(c, w2);
+    release();
+    *out = SortOut{kout, vout, true, true};
+    return true;
+}
+
 // H = TL_H (15 high bits by two global passes) for large inputs; H = 8 (ONE global pass) for
 // inputs whose 256 buckets fit LDS (<= ~1 M keys)
 template <typename K>
 static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint64_t n, int bits, Field f,
                            const char* name, SortOut* out, int H = TL_H) {
+    if (H == TL_H && sort_pre_on()) return sort_two_level_pre<K>(c, keys, vals, n, bits, f, name, out);
     const int L = bits - H;   // low bits sorted in LDS (<= 24)
     const LocalRounds lr = local_rounds(L);
     uint32_t* hist = dalloc_t<uint32_t>(c, TL_BUCKETS);
