@@ -418,6 +418,44 @@ __global__ void __launch_bounds__(1024) tl_scan_kernel(const uint32_t* __restric
     }
 }
 
+// H = 8 (a small sort's single global pass): 256 buckets, so a 1 KiB histogram instead of the
+// 128 KiB one -- for the C4 batch's many small sorts the fixed cost of zeroing, flushing and
+// scanning 32768 bins was most of the histogram time
+template <typename K>
+__global__ void __launch_bounds__(256) tl_hist8_kernel(const K* __restrict__ keys, uint64_t n, Field f, int L,
+                                                       uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+        atomicAdd(&h[(uint32_t)((((uint64_t)keys[i] >> f.lo) & f.fmask) >> L) & 255u], 1u);
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+
+// one block: the 256 bucket starts (+ the end), which are also the pass's digit bases, and the
+// largest bucket
+__global__ void __launch_bounds__(256) tl_scan8_kernel(const uint32_t* __restrict__ hist, uint32_t* __restrict__ bstart,
+                                                       uint64_t* __restrict__ maxb) {
+    __shared__ uint32_t wsum[4], wmax[4];
+    const uint32_t v = hist[threadIdx.x];
+    const uint32_t inc = wave_incl_scan_u32(v);
+    const uint32_t mx = wave_max_u32(v);
+    if (lane_id() == 63) wsum[wave_id()] = inc;
+    if (lane_id() == 0) wmax[wave_id()] = mx;
+    __syncthreads();
+    uint32_t ex = inc - v;
+    for (int w = 0; w < wave_id(); w++) ex += wsum[w];
+    bstart[threadIdx.x] = ex;
+    if (threadIdx.x == 255) bstart[256] = ex + v;
+    if (threadIdx.x == 0) {
+        uint32_t m = 0;
+        for (int w = 0; w < 4; w++) m = wmax[w] > m ? wmax[w] : m;
+        *maxb = m;
+    }
+}
+
 // one workgroup per bucket: up to TL_CAP packed words, sorted by the low L bits in LDS.  Each wave
 // owns a contiguous slice of jm x 64 words, jm = ceil(m / (waves x 64)): every wave works and the
 // work is proportional to the bucket, not to TL_CAP.
@@ -1066,6 +1104,14 @@ static bool prof_split() {   // tuning aid: QE_PROF_SPLIT=1 times the second pas
     return on;
 }
 
+static uint64_t sort_pre_min() {   // tuning knob: QE_SORT_PRE_MIN = smallest n for the lookback-free form
+    static uint64_t v = [] {
+        const char* s = getenv("QE_SORT_PRE_MIN");
+        return s ? strtoull(s, nullptr, 0) : (1ull << 25);
+    }();
+    return v;
+}
+
 static bool sort_pre_on() {
     static bool on = [] {   // tuning knob: QE_SORT_PRE=0 keeps the lookback form of the two passes
         const char* s = getenv("QE_SORT_PRE");
@@ -1163,7 +1209,11 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
 template <typename K>
 static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint64_t n, int bits, Field f,
                            const char* name, SortOut* out, int H = TL_H) {
-    if (H == TL_H && sort_pre_on()) return sort_two_level_pre<K>(c, keys, vals, n, bits, f, name, out);
+    // the lookback-free form saves ~1 us per million keys per pass but adds ~30 us of count
+    // scans: it pays from a few 10^7 keys (measured on MI355X: C3's 0.5-1e8-key sorts 2 % faster,
+    // the C4 batch's 1-10 M-key sorts slower)
+    if (H == TL_H && sort_pre_on() && n >= sort_pre_min())
+        return sort_two_level_pre<K>(c, keys, vals, n, bits, f, name, out);
     const int L = bits - H;   // low bits sorted in LDS (<= 24)
     const LocalRounds lr = local_rounds(L);
     uint32_t* hist = dalloc_t<uint32_t>(c, TL_BUCKETS);
@@ -1172,8 +1222,17 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
     uint32_t* base1 = bstart + TL_BUCKETS + 1;
     uint32_t* base2 = base1 + 256;
     uint64_t* d_max = c->d_scratch + 34;
-    QE_HIP(hipMemsetAsync(hist, 0, TL_BUCKETS * sizeof(uint32_t), c->stream));
-    {
+    if (H == 8) {
+        base1 = bstart;   // one pass: its digit IS the bucket
+        QE_HIP(hipMemsetAsync(hist, 0, 256 * sizeof(uint32_t), c->stream));
+        Timed t(c, "sort_hist", (double)sizeof(K) * n);
+        hipLaunchKernelGGL((tl_hist8_kernel<K>), dim3(grid_for(n, 256 * 16, 1024)), dim3(256), 0, c->stream, keys, n, f,
+                           L, hist);
+        QE_HIP(hipGetLastError());
+        hipLaunchKernelGGL(tl_scan8_kernel, dim3(1), dim3(256), 0, c->stream, hist, bstart, d_max);
+        QE_HIP(hipGetLastError());
+    } else {
+        QE_HIP(hipMemsetAsync(hist, 0, TL_BUCKETS * sizeof(uint32_t), c->stream));
         Timed t(c, "sort_hist", (double)sizeof(K) * n);
         hipLaunchKernelGGL((tl_hist_kernel<K>), dim3(grid_for((n + 3) / 4, 1024, 256)), dim3(1024), 0, c->stream, keys,
                            n, f, L, hist);

@@ -147,6 +147,29 @@ def test_sort_pairs_two_level_sizes(ctx, case):
     ctx.pairs_free(p)
 
 
+@pytest.mark.parametrize("case,with_vals", [("27bit", True), ("27bit", False), ("31bit", True), ("skew", True)])
+def test_sort_pairs_lookback_free_two_level(ctx, case, with_vals):
+    """n >= 2^25: the two-level sort whose global passes take their offsets from the histogram
+    read (per-tile and per-segment digit counts) instead of a lookback; 'skew' runs both passes
+    and then falls back to the LSD passes"""
+    n = (1 << 25) + 4_321
+    rng = np.random.default_rng(99 + len(case))
+    k = _keys_for(case, n, rng)
+    if with_vals:
+        v = rng.permutation(n).astype(np.uint32)
+        p = ctx.pairs_from_host(k, v)
+    else:
+        v = np.arange(n, dtype=np.uint32)
+        col = _col(ctx, k)
+        p = ctx.gather_pairs(col, None)
+    ctx.sort_pairs(p)
+    gk, gv = ctx.pairs_to_host(p)
+    order = np.argsort(k, kind="stable")
+    np.testing.assert_array_equal(gk, k[order])
+    np.testing.assert_array_equal(gv, v[order])
+    ctx.pairs_free(p)
+
+
 @pytest.mark.parametrize("n", [2, 64, 1000, 5120, 5121, 70_000, 699_999, 700_001, 1_048_576, 3_000_000])
 @pytest.mark.parametrize("case", ["27bit", "31bit", "12bit", "skew"])
 @pytest.mark.parametrize("with_vals", [True, False])
