@@ -126,7 +126,12 @@ struct MJSharedG {
     uint32_t ticket;
 };
 using MJShared64 = MJSharedG<uint64_t, 2 * MJ_TILE>;
-using MJShared32 = MJSharedG<uint32_t, 3 * MJ_TILE / 2>;
+// 2816 = 1.375 pairs per R row: 31.8 KiB of LDS, so FIVE workgroups per CU (3072 was 33.3 KiB, four)
+// -- more tiles in flight to cover the lookback wait (stamps: ~6 us of a ~26 us tile)
+#ifndef QE_MJ32_OUTCAP
+#define QE_MJ32_OUTCAP 2816
+#endif
+using MJShared32 = MJSharedG<uint32_t, QE_MJ32_OUTCAP>;
 
 // bank swizzle of the S window for the key width (sw64: u64 slots, sw32: u32 slots)
 template <typename KT>
