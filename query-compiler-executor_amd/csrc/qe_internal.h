@@ -86,6 +86,13 @@ struct qe_ctx {
     uint64_t* d_scratch = nullptr;   // 64 words
     uint64_t* h_scratch = nullptr;   // pinned, 64 words
 
+    // loader (qe_load_relation): pinned staging ring for pageable host columns
+    static constexpr int STAGE_SLOTS = 3;
+    void* h_stage[STAGE_SLOTS] = {nullptr, nullptr, nullptr};
+    hipEvent_t stage_ev[STAGE_SLOTS] = {nullptr, nullptr, nullptr};
+    size_t stage_bytes = 0;
+    double load_s = 0, load_bytes = 0;   // wall time / bytes of host -> HBM loads so far
+
     // profiling
     bool prof = false;
     std::vector<qe::PendingEvent> pending;

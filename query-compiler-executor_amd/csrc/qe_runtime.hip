@@ -1,7 +1,10 @@
 // qe_runtime.hip -- libqe context, caching HBM allocator, lookback state, profiling, the
 // relation loader (reference src/utilities.c:105-162) and the on-device splitmix64 generator.
 #include <algorithm>
+#include <chrono>
 #include <cstring>
+#include <thread>
+#include <vector>
 
 #include "qe_device.h"
 #include "qe_internal.h"
@@ -322,6 +325,47 @@ static void column_stats(qe_ctx* c, Relation& r) {
     }
 }
 
+// Host -> HBM copy of a pageable buffer (an mmap'd relation file, a numpy column): a ring of
+// pinned 32 MiB slots.  Each slot is filled by several host threads (one thread's memcpy is
+// ~10 GB/s, well below a PCIe5 x16 link) and copied with hipMemcpyAsync while the next slot
+// fills; a slot is refilled once its previous copy has completed (event).  (hipMemcpy from
+// pageable memory stages through the runtime's own small buffers, one chunk at a time.)
+static void h2d_staged(qe_ctx* c, void* dst, const void* src, size_t bytes) {
+    constexpr size_t SLOT = 32ull << 20;
+    if (!c->h_stage[0]) {
+        for (int k = 0; k < qe_ctx::STAGE_SLOTS; k++) {
+            QE_HIP(hipHostMalloc(&c->h_stage[k], SLOT, hipHostMallocDefault));
+            QE_HIP(hipEventCreateWithFlags(&c->stage_ev[k], hipEventDisableTiming));
+        }
+        c->stage_bytes = SLOT;
+    }
+    unsigned nth = std::thread::hardware_concurrency();
+    nth = nth < 2 ? 1 : (nth > 8 ? 8 : nth);
+    if (const char* e = getenv("QE_LOAD_THREADS")) nth = (unsigned)std::max(1, atoi(e));
+    int k = 0;
+    for (size_t off = 0; off < bytes; off += SLOT, k = (k + 1) % qe_ctx::STAGE_SLOTS) {
+        const size_t len = std::min(SLOT, bytes - off);
+        QE_HIP(hipEventSynchronize(c->stage_ev[k]));   // the slot's previous copy is done
+        char* stage = static_cast<char*>(c->h_stage[k]);
+        const char* from = static_cast<const char*>(src) + off;
+        if (nth == 1 || len < (1u << 20)) {
+            memcpy(stage, from, len);
+        } else {
+            std::vector<std::thread> th;
+            const size_t per = (len / nth + 4095) & ~(size_t)4095;
+            for (unsigned t = 0; t < nth; t++) {
+                const size_t a = t * per;
+                if (a >= len) break;
+                const size_t b = std::min(len, a + per);
+                th.emplace_back([=] { memcpy(stage + a, from + a, b - a); });
+            }
+            for (auto& x : th) x.join();
+        }
+        QE_HIP(hipMemcpyAsync(static_cast<char*>(dst) + off, stage, len, hipMemcpyHostToDevice, c->stream));
+        QE_HIP(hipEventRecord(c->stage_ev[k], c->stream));
+    }
+}
+
 // =============================================================================================
 // C ABI: lifecycle, relations, buffers, profiling
 // =============================================================================================
@@ -366,6 +410,10 @@ void qe_fini(qe_ctx* c) {
     if (c->lb_tickets) (void)hipFree(c->lb_tickets);
     if (c->d_scratch) (void)hipFree(c->d_scratch);
     if (c->h_scratch) (void)hipHostFree(c->h_scratch);
+    for (int k = 0; k < qe_ctx::STAGE_SLOTS; k++) {
+        if (c->h_stage[k]) (void)hipHostFree(c->h_stage[k]);
+        if (c->stage_ev[k]) (void)hipEventDestroy(c->stage_ev[k]);
+    }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -393,13 +441,20 @@ int qe_load_relation(qe_ctx* c, uint64_t rows, uint64_t ncols, const uint64_t* c
     if (rows >= 0xFFFFFFFFull) throw Error(QE_EINVAL, "relation too large for uint32 rowids");
     Relation r;
     r.rows = rows;
+    const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t j = 0; j < ncols; j++) {
         uint64_t* d = nullptr;
         QE_HIP(hipMalloc(&d, std::max<uint64_t>(rows, 1) * sizeof(uint64_t)));
-        if (rows) QE_HIP(hipMemcpyAsync(d, host_cols[j], rows * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
         r.cols.push_back(d);
+        if (!rows) continue;
+        if (getenv("QE_LOAD_DIRECT"))   // A/B only: the runtime's own pageable copy
+            QE_HIP(hipMemcpyAsync(d, host_cols[j], rows * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+        else
+            h2d_staged(c, d, host_cols[j], rows * sizeof(uint64_t));
     }
     QE_HIP(hipStreamSynchronize(c->stream));
+    c->load_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    c->load_bytes += (double)rows * ncols * sizeof(uint64_t);
     column_stats(c, r);
     c->rels.push_back(std::move(r));
     return (int)c->rels.size() - 1;
@@ -634,6 +689,14 @@ int qe_counts_to_host(qe_ctx* c, const uint32_t* d, uint64_t n, uint32_t* h) {
     QE_API_BEGIN(c)
     if (n) QE_HIP(hipMemcpyAsync(h, d, n * 4, hipMemcpyDeviceToHost, c->stream));
     QE_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_load_stats(qe_ctx* c, double* seconds, double* bytes) {
+    QE_API_BEGIN(c)
+    *seconds = c->load_s;
+    *bytes = c->load_bytes;
     return 0;
     QE_API_END(c)
 }

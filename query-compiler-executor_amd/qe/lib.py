@@ -113,6 +113,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "qe_counts_free": (None, [P, C.c_void_p]),
         "qe_counts_to_host": (I, [P, C.c_void_p, U64, VP]),
         "qe_mem_stats": (I, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+        "qe_load_stats": (I, [P, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
         "qe_mem_trim": (I, [P]),
         "qe_set_profiling": (I, [P, I]),
         "qe_reset_stats": (I, [P]),
@@ -387,6 +388,12 @@ class Ctx:
     def mem_stats(self) -> tuple[int, int]:
         a, b = C.c_uint64(), C.c_uint64()
         self._chk(self.lib.qe_mem_stats(self.h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def load_stats(self) -> tuple[float, float]:
+        """(seconds, bytes) of every host -> HBM relation load so far (PCIe included)"""
+        a, b = C.c_double(), C.c_double()
+        self._chk(self.lib.qe_load_stats(self.h, C.byref(a), C.byref(b)))
         return a.value, b.value
 
     # ---- profiling ----
