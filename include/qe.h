@@ -53,8 +53,9 @@ typedef struct { uint32_t* d; uint64_t n; uint64_t cap; uint32_t flags; } qe_lis
 /* Join input: (key, rowid) pairs in SoA -- the reference's `relation` of `tuple`s
  * (src/structs.h:7-15).  `val == NULL` means rowid i for every i (a base column).
  * match: per-row count of partner rows, filled by qe_merge_join on its sorted path (NULL
- * before), used by qe_driver_counts.  kor/kand: OR / AND of all keys when QE_PAIRS_BITS is set
- * (the sort then skips its own reduction).
+ * before), used by qe_driver_counts.  kor/kand: key bounds when QE_PAIRS_BITS is set -- every
+ * key k satisfies (k & ~kor) == 0 and (k & kand) == kand (the OR / AND of all keys, or of a
+ * superset such as the column the keys were gathered from); the sort then needs no reduction.
  * flags: QE_PAIRS_DISTINCT (no rowid twice), QE_PAIRS_SORTED (ascending by key), QE_PAIRS_BITS.
  * owns: bit 0 key, bit 1 val, bit 2 match buffer belong to the pairs (qe_pairs_free). */
 typedef struct {

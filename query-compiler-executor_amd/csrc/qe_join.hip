@@ -815,6 +815,7 @@ __global__ void __launch_bounds__(256) is_sorted_kernel(const uint64_t* __restri
 
 // keys = col[rows] in list order, plus the OR / AND of the gathered keys (the radix sort's
 // pass plan) so the sort needs no reduction pass of its own
+template <bool BITS>
 __global__ void __launch_bounds__(256) gather_keys_kernel(const uint64_t* __restrict__ col,
                                                           const uint32_t* __restrict__ rows, uint64_t n,
                                                           uint64_t* __restrict__ out,
@@ -842,6 +843,7 @@ __global__ void __launch_bounds__(256) gather_keys_kernel(const uint64_t* __rest
             }
         }
     }
+    if constexpr (!BITS) return;   // bounds known (column statistics): no reduction
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {
         o |= shfl_xor_u64(o, m);
@@ -1492,13 +1494,29 @@ int qe_gather_pairs(qe_ctx* c, qe_col col, const qe_list* rows, qe_pairs* out) {
     out->n = n;
     out->flags = (rows->flags & QE_LIST_DISTINCT) ? PF_DISTINCT : 0;
     out->owns = 1;
+    // a loaded relation's column: its load-time OR / AND bound the gathered keys too, so the
+    // gather needs no reduction and no host round trip (the sort plans on the column's bits)
+    for (auto& r : c->rels)
+        for (size_t j = 0; j < r.cols.size(); j++)
+            if (r.cols[j] == col.d && r.rows == col.n && j < r.kor.size() && !getenv("QE_GATHER_EXACT_BITS")) {
+                if (n) {
+                    Timed t(c, "gather_keys", 12.0 * n + 8.0 * n);
+                    hipLaunchKernelGGL(gather_keys_kernel<false>, dim3(grid_for((n + 3) / 4, 256, 4096)), dim3(256), 0,
+                                       c->stream, col.d, rows->d, n, out->key, (unsigned long long*)nullptr);
+                    QE_HIP(hipGetLastError());
+                }
+                out->kor = r.kor[j];
+                out->kand = r.kand[j];
+                out->flags |= QE_PAIRS_BITS;
+                return 0;
+            }
     uint64_t* d_bits = c->d_scratch + 44;
     uint64_t init[2] = {0ull, ~0ull};
     QE_HIP(hipMemcpyAsync(d_bits, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
     if (n) {
         Timed t(c, "gather_keys", 12.0 * n + 8.0 * n);
-        hipLaunchKernelGGL(gather_keys_kernel, dim3(grid_for((n + 3) / 4, 256, 4096)), dim3(256), 0, c->stream, col.d,
-                           rows->d, n, out->key, (unsigned long long*)d_bits);
+        hipLaunchKernelGGL(gather_keys_kernel<true>, dim3(grid_for((n + 3) / 4, 256, 4096)), dim3(256), 0, c->stream,
+                           col.d, rows->d, n, out->key, (unsigned long long*)d_bits);
         QE_HIP(hipGetLastError());
     }
     uint64_t kb[2];
