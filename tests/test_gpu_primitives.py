@@ -424,3 +424,25 @@ def test_merge_fills_match_counts_and_driver_counts_use_them(ctx):
     d = ctx.driver_counts(R, S, a, b, 0, 4000)
     want = _ref_nondup_counts(ctx.list_to_host(a), ctx.list_to_host(b), 0, 4000)
     np.testing.assert_array_equal(ctx.counts_to_host(d, 4000), want)
+
+
+def test_load_relation_staged_round_trip(ctx):
+    """qe_load_relation copies pageable host columns through the pinned staging ring (32 MiB
+    slots, several host threads per slot): 9 M rows = 72 MB per column, two full slots and a
+    partial one; every value lands, and the load-time OR / AND are those of the column"""
+    n = 9_000_001
+    rng = np.random.default_rng(5)
+    a = rng.integers(0, 1 << 63, n, dtype=np.uint64)
+    b = (rng.integers(0, 1 << 20, n, dtype=np.uint64) << np.uint64(4)) | np.uint64(3)
+    rel = ctx.load_relation([a, b])
+    s0, b0 = ctx.load_stats()
+    assert b0 >= 2 * n * 8 and s0 > 0
+    for j, want in enumerate((a, b)):
+        c = ctx.column(rel, j)
+        p = lib.Pairs()
+        p.key, p.val, p.match, p.n = c.d, None, None, c.n
+        got = np.empty(n, dtype=np.uint64)
+        ctx._chk(ctx.lib.qe_pairs_to_host(ctx.h, lib.C.byref(p), got.ctypes.data, None))
+        np.testing.assert_array_equal(got, want)
+    kor, kand = ctx.column_bits(rel, 1)
+    assert kor == int(np.bitwise_or.reduce(b)) and kand == int(np.bitwise_and.reduce(b))
