@@ -52,6 +52,25 @@ constexpr int LB_VAL_BITS = 46;
 constexpr uint64_t LB_VAL_MASK = (1ull << LB_VAL_BITS) - 1;
 constexpr int LB_MAX_COUNTERS = 65536;
 
+// merge-join flags (one word per launch): R row with > 1 partner, S row with > 1 partner,
+// internal error, 46-bit lookback sum overflow
+enum : uint32_t { MJF_R_FANOUT = 1u, MJF_S_DUP = 2u, MJF_ERR = 4u, MJF_OVF = 8u };
+
+// A two-level sort whose last step (the per-bucket LDS sort) has not run yet: the pairs' key /
+// val buffers are allocated but unfilled, the bucket-partitioned packed words are kept.  A merge
+// of two such sides with the same bucket geometry runs fused (tl_join); anything else that
+// reads the pairs first completes the sort (pairs_need_keys).
+struct DeferredSort {
+    uint64_t* words = nullptr;    // bucket-partitioned (field << 32 | rowid) words
+    uint32_t* bstart = nullptr;   // bucket starts (+ end)
+    uint64_t* kout = nullptr;
+    uint32_t* vout = nullptr;
+    int lo = 0, L = 0;            // field = (key >> lo) & fmask; bucket = field >> L
+    uint64_t fmask = 0, kconst = 0;
+    int lr_n = 0, lr_bits[4] = {0, 0, 0, 0};
+    bool val_ready = false;       // vout already holds the sorted rowids (written by tl_join)
+};
+
 }  // namespace qe
 
 struct qe_ctx {
@@ -92,6 +111,9 @@ struct qe_ctx {
     hipEvent_t stage_ev[STAGE_SLOTS] = {nullptr, nullptr, nullptr};
     size_t stage_bytes = 0;
     double load_s = 0, load_bytes = 0;   // wall time / bytes of host -> HBM loads so far
+
+    // two-level sorts awaiting their per-bucket step, by the pairs' key buffer
+    std::unordered_map<const void*, qe::DeferredSort> deferred;
 
     // profiling
     bool prof = false;
@@ -156,8 +178,17 @@ struct SortOut {
     bool keys_new, vals_new;
 };
 // bits (nullable): host {OR, AND} of the keys when already known; otherwise one reduction pass
+// defer = true (qe_sort_pairs only): a two-level sort may stop before its per-bucket step (see
+// DeferredSort); the returned buffers are then filled by pairs_need_keys or tl_join
 SortOut radix_sort_u64(qe_ctx* c, const uint64_t* keys, const uint32_t* vals /*nullable: iota*/, uint64_t n,
-                       bool with_vals, const uint64_t* bits = nullptr);
+                       bool with_vals, const uint64_t* bits = nullptr, bool defer = false);
+// deferred two-level sorts (qe_sort.hip): complete one before its keys (or vals) are read;
+// drop one whose pairs are freed; the fused merge of two deferred sides (false: not applicable
+// or the output outgrew nR + nS -- the caller completes both sorts and merges as usual)
+void pairs_need_keys(qe_ctx* c, const qe_pairs* p);
+void pairs_need_vals(qe_ctx* c, const qe_pairs* p);
+void pairs_drop_deferred(qe_ctx* c, const qe_pairs* p);
+bool tl_join(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS, uint32_t* oflags);
 SortOut radix_sort_u32(qe_ctx* c, const uint32_t* keys, const uint32_t* vals, uint64_t n,
                        const uint64_t* bits = nullptr);
 // OR / AND of n keys -> host out[2] (synchronises)

@@ -35,7 +35,7 @@ constexpr int MJ_WIN = 4096;              // S keys staged in LDS (32 KiB)
 constexpr uint64_t MJ_HEAVY_DEFER = 1ull << 20;
 constexpr uint64_t MJ_HEAVY_CHUNK = 1ull << 16;
 
-enum : uint32_t { MJF_R_FANOUT = 1u, MJF_S_DUP = 2u, MJF_ERR = 4u, MJF_OVF = 8u };   // OVF: the 46-bit lookback sum wrapped
+// MJF_* flags: qe_internal.h
 
 template <class F>
 __device__ __forceinline__ uint64_t lower_bound_f(uint64_t lo, uint64_t hi, uint64_t key, F at) {
@@ -1533,7 +1533,7 @@ int qe_sort_pairs(qe_ctx* c, qe_pairs* p) {
     if (p->flags & PF_SORTED) return 0;
     p->flags &= ~QE_PAIRS_MATCHED;
     uint64_t bits[2] = {p->kor, p->kand};
-    SortOut so = radix_sort_u64(c, p->key, p->val, p->n, true, (p->flags & QE_PAIRS_BITS) ? bits : nullptr);
+    SortOut so = radix_sort_u64(c, p->key, p->val, p->n, true, (p->flags & QE_PAIRS_BITS) ? bits : nullptr, true);
     if (so.keys_new) {
         if (p->owns & 1) dfree(c, p->key);
         p->key = (uint64_t*)so.keys;
@@ -1551,6 +1551,7 @@ int qe_sort_pairs(qe_ctx* c, qe_pairs* p) {
 
 int qe_is_sorted(qe_ctx* c, const qe_pairs* p, int* sorted) {
     QE_API_BEGIN(c)
+    pairs_need_keys(c, p);
     *sorted = pairs_sorted(c, p) ? 1 : 0;
     return 0;
     QE_API_END(c)
@@ -1560,8 +1561,12 @@ int qe_merge_join(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_l
     QE_API_BEGIN(c)
     const bool sorted = pairs_sorted(c, R) && pairs_sorted(c, S);
     uint32_t fl = MJF_R_FANOUT | MJF_S_DUP;
-    if (sorted) merge_sorted(c, R, S, outR, outS, &fl);
-    else merge_sequential(c, R, S, outR, outS);
+    if (!(sorted && tl_join(c, R, S, outR, outS, &fl))) {   // fused: both sides' sorts end inside the join
+        pairs_need_keys(c, R);
+        pairs_need_keys(c, S);
+        if (sorted) merge_sorted(c, R, S, outR, outS, &fl);
+        else merge_sequential(c, R, S, outR, outS);
+    }
     outR->flags = ((R->flags & PF_DISTINCT) && sorted && !(fl & MJF_R_FANOUT)) ? QE_LIST_DISTINCT : 0;
     outS->flags = ((S->flags & PF_DISTINCT) && sorted && !(fl & MJF_S_DUP)) ? QE_LIST_DISTINCT : 0;
     return 0;
@@ -1571,6 +1576,8 @@ int qe_merge_join(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_l
 int qe_merge_join_counts(qe_ctx* c, qe_pairs* R, qe_pairs* S, uint64_t* pairs) {
     QE_API_BEGIN(c)
     if (!pairs_sorted(c, R) || !pairs_sorted(c, S)) throw Error(QE_EINVAL, "qe_merge_join_counts needs sorted inputs");
+    pairs_need_keys(c, R);
+    pairs_need_keys(c, S);
     const bool r_done = (R->flags & QE_PAIRS_MATCHED) && (R->match || R->n == 0);
     const uint64_t Q = merge_count_side(c, S, R);
     if (!r_done) {
@@ -1587,6 +1594,7 @@ int qe_merge_join_counts(qe_ctx* c, qe_pairs* R, qe_pairs* S, uint64_t* pairs) {
 int qe_checksum_weighted(qe_ctx* c, qe_col col, const qe_pairs* p, uint64_t* sum) {
     QE_API_BEGIN(c)
     if (p->n && !p->match) throw Error(QE_EINVAL, "qe_checksum_weighted needs match counts");
+    pairs_need_vals(c, p);
     unsigned long long* d = (unsigned long long*)(c->d_scratch + 40);
     QE_HIP(hipMemsetAsync(d, 0, 8, c->stream));
     if (p->n) {
@@ -1609,6 +1617,8 @@ int qe_set_materialize_limit(qe_ctx* c, uint64_t pairs) {
 
 int qe_scan_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS) {
     QE_API_BEGIN(c)
+    pairs_need_keys(c, R);
+    pairs_need_keys(c, S);
     uint64_t n = std::min(R->n, S->n);
     outR->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
     outS->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
@@ -1626,6 +1636,18 @@ int qe_driver_counts(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const qe_l
     QE_API_BEGIN(c)
     if (mode != 0 && mode != 1) throw Error(QE_EINVAL, "mode");
     const bool sorted_inputs = R && S && (R->flags & PF_SORTED) && (S->flags & PF_SORTED);
+    // the fast path reads the driving side's rowids + match counts (a fused join writes both) or,
+    // without match counts, both sides' sorted keys; the general path reads the lists only
+    const qe_pairs* A = mode == 0 ? R : S;
+    const qe_pairs* B = mode == 0 ? S : R;
+    if (sorted_inputs && (B->flags & PF_DISTINCT)) {
+        if (A->match) {
+            pairs_need_vals(c, A);
+        } else {
+            pairs_need_keys(c, A);
+            pairs_need_keys(c, B);
+        }
+    }
     if (sorted_inputs && mode == 0 && (S->flags & PF_DISTINCT)) *d_counts = driver_counts_sorted(c, R, S, rows);
     else if (sorted_inputs && mode == 1 && (R->flags & PF_DISTINCT)) *d_counts = driver_counts_sorted(c, S, R, rows);
     else *d_counts = driver_counts_general(c, outR, outS, mode, rows);

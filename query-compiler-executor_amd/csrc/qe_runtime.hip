@@ -653,6 +653,7 @@ int qe_pairs_from_host(qe_ctx* c, const uint64_t* key, const uint32_t* val, uint
 
 int qe_pairs_to_host(qe_ctx* c, const qe_pairs* p, uint64_t* key, uint32_t* val) {
     QE_API_BEGIN(c)
+    pairs_need_keys(c, p);
     if (p->n) {
         if (key) QE_HIP(hipMemcpyAsync(key, p->key, p->n * 8, hipMemcpyDeviceToHost, c->stream));
         if (val) {
@@ -671,6 +672,7 @@ int qe_pairs_to_host(qe_ctx* c, const qe_pairs* p, uint64_t* key, uint32_t* val)
 
 void qe_pairs_free(qe_ctx* c, qe_pairs* p) {
     if (!c || !p) return;
+    pairs_drop_deferred(c, p);
     if (p->owns & 1) dfree(c, p->key);
     if (p->owns & 2) dfree(c, p->val);
     if (p->owns & 4) dfree(c, p->match);

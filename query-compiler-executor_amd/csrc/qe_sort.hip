@@ -23,6 +23,7 @@
 //                      one chain per digit) -- its latency overlaps the staging -- and the tile
 //                      is written as runs of equal digits.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "qe_device.h"
@@ -844,6 +845,257 @@ __global__ void __launch_bounds__(TL2_NT, 4) tl_pass2_kernel(const uint64_t* __r
     }
 }
 
+// ---- fused per-bucket sort + merge join (tl_join) ------------------------------------------
+// Both join sides went through the two global passes of the two-level sort with the same bucket
+// geometry, so equal keys share a bucket number and bucket b of R joins bucket b of S only.
+// One workgroup per bucket (taken in order by ticket): both buckets' packed words are sorted in
+// LDS (the per-bucket step of the sort, done here instead of writing sorted key + rowid arrays
+// and reading them back in the merge), each sorted R row finds its S run by binary searches in
+// LDS, a block scan and a lookback over buckets give the output offsets, and the pairs are
+// written in the reference's order (key, then R order, then S order).  Also written: R's match
+// count and rowid per sorted row (what qe_driver_counts reads).
+//
+// lds_sort_words: stable LDS radix sort of m <= NT x ITEMS words held in registers in the
+// wave-contiguous layout (wave w owns jm x 64 consecutive words); on return `stage` holds the
+// sorted words (the same ranking rounds as tl_local_kernel).
+template <int NT, int ITEMS>
+__device__ __forceinline__ void lds_sort_words(uint64_t (&word)[ITEMS], uint32_t m, const LocalRounds& lr,
+                                               uint64_t* stage, uint32_t (*whist)[256], uint32_t* bexcl,
+                                               uint32_t* wsum) {
+    constexpr int NW = NT / 64, BINS = 256;
+    const int w = wave_id(), l = lane_id();
+    const uint64_t lt = lanemask_lt();
+    const uint32_t jm = (m + NW * 64 - 1) / (NW * 64);
+    const uint32_t wbase = (uint32_t)w * jm * 64;
+    if (lr.n == 0) {   // no bits below the bucket: already in order
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint32_t i = wbase + (uint32_t)j * 64 + l;
+            if ((uint32_t)j < jm && i < m) stage[i] = word[j];
+        }
+        __syncthreads();
+        return;
+    }
+    int dsh = 32;
+    for (int r = 0; r < lr.n; r++) {
+        const int bits = lr.bits[r];
+        if (r > 0) dsh += lr.bits[r - 1];
+        const uint32_t mask = (1u << bits) - 1u;
+        for (int i = threadIdx.x; i < NW * BINS; i += NT) (&whist[0][0])[i] = 0;
+        __syncthreads();
+        uint32_t pos[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            pos[j] = 0;
+            if ((uint32_t)j >= jm) continue;   // wave-uniform
+            const uint32_t i = wbase + (uint32_t)j * 64 + l;
+            const bool ok = i < m;
+            const uint32_t d = (uint32_t)(word[j] >> dsh) & mask;
+            uint64_t peers = __ballot(ok);
+#pragma unroll
+            for (int b = 0; b < 8; b++) {
+                if (b >= bits) break;
+                const bool bit = (d >> b) & 1u;
+                const uint64_t mm = __ballot(bit);
+                peers &= bit ? mm : ~mm;
+            }
+            const int leader = peers ? (__ffsll((unsigned long long)peers) - 1) : 0;
+            uint32_t old = 0;
+            if (ok && l == leader) {
+                old = whist[w][d];
+                whist[w][d] = old + (uint32_t)__popcll(peers);
+            }
+            old = (uint32_t)__shfl((int)old, leader, 64);
+            pos[j] = old + (uint32_t)__popcll(peers & lt);
+        }
+        __syncthreads();
+        uint32_t tot = 0;
+        if (threadIdx.x < BINS) {
+#pragma unroll
+            for (int ww = 0; ww < NW; ww++) {
+                const uint32_t cc = whist[ww][threadIdx.x];
+                whist[ww][threadIdx.x] = tot;
+                tot += cc;
+            }
+        }
+        const uint32_t inc = wave_incl_scan_u32(tot);
+        if (l == 63) wsum[w] = inc;
+        __syncthreads();
+        if (threadIdx.x < BINS) {
+            uint32_t ex = inc - tot;
+            for (int ww = 0; ww < w; ww++) ex += wsum[ww];
+            bexcl[threadIdx.x] = ex;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint32_t i = wbase + (uint32_t)j * 64 + l;
+            if ((uint32_t)j < jm && i < m) {
+                const uint32_t d = (uint32_t)(word[j] >> dsh) & mask;
+                stage[bexcl[d] + whist[w][d] + pos[j]] = word[j];
+            }
+        }
+        __syncthreads();
+        if (r + 1 < lr.n) {
+#pragma unroll
+            for (int j = 0; j < ITEMS; j++) {
+                const uint32_t i = wbase + (uint32_t)j * 64 + l;
+                word[j] = ((uint32_t)j < jm && i < m) ? stage[i] : 0;
+            }
+            __syncthreads();   // every read of stage before the next round writes it
+        }
+    }
+}
+
+constexpr int TJ_NT = 1024, TJ_ITEMS = (TL_CAP + TJ_NT - 1) / TJ_NT;   // 5 words per thread per side
+static_assert(TJ_NT * TJ_ITEMS >= TL_CAP, "a bucket fits the workgroup's registers");
+
+__device__ __forceinline__ uint32_t fld(uint64_t w) { return (uint32_t)(w >> 32); }   // the key field
+
+__global__ void __launch_bounds__(TJ_NT) tl_join_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict__ bsR,
+                                                        const uint64_t* __restrict__ wS, const uint32_t* __restrict__ bsS,
+                                                        LocalRounds lr, uint32_t* __restrict__ matchR,
+                                                        uint32_t* __restrict__ valR, uint32_t* __restrict__ outR,
+                                                        uint32_t* __restrict__ outS, uint64_t cap,
+                                                        uint32_t* __restrict__ flags, uint64_t* status, uint32_t* ticket,
+                                                        uint32_t epoch, uint32_t nb, uint64_t* total_out) {
+    constexpr int NW = TJ_NT / 64;
+    constexpr uint32_t Q = TJ_ITEMS;          // sorted R rows per thread in the walk (consecutive)
+    __shared__ uint64_t sR[TL_CAP];
+    __shared__ uint64_t sS[TL_CAP];
+    __shared__ uint32_t loc[TL_CAP];          // per sorted R row: S run start | run length << 16
+    __shared__ uint32_t roff[TL_CAP];         // per sorted R row: bucket-relative output offset
+    __shared__ uint32_t whist[NW][256];
+    __shared__ uint32_t bexcl[256];
+    __shared__ uint32_t wsum[NW];
+    __shared__ uint64_t s_excl;
+    __shared__ uint32_t s_flag, s_ticket;
+    const uint32_t b = take_ticket(ticket, &s_ticket);   // buckets in order: the lookback cannot deadlock
+    const uint32_t r0 = bsR[b], mR = bsR[b + 1] - r0, s0 = bsS[b], mS = bsS[b + 1] - s0;
+    if (threadIdx.x == 0) s_flag = 0;
+    const int w = wave_id(), l = lane_id();
+    {
+        uint64_t wr[TJ_ITEMS], ws[TJ_ITEMS];   // both buckets' loads in flight before any ranking
+        const uint32_t jmR = (mR + NW * 64 - 1) / (NW * 64), jmS = (mS + NW * 64 - 1) / (NW * 64);
+#pragma unroll
+        for (int j = 0; j < TJ_ITEMS; j++) {
+            const uint32_t iR = (uint32_t)w * jmR * 64 + (uint32_t)j * 64 + l;
+            const uint32_t iS = (uint32_t)w * jmS * 64 + (uint32_t)j * 64 + l;
+            wr[j] = ((uint32_t)j < jmR && iR < mR) ? wR[r0 + iR] : 0;
+            ws[j] = ((uint32_t)j < jmS && iS < mS) ? wS[s0 + iS] : 0;
+        }
+        lds_sort_words<TJ_NT, TJ_ITEMS>(wr, mR, lr, sR, whist, bexcl, wsum);
+        lds_sort_words<TJ_NT, TJ_ITEMS>(ws, mS, lr, sS, whist, bexcl, wsum);
+    }
+    // walk: thread t owns sorted R rows [t*Q, t*Q + Q); its S range from two searches, then one
+    // lower / upper bound pair per row inside that range
+    const uint32_t e0 = threadIdx.x * Q;
+    const uint32_t nv = mR > e0 ? (mR - e0 < Q ? mR - e0 : Q) : 0u;
+    uint32_t cnt[Q], lo[Q], tsum = 0, myflag = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < Q; j++) cnt[j] = lo[j] = 0;
+    if (nv) {
+        const uint32_t kf = fld(sR[e0]), kl = fld(sR[e0 + nv - 1]);
+        uint32_t a = 0, an = mS;
+        while (an) {   // lower_bound(kf)
+            const uint32_t h = an >> 1;
+            if (fld(sS[a + h]) < kf) {
+                a += h + 1;
+                an -= h + 1;
+            } else {
+                an = h;
+            }
+        }
+        uint32_t e = a, en = mS - a;
+        while (en) {   // upper_bound(kl)
+            const uint32_t h = en >> 1;
+            if (fld(sS[e + h]) <= kl) {
+                e += h + 1;
+                en -= h + 1;
+            } else {
+                en = h;
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < Q; j++) {
+            if (j >= nv) continue;
+            const uint32_t key = fld(sR[e0 + j]);
+            uint32_t x = a, xn = e - a;
+            while (xn) {
+                const uint32_t h = xn >> 1;
+                if (fld(sS[x + h]) < key) {
+                    x += h + 1;
+                    xn -= h + 1;
+                } else {
+                    xn = h;
+                }
+            }
+            uint32_t y = x, yn = e - x;
+            while (yn) {
+                const uint32_t h = yn >> 1;
+                if (fld(sS[y + h]) <= key) {
+                    y += h + 1;
+                    yn -= h + 1;
+                } else {
+                    yn = h;
+                }
+            }
+            lo[j] = x;
+            cnt[j] = y - x;
+            tsum += y - x;
+            if (y - x > 1) myflag |= MJF_R_FANOUT;
+            if (y > x && e0 + j + 1 < mR && fld(sR[e0 + j + 1]) == key) myflag |= MJF_S_DUP;
+        }
+    }
+    // block scan of the per-thread pair counts (a bucket's pairs < 2^32: <= TL_CAP^2)
+    const uint32_t inc = wave_incl_scan_u32(tsum);
+    if (l == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t run = inc - tsum, btotal = 0;
+    for (int ww = 0; ww < NW; ww++) {
+        if (ww < w) run += wsum[ww];
+        btotal += wsum[ww];
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < Q; j++) {
+        if (j >= nv) continue;
+        loc[e0 + j] = lo[j] | (cnt[j] << 16);   // both < TL_CAP < 2^16
+        roff[e0 + j] = run;
+        run += cnt[j];
+    }
+    if (w == 0) {
+        lookback_publish(status, epoch, b, btotal);
+        const uint64_t ex = lookback_wait(status, epoch, b, btotal);
+        if (l == 0) {
+            s_excl = ex;
+            if (b == nb - 1) *total_out = ex + btotal;
+            if (ex + btotal > LB_VAL_MASK) atomicOr(flags, MJF_OVF);
+        }
+    }
+    if (myflag) atomicOr(&s_flag, myflag);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_flag) {
+        const uint32_t seen = __hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (s_flag & ~seen) atomicOr(flags, s_flag);
+    }
+    const uint64_t gofs = s_excl;
+    const bool room = gofs + btotal <= cap;
+    // emission: consecutive threads take consecutive sorted R rows, so with fan-out ~1 the
+    // stores of a wave-instruction are consecutive
+    for (uint32_t i = threadIdx.x; i < mR; i += TJ_NT) {
+        const uint32_t v = loc[i], c = v >> 16, s = v & 0xFFFFu;
+        const uint32_t rr = (uint32_t)sR[i];
+        matchR[r0 + i] = c;
+        valR[r0 + i] = rr;
+        if (!room) continue;
+        const uint64_t o = gofs + roff[i];
+        for (uint32_t k = 0; k < c; k++) {
+            outR[o + k] = rr;
+            outS[o + k] = (uint32_t)sS[s + k];
+        }
+    }
+}
+
 // Non-packable pairs (64-bit keys with > 32 varying bits AND a rowid): key and rowid staged
 // separately.  Kept simple: rare in this workload (never in the measured configs).
 template <typename K, bool VIN>
@@ -1104,6 +1356,16 @@ static bool prof_split() {   // tuning aid: QE_PROF_SPLIT=1 times the second pas
     return on;
 }
 
+// QE_FUSED_JOIN=1 (read at every sort): leave the per-bucket step of large two-level sorts to a
+// fused merge (tl_join).  Off by default: measured on MI355X it is SLOWER -- 3.35 ms per
+// 1e8 x 1e8 join against 2.2 ms for two per-bucket sorts + the merge -- because its 137 KiB of
+// LDS (both buckets, per-row runs and offsets) leave one workgroup per CU, so the load, ranking,
+// search and store phases of a bucket never overlap another bucket's.
+static bool fused_on() {
+    const char* s = getenv("QE_FUSED_JOIN");
+    return s && s[0] == '1';
+}
+
 static uint64_t sort_pre_min() {   // tuning knob: QE_SORT_PRE_MIN = smallest n for the lookback-free form
     static uint64_t v = [] {
         const char* s = getenv("QE_SORT_PRE_MIN");
@@ -1123,7 +1385,7 @@ static bool sort_pre_on() {
 // the two-level sort (H = TL_H) with both global passes lookback-free (see tl_hist_tiles_kernel)
 template <typename K>
 static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, uint64_t n, int bits, Field f,
-                               const char* name, SortOut* out) {
+                               const char* name, SortOut* out, bool defer = false) {
     const int L = bits - TL_H;
     const LocalRounds lr = local_rounds(L);
     const uint32_t nt = (uint32_t)((n + RTILE - 1) / RTILE);
@@ -1191,6 +1453,28 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
         release();
         return false;
     }
+    if constexpr (sizeof(K) == 8) {
+        if (defer && fused_on()) {   // the per-bucket step waits for the consumer (tl_join / pairs_need_keys)
+            DeferredSort d;
+            d.words = w2;
+            d.bstart = bstart;
+            d.kout = (uint64_t*)kout;
+            d.vout = vout;
+            d.lo = f.lo;
+            d.L = L;
+            d.fmask = f.fmask;
+            d.kconst = f.kconst;
+            d.lr_n = lr.n;
+            for (int r = 0; r < 4; r++) d.lr_bits[r] = lr.bits[r];
+            c->deferred[kout] = d;
+            dfree(c, w1);
+            dfree(c, tcnt);
+            dfree(c, gcnt);
+            dfree(c, hist);
+            *out = SortOut{kout, vout, true, true};
+            return true;
+        }
+    }
     {
         Timed t(c, "sort_local", 8.0 * n + ((double)sizeof(K) + 4) * n);
         hipLaunchKernelGGL((tl_local_kernel<K, IN_WORD>), dim3(TL_BUCKETS), dim3(TL_NT), 0, c->stream, w2, nullptr,
@@ -1208,12 +1492,12 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
 // inputs whose 256 buckets fit LDS (<= ~1 M keys)
 template <typename K>
 static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint64_t n, int bits, Field f,
-                           const char* name, SortOut* out, int H = TL_H) {
+                           const char* name, SortOut* out, int H = TL_H, bool defer = false) {
     // the lookback-free form saves ~1 us per million keys per pass but adds ~30 us of count
     // scans: it pays from a few 10^7 keys (measured on MI355X: C3's 0.5-1e8-key sorts 2 % faster,
     // the C4 batch's 1-10 M-key sorts slower)
     if (H == TL_H && sort_pre_on() && n >= sort_pre_min())
-        return sort_two_level_pre<K>(c, keys, vals, n, bits, f, name, out);
+        return sort_two_level_pre<K>(c, keys, vals, n, bits, f, name, out, defer);
     const int L = bits - H;   // low bits sorted in LDS (<= 24)
     const LocalRounds lr = local_rounds(L);
     uint32_t* hist = dalloc_t<uint32_t>(c, TL_BUCKETS);
@@ -1354,7 +1638,7 @@ static SortOut sort_kv_unpacked(qe_ctx* c, const K* keys, const uint32_t* vals, 
 
 template <typename K>
 static SortOut radix_sort_impl(qe_ctx* c, const K* keys, const uint32_t* vals, uint64_t n, bool with_vals,
-                               const char* name, const uint64_t* bits) {
+                               const char* name, const uint64_t* bits, bool defer = false) {
     SortOut so{(void*)keys, (uint32_t*)vals, false, false};
     if (n < 2) return so;
     if (n >= 0xFFFFFFFFull) throw Error(QE_EINVAL, "sort input too large");
@@ -1399,7 +1683,7 @@ static SortOut radix_sort_impl(qe_ctx* c, const K* keys, const uint32_t* vals, u
         }
         if (two_level_on() && nb >= 20 && nb <= TL_H + 16 && n >= (1u << 20) && n <= 4000ull * TL_BUCKETS) {
             SortOut so2;
-            if (sort_two_level<K>(c, keys, vals, n, nb, f, name, &so2)) return so2;
+            if (sort_two_level<K>(c, keys, vals, n, nb, f, name, &so2, TL_H, defer)) return so2;
         }
         switch (width <= 8 ? 8 : width) {
         case 8: return sort_packed<K, 8>(c, keys, vals, n, pd, f, name);
@@ -1417,13 +1701,111 @@ static SortOut radix_sort_impl(qe_ctx* c, const K* keys, const uint32_t* vals, u
 }
 
 SortOut radix_sort_u64(qe_ctx* c, const uint64_t* keys, const uint32_t* vals, uint64_t n, bool with_vals,
-                       const uint64_t* bits) {
+                       const uint64_t* bits, bool defer) {
     return radix_sort_impl<uint64_t>(c, keys, vals, n, with_vals, with_vals ? "sort_pass_k64v32" : "sort_pass_k64",
-                                     bits);
+                                     bits, defer && with_vals);
 }
 
 SortOut radix_sort_u32(qe_ctx* c, const uint32_t* keys, const uint32_t* vals, uint64_t n, const uint64_t* bits) {
     return radix_sort_impl<uint32_t>(c, keys, vals, n, true, "sort_pass_k32v32", bits);
+}
+
+static LocalRounds rounds_of(const DeferredSort& d) {
+    LocalRounds lr{d.lr_n, {d.lr_bits[0], d.lr_bits[1], d.lr_bits[2], d.lr_bits[3]}};
+    return lr;
+}
+
+static void drop(qe_ctx* c, const DeferredSort& d) {
+    dfree(c, d.words);
+    dfree(c, d.bstart);
+}
+
+void pairs_need_keys(qe_ctx* c, const qe_pairs* p) {
+    if (!p || !p->key) return;
+    auto it = c->deferred.find(p->key);
+    if (it == c->deferred.end()) return;
+    const DeferredSort d = it->second;
+    c->deferred.erase(it);
+    const Field f{d.lo, d.fmask, d.kconst};
+    {
+        Timed t(c, "sort_local", 8.0 * p->n + 12.0 * p->n);
+        hipLaunchKernelGGL((tl_local_kernel<uint64_t, IN_WORD>), dim3(TL_BUCKETS), dim3(TL_NT), 0, c->stream, d.words,
+                           nullptr, nullptr, d.kout, d.vout, d.bstart, 0u, f, rounds_of(d));
+        QE_HIP(hipGetLastError());
+    }
+    drop(c, d);
+}
+
+void pairs_need_vals(qe_ctx* c, const qe_pairs* p) {
+    if (!p || !p->key) return;
+    auto it = c->deferred.find(p->key);
+    if (it != c->deferred.end() && it->second.val_ready) return;
+    pairs_need_keys(c, p);
+}
+
+void pairs_drop_deferred(qe_ctx* c, const qe_pairs* p) {
+    if (!p || !p->key) return;
+    auto it = c->deferred.find(p->key);
+    if (it == c->deferred.end()) return;
+    drop(c, it->second);
+    c->deferred.erase(it);
+}
+
+bool tl_join(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS, uint32_t* oflags) {
+    auto iR = c->deferred.find(R->key), iS = c->deferred.find(S->key);
+    if (iR == c->deferred.end() || iS == c->deferred.end() || R->key == S->key) return false;
+    DeferredSort& dR = iR->second;
+    const DeferredSort& dS = iS->second;
+    if (dR.lo != dS.lo || dR.L != dS.L || dR.fmask != dS.fmask || dR.kconst != dS.kconst ||
+        dR.lr_n != dS.lr_n)
+        return false;   // different bucket geometry
+    const uint64_t nR = R->n, nS = S->n;
+    if (!R->match) {
+        R->match = dalloc_t<uint32_t>(c, nR);
+        R->owns |= 4;
+    }
+    const uint64_t cap = nR + nS;
+    uint32_t* oR = dalloc_t<uint32_t>(c, cap);
+    uint32_t* oS = dalloc_t<uint32_t>(c, cap);
+    uint32_t* d_flags = (uint32_t*)(c->d_scratch + 16);
+    QE_HIP(hipMemsetAsync(d_flags, 0, 4, c->stream));
+    {
+        LBSlot s = lb_acquire(c, TL_BUCKETS);
+        // algorithmic bytes: both sides' words in, R's match + rowid out (+ 8 B per pair below)
+        Timed t(c, "tl_join", 8.0 * (double)(nR + nS) + 8.0 * (double)nR);
+        hipLaunchKernelGGL(tl_join_kernel, dim3(TL_BUCKETS), dim3(TJ_NT), 0, c->stream, dR.words, dR.bstart, dS.words,
+                           dS.bstart, rounds_of(dR), R->match, dR.vout, oR, oS, cap, d_flags, s.status, s.ticket,
+                           s.epoch, (uint32_t)TL_BUCKETS, c->d_scratch + 17);
+        QE_HIP(hipGetLastError());
+    }
+    uint64_t h[2];
+    read_words(c, c->d_scratch + 16, h, 2);
+    const uint32_t fl = (uint32_t)h[0];
+    const uint64_t P = h[1];
+    if (P > cap || (fl & MJF_OVF)) {   // outgrew the optimistic buffers: the caller merges as usual
+        dfree(c, oR);
+        dfree(c, oS);
+        return false;
+    }
+    if (c->prof && !c->pending.empty()) c->pending.back().bytes += 8.0 * (double)P;
+    dR.val_ready = true;
+    R->flags |= QE_PAIRS_MATCHED;
+    *oflags = fl;
+    outR->n = outS->n = P;
+    if (P > c->mat_limit) {   // R->match stays valid: the caller may take the aggregate form
+        dfree(c, oR);
+        dfree(c, oS);
+        outR->d = outS->d = nullptr;
+        outR->cap = outS->cap = 0;
+        char msg[160];
+        snprintf(msg, sizeof msg, "merge join of %llu pairs exceeds the materialisation limit %llu",
+                 (unsigned long long)P, (unsigned long long)c->mat_limit);
+        throw Error(QE_ETOOBIG, msg);
+    }
+    outR->d = oR;
+    outS->d = oS;
+    outR->cap = outS->cap = cap;
+    return true;
 }
 
 }  // namespace qe

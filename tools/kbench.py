@@ -96,6 +96,7 @@ def main():
         R = ctx.gather_pairs(ctx.column(r0, 1), None)
         ctx.sort_pairs(R)
         rows = lib.List()
+        ctx.is_sorted(R)           # completes a deferred sort before its rowids are read directly
         rows.d, rows.n, rows.cap = R.val, R.n, R.n
         for rep in range(a.reps):
             p = ctx.gather_pairs(ctx.column(r1, 1), rows)
