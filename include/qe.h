@@ -175,6 +175,9 @@ int qe_join_payloads_multi(qe_ctx*, const uint32_t* d_counts, uint64_t rows, con
                            const qe_list* const* edits, int nedits, qe_list* outs);
 /* a12: print_sums' inner loop (src/utilities.c:216-219): sum of col[rowid] mod 2^64. */
 int qe_checksum(qe_ctx*, qe_col col, const qe_list* rows, uint64_t* sum);
+/* print_sums' whole select loop (src/utilities.c:199-221) for n (column, list) pairs: every sum
+ * is computed before one host round trip; sums[k] = qe_checksum(cols[k], rows[k]). */
+int qe_checksums(qe_ctx*, int n, const qe_col* cols, const qe_list* const* rows, uint64_t* sums);
 /* a12 over an unmaterialised join side: sum of col[p->val[i]] * p->match[i] mod 2^64, which is
  * qe_checksum over the list qe_merge_join would have produced for that side
  * (sum_pairs col(pR) = sum_k (sum_{r in R_k} col(r)) * |S_k|). */

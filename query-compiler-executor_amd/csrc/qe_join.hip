@@ -1758,6 +1758,29 @@ int qe_checksum(qe_ctx* c, qe_col col, const qe_list* rows, uint64_t* sum) {
     QE_API_END(c)
 }
 
+int qe_checksums(qe_ctx* c, int n, const qe_col* cols, const qe_list* const* rows, uint64_t* sums) {
+    QE_API_BEGIN(c)
+    if (n < 0) throw Error(QE_EINVAL, "n");
+    for (int k0 = 0; k0 < n; k0 += 32) {   // 32 sums per round trip (the pinned scratch holds 64 words)
+        const int m = std::min(32, n - k0);
+        unsigned long long* d = (unsigned long long*)dalloc_t<uint64_t>(c, 32);
+        QE_HIP(hipMemsetAsync(d, 0, 32 * 8, c->stream));
+        for (int k = 0; k < m; k++) {
+            const qe_list* r = rows[k0 + k];
+            const uint64_t len = r ? r->n : cols[k0 + k].n;
+            if (!len) continue;
+            Timed t(c, "checksum", r ? 12.0 * len : 8.0 * len);
+            hipLaunchKernelGGL(checksum_kernel, dim3(grid_for(len, 256 * 16, 8192)), dim3(256), 0, c->stream,
+                               cols[k0 + k].d, r ? r->d : nullptr, len, d + k);
+            QE_HIP(hipGetLastError());
+        }
+        read_words(c, (const uint64_t*)d, sums + k0, m);
+        dfree(c, d);
+    }
+    return 0;
+    QE_API_END(c)
+}
+
 }  // extern "C"
 
 #ifdef QE_DIAG_STAMPS

@@ -525,11 +525,37 @@ static void print_sums(exec_t* x, const query_t* q, const mra_t* M) {
         exists_t e0 = relation_exists(M, q->rels[q->sel[0]], q->sel[0]);
         if (e0.idx != -1) qe_set_last_result_rows(x->q, M->v[e0.ent]->e[e0.idx].list->n);
     }
+    /* the plain sums of the selects before the first missing binding are computed together (one
+     * host round trip); the line is then printed in order exactly as the loop below prints it */
+    size_t nb = 0;
+    qe_col* bc = (qe_col*)calloc(q->nsel ? q->nsel : 1, sizeof(qe_col));
+    const qe_list** bl = (const qe_list**)calloc(q->nsel ? q->nsel : 1, sizeof(qe_list*));
+    uint64_t* bs = (uint64_t*)calloc(q->nsel ? q->nsel : 1, sizeof(uint64_t));
+    for (size_t i = 0; i < q->nsel; i++) {
+        uint64_t b = q->sel[2 * i], colno = q->sel[2 * i + 1];
+        exists_t ex = relation_exists(M, q->rels[b], b);
+        if (ex.idx == -1) break;
+        const qe_list* l = M->v[ex.ent]->e[ex.idx].list;
+        if (l->n == 0 || (l->flags & (QE_LIST_AGG | QE_LIST_DEAD))) continue;
+        if (qe_relation_column(x->q, (int)q->rels[b], (int)colno, &bc[nb]) != 0) break;   /* fails in order below */
+        bl[nb++] = l;
+    }
+    int brc = nb ? qe_checksums(x->q, (int)nb, bc, bl, bs) : 0;
+    free(bc);
+    free(bl);
+    if (brc != 0) {
+        free(bs);
+        chk(x, brc);
+    }
+    size_t k = 0;
     for (size_t i = 0; i < q->nsel; i++) {
         uint64_t b = q->sel[2 * i], colno = q->sel[2 * i + 1];
         uint32_t relation = q->rels[b];
         exists_t ex = relation_exists(M, relation, b);
-        if (ex.idx == -1) fail(x, QE_EEXIT, "Something went really wrong...");
+        if (ex.idx == -1) {
+            free(bs);
+            fail(x, QE_EEXIT, "Something went really wrong...");
+        }
         const qe_list* l = M->v[ex.ent]->e[ex.idx].list;
         if (l->n == 0) {
             fputs("NULL ", x->out);
@@ -540,6 +566,9 @@ static void print_sums(exec_t* x, const query_t* q, const mra_t* M) {
                 if (x->aggs[a].l == l) agg = &x->aggs[a].p;
             if (agg) {
                 chk(x, qe_checksum_weighted(x->q, column(x, relation, colno), agg, &s));
+            } else if (!(l->flags & (QE_LIST_AGG | QE_LIST_DEAD)) && k < nb) {
+                (void)column(x, relation, colno);   /* the same validation, at its place in the line */
+                s = bs[k++];
             } else {
                 need_data(x, l);
                 chk(x, qe_checksum(x->q, column(x, relation, colno), l, &s));
@@ -547,6 +576,7 @@ static void print_sums(exec_t* x, const query_t* q, const mra_t* M) {
             fprintf(x->out, "%lu ", (unsigned long)s);
         }
     }
+    free(bs);
     fputc('\n', x->out);
 }
 

@@ -88,6 +88,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
                                        C.POINTER(List)]),
         "qe_relation_column_bits": (I, [P, I, I, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "qe_checksum": (I, [P, Col, C.POINTER(List), C.POINTER(C.c_uint64)]),
+        "qe_checksums": (I, [P, I, C.POINTER(Col), C.POINTER(C.POINTER(List)), C.POINTER(C.c_uint64)]),
         "qe_checksum_weighted": (I, [P, Col, C.POINTER(Pairs), C.POINTER(C.c_uint64)]),
         "qe_merge_join_counts": (I, [P, C.POINTER(Pairs), C.POINTER(Pairs), C.POINTER(C.c_uint64)]),
         "qe_set_materialize_limit": (I, [P, U64]),
