@@ -71,6 +71,15 @@ struct DeferredSort {
     bool val_ready = false;       // vout already holds the sorted rowids (written by tl_join)
 };
 
+// The two-level sort's histogram, computed while the keys were gathered (gather_with_hist): the
+// sort of those keys skips its histogram read.  Kept by the pairs' key buffer.
+struct PreHist {
+    uint32_t* tcnt = nullptr;   // per first-pass tile digit counts
+    uint32_t* gcnt = nullptr;   // per (digit, group) segment digit counts
+    int lo = 0, L = 0;
+    uint64_t fmask = 0;
+};
+
 }  // namespace qe
 
 struct qe_ctx {
@@ -114,6 +123,7 @@ struct qe_ctx {
 
     // two-level sorts awaiting their per-bucket step, by the pairs' key buffer
     std::unordered_map<const void*, qe::DeferredSort> deferred;
+    std::unordered_map<const void*, qe::PreHist> prehist;
 
     // profiling
     bool prof = false;
@@ -187,7 +197,11 @@ SortOut radix_sort_u64(qe_ctx* c, const uint64_t* keys, const uint32_t* vals /*n
 // or the output outgrew nR + nS -- the caller completes both sorts and merges as usual)
 void pairs_need_keys(qe_ctx* c, const qe_pairs* p);
 void pairs_need_vals(qe_ctx* c, const qe_pairs* p);
-void pairs_drop_deferred(qe_ctx* c, const qe_pairs* p);
+void pairs_drop_deferred(qe_ctx* c, const qe_pairs* p);   // (also drops a gathered histogram)
+// keys = col[rows] for a list whose sort will be the lookback-free two-level one: the sort's
+// histogram is built in the same pass (false: not that sort -- the caller gathers plainly)
+bool gather_with_hist(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint64_t n, uint64_t kor, uint64_t kand,
+                      uint64_t* keys);
 bool tl_join(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS, uint32_t* oflags);
 SortOut radix_sort_u32(qe_ctx* c, const uint32_t* keys, const uint32_t* vals, uint64_t n,
                        const uint64_t* bits = nullptr);

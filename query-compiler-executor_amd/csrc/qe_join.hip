@@ -1499,7 +1499,10 @@ int qe_gather_pairs(qe_ctx* c, qe_col col, const qe_list* rows, qe_pairs* out) {
     for (auto& r : c->rels)
         for (size_t j = 0; j < r.cols.size(); j++)
             if (r.cols[j] == col.d && r.rows == col.n && j < r.kor.size() && !getenv("QE_GATHER_EXACT_BITS")) {
-                if (n) {
+                if (n && !(getenv("QE_GATHER_HIST") && getenv("QE_GATHER_HIST")[0] == '0') &&
+                    gather_with_hist(c, col.d, rows->d, n, r.kor[j], r.kand[j], out->key)) {
+                    // gathered together with the histogram its sort will read
+                } else if (n) {
                     Timed t(c, "gather_keys", 12.0 * n + 8.0 * n);
                     hipLaunchKernelGGL(gather_keys_kernel<false>, dim3(grid_for((n + 3) / 4, 256, 4096)), dim3(256), 0,
                                        c->stream, col.d, rows->d, n, out->key, (unsigned long long*)nullptr);
@@ -1535,6 +1538,7 @@ int qe_sort_pairs(qe_ctx* c, qe_pairs* p) {
     uint64_t bits[2] = {p->kor, p->kand};
     SortOut so = radix_sort_u64(c, p->key, p->val, p->n, true, (p->flags & QE_PAIRS_BITS) ? bits : nullptr, true);
     if (so.keys_new) {
+        pairs_drop_deferred(c, p);   // a gathered histogram the sort did not take dies with the keys
         if (p->owns & 1) dfree(c, p->key);
         p->key = (uint64_t*)so.keys;
         p->owns |= 1;

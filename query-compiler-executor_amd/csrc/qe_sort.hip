@@ -639,6 +639,58 @@ __global__ void __launch_bounds__(1024) tl_hist_tiles_kernel(const K* __restrict
         if (h[i]) atomicAdd(&gcnt[((uint64_t)(i >> 7) * G + g) * 128 + (i & 127)], h[i]);
 }
 
+// tl_hist_tiles_kernel fused into the gather that produces the keys: keys = col[rows] in list
+// order, and the same per-tile / per-segment counts (one pass instead of a gather + a re-read)
+__global__ void __launch_bounds__(1024) tl_gather_hist_kernel(const uint64_t* __restrict__ col,
+                                                              const uint32_t* __restrict__ rows, uint64_t n,
+                                                              uint64_t* __restrict__ keys, Field f, int L, uint32_t nt,
+                                                              uint32_t G, uint32_t Q, uint32_t* __restrict__ tcnt,
+                                                              uint32_t* __restrict__ gcnt) {
+    __shared__ uint32_t h[TL_BUCKETS];
+    __shared__ uint32_t th[2][256];
+    for (int i = threadIdx.x; i < TL_BUCKETS; i += 1024) h[i] = 0;
+    if (threadIdx.x < 512) (&th[0][0])[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t g = blockIdx.x / Q, q = blockIdx.x % Q;
+    const uint32_t t_end = (g + 1) * TL_TPG < nt ? (g + 1) * TL_TPG : nt;
+    uint32_t prev = 0, par = 0;
+    for (uint32_t t = g * TL_TPG + q; t < t_end; t += Q, par ^= 1u) {
+        const uint64_t base = (uint64_t)t * RTILE;
+        uint32_t r[8];
+        uint64_t k[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint64_t i = base + (uint64_t)j * 1024 + threadIdx.x;
+            r[j] = i < n ? rows[i] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {   // 8 random gathers in flight per thread
+            const uint64_t i = base + (uint64_t)j * 1024 + threadIdx.x;
+            k[j] = i < n ? col[r[j]] : 0;
+        }
+        if (t != g * TL_TPG + q && threadIdx.x < 256) {
+            tcnt[(uint64_t)prev * 256 + threadIdx.x] = th[par ^ 1u][threadIdx.x];
+            th[par ^ 1u][threadIdx.x] = 0;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint64_t i = base + (uint64_t)j * 1024 + threadIdx.x;
+            if (i < n) {
+                keys[i] = k[j];
+                const uint32_t b = (uint32_t)((((k[j] >> f.lo) & f.fmask) >> L) & (TL_BUCKETS - 1));
+                atomicAdd(&h[((b & 255u) << 7) | (b >> 8)], 1u);
+                atomicAdd(&th[par][b & 255u], 1u);
+            }
+        }
+        __syncthreads();
+        prev = t;
+    }
+    if (g * TL_TPG + q < t_end && threadIdx.x < 256) tcnt[(uint64_t)prev * 256 + threadIdx.x] = th[par ^ 1u][threadIdx.x];
+    __syncthreads();
+    for (int i = threadIdx.x; i < TL_BUCKETS; i += 1024)
+        if (h[i]) atomicAdd(&gcnt[((uint64_t)(i >> 7) * G + g) * 128 + (i & 127)], h[i]);
+}
+
 // the bucket histogram in natural order (bucket = d2 << 8 | d1) from the segment counts
 __global__ void __launch_bounds__(128) tl_gsum_kernel(const uint32_t* __restrict__ gcnt, uint32_t G,
                                                       uint32_t* __restrict__ hist) {
@@ -1405,11 +1457,23 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
         dfree(c, hist);
         dfree(c, bstart);
     };
-    QE_HIP(hipMemsetAsync(gcnt, 0, (size_t)nseg * 128 * sizeof(uint32_t), c->stream));
+    auto ph = c->prehist.find(keys);   // counted while the keys were gathered?
+    const bool have = ph != c->prehist.end() && ph->second.lo == f.lo && ph->second.L == L &&
+                      ph->second.fmask == f.fmask;
+    if (have) {
+        dfree(c, tcnt);
+        dfree(c, gcnt);
+        tcnt = ph->second.tcnt;
+        gcnt = ph->second.gcnt;
+        c->prehist.erase(ph);
+    } else {
+        QE_HIP(hipMemsetAsync(gcnt, 0, (size_t)nseg * 128 * sizeof(uint32_t), c->stream));
+    }
     {
-        Timed t(c, "sort_hist", (double)sizeof(K) * n);
-        hipLaunchKernelGGL((tl_hist_tiles_kernel<K>), dim3(G * Q), dim3(1024), 0, c->stream, keys, n, f, L, nt, G, Q,
-                           tcnt, gcnt);
+        Timed t(c, "sort_hist", have ? 0.0 : (double)sizeof(K) * n);
+        if (!have)
+            hipLaunchKernelGGL((tl_hist_tiles_kernel<K>), dim3(G * Q), dim3(1024), 0, c->stream, keys, n, f, L, nt, G,
+                               Q, tcnt, gcnt);
         QE_HIP(hipGetLastError());
         hipLaunchKernelGGL(tl_gsum_kernel, dim3(256), dim3(128), 0, c->stream, gcnt, G, hist);
         QE_HIP(hipGetLastError());
@@ -1745,10 +1809,54 @@ void pairs_need_vals(qe_ctx* c, const qe_pairs* p) {
 
 void pairs_drop_deferred(qe_ctx* c, const qe_pairs* p) {
     if (!p || !p->key) return;
+    auto ph = c->prehist.find(p->key);   // gathered with a histogram but never sorted (a scan join)
+    if (ph != c->prehist.end()) {
+        dfree(c, ph->second.tcnt);
+        dfree(c, ph->second.gcnt);
+        c->prehist.erase(ph);
+    }
     auto it = c->deferred.find(p->key);
     if (it == c->deferred.end()) return;
     drop(c, it->second);
     c->deferred.erase(it);
+}
+
+bool gather_with_hist(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint64_t n, uint64_t kor, uint64_t kand,
+                      uint64_t* keys) {
+    // exactly the plan radix_sort_impl will choose for these keys and bounds: the packed
+    // two-level sort in its lookback-free form
+    if (n < 2 || n >= 0xFFFFFFFFull) return false;
+    const uint64_t vary = kor & ~kand;
+    if (!vary) return false;
+    const int lo = __builtin_ctzll(vary), hi = 64 - __builtin_clzll(vary), nb = hi - lo;
+    if (nb > 32 || !two_level_on() || n <= (uint64_t)TL_CAP) return false;
+    if (nb >= 12 && nb <= 8 + 24 && n <= 700000) return false;
+    if (!(nb >= 20 && nb <= TL_H + 16 && n >= (1u << 20) && n <= 4000ull * TL_BUCKETS)) return false;
+    if (!sort_pre_on() || n < sort_pre_min()) return false;
+    const uint64_t fmask = (1ull << nb) - 1;
+    const Field f{lo, fmask, kand & ~(fmask << lo)};
+    const int L = nb - TL_H;
+    const uint32_t nt = (uint32_t)((n + RTILE - 1) / RTILE);
+    const uint32_t G = (nt + TL_TPG - 1) / TL_TPG;
+    const uint32_t Q = G >= 256 ? 1u : 256u / G;
+    const uint32_t nseg = 256u * G;
+    uint32_t* tcnt = dalloc_t<uint32_t>(c, (size_t)nt * 256);
+    uint32_t* gcnt = dalloc_t<uint32_t>(c, (size_t)nseg * 128);
+    QE_HIP(hipMemsetAsync(gcnt, 0, (size_t)nseg * 128 * sizeof(uint32_t), c->stream));
+    {
+        Timed t(c, "gather_keys", 12.0 * n + 8.0 * n);
+        hipLaunchKernelGGL(tl_gather_hist_kernel, dim3(G * Q), dim3(1024), 0, c->stream, col, rows, n, keys, f, L, nt, G,
+                           Q, tcnt, gcnt);
+        QE_HIP(hipGetLastError());
+    }
+    PreHist ph;
+    ph.tcnt = tcnt;
+    ph.gcnt = gcnt;
+    ph.lo = lo;
+    ph.L = L;
+    ph.fmask = fmask;
+    c->prehist[keys] = ph;
+    return true;
 }
 
 bool tl_join(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS, uint32_t* oflags) {

@@ -446,3 +446,31 @@ def test_load_relation_staged_round_trip(ctx):
         np.testing.assert_array_equal(got, want)
     kor, kand = ctx.column_bits(rel, 1)
     assert kor == int(np.bitwise_or.reduce(b)) and kand == int(np.bitwise_and.reduce(b))
+
+
+def test_gather_with_histogram_then_sort(ctx):
+    """a gathered list of >= 2^25 rowids whose sort is the lookback-free two-level one: the gather
+    also builds that sort's histogram (tl_gather_hist_kernel); sorted (key, rowid) must equal the
+    stable numpy sort.  A gathered-but-never-sorted side (freed) must leave nothing behind."""
+    n = (1 << 25) + 12_345
+    rng = np.random.default_rng(21)
+    colv = rng.integers(0, 100_000_000, 50_000_000, dtype=np.uint64)
+    col = _col(ctx, colv)
+    rows = rng.integers(0, len(colv), n, dtype=np.uint32)      # duplicates: fan-out like a join output
+    lst = ctx.list_from_host(rows)
+    p = ctx.gather_pairs(col, lst)
+    ctx.pairs_free(p)                                          # histogram dropped with the keys
+    ctx.set_profiling(True)
+    ctx.reset_stats()
+    p = ctx.gather_pairs(col, lst)
+    ctx.sort_pairs(p)
+    hist_launches = ctx.kernel_stats().get("sort_hist", {})
+    ctx.set_profiling(False)
+    gk, gv = ctx.pairs_to_host(p)
+    k = colv[rows]
+    order = np.argsort(k, kind="stable")
+    np.testing.assert_array_equal(gk, k[order])
+    np.testing.assert_array_equal(gv, rows[order])
+    assert hist_launches.get("alg_bytes", 0) == 0              # the sort read no histogram of its own
+    ctx.pairs_free(p)
+    ctx.list_free(lst)
