@@ -132,6 +132,10 @@ using MJShared64 = MJSharedG<uint64_t, 2 * MJ_TILE>;
 #define QE_MJ32_OUTCAP 2816
 #endif
 using MJShared32 = MJSharedG<uint32_t, QE_MJ32_OUTCAP>;
+// 2176 = 1.0625 pairs per R row: 26.0 KiB, SIX workgroups per CU -- for |S| <= |R|, where the mean
+// fan-out per R row is at most ~1 (C3's joins: 3.19 -> 3.00 ms per query, same-box A/B); a tile
+// with more pairs takes the binary-search emission
+using MJShared32s = MJSharedG<uint32_t, 2176>;
 
 // bank swizzle of the S window for the key width (sw64: u64 slots, sw32: u32 slots)
 template <typename KT>
@@ -1196,7 +1200,11 @@ void merge_sorted(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_l
         // 32-bit tile offsets when R's keys vary only below bit 32 (known from the producer's
         // OR / AND): every key a tile compares then differs from its first R key by < 2^32
         const bool key32 = (R->flags & QE_PAIRS_BITS) && ((R->kor & ~R->kand) >> 32) == 0;
-        if (key32)
+        if (key32 && nS <= nR)
+            hipLaunchKernelGGL(mj_fused<MJShared32s>, dim3(nt), dim3(MJB), 0, c->stream, R->key, R->val, nR, S->key,
+                               S->val, nS, win, tc, R->match, oR, oS, cap, d_flags, s.status, s.ticket, s.epoch, nt,
+                               c->d_scratch + 17, heavy, (uint32_t*)(c->d_scratch + 19));
+        else if (key32)
             hipLaunchKernelGGL(mj_fused<MJShared32>, dim3(nt), dim3(MJB), 0, c->stream, R->key, R->val, nR, S->key,
                                S->val, nS, win, tc, R->match, oR, oS, cap, d_flags, s.status, s.ticket, s.epoch, nt,
                                c->d_scratch + 17, heavy, (uint32_t*)(c->d_scratch + 19));
