@@ -590,7 +590,10 @@ __global__ void __launch_bounds__(TL_NT) tl_local_kernel(const uint64_t* __restr
 // starts at tcnt[g * TL_TPG][d1]; pass 2 gives every segment a workgroup that places its keys of
 // digit d2 from gcnt[s][d2] on -- again without a lookback.  Segments average RTILE keys
 // (TL_TPG tiles x RTILE keys / 256 digits), and a larger one is walked in sub-tiles.
-constexpr uint32_t TL_TPG = 256;
+#ifndef QE_TL_TPG
+#define QE_TL_TPG 256
+#endif
+constexpr uint32_t TL_TPG = QE_TL_TPG;   // first-pass tiles per group
 static_assert(RTILE == 8192, "tl_hist_tiles_kernel counts 8192-key first-pass tiles (1024 threads x 8)");
 
 template <typename K>
