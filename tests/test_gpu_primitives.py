@@ -474,3 +474,28 @@ def test_gather_with_histogram_then_sort(ctx):
     assert hist_launches.get("alg_bytes", 0) == 0              # the sort read no histogram of its own
     ctx.pairs_free(p)
     ctx.list_free(lst)
+
+
+@pytest.mark.parametrize("n", [3_000_000, (1 << 25) + 999])
+def test_sort_pairs_crowded_buckets(ctx, n):
+    """crowded buckets of ~5000 words (the per-bucket LDS sort's capacity is 5120), with the
+    two-level sort's lookback (3 M) and lookback-free (2^25) global passes.  (A four-per-CU
+    per-bucket variant capped at 4480 words plus a second launch for larger buckets measured
+    0.75 ms SLOWER per C3 query, so there is one 5120-word variant.)"""
+    rng = np.random.default_rng(n)
+    k = rng.integers(0, 1 << 27, n, dtype=np.uint64)      # 27 varying bits: bucket = key >> 12
+    for b in (7, 1000, 20000):
+        cur = int(np.count_nonzero((k >> np.uint64(12)) == np.uint64(b)))
+        extra = 5000 - cur
+        idx = rng.choice(n, extra, replace=False)
+        k[idx] = (np.uint64(b) << np.uint64(12)) | rng.integers(0, 4096, extra, dtype=np.uint64)
+    sizes = np.bincount((k >> np.uint64(12)).astype(np.int64))
+    assert 4480 < sizes.max() <= 5120
+    v = rng.permutation(n).astype(np.uint32)
+    p = ctx.pairs_from_host(k, v)
+    ctx.sort_pairs(p)
+    gk, gv = ctx.pairs_to_host(p)
+    order = np.argsort(k, kind="stable")
+    np.testing.assert_array_equal(gk, k[order])
+    np.testing.assert_array_equal(gv, v[order])
+    ctx.pairs_free(p)
