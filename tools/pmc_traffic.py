@@ -41,7 +41,7 @@ STAGES = [
     (r"mj_fused", "mj_fused"),
     (r"mj_partition", "mj_partition"),
     (r"mj_tile<1>", "mj_write"),
-    (r"gather_keys_kernel", "gather_keys"),
+    (r"gather_keys_kernel|tl_gather_hist_kernel", "gather_keys"),
     (r"expand_kernel<1>", "payload_expand"),
     (r"expand_kernel<0>|tile_scan_kernel", "payload_count"),
     (r"NonzeroPairsOp", "payload_prune"),
