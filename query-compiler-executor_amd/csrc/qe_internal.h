@@ -113,6 +113,7 @@ struct qe_ctx {
     // small device scratch + pinned host mirror for scalar results
     uint64_t* d_scratch = nullptr;   // 64 words
     uint64_t* h_scratch = nullptr;   // pinned, 64 words
+    hipEvent_t wait_ev = nullptr;    // polled for scalar results (read_u64 / read_words)
 
     // loader (qe_load_relation): pinned staging ring for pageable host columns
     static constexpr int STAGE_SLOTS = 3;

@@ -154,15 +154,36 @@ Timed::~Timed() {
 
 void sync(qe_ctx* c) { QE_HIP(hipStreamSynchronize(c->stream)); }
 
+// Wait for a scalar result the host needs to go on (a list length, a pair count, a sum): the
+// host polls an event instead of sleeping in hipStreamSynchronize, so the next launches follow
+// the result by a few microseconds (the trace showed ~22 us between such a read and the next
+// kernel, ~16 of them per C3 query).  QE_SPIN_WAIT=0 restores the blocking wait.
+static void wait_result(qe_ctx* c) {
+    static const bool spin = [] {
+        const char* s = getenv("QE_SPIN_WAIT");
+        return !(s && s[0] == '0');
+    }();
+    if (!spin) {
+        QE_HIP(hipStreamSynchronize(c->stream));
+        return;
+    }
+    if (!c->wait_ev) QE_HIP(hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming));
+    QE_HIP(hipEventRecord(c->wait_ev, c->stream));
+    hipError_t e;
+    while ((e = hipEventQuery(c->wait_ev)) == hipErrorNotReady) {
+    }
+    QE_HIP(e);
+}
+
 uint64_t read_u64(qe_ctx* c, const uint64_t* d) {
     QE_HIP(hipMemcpyAsync(c->h_scratch, d, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
-    QE_HIP(hipStreamSynchronize(c->stream));
+    wait_result(c);
     return c->h_scratch[0];
 }
 
 void read_words(qe_ctx* c, const uint64_t* d, uint64_t* h, int n) {
     QE_HIP(hipMemcpyAsync(c->h_scratch, d, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
-    QE_HIP(hipStreamSynchronize(c->stream));
+    wait_result(c);
     memcpy(h, c->h_scratch, n * sizeof(uint64_t));
 }
 
@@ -410,6 +431,7 @@ void qe_fini(qe_ctx* c) {
     if (c->lb_tickets) (void)hipFree(c->lb_tickets);
     if (c->d_scratch) (void)hipFree(c->d_scratch);
     if (c->h_scratch) (void)hipHostFree(c->h_scratch);
+    if (c->wait_ev) (void)hipEventDestroy(c->wait_ev);
     for (int k = 0; k < qe_ctx::STAGE_SLOTS; k++) {
         if (c->h_stage[k]) (void)hipHostFree(c->h_stage[k]);
         if (c->stage_ev[k]) (void)hipEventDestroy(c->stage_ev[k]);
