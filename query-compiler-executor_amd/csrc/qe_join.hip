@@ -56,10 +56,16 @@ __device__ __forceinline__ uint64_t upper_bound_f(uint64_t lo, uint64_t hi, uint
     return lo;
 }
 
+// zero_a / zero_b (nullable): result words of the merge that follows, cleared here instead of by
+// two memset launches
 __global__ void __launch_bounds__(256) mj_partition(const uint64_t* __restrict__ rk, uint64_t nR,
                                                     const uint64_t* __restrict__ sk, uint64_t nS, uint32_t ntiles,
-                                                    uint64_t* __restrict__ win) {
+                                                    uint64_t* __restrict__ win, uint64_t* zero_a, uint64_t* zero_b) {
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t == 0) {
+        if (zero_a) *zero_a = 0;
+        if (zero_b) *zero_b = 0;
+    }
     if (t >= ntiles) return;
     uint64_t first = (uint64_t)t * MJ_TILE;
     uint64_t last = std::min<uint64_t>(nR, first + MJ_TILE) - 1;
@@ -1180,11 +1186,10 @@ void merge_sorted(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_l
     uint64_t* win = dalloc_t<uint64_t>(c, 2 * (uint64_t)nt);
     uint64_t* tc = dalloc_t<uint64_t>(c, nt);
     uint32_t* d_flags = (uint32_t*)(c->d_scratch + 16);
-    QE_HIP(hipMemsetAsync(d_flags, 0, 4, c->stream));
     {
-        Timed t(c, "mj_partition", 0);
+        Timed t(c, "mj_partition", 0);   // also clears the flags word and the heavy-tile count
         hipLaunchKernelGGL(mj_partition, dim3((nt + 255) / 256), dim3(256), 0, c->stream, R->key, nR, S->key, nS, nt,
-                           win);
+                           win, c->d_scratch + 16, c->d_scratch + 19);
         QE_HIP(hipGetLastError());
     }
     // single pass with room for nR + nS pairs (every fan-out <= 1 + |S|/|R| case); the exact
@@ -1193,7 +1198,6 @@ void merge_sorted(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_l
     uint32_t* oR = dalloc_t<uint32_t>(c, cap);
     uint32_t* oS = dalloc_t<uint32_t>(c, cap);
     uint32_t* heavy = dalloc_t<uint32_t>(c, nt);
-    QE_HIP(hipMemsetAsync(c->d_scratch + 19, 0, 8, c->stream));
     {
         LBSlot s = lb_acquire(c, nt);
         Timed t(c, "mj_fused", 12.0 * nR + 12.0 * nS + 4.0 * nR);   // + 8 B per pair, added below
@@ -1284,7 +1288,7 @@ uint64_t merge_count_side(qe_ctx* c, qe_pairs* A, const qe_pairs* B) {
     {
         Timed t(c, "mj_count", 12.0 * nA + 12.0 * nB + 4.0 * nA);
         hipLaunchKernelGGL(mj_partition, dim3((nt + 255) / 256), dim3(256), 0, c->stream, A->key, nA, B->key, nB, nt,
-                           win);
+                           win, nullptr, nullptr);
         QE_HIP(hipGetLastError());
         LBSlot s = lb_acquire(c, nt);
         const bool key32 = (A->flags & QE_PAIRS_BITS) && ((A->kor & ~A->kand) >> 32) == 0;
@@ -1437,7 +1441,7 @@ uint32_t* driver_counts_sorted(qe_ctx* c, const qe_pairs* A, const qe_pairs* B, 
     {
         Timed t(c, "mj_annotate", 12.0 * A->n + 8.0 * B->n);
         hipLaunchKernelGGL(mj_partition, dim3((nt + 255) / 256), dim3(256), 0, c->stream, A->key, A->n, B->key, B->n,
-                           nt, win);
+                           nt, win, nullptr, nullptr);
         QE_HIP(hipGetLastError());
         hipLaunchKernelGGL(mj_tile<0>, dim3(nt), dim3(MJB), 0, c->stream, A->key, A->val, A->n, B->key, B->val, B->n,
                            win, tc, nullptr, nullptr, d_flags, cnt, nullptr);

@@ -357,6 +357,41 @@ __global__ void __launch_bounds__(1024) tl_hist_kernel(const K* __restrict__ key
         if (h[i]) atomicAdd(&hist[i], h[i]);
 }
 
+// one block: bucket starts (+ the end) and the largest bucket only -- the lookback-free form
+// computes its digit bases in the count scans, so it needs none of tl_scan_kernel's marginals
+// (whose serial loops made that kernel ~22 us per sort)
+__global__ void __launch_bounds__(1024) tl_bstart_kernel(const uint32_t* __restrict__ hist, uint32_t* __restrict__ bstart,
+                                                         uint64_t* __restrict__ maxb) {
+    constexpr int PER = TL_BUCKETS / 1024;
+    __shared__ uint32_t wsum[16], wmax[16];
+    const int t = threadIdx.x;
+    uint32_t v[PER], mine = 0, mx = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        v[k] = hist[t * PER + k];
+        mine += v[k];
+        mx = v[k] > mx ? v[k] : mx;
+    }
+    const uint32_t inc = wave_incl_scan_u32(mine);
+    mx = wave_max_u32(mx);
+    if (lane_id() == 63) wsum[wave_id()] = inc;
+    if (lane_id() == 0) wmax[wave_id()] = mx;
+    __syncthreads();
+    uint32_t run = inc - mine;
+    for (int w = 0; w < wave_id(); w++) run += wsum[w];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        bstart[t * PER + k] = run;
+        run += v[k];
+    }
+    if (t == 1023) bstart[TL_BUCKETS] = run;
+    if (t == 0) {
+        uint32_t m = 0;
+        for (int w = 0; w < 16; w++) m = wmax[w] > m ? wmax[w] : m;
+        *maxb = m;
+    }
+}
+
 // one block: bucket starts (exclusive scan, plus the end), the two global passes' digit bases (the
 // histogram's marginals over the low 8 / high 7 bucket bits) and the largest bucket
 __global__ void __launch_bounds__(1024) tl_scan_kernel(const uint32_t* __restrict__ hist, uint32_t* __restrict__ bstart,
@@ -1450,9 +1485,7 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     uint32_t* tcnt = dalloc_t<uint32_t>(c, (size_t)nt * 256);
     uint32_t* gcnt = dalloc_t<uint32_t>(c, (size_t)nseg * 128);
     uint32_t* hist = dalloc_t<uint32_t>(c, TL_BUCKETS);
-    uint32_t* bstart = dalloc_t<uint32_t>(c, TL_BUCKETS + 1 + 512);
-    uint32_t* base1 = bstart + TL_BUCKETS + 1;
-    uint32_t* base2 = base1 + 256;
+    uint32_t* bstart = dalloc_t<uint32_t>(c, TL_BUCKETS + 1);
     uint64_t* d_max = c->d_scratch + 34;
     auto release = [&] {
         dfree(c, tcnt);
@@ -1480,7 +1513,7 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
         QE_HIP(hipGetLastError());
         hipLaunchKernelGGL(tl_gsum_kernel, dim3(256), dim3(128), 0, c->stream, gcnt, G, hist);
         QE_HIP(hipGetLastError());
-        hipLaunchKernelGGL(tl_scan_kernel, dim3(1), dim3(1024), 0, c->stream, hist, bstart, base1, base2, d_max);
+        hipLaunchKernelGGL(tl_bstart_kernel, dim3(1), dim3(1024), 0, c->stream, hist, bstart, d_max);
         QE_HIP(hipGetLastError());
     }
     {
