@@ -499,3 +499,29 @@ def test_sort_pairs_crowded_buckets(ctx, n):
     np.testing.assert_array_equal(gk, k[order])
     np.testing.assert_array_equal(gv, v[order])
     ctx.pairs_free(p)
+
+
+def test_checksums_batched(ctx):
+    """qe_checksums: print_sums' select loop with one round trip -- 40 (column, list) pairs (two
+    rounds of 32), an empty list, a whole column (no list); every sum mod 2^64 as qe_checksum"""
+    rng = np.random.default_rng(31)
+    cols = [rng.integers(0, 1 << 64, 50_000, dtype=np.uint64) for _ in range(3)]
+    rels = [_col(ctx, c) for c in cols]
+    lists, want, hosts = [], [], []
+    for k in range(40):
+        j = k % 3
+        n = 0 if k == 5 else int(rng.integers(1, 20_000))
+        rows = rng.integers(0, 50_000, n, dtype=np.uint32)
+        hosts.append(ctx.list_from_host(rows))
+        lists.append(hosts[-1])
+        want.append(int(cols[j][rows].sum(dtype=np.uint64)) if n else 0)
+    cc = (lib.Col * 41)(*([rels[k % 3] for k in range(40)] + [rels[0]]))
+    lp = (lib.C.POINTER(lib.List) * 41)(*([lib.C.pointer(l) for l in lists] + [lib.C.POINTER(lib.List)()]))
+    want.append(int(cols[0].sum(dtype=np.uint64)))
+    out = (lib.C.c_uint64 * 41)()
+    ctx._chk(ctx.lib.qe_checksums(ctx.h, 41, cc, lp, out))
+    assert list(out) == want
+    for k in (0, 7, 39):
+        assert ctx.checksum(rels[k % 3], lists[k]) == want[k]
+    for l in hosts:
+        ctx.list_free(l)
