@@ -25,10 +25,19 @@
 
 namespace qe {
 
-constexpr int MJB = 256;
+// 512 threads x 8 = 4096 R rows per tile with an 8192-key S window: half the tiles (and lookbacks
+// and window searches) of 256 x 8, at three tiles per CU for 32-bit keys -- same-box A/B
+// 1.10 -> 0.98 ms per 1e8 x 1e8 join
+#ifndef QE_MJB
+#define QE_MJB 512
+#endif
+#ifndef QE_MJ_WIN
+#define QE_MJ_WIN 8192
+#endif
+constexpr int MJB = QE_MJB;               // threads per merge tile
 constexpr int MJ_ITEMS = 8;
-constexpr int MJ_TILE = MJB * MJ_ITEMS;   // 2048 R elements per tile
-constexpr int MJ_WIN = 4096;              // S keys staged in LDS (32 KiB)
+constexpr int MJ_TILE = MJB * MJ_ITEMS;   // 4096 R elements per tile
+constexpr int MJ_WIN = QE_MJ_WIN;         // S keys staged in LDS (64 KiB as u64, 32 KiB as u32)
 // a tile with more pairs than this is not emitted by its own workgroup: it is listed and
 // expanded afterwards by mj_heavy_prep + mj_heavy_emit, MJ_HEAVY_CHUNK pairs per workgroup
 // (a skewed key can put 1e8 pairs in one tile)
@@ -132,16 +141,17 @@ struct MJSharedG {
     uint32_t ticket;
 };
 using MJShared64 = MJSharedG<uint64_t, 2 * MJ_TILE>;
-// 2816 = 1.375 pairs per R row: 31.8 KiB of LDS, so FIVE workgroups per CU (3072 was 33.3 KiB, four)
-// -- more tiles in flight to cover the lookback wait (stamps: ~6 us of a ~26 us tile)
+// 1.375 pairs per R row staged (with 256-thread tiles: 31.8 KiB of LDS, FIVE workgroups per CU
+// against four at 1.5) -- more tiles in flight to cover the lookback wait (stamps: ~6 us of a
+// ~26 us tile)
 #ifndef QE_MJ32_OUTCAP
-#define QE_MJ32_OUTCAP 2816
+#define QE_MJ32_OUTCAP (11 * MJ_TILE / 8)
 #endif
 using MJShared32 = MJSharedG<uint32_t, QE_MJ32_OUTCAP>;
-// 2176 = 1.0625 pairs per R row: 26.0 KiB, SIX workgroups per CU -- for |S| <= |R|, where the mean
-// fan-out per R row is at most ~1 (C3's joins: 3.19 -> 3.00 ms per query, same-box A/B); a tile
-// with more pairs takes the binary-search emission
-using MJShared32s = MJSharedG<uint32_t, 2176>;
+// 1.0625 pairs per R row (256-thread tiles: 26.0 KiB, SIX workgroups per CU) -- for |S| <= |R|,
+// where the mean fan-out per R row is at most ~1 (C3's joins: 3.19 -> 3.00 ms per query, same-box
+// A/B); a tile with more pairs takes the binary-search emission
+using MJShared32s = MJSharedG<uint32_t, 17 * MJ_TILE / 16>;
 
 // bank swizzle of the S window for the key width (sw64: u64 slots, sw32: u32 slots)
 template <typename KT>
@@ -522,7 +532,11 @@ __global__ void __launch_bounds__(MJB) mj_tile(const uint64_t* __restrict__ rk, 
         uint64_t s = wave_sum_u64(tsum);
         if (lane_id() == 0) sh.red[wave_id()] = s;
         mj_publish_flags(sh, f, flags);   // contains the barrier
-        if (threadIdx.x == 0) tile_counts[tile] = sh.red[0] + sh.red[1] + sh.red[2] + sh.red[3];
+        if (threadIdx.x == 0) {
+            uint64_t tc = 0;
+            for (int w = 0; w < MJB / 64; w++) tc += sh.red[w];
+            tile_counts[tile] = tc;
+        }
         return;
     }
     uint64_t btotal;
