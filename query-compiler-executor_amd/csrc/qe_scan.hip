@@ -23,6 +23,14 @@ namespace qe {
 #endif
 constexpr int CB = QE_CB;   // block
 constexpr int FS_ITEMS = QE_FS_ITEMS;   // filter scan: steps of 2 x CB rows per tile
+#ifndef QE_RF_ITEMS
+#define QE_RF_ITEMS 8
+#endif
+#ifndef QE_NZ_ITEMS
+#define QE_NZ_ITEMS 8
+#endif
+constexpr int RF_ITEMS = QE_RF_ITEMS;   // filter refine: steps per tile (TILE = CB * ITEMS * VEC)
+constexpr int NZ_ITEMS = QE_NZ_ITEMS;   // join_payloads pruning: steps per tile
 constexpr int CNW = CB / 64;
 
 enum { OP_EQ = 0, OP_GT = 1, OP_LT = 2 };
@@ -278,9 +286,9 @@ uint64_t filter_refine(qe_ctx* c, const uint64_t* col, const uint32_t* in, uint6
                        uint32_t* out) {
     double b = 12.0 * n;
     switch (op) {
-    case '=': return run_compact<4, 1>(c, "filter_refine", b, FilterRefineOp<OP_EQ>{col, in, v}, n, out, nullptr);
-    case '>': return run_compact<4, 1>(c, "filter_refine", b, FilterRefineOp<OP_GT>{col, in, v}, n, out, nullptr);
-    case '<': return run_compact<4, 1>(c, "filter_refine", b, FilterRefineOp<OP_LT>{col, in, v}, n, out, nullptr);
+    case '=': return run_compact<RF_ITEMS, 1>(c, "filter_refine", b, FilterRefineOp<OP_EQ>{col, in, v}, n, out, nullptr);
+    case '>': return run_compact<RF_ITEMS, 1>(c, "filter_refine", b, FilterRefineOp<OP_GT>{col, in, v}, n, out, nullptr);
+    case '<': return run_compact<RF_ITEMS, 1>(c, "filter_refine", b, FilterRefineOp<OP_LT>{col, in, v}, n, out, nullptr);
     default: throw Error(QE_EINVAL, "Wrong operator");
     }
 }
@@ -292,7 +300,7 @@ uint64_t scan_join_k(qe_ctx* c, const uint64_t* rk, const uint32_t* rv, const ui
 
 uint64_t compact_nonzero_pairs(qe_ctx* c, const uint32_t* nz, uint64_t nzw, const uint32_t* last,
                                const uint32_t* edit, uint64_t n, uint32_t* out_last, uint32_t* out_edit) {
-    return run_compact<4, 2>(c, "payload_prune", 8.0 * n, NonzeroPairsOp{nz, last, edit, nzw}, n, out_last,
+    return run_compact<NZ_ITEMS, 2>(c, "payload_prune", 8.0 * n, NonzeroPairsOp{nz, last, edit, nzw}, n, out_last,
                              out_edit);
 }
 
