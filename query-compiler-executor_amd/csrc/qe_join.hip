@@ -1051,7 +1051,12 @@ __global__ void __launch_bounds__(XB) expand_kernel(const uint32_t* __restrict__
     // this thread's 8 payloads, all loads in flight at once (idx is read in order, vals[idx] is
     // the random gather)
     uint32_t v[X_ITEMS];
-    if (idx && e0 + X_ITEMS <= tn) {
+    if (!idx && e0 + X_ITEMS <= tn) {   // payloads already in sorted order
+        uint4 a = *reinterpret_cast<const uint4*>(vals + base + e0);
+        uint4 b = *reinterpret_cast<const uint4*>(vals + base + e0 + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else if (idx && e0 + X_ITEMS <= tn) {
         uint4 a = *reinterpret_cast<const uint4*>(idx + base + e0);
         uint4 b = *reinterpret_cast<const uint4*>(idx + base + e0 + 4);
         uint32_t p[X_ITEMS] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
@@ -1696,7 +1701,11 @@ int qe_join_payloads_multi(qe_ctx* c, const uint32_t* d_counts, uint64_t rows, c
         outs[k].flags = 0;
         outs[k].d = nullptr;
     }
-    // 1. positions whose driver count is 0 emit nothing: keep (last[i], i) for the others
+    // 1. positions whose driver count is 0 emit nothing: keep (last[i], i) for the others -- or,
+    //    with one edit list, (last[i], edit[i]): the stable sort below then leaves the payloads in
+    //    the order edit[perm] would have, and the expansion reads them in order instead of
+    //    gathering one 128-B line per 4-B payload
+    const bool direct = nedits == 1;
     uint32_t* pl = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
     uint32_t* pi = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
     uint64_t m = 0;
@@ -1709,7 +1718,7 @@ int qe_join_payloads_multi(qe_ctx* c, const uint32_t* d_counts, uint64_t rows, c
                                d_counts, rows, nz);
             QE_HIP(hipGetLastError());
         }
-        m = compact_nonzero_pairs(c, nz, nw, last->d, nullptr, n, pl, pi);
+        m = compact_nonzero_pairs(c, nz, nw, last->d, direct ? edits[0]->d : nullptr, n, pl, pi);
         dfree(c, nz);
     }
     // 2. one stable sort by `last` for every edit list (the reference sorts R = (last, edit)
@@ -1752,8 +1761,8 @@ int qe_join_payloads_multi(qe_ctx* c, const uint32_t* d_counts, uint64_t rows, c
         outs[k].flags = ((edits[k]->flags & QE_LIST_DISTINCT) && !(mflag & 1u)) ? QE_LIST_DISTINCT : 0;
         if (P) {
             Timed t(c, "payload_expand", 12.0 * m + 4.0 * P);
-            hipLaunchKernelGGL(expand_kernel<1>, dim3(nt), dim3(XB), 0, c->stream, sk, edits[k]->d, m, d_counts, tc,
-                               outs[k].d, nullptr, sidx);
+            hipLaunchKernelGGL(expand_kernel<1>, dim3(nt), dim3(XB), 0, c->stream, sk, direct ? sidx : edits[k]->d, m,
+                               d_counts, tc, outs[k].d, nullptr, direct ? nullptr : sidx);
             QE_HIP(hipGetLastError());
         }
     }

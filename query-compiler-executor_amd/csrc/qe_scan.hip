@@ -113,13 +113,20 @@ struct NonzeroPairsOp {        // join_payloads: keep (last[i], edit[i] or i) wh
     const uint32_t *nz, *last, *edit;   // nz: bit r set <=> count[r] > 0; edit == null: emit i
     uint64_t nzw;                        // words in nz (a rowid past the driver's rows never matches)
     __device__ __forceinline__ void load(uint64_t base, uint64_t n, bool* f, uint32_t* v0, uint32_t* v1) const {
-        uint32_t l[4];
+        uint32_t l[4], e[4];
         if (base + 3 < n) {
             uint4 x = *reinterpret_cast<const uint4*>(last + base);
             l[0] = x.x; l[1] = x.y; l[2] = x.z; l[3] = x.w;
+            if (edit) {
+                uint4 y = *reinterpret_cast<const uint4*>(edit + base);
+                e[0] = y.x; e[1] = y.y; e[2] = y.z; e[3] = y.w;
+            }
         } else {
 #pragma unroll
-            for (int k = 0; k < 4; k++) l[k] = base + k < n ? last[base + k] : 0;
+            for (int k = 0; k < 4; k++) {
+                l[k] = base + k < n ? last[base + k] : 0;
+                if (edit) e[k] = base + k < n ? edit[base + k] : 0;
+            }
         }
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -127,7 +134,7 @@ struct NonzeroPairsOp {        // join_payloads: keep (last[i], edit[i] or i) wh
             bool ok = i < n;
             f[k] = ok && (l[k] >> 5) < nzw && ((nz[l[k] >> 5] >> (l[k] & 31)) & 1u);
             v0[k] = l[k];
-            v1[k] = ok ? (edit ? edit[i] : (uint32_t)i) : 0;
+            v1[k] = ok ? (edit ? e[k] : (uint32_t)i) : 0;
         }
     }
 };
