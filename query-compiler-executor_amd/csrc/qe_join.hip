@@ -119,13 +119,15 @@ __device__ __forceinline__ uint32_t rpad(uint32_t e) { return e + (e >> 3); }
 // touches lies in [first R key, last R key] (the S window is bounded by those), so when R's
 // varying bits are all below bit 32 the tile works on 32-bit offsets -- one-op compares in the
 // VALU-bound walk, half the LDS bytes, and (with a 1.5x output stage) 4 workgroups per CU.
-template <typename KT, int OUTCAP>
+template <typename KT, int OUTCAP, int WIN = MJ_WIN>
 struct MJSharedG {
     using Key = KT;
     static constexpr int kOutCap = OUTCAP;   // pairs a balanced tile stages in LDS
+    static constexpr int kWin = WIN;         // S keys a tile stages in LDS (a wider window: global walk)
+    static_assert(WIN % MJB == 0, "the window is staged MJB keys per round");
     KT r[MJ_TILE + MJ_TILE / 8];
     union {                       // the S window is dead once every thread has walked (a barrier
-        KT s[MJ_WIN];             // separates the walk from the emission's use of the space)
+        KT s[WIN];                // separates the walk from the emission's use of the space)
         struct {
             uint32_t lo[MJ_TILE];     // window-relative S start per R element
             uint32_t off[MJ_TILE];    // tile-relative output offset per R element
@@ -147,7 +149,15 @@ using MJShared64 = MJSharedG<uint64_t, 2 * MJ_TILE>;
 #ifndef QE_MJ32_OUTCAP
 #define QE_MJ32_OUTCAP (11 * MJ_TILE / 8)
 #endif
-using MJShared32 = MJSharedG<uint32_t, QE_MJ32_OUTCAP>;
+// S window of the 32-bit tile, tunable separately from the 64-bit one.  A 4096-row R tile spans
+// |S|/|R| x 4096 S keys, so one of C3's joins (|S|/|R| ~ 2.15) puts ~8800 behind each tile --
+// past 8192 -- and walks S in global memory.  A 12288-key window (48 KiB, still two workgroups
+// per CU) was measured against 8192 on one box (C3 mj_fused 2.98 vs 2.95 ms per query, end to
+// end 20.0 vs 20.0 ms): no gain -- the wider staging costs what the LDS walk saves -- so 8192 stays
+#ifndef QE_MJ32_WIN
+#define QE_MJ32_WIN MJ_WIN
+#endif
+using MJShared32 = MJSharedG<uint32_t, QE_MJ32_OUTCAP, QE_MJ32_WIN>;
 // 1.0625 pairs per R row (256-thread tiles: 26.0 KiB, SIX workgroups per CU) -- for |S| <= |R|,
 // where the mean fan-out per R row is at most ~1 (C3's joins: 3.19 -> 3.00 ms per query, same-box
 // A/B); a tile with more pairs takes the binary-search emission
@@ -168,7 +178,7 @@ __device__ __forceinline__ void mj_stage(SH& sh, const uint64_t* rk, uint64_t ba
                                          const uint64_t* sk, uint64_t wlo, uint64_t wn, uint64_t kbase) {
     using KT = typename SH::Key;
     if (threadIdx.x == 0) sh.flag = 0;
-    constexpr int RS = MJ_TILE / MJB, SS = MJ_WIN / MJB;
+    constexpr int RS = MJ_TILE / MJB, SS = SH::kWin / MJB;
     uint64_t rr[RS], ss[SS];
     const uint32_t t = threadIdx.x;
     if (tn == MJ_TILE) {   // base is a multiple of MJ_TILE: 16-B aligned pairs
@@ -187,7 +197,7 @@ __device__ __forceinline__ void mj_stage(SH& sh, const uint64_t* rk, uint64_t ba
             rr[2 * k + 1] = i + 1 < tn ? rk[base + i + 1] : 0;
         }
     }
-    const bool sw = wn <= MJ_WIN;
+    const bool sw = wn <= (uint64_t)SH::kWin;
     if (sw) {
 #pragma unroll
         for (int k = 0; k < SS; k++) {
@@ -346,7 +356,7 @@ template <class SH>
 __device__ __forceinline__ uint64_t mj_walk(const SH& sh, const uint64_t* sk, uint64_t wlo, uint64_t wn,
                                             uint32_t tn, uint64_t kbase, uint32_t (&cnt)[MJ_ITEMS],
                                             uint32_t (&lo_rel)[MJ_ITEMS]) {
-    if (wn <= MJ_WIN) return mj_walk_t<true>(sh, sk, wlo, wn, tn, kbase, cnt, lo_rel);
+    if (wn <= (uint64_t)SH::kWin) return mj_walk_t<true>(sh, sk, wlo, wn, tn, kbase, cnt, lo_rel);
     // a window beyond LDS: inside a skewed key's run.  When the whole R tile holds one key the
     // window [lower_bound(first), upper_bound(last)) IS that key's S run -- every row matches all
     // of it, no search (the per-thread global binary searches cost ~24 dependent HBM round trips)
