@@ -30,6 +30,7 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "query-compiler-executor_amd"))
+sys.path.insert(0, ROOT)
 
 METRIC = "joined tuples/sec + achieved HBM GB/s, 4-rel chain join, 1/2/4/8 MI355X"
 QUERY = "0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>1000000000&3.2<3000000000|1.2 2.2 3.2\n"
@@ -227,13 +228,13 @@ def main():
     if args.rows is None and args.workload != "c5":
         args.rows = 100_000_000
     if args.workload == "c5":
-        from qe import c5bench
+        from benchmarks import c5 as c5bench
         if world > 1 or args.plan == "dist":
             res = c5bench.run_dist(args, log)
         else:
             res = c5bench.run_single(args, log, roofline_fn=roofline, traffic_fn=lambda: load_traffic("c5"))
     elif args.workload == "c4":
-        from qe import c4bench
+        from benchmarks import c4 as c4bench
         if world > 1:
             res = c4bench.run_dist(args, log)
         else:

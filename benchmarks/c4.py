@@ -16,9 +16,11 @@ import json
 import os
 import time
 
-from . import datagen as dg
+from qe import datagen as dg
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from .cpuref import CpuRef, cpu_model, pin_one_core
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden", "c4.json")
 METRIC = "queries/sec, SIGMOD-2018-style batch (C4: 14 relations, gated query set)"
 
@@ -29,59 +31,37 @@ def load_queries() -> list[str]:
     return [c["input"] for c in doc["cases"] if c["rc"] == 0]
 
 
-def gen_c4(ctx, scale: float = 1.0) -> list:
-    specs = dg.c4_spec(scale)
-    for r, sp in enumerate(specs):
-        ctx.gen_relation(sp.rows, sp.kinds, seed=dg.C4_SEED, gen_rel=r)
-    ctx.sync()
-    return specs
+gen_c4 = dg.gen_c4
 
 
 def cpu_sample(queries: list[str], gpu_ctx, budget_s: float = 20.0) -> dict:
     """oracle/cpu_ref, one core, on the first queries of the batch until ~budget_s of CPU time;
     the GPU runs the same queries one by one for a byte comparison."""
-    import ctypes as C
-
-    so = os.path.join(ROOT, "oracle", "build", "libcpuref.so")
-    lib = C.CDLL(so)
-    lib.cpuref_create.restype = C.c_void_p
-    lib.cpuref_add_relation.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_void_p)]
-    lib.cpuref_run_str.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
-    lib.cpuref_destroy.argtypes = [C.c_void_p]
     specs = dg.c4_spec(1.0)
-    rels = dg.make_relations(specs, dg.C4_SEED)
-    h = lib.cpuref_create()
-    keep = []
-    for sp, cols in zip(specs, rels):
-        arr = (C.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
-        keep.append(arr)
-        lib.cpuref_add_relation(h, sp.rows, len(cols), arr)
-    try:
-        os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
-    except Exception:
-        pass
+    cr = CpuRef()
+    for cols in dg.make_relations(specs, dg.C4_SEED):
+        cr.add_relation(cols)
+    pin_one_core()
     done, cpu_outs, t_cpu = 0, [], 0.0
     for q in queries:
-        out, n = C.c_void_p(), C.c_size_t()
-        t0 = time.perf_counter()
-        lib.cpuref_run_str(h, q.encode(), C.byref(out), C.byref(n))
-        t_cpu += time.perf_counter() - t0
-        cpu_outs.append(C.string_at(out, n.value).decode("latin-1"))
+        out, _, dt = cr.run(q)
+        t_cpu += dt
+        cpu_outs.append(out)
         done += 1
         if t_cpu > budget_s:
             break
-    lib.cpuref_destroy(h)
+    cr.close()
     gpu_outs = [gpu_ctx.run(q)[0] for q in queries[:done]]
     return {"value": round(done / t_cpu, 3), "unit": "queries/s", "cores": 1, "kind": "port",
             "sample": f"first {done} of {len(queries)} C4 queries at full size; oracle/cpu_ref single-threaded, "
                       f"{t_cpu:.1f} s",
-            "seconds": round(t_cpu, 3), "queries": done, "parity_with_gpu": cpu_outs == gpu_outs}
+            "seconds": round(t_cpu, 3), "queries": done, "cpu_model": cpu_model(), "parity_with_gpu": cpu_outs == gpu_outs}
 
 
 def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
     import torch
 
-    from . import lib
+    from qe import lib
     torch.cuda.init()
     ctx = lib.Ctx(0)
     queries = load_queries()
@@ -128,7 +108,7 @@ def run_dist(args, log) -> dict | None:
     import torch
     import torch.distributed as dist
 
-    from . import lib
+    from qe import lib
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -12,74 +12,37 @@ sum_i col[rowid_i] * count_i per select, which is exactly the checksum of the li
 reference would build (proved against the reference at 20 k rows in §9.5 and
 checked here against the C5 goldens and against numpy aggregate truth at 1e8 rows).
 One step = one execution of the query (both sorts, both count passes, both checksums).
-`value` = pairs of the join (joined tuples, counted not materialised) per second.
+`value` = input rows (both sides) per second; the join's pair count (counted, not materialised)
+is reported beside it as `pairs` and `pairs_counted_per_s`.
 """
 from __future__ import annotations
 
-import ctypes as C
 import os
 import time
 
-from . import datagen as dg
+from qe import datagen as dg
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-METRIC = "joined tuples/sec + achieved HBM GB/s, 4-rel chain join, 1/2/4/8 MI355X"
+from .cpuref import CpuRef, cpu_model, pin_one_core
 
-
-def gen_c5(ctx, rows: int, row_start: int = 0, total_rows: int | None = None) -> list:
-    """relations r0, r1 of c5_spec(total_rows) -- rows [row_start, row_start + rows) of each.
-    The Zipf CDF is built by libqe in a fixed summation order: the same keys on every run."""
-    n = total_rows or rows
-    specs = dg.c5_spec(n)
-    ctx.set_zipf(n, dg.C5_THETA, dg.C5_PERM_SEED)
-    try:
-        for r, sp in enumerate(specs):
-            ctx.gen_relation(rows, sp.kinds, seed=dg.C5_SEED, gen_rel=r, row_start=row_start)
-    finally:
-        ctx.set_zipf_table(0, 0, 0)
-    return specs
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+METRIC = "input rows/sec, C5 2-relation Zipf(0.9) join, 1e9 rows/side (pairs counted, not materialised)"
 
 
-def column_prefix(ctx, rel: int, col: int, m: int):
-    """the first m values of a device column, on the host"""
-    import numpy as np
-    from . import lib
-    c = ctx.column(rel, col)
-    p = lib.Pairs()
-    p.key, p.val, p.match, p.n = c.d, None, None, min(m, c.n)
-    out = np.empty(p.n, dtype=np.uint64)
-    ctx._chk(ctx.lib.qe_pairs_to_host(ctx.h, C.byref(p), out.ctypes.data, None))
-    return out
+gen_c5 = dg.gen_c5
 
 
 def cpu_sample(ctx, sample_rows: int, budget_note: str = "") -> dict:
     """oracle/cpu_ref, one core, on the first `sample_rows` rows of both relations (same Zipf
     columns, so the heavy keys collide as at full size; the join is small enough to
     materialise).  The GPU runs the same sample through both of its paths for a byte check."""
-    from . import lib
-    cols = [[column_prefix(ctx, r, c, sample_rows) for c in range(3)] for r in range(2)]
-    so = os.path.join(ROOT, "oracle", "build", "libcpuref.so")
-    cl = C.CDLL(so)
-    cl.cpuref_create.restype = C.c_void_p
-    cl.cpuref_add_relation.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_void_p)]
-    cl.cpuref_run_str.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
-    cl.cpuref_destroy.argtypes = [C.c_void_p]
-    h = cl.cpuref_create()
-    keep = []
+    from qe import lib
+    cols = [[ctx.column_range_to_host(r, c, 0, sample_rows) for c in range(3)] for r in range(2)]
+    cr = CpuRef()
     for cs in cols:
-        arr = (C.c_void_p * 3)(*[c.ctypes.data for c in cs])
-        keep.append(arr)
-        cl.cpuref_add_relation(h, sample_rows, 3, arr)
-    try:
-        os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
-    except Exception:
-        pass
-    out, n = C.c_void_p(), C.c_size_t()
-    t0 = time.perf_counter()
-    cl.cpuref_run_str(h, dg.C5_QUERY.encode(), C.byref(out), C.byref(n))
-    dt = time.perf_counter() - t0
-    cpu_out = C.string_at(out, n.value).decode("latin-1")
-    cl.cpuref_destroy(h)
+        cr.add_relation(cs)
+    pin_one_core()
+    cpu_out, _, dt = cr.run(dg.C5_QUERY)
+    cr.close()
     # the same sample on the GPU: materialised (default limit) and aggregate (limit 0)
     g = lib.Ctx(ctx.device) if hasattr(ctx, "device") else lib.Ctx(0)
     for cs in cols:
@@ -89,18 +52,18 @@ def cpu_sample(ctx, sample_rows: int, budget_note: str = "") -> dict:
     g.set_materialize_limit(0)
     agg, _ = g.run(dg.C5_QUERY)
     g.close()
-    return {"value": round(pairs / dt, 1), "unit": "joined tuples/s", "cores": 1, "kind": "port",
+    return {"value": round(2 * sample_rows / dt, 1), "unit": "input rows/s", "cores": 1, "kind": "port",
             "sample": f"first {sample_rows} rows of both C5 relations (same device-made Zipf columns), "
                       f"{pairs} pairs materialised by oracle/cpu_ref single-threaded in {dt:.2f} s{budget_note}",
             "seconds": round(dt, 3), "pairs": pairs,
-            "input_rows_per_s": round(2 * sample_rows / dt, 1),
+            "pairs_per_s": round(pairs / dt, 1), "cpu_model": cpu_model(),
             "parity_with_gpu": cpu_out == mat == agg}
 
 
 def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
     import torch
 
-    from . import lib
+    from qe import lib
     torch.cuda.init()
     rows = args.rows or dg.C5_ROWS
     ctx = lib.Ctx(0)
@@ -125,7 +88,7 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
     kern = sorted(stats.items(), key=lambda kv: -kv[1]["ms"])
     ms = dt / args.steps * 1e3
     res = {
-        "metric": METRIC, "value": round(pairs * args.steps / dt, 1), "unit": "joined tuples/s", "n_gpus": 1,
+        "metric": METRIC, "value": round(2 * rows * args.steps / dt, 1), "unit": "input rows/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
         "data": "synthetic: qe.datagen.c5_spec(%d) generated in HBM (seed %d, Zipf %.1f, shared permutation)"
@@ -135,7 +98,7 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
                    "pairs": pairs, "materialised": False,
                    "path": "libqe faithful executor: sort both sides, qe_merge_join_counts (aggregate form: "
                            "P > INT32_MAX), qe_checksum_weighted",
-                   "input_rows_per_s": round(2 * rows * args.steps / dt, 1),
+                   "pairs_counted_per_s": round(pairs * args.steps / dt, 1),
                    "stdout": out, "parallelism": "single GPU"},
         "roofline": roofline_fn(stats, traffic_fn() if traffic_fn else None) if roofline_fn else None,
         "stages": {k: {"ms_per_step": round(s["ms"] / args.steps, 3), "launches_per_step": s["launches"] / args.steps}
@@ -158,8 +121,8 @@ def run_dist(args, log) -> dict | None:
 
     import numpy as np
 
-    from . import lib
-    from .dist import DistAggJoin, GPUEngine
+    from qe import lib
+    from qe.dist import DistAggJoin, GPUEngine
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -207,7 +170,7 @@ def run_dist(args, log) -> dict | None:
     if rank == 0:
         kern = sorted(stats.items(), key=lambda kv: -kv[1]["ms"])
         res = {
-            "metric": METRIC, "value": round(pairs * args.steps / dt, 1), "unit": "joined tuples/s",
+            "metric": METRIC, "value": round(2 * rows * args.steps / dt, 1), "unit": "input rows/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u64",
             "data": "synthetic: qe.datagen.c5_spec(%d) generated in HBM on every rank (seed %d, Zipf %.1f)"
@@ -218,7 +181,7 @@ def run_dist(args, log) -> dict | None:
                        "path": "qe.dist.DistAggJoin: heavy keys split by row slice + all-reduced counts; light keys "
                                "bucketed locally (qe_bucket_select), sorted, qe_merge_join_counts, "
                                "qe_checksum_weighted; sums all-reduced",
-                       "input_rows_per_s": round(2 * rows * args.steps / dt, 1),
+                       "pairs_counted_per_s": round(pairs * args.steps / dt, 1),
                        "stdout": out + "\n" if not out.endswith("\n") else out,
                        "parallelism": f"hash buckets + heavy split x{world}"},
             "stages": {k: {"ms_per_step": round(s["ms"] / args.steps, 3)} for k, s in kern[:10]},

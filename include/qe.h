@@ -38,6 +38,7 @@ enum {
     QE_ENOMEM = -3,      /* device allocation failed */
     QE_EEXIT = -4,       /* the reference would have called exit(EXIT_FAILURE) here */
     QE_ETOOBIG = -5,     /* a join result beyond the materialisation limit (qe_set_materialize_limit) */
+    QE_ENOTSUP = -6,     /* outside the partitioned plan's domain (include/qe_plan.h): run it faithfully */
 };
 
 typedef struct qe_ctx qe_ctx;

@@ -1,0 +1,94 @@
+/*
+ * qe_plan.h -- the key-partitioned multi-GPU plan as host C over an engine.
+ *
+ * The reference is single-threaded (main/queries_main.c:37 -> execute_queries,
+ * src/utilities.c:289-300).  Its join path shards by key: R ⋈ S = ⋃_g R_g ⋈ S_g with
+ * g = part(key), and every printed number is a sum mod 2^64 (src/utilities.c:216-219), so a query
+ * whose output is the relational answer can run on N ranks -- each rank filters its rowid slice,
+ * exchanges the derived join sides by key (an RCCL all-to-all), joins its bucket locally and
+ * all-reduces the sums.
+ *
+ * Not every query's output IS the relational answer: the reference's mid_result state machine
+ * (src/join.c:152-628) prints positional garbage for some shapes (scan_join of unrelated lists,
+ * join_payloads zipping misaligned lists, merges of stale "sorted" lists, stale entries of a
+ * relation used twice).  qe_plan_check replays that state machine on the bindings alone (no data)
+ * and accepts a query only when every list a later predicate or select reads is provably the
+ * relational projection of its binding; a refused query (QE_ENOTSUP) is run by the engine's
+ * fallback -- libqe's faithful executor on one rank, relations being replicated.
+ *
+ * The plan is engine-agnostic: libqe supplies the device + RCCL engine (qe_run_queries_dist in
+ * qe.h), the tests supply a numpy + gloo engine through ctypes (tests/plan_engine.py), so one
+ * implementation is exercised both ways.
+ */
+#ifndef QE_PLAN_H
+#define QE_PLAN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* An engine array: a rowid list (uint32) or a key array (uint64), owned by the engine; 0 = none.
+ * Handles given to the plan are released by it (release) unless noted. */
+typedef uint64_t qe_h;
+
+typedef struct qe_engine {
+    void* u;                    /* the engine's state, passed back to every call */
+    uint32_t rank, world;
+    /* relation metadata (replicated on every rank) */
+    int (*rel_count)(void* u, uint32_t* n);
+    int (*rel_shape)(void* u, uint32_t rel, uint64_t* rows, uint32_t* ncols);
+    /* a1 on rows [start, end): rowids (global numbering) with col[r] op v, ascending */
+    int (*scan)(void* u, uint32_t rel, uint32_t col, uint64_t start, uint64_t end, char op, uint64_t v, qe_h* out);
+    /* rowids start .. start + n - 1 */
+    int (*iota)(void* u, uint64_t start, uint64_t n, qe_h* out);
+    /* a2: the rowids r of `rows` with col[r] op v, in order (`rows` is consumed) */
+    int (*refine)(void* u, uint32_t rel, uint32_t col, qe_h rows, char op, uint64_t v, qe_h* out);
+    /* a4: keys col[rows[i]] (`rows` is borrowed) */
+    int (*keys)(void* u, uint32_t rel, uint32_t col, qe_h rows, qe_h* out);
+    /* a whole base relation as a join side: one rank -- the column itself, *rowids = 0 (row i);
+     * N ranks -- this rank's hash bucket of the replicated column, as keys + rowids */
+    int (*base_side)(void* u, uint32_t rel, uint32_t col, qe_h* keys, qe_h* rowids);
+    /* hash-partition (keys, cols[0..ncols)) on the key and all-to-all them; the inputs are
+     * consumed.  start queues the exchange (the plan works on the other join side meanwhile),
+     * finish returns this rank's bucket */
+    int (*exchange_start)(void* u, qe_h keys, const qe_h* cols, int ncols, qe_h* ticket);
+    int (*exchange_finish)(void* u, qe_h ticket, qe_h* keys, qe_h* cols);
+    /* a5-a8 on a rank's bucket: sort both sides by key, merge; oa[i] = va[ia[i]] (or ia[i] when
+     * va == 0), likewise ob -- aligned, every matching pair once.  Inputs are borrowed. */
+    int (*join)(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, qe_h* oa, qe_h* ob);
+    /* out[i] = src[idx[i]] (both borrowed) */
+    int (*take)(void* u, qe_h src, qe_h idx, qe_h* out);
+    int (*length)(void* u, qe_h h, uint64_t* n);
+    /* a12, local: sums[k] = sum of col_k[rows_k[i]] mod 2^64 (rows borrowed) */
+    int (*checksums)(void* u, int n, const uint32_t* rels, const uint32_t* cols, const qe_h* rows, uint64_t* sums);
+    /* in place: v[i] = sum over ranks mod 2^64 */
+    int (*allreduce)(void* u, uint64_t* v, int n);
+    void (*release)(void* u, qe_h h);
+    /* a query outside the plan's domain (nullable): `query` is a parsed, arranged query_t of
+     * host/qe_query.h, `out` the FILE* the batch prints to (rank 0's matters); returns 0 or the
+     * reference's exit code path (QE_EEXIT) -- identical on every rank */
+    int (*fallback)(void* u, void* query, void* out);
+} qe_engine;
+
+/* Replay the reference's variant choice and list bookkeeping for every query of `text` on the
+ * bindings alone; accepted[i] = 1 when query i's output is the relational answer (nullable).
+ * Returns the number of queries. */
+int qe_plan_check_text(const qe_engine* e, const char* text, uint8_t* accepted, size_t cap);
+/* The first refusal reason of the last qe_plan_check_text / qe_plan_run_text call on this thread. */
+const char* qe_plan_why(void);
+
+/* Run every query of `text` (the reference's protocol: F lines skipped, every query parsed before
+ * any runs) with the partitioned plan, refused queries through e->fallback (QE_ENOTSUP when there
+ * is none).  Every rank calls it with the same text; *out (malloc'd, free with free()) is the
+ * stdout the reference would print (meaningful on rank 0).  *rows (nullable): the global row count
+ * of the last printed query's first select.  *nrefused (nullable): queries sent to the fallback. */
+int qe_plan_run_text(const qe_engine* e, const char* text, char** out, size_t* outlen, uint64_t* rows,
+                     uint64_t* nrefused);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QE_PLAN_H */

@@ -1764,6 +1764,17 @@ int qe_join_payloads_multi(qe_ctx* c, const uint32_t* d_counts, uint64_t rows, c
         mflag = (uint32_t)h[0];
         P = h[1];
     }
+    if (P > c->mat_limit) {   // the reference's DArray cannot hold it either (src/DArray.h:14-15)
+        if (tc) dfree(c, tc);
+        if (so.keys_new) dfree(c, so.keys);
+        if (so.vals_new) dfree(c, so.vals);
+        dfree(c, pl);
+        dfree(c, pi);
+        char msg[160];
+        snprintf(msg, sizeof msg, "join_payloads of %llu rowids exceeds the materialisation limit %llu",
+                 (unsigned long long)P, (unsigned long long)c->mat_limit);
+        throw Error(QE_ETOOBIG, msg);
+    }
     // 4. per edit list: edit[perm[i]] x multiplicity, in sorted order
     for (int k = 0; k < nedits; k++) {
         outs[k].d = dalloc_t<uint32_t>(c, std::max<uint64_t>(P, 1));

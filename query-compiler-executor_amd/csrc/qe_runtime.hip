@@ -458,11 +458,25 @@ int qe_sync(qe_ctx* c) {
     QE_API_END(c)
 }
 
+/* frees a relation's columns unless the relation was stored (a failed load or generate must not
+ * leak the columns it already allocated) */
+struct ColsGuard {
+    std::vector<uint64_t*>& cols;
+    bool keep = false;
+    explicit ColsGuard(std::vector<uint64_t*>& v) : cols(v) {}
+    ~ColsGuard() {
+        if (keep) return;
+        for (uint64_t* d : cols) (void)hipFree(d);
+        cols.clear();
+    }
+};
+
 int qe_load_relation(qe_ctx* c, uint64_t rows, uint64_t ncols, const uint64_t* const* host_cols) {
     QE_API_BEGIN(c)
     if (rows >= 0xFFFFFFFFull) throw Error(QE_EINVAL, "relation too large for uint32 rowids");
     Relation r;
     r.rows = rows;
+    ColsGuard guard(r.cols);
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t j = 0; j < ncols; j++) {
         uint64_t* d = nullptr;
@@ -478,6 +492,7 @@ int qe_load_relation(qe_ctx* c, uint64_t rows, uint64_t ncols, const uint64_t* c
     c->load_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     c->load_bytes += (double)rows * ncols * sizeof(uint64_t);
     column_stats(c, r);
+    guard.keep = true;
     c->rels.push_back(std::move(r));
     return (int)c->rels.size() - 1;
     QE_API_END(c)
@@ -487,15 +502,21 @@ int qe_gen_relation(qe_ctx* c, uint64_t rows, uint64_t ncols, const int* kinds, 
                     uint64_t seed, uint32_t gen_rel, uint64_t row_start) {
     QE_API_BEGIN(c)
     if (rows >= 0xFFFFFFFFull) throw Error(QE_EINVAL, "relation too large for uint32 rowids");
+    for (uint64_t j = 0; j < ncols; j++) {      /* every column checked before anything is allocated */
+        if (kinds[j] == 0 && mods[j] == 0) throw Error(QE_EINVAL, "mod 0");
+        if (kinds[j] == 2 && (!c->zipf_cdf || mods[j] != c->zipf_domain))
+            throw Error(QE_EINVAL, "no Zipf table for this domain");
+        if (kinds[j] < 0 || kinds[j] > 2) throw Error(QE_EINVAL, "unknown column kind");
+    }
     Relation r;
     r.rows = rows;
+    ColsGuard guard(r.cols);
     for (uint64_t j = 0; j < ncols; j++) {
         uint64_t* d = nullptr;
         QE_HIP(hipMalloc(&d, std::max<uint64_t>(rows, 1) * sizeof(uint64_t)));
+        r.cols.push_back(d);
         uint64_t base = (seed << 40) | ((uint64_t)gen_rel << 36) | ((uint64_t)j << 32);
-        if (kinds[j] == 0 && mods[j] == 0) throw Error(QE_EINVAL, "mod 0");
         if (kinds[j] == 2) {
-            if (!c->zipf_cdf || mods[j] != c->zipf_domain) throw Error(QE_EINVAL, "no Zipf table for this domain");
             uint32_t b = 2;
             while (b < 64 && ((c->zipf_domain - 1) >> b) != 0) b++;
             b += b & 1;
@@ -505,17 +526,15 @@ int qe_gen_relation(qe_ctx* c, uint64_t rows, uint64_t ncols, const int* kinds, 
                 hipLaunchKernelGGL(gen_zipf_kernel, dim3(grid_for(rows, 256 * 8, 8192)), dim3(256), 0, c->stream, d,
                                    rows, base, row_start, c->zipf_cdf, c->zipf_guide, c->zipf_domain, b / 2, k[0],
                                    k[1], k[2], k[3]);
-        } else if (kinds[j] != 0 && kinds[j] != 1) {
-            throw Error(QE_EINVAL, "unknown column kind");
         } else if (rows) {
             hipLaunchKernelGGL(gen_column_kernel, dim3(grid_for(rows, 256 * 8, 8192)), dim3(256), 0, c->stream, d,
                                rows, base, row_start, kinds[j], mods[j]);
         }
         QE_HIP(hipGetLastError());
-        r.cols.push_back(d);
     }
     QE_HIP(hipStreamSynchronize(c->stream));
     column_stats(c, r);
+    guard.keep = true;
     c->rels.push_back(std::move(r));
     return (int)c->rels.size() - 1;
     QE_API_END(c)

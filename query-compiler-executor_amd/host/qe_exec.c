@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include "../../include/qe.h"
+#include "qe_query.h"
 
 /* ------------------------------------------------------------------------------------------ */
 /* model                                                                                        */
@@ -29,19 +30,6 @@ typedef struct {                 /* mid_result (src/structs.h:44-49), list in HB
 
 typedef struct { mid_t* e; size_t n, cap; } entity_t;
 typedef struct { entity_t** v; size_t n, cap; } mra_t;
-
-typedef struct {                 /* predicate (src/structs.h:29-34) */
-    int type;                    /* 0 join, 1 filter, -1 unparsed */
-    uint64_t frel, fcol, srel, scol;   /* filter: srel = constant, scol = 0 (what is_match reads) */
-    char op;
-    uint64_t cval;               /* uint32 constant, zero-extended (src/filter.c:70) */
-} pred_t;
-
-typedef struct {
-    uint32_t* rels; size_t nrels;
-    pred_t* preds; size_t npreds;
-    uint64_t* sel; size_t nsel;
-} query_t;
 
 typedef struct { ptrdiff_t ent, idx; } exists_t;
 
@@ -584,114 +572,6 @@ static void print_sums(exec_t* x, const query_t* q, const mra_t* M) {
 /* frontend                                                                                     */
 /* ------------------------------------------------------------------------------------------ */
 
-static void parse_relations(const char* s, query_t* q) {         /* src/parsing.c:4-28 */
-    size_t sp = 0;
-    for (size_t i = 0; s[i]; i++) sp += s[i] == ' ';
-    q->nrels = sp + 1;
-    q->rels = (uint32_t*)calloc(q->nrels, sizeof(uint32_t));
-    char cur[16];
-    const char* ptr = s;
-    int adv;
-    size_t i = 0;
-    while (i < q->nrels && sscanf(ptr, "%15[^ ]%n", cur, &adv) == 1) {
-        ptr += adv;
-        q->rels[i++] = (uint32_t)(int)strtol(cur, NULL, 10);
-        if (*ptr != ' ') break;
-        ptr++;
-    }
-}
-
-static void parse_predicates(const char* s, query_t* q) {        /* src/parsing.c:30-88 */
-    size_t amp = 0;
-    for (size_t i = 0; s[i]; i++) amp += s[i] == '&';
-    q->npreds = amp + 1;
-    q->preds = (pred_t*)calloc(q->npreds, sizeof(pred_t));
-    for (size_t i = 0; i < q->npreds; i++) q->preds[i].type = -1;
-    char cur[128];
-    const char* ptr = s;
-    int adv;
-    size_t i = 0;
-    while (i < q->npreds && sscanf(ptr, "%127[^&]%n", cur, &adv) == 1) {
-        ptr += adv;
-        int a, b, c2, d;
-        unsigned ua, ub, uc;
-        char op;
-        if (sscanf(cur, "%d.%d%c%d.%d", &a, &b, &op, &c2, &d) == 5) {
-            pred_t* p = &q->preds[i++];
-            p->type = 0;
-            p->frel = (uint32_t)a;
-            p->fcol = (uint32_t)b;
-            p->srel = (uint32_t)c2;
-            p->scol = (uint32_t)d;
-            p->op = op;
-        } else if (sscanf(cur, "%u.%u%c%u", &ua, &ub, &op, &uc) == 4) {
-            pred_t* p = &q->preds[i++];
-            p->type = 1;
-            p->frel = ua;
-            p->fcol = ub;
-            p->op = op;
-            p->cval = (uint64_t)uc;
-            p->srel = (uint64_t)uc;
-            p->scol = 0;
-        }
-        if (*ptr != '&') break;
-        ptr++;
-    }
-}
-
-static void parse_select(const char* s, query_t* q) {           /* src/parsing.c:90-116 */
-    size_t sp = 0;
-    for (size_t i = 0; s[i]; i++) sp += s[i] == ' ';
-    q->nsel = sp + 1;
-    q->sel = (uint64_t*)calloc(2 * q->nsel, sizeof(uint64_t));
-    char tmp[128];
-    const char* ptr = s;
-    int adv;
-    size_t i = 0;
-    while (i < q->nsel && sscanf(ptr, "%127[^ ]%n", tmp, &adv) == 1) {
-        ptr += adv;
-        int r = 0, c = 0;
-        sscanf(tmp, "%d.%d", &r, &c);
-        q->sel[2 * i] = (uint64_t)(int64_t)r;
-        q->sel[2 * i + 1] = (uint64_t)(int64_t)c;
-        i++;
-        if (*ptr != ' ') break;
-        ptr++;
-    }
-}
-
-static void swap_preds(query_t* q, ptrdiff_t i, ptrdiff_t j) {
-    if (i == j) return;
-    pred_t t = q->preds[i];
-    q->preds[i] = q->preds[j];
-    q->preds[j] = t;
-}
-
-static int is_match(const pred_t* l, const pred_t* r) {         /* src/pred_arrange.c:29-48 */
-    return (l->fcol == r->fcol && l->frel == r->frel) || (l->fcol == r->scol && l->frel == r->srel) ||
-           (l->scol == r->fcol && l->srel == r->frel) || (l->scol == r->scol && l->srel == r->srel);
-}
-
-static void arrange_predicates(query_t* q) {                    /* src/pred_arrange.c:50-93 */
-    ptrdiff_t n = (ptrdiff_t)q->npreds, index = 0;
-    for (ptrdiff_t i = 1; i < n; i++) {                          /* group_filters: p[0] never examined */
-        if (q->preds[i].type == 1) {
-            ptrdiff_t s = i;
-            for (ptrdiff_t j = 0; j < i - index; j++, s--) swap_preds(q, s, s - 1);
-            index++;
-        }
-    }
-    for (ptrdiff_t i = index; i < n - 1;) {                      /* group_matches, index lag kept */
-        int swapped = 0;
-        for (ptrdiff_t j = i + 1; j < n; j++)
-            if (is_match(&q->preds[i], &q->preds[j])) {
-                swap_preds(q, ++index, j);
-                swapped = 1;
-            }
-        i = swapped ? index : i + 1;
-    }
-}
-
 static int query_valid(exec_t* x, const query_t* q) {
     int nrel = qe_relation_count(x->q);
     for (size_t i = 0; i < q->nrels; i++)
@@ -752,10 +632,31 @@ static int run_all(exec_t* x, query_t* qs, size_t nq) {
         return x->jb_code;
     }
     for (size_t qi = 0; qi < nq; qi++) {
-        arrange_predicates(&qs[qi]);
+        qe_arrange_predicates(&qs[qi]);
         execute_query(x, &qs[qi]);
     }
     return 0;
+}
+
+/* one parsed, already arranged query through the faithful executor, printing to `out` (the
+ * partitioned plan's fallback for queries outside its domain, qe_plan.h) */
+int qe_exec_query(qe_ctx* ctx, query_t* q, FILE* out) {
+    exec_t x;
+    memset(&x, 0, sizeof(x));
+    x.q = ctx;
+    const char* e = getenv("QE_DLE");
+    x.dle = !(e && e[0] == '0');
+    x.out = out;
+    int rc = 0;
+    if (setjmp(x.jb) != 0) {
+        free_lists(&x);
+        rc = x.jb_code;
+    } else {
+        execute_query(&x, q);
+    }
+    free(x.lists);
+    free(x.aggs);
+    return rc;
 }
 
 int qe_run_queries(qe_ctx* ctx, const char* text, char** out, size_t* outlen) {
@@ -771,47 +672,11 @@ int qe_run_queries(qe_ctx* ctx, const char* text, char** out, size_t* outlen) {
     x.out = open_memstream(out, outlen);
     if (!x.out) return QE_ENOMEM;
 
-    /* parser() (src/parsing.c:118-148): every line until EOF, 'F' lines skipped, the three
-     * scan buffers persist across lines as the reference's stack arrays do */
-    size_t len = strlen(text);
-    char* rb = (char*)calloc(len + 2, 1);
-    char* pb = (char*)calloc(len + 2, 1);
-    char* sb = (char*)calloc(len + 2, 1);
-    char* line = (char*)malloc(len + 2);
-    size_t nq_ = 0, capq = 16;  /* parsed before anything runs (main/queries_main.c:31-37) */
-    query_t* qs_ = (query_t*)malloc(capq * sizeof(query_t));
-    const char* s = text;
-    while (*s) {
-        const char* e = strchr(s, '\n');
-        size_t ll = e ? (size_t)(e - s) + 1 : strlen(s);
-        memcpy(line, s, ll);
-        line[ll] = 0;
-        s += ll;
-        if (line[0] == 'F') continue;
-        sscanf(line, "%[0-9 ]%*[|]%[0-9.=<>&]%*[|]%[0-9. ]", rb, pb, sb);
-        if (nq_ == capq) {
-            capq *= 2;
-            qs_ = (query_t*)realloc(qs_, capq * sizeof(query_t));
-        }
-        parse_relations(rb, &qs_[nq_]);
-        parse_predicates(pb, &qs_[nq_]);
-        parse_select(sb, &qs_[nq_]);
-        nq_++;
-    }
-    query_t* qs = qs_;
-    size_t nq = nq_;
-    free(line);
-    free(rb);
-    free(pb);
-    free(sb);
+    size_t nq = 0;
+    query_t* qs = qe_parse_text(text, &nq);   /* parsed before anything runs (main/queries_main.c:31-37) */
 
     int rc = run_all(&x, qs, nq);
-    for (size_t i = 0; i < nq; i++) {
-        free(qs[i].rels);
-        free(qs[i].preds);
-        free(qs[i].sel);
-    }
-    free(qs);
+    qe_free_queries(qs, nq);
     free(x.lists);
     free(x.aggs);
     fclose(x.out);

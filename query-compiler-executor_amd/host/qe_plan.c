@@ -1,0 +1,804 @@
+/*
+ * qe_plan.c -- the key-partitioned plan of include/qe_plan.h: (1) the domain check, a replay of
+ * the reference's mid_result state machine on bindings alone, and (2) the relational plan itself
+ * over an engine (filters on rank slices, hash exchange of derived join sides, local sort-merge
+ * joins, all-reduced checksums).  Host C; the engine does every row-sized step.
+ *
+ * Reference anchors: execute_query src/utilities.c:258-287, execute_filter src/filter.c:66-100,
+ * build_relations src/join.c:152-292, update_mid_results src/join.c:507-628, fix_all_mid_results
+ * src/join.c:486-505, join_payloads src/join.c:426-484, print_sums src/utilities.c:197-224.
+ */
+#define _GNU_SOURCE
+#include "../../include/qe_plan.h"
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/qe.h"
+#include "qe_query.h"
+
+static __thread char g_why[256];
+
+const char* qe_plan_why(void) { return g_why; }
+
+/* ============================================================================================ */
+/* (1) the domain check                                                                          */
+/* ============================================================================================ */
+
+/* A symbolic rowid list.  ok: its multiset is the projection on its binding of the relation its
+ * component denotes (the relational answer); tag: lists with one tag are positionally aligned
+ * (rows of one tuple sequence); len: lists with one len id have equal lengths; distinct: no rowid
+ * twice; sorted: the binding column it is ascending on (-1: none). */
+typedef struct { int tag, len, ok, distinct, sorted; } slist;
+typedef struct { uint64_t relation, pid; int32_t lcs; int l; } smid;   /* mid_result, list by index */
+typedef struct { smid* e; size_t n; } sent;
+
+typedef struct {
+    const query_t* q;
+    slist* L; size_t nl, capl;
+    sent* E; size_t ne, cape;
+    size_t cap_entries;
+    int fresh;
+    int* parent;                /* union-find over bindings: the components joined so far */
+    const uint8_t* live;        /* binding read by a later predicate or a select */
+} replay_t;
+
+static int refuse(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_why, sizeof g_why, fmt, ap);
+    va_end(ap);
+    return QE_ENOTSUP;
+}
+
+static int new_slist(replay_t* r, int tag, int len, int ok, int distinct, int sorted) {
+    if (r->nl == r->capl) {
+        r->capl = r->capl ? 2 * r->capl : 32;
+        r->L = (slist*)realloc(r->L, r->capl * sizeof(slist));
+    }
+    slist s = {tag, len, ok, distinct, sorted};
+    r->L[r->nl] = s;
+    return (int)r->nl++;
+}
+
+static sent* s_new_entity(replay_t* r) {
+    if (r->ne == r->cape) {
+        r->cape = r->cape ? 2 * r->cape : 8;
+        r->E = (sent*)realloc(r->E, r->cape * sizeof(sent));
+    }
+    sent* E = &r->E[r->ne++];
+    E->e = (smid*)calloc(r->cap_entries, sizeof(smid));
+    E->n = 0;
+    return E;
+}
+
+static void s_push(replay_t* r, sent* E, smid m) {
+    (void)r;
+    E->e[E->n++] = m;     /* an entry is pushed only for a (relation, pid) with none anywhere */
+}
+
+typedef struct { ptrdiff_t ent, idx; } sexists_t;
+
+static sexists_t s_exists(const replay_t* r, uint64_t relation, uint64_t pid) {   /* relation_exists */
+    sexists_t ex = {-1, -1};
+    for (ptrdiff_t i = (ptrdiff_t)r->ne - 1; i >= 0; i--)
+        for (size_t j = 0; j < r->E[i].n; j++)
+            if (r->E[i].e[j].relation == relation && r->E[i].e[j].pid == pid) {
+                ex.ent = i;
+                ex.idx = (ptrdiff_t)j;
+                return ex;
+            }
+    return ex;
+}
+
+static ptrdiff_t s_exists_current(const sent* E, uint64_t relation, uint64_t pid) {
+    ptrdiff_t f = -1;
+    for (size_t i = 0; i < E->n; i++)
+        if (E->e[i].relation == relation && E->e[i].pid == pid) f = (ptrdiff_t)i;
+    return f;
+}
+
+static int uf_find(int* p, int x) {
+    while (p[x] != x) x = p[x] = p[p[x]];
+    return x;
+}
+
+/* the join's inputs as build_relations picks them: list index or -1 (the whole base relation) */
+typedef struct { int variant; int lR, lS; } sjoin_t;
+
+/* build_relations (src/join.c:152-292) on symbolic entries: the variant, the inputs and the
+ * entries' last_column_sorted side effects, exactly as the reference (quirks included) */
+static sjoin_t s_build_relations(replay_t* r, const pred_t* p) {
+    const query_t* q = r->q;
+    sjoin_t j = {0, -1, -1};
+    uint64_t lhs_rel = q->rels[p->frel], lhs_col = p->fcol;
+    uint64_t rhs_rel = q->rels[p->srel], rhs_col = p->scol;
+    if (lhs_rel == rhs_rel && lhs_col == rhs_col) {
+        j.variant = 5;                                   /* DO_NOTHING */
+        return j;
+    }
+    sent* E = r->ne == 0 ? s_new_entity(r) : &r->E[r->ne - 1];
+    ptrdiff_t li = s_exists_current(E, lhs_rel, p->frel);
+    ptrdiff_t ri = s_exists_current(E, rhs_rel, p->srel);
+    if (li != -1 && ri == -1) {
+        j.lR = E->e[li].l;
+        sexists_t ex = s_exists(r, rhs_rel, p->srel);
+        smid* T = ex.idx != -1 ? &r->E[ex.ent].e[ex.idx] : NULL;
+        if (T) j.lS = T->l;
+        smid* mid = &E->e[li];
+        if (!T) {
+            if (mid->lcs == (int32_t)lhs_col) { j.variant = 3; return j; }
+            mid->lcs = (int32_t)lhs_col;
+            j.variant = 1;
+            return j;
+        }
+        if (mid->lcs == (int32_t)lhs_col && T->lcs == (int32_t)rhs_col) j.variant = 4;
+        else if (mid->lcs == (int32_t)lhs_col) j.variant = 3;
+        else if (T->lcs == (int32_t)rhs_col) j.variant = 2;
+        else j.variant = 1;
+        return j;
+    }
+    if (li != -1 && ri != -1) {
+        j.lR = E->e[li].l;
+        j.lS = E->e[ri].l;
+        j.variant = 4;
+        return j;
+    }
+    if (li == -1 && ri != -1) {
+        j.lS = E->e[ri].l;
+        sexists_t ex = s_exists(r, lhs_rel, p->frel);
+        smid* T = ex.idx != -1 ? &r->E[ex.ent].e[ex.idx] : NULL;
+        if (T) j.lR = T->l;
+        smid* mid = &E->e[ri];
+        if (!T) {
+            if (mid->lcs == (int32_t)rhs_col) { j.variant = 2; return j; }
+            mid->lcs = (int32_t)rhs_col;
+            j.variant = 1;
+            return j;
+        }
+        if (mid->lcs == (int32_t)rhs_col && T->lcs == (int32_t)lhs_col) j.variant = 4;
+        else if (mid->lcs == (int32_t)rhs_col) j.variant = 3;    /* reference quirk, src/join.c:258-259 */
+        else if (mid->lcs == (int32_t)lhs_col) j.variant = 2;    /* reference quirk, src/join.c:261-262 */
+        else j.variant = 1;
+        return j;
+    }
+    s_new_entity(r);                                     /* src/join.c:270-285 */
+    j.variant = (rhs_rel != lhs_rel || p->frel != p->srel) ? 1 : 4;
+    return j;
+}
+
+typedef struct { int* w; size_t n, cap; } wset;   /* lists written by the current join */
+
+static void w_add(wset* w, int l) {
+    if (w->n == w->cap) {
+        w->cap = w->cap ? 2 * w->cap : 16;
+        w->w = (int*)realloc(w->w, w->cap * sizeof(int));
+    }
+    w->w[w->n++] = l;
+}
+
+static int w_has(const wset* w, int l) {
+    for (size_t i = 0; i < w->n; i++)
+        if (w->w[i] == l) return 1;
+    return 0;
+}
+
+/* fix_all_mid_results (src/join.c:486-505): every other entry of the entity gets
+ * join_payloads(driver = the join's distinct pairs on this side, last = the updated entry's list,
+ * edit = the entry's list) -- a positional zip of edit with last, each row repeated by the number
+ * of DISTINCT partner rowids.  That is the relational projection only when edit is aligned with
+ * last, both are relational, and the other side's rowids are distinct (so distinct pairs = matches). */
+static int s_fix_all(replay_t* r, sexists_t ex, uint64_t relR, uint64_t relS, smid tmp, int other_distinct,
+                     int join_len, wset* w) {
+    sent* E = &r->E[ex.ent];
+    const slist upd = r->L[E->e[ex.idx].l];
+    const int tag = ++r->fresh;
+    const int len = other_distinct ? join_len : ++r->fresh;
+    for (size_t i = 0; i < E->n; i++) {
+        if ((ptrdiff_t)i == ex.idx) continue;
+        smid* ed = &E->e[i];
+        if (ed->relation == relR || ed->relation == relS) continue;   /* left stale (post pass) */
+        const slist edl = r->L[ed->l];
+        if (edl.len != upd.len)
+            return refuse("join_payloads on lists of possibly different lengths (binding %llu)",
+                          (unsigned long long)ed->pid);
+        const int ok = edl.tag == upd.tag && edl.ok && upd.ok && other_distinct;
+        if (r->live[ed->pid] && !ok)
+            return refuse("binding %llu is read later but join_payloads makes it %s", (unsigned long long)ed->pid,
+                          edl.tag != upd.tag ? "a zip of misaligned lists" : "a non-relational multiset");
+        ed->l = new_slist(r, tag, len, ok, 0, -1);
+        w_add(w, ed->l);
+    }
+    E->e[ex.idx] = tmp;
+    w_add(w, tmp.l);
+    return 0;
+}
+
+static int s_join(replay_t* r, const pred_t* p) {
+    const query_t* q = r->q;
+    sjoin_t j = s_build_relations(r, p);
+    if (j.variant == 5) return refuse("join of a column with itself (reference DO_NOTHING)");
+    if (j.variant == 4) return refuse("positional scan_join");
+    const int a = (int)p->frel, b = (int)p->srel;
+    if (uf_find(r->parent, a) == uf_find(r->parent, b))
+        return refuse("join inside one component (bindings %d and %d are already joined)", a, b);
+    /* a whole base relation stands for its binding only while that binding has no list yet: the
+     * last branch of build_relations gathers both sides from the base relations even when a
+     * binding already has a (filtered or joined) list in an older entity */
+    if (j.lR < 0 && s_exists(r, q->rels[p->frel], p->frel).idx != -1)
+        return refuse("join reads the whole relation of binding %d, which already has a list", a);
+    if (j.lS < 0 && s_exists(r, q->rels[p->srel], p->srel).idx != -1)
+        return refuse("join reads the whole relation of binding %d, which already has a list", b);
+    if (j.lR >= 0 && !r->L[j.lR].ok) return refuse("join input of binding %d is not relational", a);
+    if (j.lS >= 0 && !r->L[j.lS].ok) return refuse("join input of binding %d is not relational", b);
+    if (j.variant == 2 && (j.lS < 0 || r->L[j.lS].sorted != (int)p->scol))
+        return refuse("merge on a list taken as sorted that is not (binding %d)", b);
+    if (j.variant == 3 && (j.lR < 0 || r->L[j.lR].sorted != (int)p->fcol))
+        return refuse("merge on a list taken as sorted that is not (binding %d)", a);
+    const int dR = j.lR < 0 ? 1 : r->L[j.lR].distinct;
+    const int dS = j.lS < 0 ? 1 : r->L[j.lS].distinct;
+    const int tag = ++r->fresh, len = ++r->fresh;
+    const uint64_t relR = q->rels[p->frel], relS = q->rels[p->srel];
+    smid tR = {relR, p->frel, (int32_t)p->fcol, new_slist(r, tag, len, 1, 0, (int)p->fcol)};
+    smid tS = {relS, p->srel, (int32_t)p->scol, new_slist(r, tag, len, 1, 0, (int)p->scol)};
+    wset w = {NULL, 0, 0};
+    int rc = 0;
+    sexists_t ex;
+    /* update_mid_results (src/join.c:507-628) */
+    switch (j.variant) {
+    case 1:
+        ex = s_exists(r, relR, p->frel);
+        if (ex.idx == -1) { s_push(r, &r->E[r->ne - 1], tR); w_add(&w, tR.l); }
+        else rc = s_fix_all(r, ex, relR, relS, tR, dS, len, &w);
+        if (rc) break;
+        ex = s_exists(r, relS, p->srel);
+        if (ex.idx == -1) { s_push(r, &r->E[r->ne - 1], tS); w_add(&w, tS.l); }
+        else rc = s_fix_all(r, ex, relR, relS, tS, dR, len, &w);
+        break;
+    case 2:
+        ex = s_exists(r, relR, p->frel);
+        if (ex.idx == -1) s_push(r, &r->E[r->ne - 1], tR);
+        else r->E[ex.ent].e[ex.idx] = tR;
+        w_add(&w, tR.l);
+        ex = s_exists(r, relS, p->srel);
+        if (ex.idx == -1) { rc = refuse("the reference exits here (update of a missing entry)"); break; }
+        rc = s_fix_all(r, ex, relR, relS, tS, dR, len, &w);
+        break;
+    case 3:
+        ex = s_exists(r, relS, p->srel);
+        if (ex.idx == -1) s_push(r, &r->E[r->ne - 1], tS);
+        else r->E[ex.ent].e[ex.idx] = tS;
+        w_add(&w, tS.l);
+        ex = s_exists(r, relR, p->frel);
+        if (ex.idx == -1) { rc = refuse("the reference exits here (update of a missing entry)"); break; }
+        rc = s_fix_all(r, ex, relR, relS, tR, dS, len, &w);
+        break;
+    }
+    if (rc == 0) {
+        /* the components merge; every entry of either that this join did not rewrite is stale */
+        const int ca = uf_find(r->parent, a), cb = uf_find(r->parent, b);
+        for (size_t e = 0; e < r->ne; e++)
+            for (size_t i = 0; i < r->E[e].n; i++) {
+                smid* m = &r->E[e].e[i];
+                const int c = uf_find(r->parent, (int)m->pid);
+                if ((c == ca || c == cb) && !w_has(&w, m->l)) {
+                    r->L[m->l].ok = 0;
+                    r->L[m->l].len = ++r->fresh;
+                }
+            }
+        r->parent[ca] = cb;
+    }
+    free(w.w);
+    return rc;
+}
+
+static int op_valid(char op) { return op == '=' || op == '<' || op == '>'; }
+
+static int s_query_valid(const qe_engine* e, const query_t* q) {
+    uint32_t nrel = 0;
+    if (e->rel_count(e->u, &nrel) != 0) return 0;
+    uint64_t rows;
+    uint32_t nc;
+    for (size_t i = 0; i < q->nrels; i++)
+        if (q->rels[i] >= nrel) return 0;
+#define COL_OK(b, c) ((b) < q->nrels && e->rel_shape(e->u, q->rels[(b)], &rows, &nc) == 0 && (c) < nc)
+    for (size_t i = 0; i < q->npreds; i++) {
+        const pred_t* p = &q->preds[i];
+        if (p->type < 0 || !COL_OK(p->frel, p->fcol)) return 0;
+        if (p->type == 0 && !COL_OK(p->srel, p->scol)) return 0;
+    }
+    for (size_t i = 0; i < q->nsel; i++)
+        if (!COL_OK(q->sel[2 * i], q->sel[2 * i + 1])) return 0;
+#undef COL_OK
+    return 1;
+}
+
+/* 0: the query's output is the relational answer the plan computes; QE_ENOTSUP otherwise */
+static int plan_check(const qe_engine* e, const query_t* q) {
+    g_why[0] = 0;
+    if (!s_query_valid(e, q)) return refuse("out-of-range relation / column / binding (the reference is undefined)");
+    if (q->nsel == 0) return refuse("no select");
+    replay_t r;
+    memset(&r, 0, sizeof r);
+    r.q = q;
+    r.cap_entries = q->nrels + 1;
+    r.parent = (int*)malloc((q->nrels + 1) * sizeof(int));
+    for (size_t i = 0; i <= q->nrels; i++) r.parent[i] = (int)i;
+    uint8_t* live = (uint8_t*)calloc(q->nrels + 1, 1);
+    r.live = live;
+    int rc = 0, seen_join = 0;
+    for (size_t i = 0; rc == 0 && i < q->npreds; i++) {
+        memset(live, 0, q->nrels + 1);
+        for (size_t k = i + 1; k < q->npreds; k++) {
+            live[q->preds[k].frel] = 1;
+            if (q->preds[k].type == 0) live[q->preds[k].srel] = 1;
+        }
+        for (size_t s = 0; s < q->nsel; s++) live[q->sel[2 * s]] = 1;
+        const pred_t* p = &q->preds[i];
+        if (p->type == 1) {                              /* execute_filter (src/filter.c:66-100) */
+            if (!op_valid(p->op)) { rc = refuse("filter operator '%c'", p->op); break; }
+            if (seen_join) { rc = refuse("filter after a join"); break; }
+            sexists_t ex = s_exists(&r, q->rels[p->frel], p->frel);
+            if (ex.idx != -1) {
+                slist* l = &r.L[r.E[ex.ent].e[ex.idx].l];
+                l->tag = ++r.fresh;
+                l->len = ++r.fresh;
+            } else {
+                sent* E = r.ne == 0 ? s_new_entity(&r) : &r.E[r.ne - 1];
+                const int tag = ++r.fresh, len = ++r.fresh;
+                smid m = {q->rels[p->frel], p->frel, -1, new_slist(&r, tag, len, 1, 1, -1)};
+                s_push(&r, E, m);
+            }
+        } else {
+            seen_join = 1;
+            rc = s_join(&r, p);
+        }
+    }
+    for (size_t s = 0; rc == 0 && s < q->nsel; s++) {   /* print_sums (src/utilities.c:197-224) */
+        const uint64_t b = q->sel[2 * s];
+        sexists_t ex = s_exists(&r, q->rels[b], b);
+        if (ex.idx == -1) rc = refuse("select of binding %llu without a list (the reference exits)", (unsigned long long)b);
+        else if (!r.L[r.E[ex.ent].e[ex.idx].l].ok)
+            rc = refuse("select of binding %llu whose list is not relational", (unsigned long long)b);
+    }
+    for (size_t i = 0; i < r.ne; i++) free(r.E[i].e);
+    free(r.E);
+    free(r.L);
+    free(r.parent);
+    free(live);
+    return rc;
+}
+
+/* ============================================================================================ */
+/* (2) the relational plan                                                                      */
+/* ============================================================================================ */
+
+#define NONE ((qe_h)0)
+
+typedef struct { int b; qe_h rows; int whole; } member;          /* whole: every row of the relation */
+typedef struct { member* m; int n; uint64_t size; int alive; } comp_t;
+
+typedef struct {
+    const qe_engine* e;
+    const query_t* q;
+    comp_t* C; int nc;
+    int* comp_of;               /* binding -> component, -1 none */
+    qe_h* list;                 /* filtered, not yet joined bindings */
+    uint64_t* list_size;
+    int rc;
+} plan_t;
+
+#define ECHK(call)                                   \
+    do {                                             \
+        int rc_ = (call);                            \
+        if (rc_ != 0) { P->rc = rc_; return rc_; }   \
+    } while (0)
+
+static void owned_range(const plan_t* P, uint64_t rows, uint64_t* s, uint64_t* t) {
+    const uint64_t W = P->e->world, r = P->e->rank;
+    *s = rows * r / W;
+    *t = rows * (r + 1) / W;
+}
+
+static uint64_t rel_rows(const plan_t* P, uint32_t rel) {
+    uint64_t rows = 0;
+    uint32_t nc = 0;
+    P->e->rel_shape(P->e->u, rel, &rows, &nc);
+    return rows;
+}
+
+static int allreduce1(plan_t* P, uint64_t* v) {
+    if (P->e->world == 1) return 0;
+    return P->e->allreduce(P->e->u, v, 1);
+}
+
+static void rel(plan_t* P, qe_h h) {
+    if (h != NONE) P->e->release(P->e->u, h);
+}
+
+static int component(plan_t* P, int b) {
+    if (P->comp_of[b] >= 0) return P->comp_of[b];
+    comp_t* c = &P->C[P->nc];
+    c->m = (member*)calloc(P->q->nrels + 1, sizeof(member));
+    c->n = 1;
+    c->alive = 1;
+    c->m[0].b = b;
+    if (P->list[b] != NONE) {
+        c->m[0].rows = P->list[b];
+        c->size = P->list_size[b];
+        P->list[b] = NONE;
+    } else {
+        c->m[0].whole = 1;
+        c->size = rel_rows(P, P->q->rels[b]);
+    }
+    P->comp_of[b] = P->nc;
+    return P->nc++;
+}
+
+static int rows_of(plan_t* P, member* m) {
+    if (m->whole) {
+        uint64_t s, t;
+        owned_range(P, rel_rows(P, P->q->rels[m->b]), &s, &t);
+        ECHK(P->e->iota(P->e->u, s, t - s, &m->rows));
+        m->whole = 0;
+    }
+    return 0;
+}
+
+static int member_idx(const comp_t* c, int b) {
+    for (int i = 0; i < c->n; i++)
+        if (c->m[i].b == b) return i;
+    return -1;
+}
+
+/* one join side: keys + (vals | positions) and the bindings carried through the join */
+typedef struct {
+    qe_h keys, vals;            /* vals: rowids aligned with keys, or NONE (row = position / base row i) */
+    int ncar;
+    int car_b[64];
+    qe_h car_rows[64];          /* NONE: the binding's rowids are `vals` */
+    qe_h ticket;                /* an exchange in flight */
+    int keep_n;
+    int keep_b[64];
+    int base;                   /* keys is a whole base column (vals NONE = row i) */
+} side_t;
+
+static int side_start(plan_t* P, int cid, int b, uint32_t col, const uint8_t* need, side_t* s) {
+    const qe_engine* e = P->e;
+    comp_t* c = &P->C[cid];
+    memset(s, 0, sizeof *s);
+    if (c->n == 1 && c->m[0].b == b && c->m[0].whole) {      /* a whole base relation: never exchanged */
+        ECHK(e->base_side(e->u, P->q->rels[b], col, &s->keys, &s->vals));
+        s->base = 1;
+        if (need[b]) {
+            s->ncar = 1;
+            s->car_b[0] = b;
+            s->car_rows[0] = NONE;
+        }
+        return 0;
+    }
+    member* mb = &c->m[member_idx(c, b)];
+    ECHK(rows_of(P, mb));
+    ECHK(e->keys(e->u, P->q->rels[b], col, mb->rows, &s->keys));
+    qe_h cols[64];
+    int nk = 0;
+    for (size_t x = 0; x <= P->q->nrels; x++) {               /* carried: the bindings read later */
+        int mi = member_idx(c, (int)x);
+        if (mi < 0 || !need[x]) continue;
+        ECHK(rows_of(P, &c->m[mi]));
+        s->keep_b[nk] = (int)x;
+        cols[nk++] = c->m[mi].rows;
+    }
+    s->keep_n = nk;
+    if (e->world > 1) {
+        /* the carried lists travel with the keys (consumed); the others are dropped */
+        for (int i = 0; i < c->n; i++) {
+            int kept = 0;
+            for (int k = 0; k < nk; k++) kept |= c->m[i].b == s->keep_b[k];
+            if (!kept) rel(P, c->m[i].rows);
+            c->m[i].rows = NONE;
+        }
+        ECHK(e->exchange_start(e->u, s->keys, cols, nk, &s->ticket));
+        s->keys = NONE;
+        return 0;
+    }
+    for (int k = 0; k < nk; k++) {
+        s->car_b[k] = s->keep_b[k];
+        s->car_rows[k] = cols[k];
+    }
+    s->ncar = nk;
+    if (nk == 1) {                                           /* the only carried list rides as vals */
+        s->vals = cols[0];
+        s->car_rows[0] = NONE;
+    }
+    for (int i = 0; i < c->n; i++) {                         /* ownership moves to the side */
+        int kept = 0;
+        for (int k = 0; k < nk; k++) kept |= c->m[i].b == s->keep_b[k];
+        if (!kept) rel(P, c->m[i].rows);
+        c->m[i].rows = NONE;
+    }
+    return 0;
+}
+
+static int side_finish(plan_t* P, side_t* s) {
+    if (!s->ticket) return 0;
+    qe_h cols[64];
+    ECHK(P->e->exchange_finish(P->e->u, s->ticket, &s->keys, cols));
+    s->ticket = NONE;
+    s->ncar = s->keep_n;
+    for (int k = 0; k < s->keep_n; k++) {
+        s->car_b[k] = s->keep_b[k];
+        s->car_rows[k] = cols[k];
+    }
+    if (s->keep_n == 1) {
+        s->vals = cols[0];
+        s->car_rows[0] = NONE;
+    }
+    return 0;
+}
+
+static void free_comp(plan_t* P, int cid) {
+    comp_t* c = &P->C[cid];
+    for (int i = 0; i < c->n; i++) rel(P, c->m[i].rows);
+    free(c->m);
+    c->m = NULL;
+    c->n = 0;
+    c->alive = 0;
+}
+
+static int do_join(plan_t* P, const pred_t* p, const uint8_t* need) {
+    const qe_engine* e = P->e;
+    const int ba = (int)p->frel, bb = (int)p->srel;
+    const int A = component(P, ba), B = component(P, bb);
+    side_t sa, sb;
+    /* derived sides first, so their exchanges overlap the base side's local bucket scan */
+    const int a_base = P->C[A].n == 1 && P->C[A].m[0].whole;
+    if (a_base) {
+        ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, &sb));
+        ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, &sa));
+    } else {
+        ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, &sa));
+        ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, &sb));
+    }
+    ECHK(side_finish(P, &sa));
+    ECHK(side_finish(P, &sb));
+    qe_h oa = NONE, ob = NONE;
+    ECHK(e->join(e->u, sa.keys, sa.vals, sb.keys, sb.vals, &oa, &ob));
+    /* the merged component: carried bindings, rowids = o (vals rode along) or take(rows, o) */
+    member* m = (member*)calloc(P->q->nrels + 1, sizeof(member));
+    int n = 0;
+    side_t* sides[2] = {&sa, &sb};
+    qe_h outs[2] = {oa, ob};
+    int used[2] = {0, 0};
+    for (int k = 0; k < 2; k++) {
+        side_t* s = sides[k];
+        for (int i = 0; i < s->ncar; i++) {
+            m[n].b = s->car_b[i];
+            if (s->car_rows[i] == NONE) {
+                m[n].rows = outs[k];
+                used[k] = 1;
+            } else {
+                ECHK(e->take(e->u, s->car_rows[i], outs[k], &m[n].rows));
+                rel(P, s->car_rows[i]);
+            }
+            n++;
+        }
+    }
+    if (n == 0) {                                           /* nothing read later: keep the count */
+        m[0].b = ba;
+        m[0].rows = oa;
+        used[0] = 1;
+        n = 1;
+    }
+    rel(P, sa.keys);                     /* (a borrowed base column: the engine's release is a no-op) */
+    rel(P, sb.keys);
+    rel(P, sa.vals);
+    rel(P, sb.vals);
+    if (!used[0]) rel(P, oa);
+    if (!used[1]) rel(P, ob);
+    uint64_t size = 0;
+    ECHK(e->length(e->u, m[0].rows, &size));
+    ECHK(allreduce1(P, &size));
+    /* A absorbs B */
+    free_comp(P, A);
+    free_comp(P, B);
+    for (size_t x = 0; x <= P->q->nrels; x++)
+        if (P->comp_of[x] == A || P->comp_of[x] == B) P->comp_of[x] = A;
+    P->C[A].m = m;
+    P->C[A].n = n;
+    P->C[A].size = size;
+    P->C[A].alive = 1;
+    return 0;
+}
+
+static uint64_t join_cost(plan_t* P, const pred_t* p) {
+    uint64_t c = 0;
+    const int bs[2] = {(int)p->frel, (int)p->srel};
+    for (int k = 0; k < 2; k++) {
+        const int b = bs[k];
+        if (P->comp_of[b] >= 0) c += P->C[P->comp_of[b]].size;
+        else if (P->list[b] != NONE) c += P->list_size[b];
+        else c += rel_rows(P, P->q->rels[b]);
+    }
+    return c;
+}
+
+static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t* rows_out) {
+    plan_t PP;
+    plan_t* P = &PP;
+    memset(P, 0, sizeof *P);
+    P->e = e;
+    P->q = q;
+    const size_t nb = q->nrels + 1;
+    P->C = (comp_t*)calloc(nb + q->npreds + 1, sizeof(comp_t));
+    P->comp_of = (int*)malloc(nb * sizeof(int));
+    P->list = (qe_h*)calloc(nb, sizeof(qe_h));
+    P->list_size = (uint64_t*)calloc(nb, sizeof(uint64_t));
+    for (size_t i = 0; i < nb; i++) P->comp_of[i] = -1;
+    const int reorder = !(getenv("QE_DIST_REORDER") && getenv("QE_DIST_REORDER")[0] == '0');
+    uint8_t* need = (uint8_t*)calloc(nb, 1);
+    int* pending = (int*)malloc((q->npreds + 1) * sizeof(int));
+    size_t k = 0;
+    int rc = 0;
+    while (rc == 0 && k < q->npreds) {
+        const pred_t* p = &q->preds[k];
+        if (p->type == 1) {                                  /* filters (they all precede the joins) */
+            const int b = (int)p->frel;
+            const uint32_t relid = q->rels[b];
+            if (P->list[b] != NONE) {
+                qe_h nl = NONE;
+                rc = e->refine(e->u, relid, (uint32_t)p->fcol, P->list[b], p->op, p->cval, &nl);
+                P->list[b] = nl;
+                uint64_t n = 0;
+                if (!rc) rc = e->length(e->u, nl, &n);
+                if (!rc) rc = allreduce1(P, &n);
+                P->list_size[b] = n;
+                if (!rc) fprintf(out, "%d\n", (int)(uint32_t)n);        /* src/filter.c:32 */
+            } else {
+                uint64_t s, t;
+                owned_range(P, rel_rows(P, relid), &s, &t);
+                rc = e->scan(e->u, relid, (uint32_t)p->fcol, s, t, p->op, p->cval, &P->list[b]);
+                uint64_t n = 0;
+                if (!rc) rc = e->length(e->u, P->list[b], &n);
+                if (!rc) rc = allreduce1(P, &n);
+                P->list_size[b] = n;
+            }
+            k++;
+            continue;
+        }
+        size_t end = k;                                      /* the run of joins */
+        while (end < q->npreds && q->preds[end].type == 0) end++;
+        size_t np = 0;
+        for (size_t i = k; i < end; i++) pending[np++] = (int)i;
+        while (rc == 0 && np) {
+            size_t jbest = 0;
+            if (reorder) {                                   /* greedy: the smallest |A| + |B| first */
+                uint64_t best = UINT64_MAX;
+                for (size_t i = 0; i < np; i++) {
+                    uint64_t c = join_cost(P, &q->preds[pending[i]]);
+                    if (c < best) { best = c; jbest = i; }
+                }
+            }
+            const pred_t* jp = &q->preds[pending[jbest]];
+            for (size_t i = jbest; i + 1 < np; i++) pending[i] = pending[i + 1];
+            np--;
+            /* bindings read later: the remaining joins, later predicates, the selects */
+            memset(need, 0, nb);
+            for (size_t s = 0; s < q->nsel; s++) need[q->sel[2 * s]] = 1;
+            for (size_t i = 0; i < np; i++) {
+                need[q->preds[pending[i]].frel] = 1;
+                need[q->preds[pending[i]].srel] = 1;
+            }
+            for (size_t i = end; i < q->npreds; i++) {
+                need[q->preds[i].frel] = 1;
+                if (q->preds[i].type == 0) need[q->preds[i].srel] = 1;
+            }
+            rc = do_join(P, jp, need);
+        }
+        k = end;
+    }
+    /* print_sums: every select's sum at once, one all-reduce */
+    uint64_t* sums = (uint64_t*)calloc(q->nsel + 1, sizeof(uint64_t));
+    uint32_t* srel = (uint32_t*)calloc(q->nsel + 1, sizeof(uint32_t));
+    uint32_t* scol = (uint32_t*)calloc(q->nsel + 1, sizeof(uint32_t));
+    qe_h* srows = (qe_h*)calloc(q->nsel + 1, sizeof(qe_h));
+    uint64_t* ssize = (uint64_t*)calloc(q->nsel + 1, sizeof(uint64_t));
+    int ns = 0;
+    for (size_t s = 0; rc == 0 && s < q->nsel; s++) {
+        const int b = (int)q->sel[2 * s];
+        uint64_t size;
+        qe_h rows;
+        if (P->comp_of[b] >= 0) {
+            comp_t* c = &P->C[P->comp_of[b]];
+            member* m = &c->m[member_idx(c, b)];
+            rc = rows_of(P, m);
+            rows = m->rows;
+            size = c->size;
+        } else {
+            rows = P->list[b];
+            size = P->list_size[b];
+        }
+        ssize[s] = size;
+        if (size == 0 || rc) continue;
+        srel[ns] = q->rels[b];
+        scol[ns] = (uint32_t)q->sel[2 * s + 1];
+        srows[ns++] = rows;
+    }
+    if (rc == 0 && ns) rc = e->checksums(e->u, ns, srel, scol, srows, sums);
+    if (rc == 0 && ns && e->world > 1) rc = e->allreduce(e->u, sums, ns);
+    if (rc == 0) {
+        int j = 0;
+        for (size_t s = 0; s < q->nsel; s++) {
+            if (ssize[s] == 0) fputs("NULL ", out);
+            else fprintf(out, "%lu ", (unsigned long)sums[j++]);
+        }
+        fputc('\n', out);
+        if (rows_out) *rows_out = ssize[0];
+    }
+    free(sums);
+    free(srel);
+    free(scol);
+    free(srows);
+    free(ssize);
+    for (int i = 0; i < P->nc; i++)
+        if (P->C[i].alive) free_comp(P, i);
+    for (size_t b = 0; b < nb; b++) rel(P, P->list[b]);
+    free(P->C);
+    free(P->comp_of);
+    free(P->list);
+    free(P->list_size);
+    free(need);
+    free(pending);
+    return rc ? rc : P->rc;
+}
+
+/* ============================================================================================ */
+/* text drivers                                                                                   */
+/* ============================================================================================ */
+
+int qe_plan_check_text(const qe_engine* e, const char* text, uint8_t* accepted, size_t cap) {
+    size_t nq = 0;
+    query_t* qs = qe_parse_text(text, &nq);
+    char first[256] = "";
+    for (size_t i = 0; i < nq; i++) {
+        qe_arrange_predicates(&qs[i]);
+        int ok = plan_check(e, &qs[i]) == 0;
+        if (!ok && !first[0]) snprintf(first, sizeof first, "%s", g_why);
+        if (accepted && i < cap) accepted[i] = (uint8_t)ok;
+    }
+    snprintf(g_why, sizeof g_why, "%s", first);
+    qe_free_queries(qs, nq);
+    return (int)nq;
+}
+
+int qe_plan_run_text(const qe_engine* e, const char* text, char** out, size_t* outlen, uint64_t* rows,
+                     uint64_t* nrefused) {
+    *out = NULL;
+    *outlen = 0;
+    FILE* f = open_memstream(out, outlen);
+    if (!f) return QE_ENOMEM;
+    size_t nq = 0;
+    query_t* qs = qe_parse_text(text, &nq);     /* parsed before anything runs (main/queries_main.c:31-37) */
+    int rc = 0;
+    uint64_t refused = 0;
+    char first[256] = "";
+    for (size_t i = 0; rc == 0 && i < nq; i++) {
+        qe_arrange_predicates(&qs[i]);
+        if (plan_check(e, &qs[i]) != 0) {
+            if (!first[0]) snprintf(first, sizeof first, "%s", g_why);
+            refused++;
+            rc = e->fallback ? e->fallback(e->u, &qs[i], f) : QE_ENOTSUP;
+            continue;
+        }
+        uint64_t r = 0;
+        rc = plan_query(e, &qs[i], f, &r);
+        if (rc == 0 && rows) *rows = r;
+    }
+    snprintf(g_why, sizeof g_why, "%s", first);
+    qe_free_queries(qs, nq);
+    fclose(f);
+    if (nrefused) *nrefused = refused;
+    return rc;
+}

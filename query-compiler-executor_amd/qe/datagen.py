@@ -237,3 +237,29 @@ def c5_spec(rows: int = C5_ROWS, theta: float = C5_THETA, domain: int | None = N
     d = domain if domain is not None else rows
     z = ("zipf", d, theta, C5_PERM_SEED)
     return [RelSpec(rows, [("mod", rows), z, ("hi32",)]), RelSpec(rows, [z, ("mod", rows), ("hi32",)])]
+
+
+# ---- device-side generation of the bench workloads (libqe's generator, bit-exact with the above) --
+def gen_c4(ctx, scale: float = 1.0) -> list[RelSpec]:
+    """the 14 C4 relations generated in HBM by libqe (qe_gen_relation)"""
+    specs = c4_spec(scale)
+    for r, sp in enumerate(specs):
+        ctx.gen_relation(sp.rows, sp.kinds, seed=C4_SEED, gen_rel=r)
+    ctx.sync()
+    return specs
+
+
+def gen_c5(ctx, rows: int, row_start: int = 0, total_rows: int | None = None) -> list[RelSpec]:
+    """relations r0, r1 of c5_spec(total_rows) -- rows [row_start, row_start + rows) of each --
+    generated in HBM.  The Zipf CDF is built by libqe in a fixed summation order: the same keys on
+    every run."""
+    n = total_rows or rows
+    specs = c5_spec(n)
+    ctx.set_zipf(n, C5_THETA, C5_PERM_SEED)
+    try:
+        for r, sp in enumerate(specs):
+            ctx.gen_relation(rows, sp.kinds, seed=C5_SEED, gen_rel=r, row_start=row_start)
+    finally:
+        ctx.set_zipf_table(0, 0, 0)
+    return specs
+

@@ -316,6 +316,17 @@ class Ctx:
         self._chk(self.lib.qe_pairs_to_host(self.h, C.byref(p), k.ctypes.data, None))
         return k
 
+    def column_range_to_host(self, rel: int, col: int, start: int, n: int) -> np.ndarray:
+        """values [start, start + n) of a device column, on the host"""
+        c = self.column(rel, col)
+        n = max(0, min(n, c.n - start))
+        k = np.empty(n, dtype=np.uint64)
+        if n:
+            p = Pairs()
+            p.key, p.val, p.match, p.n = c.d + 8 * start, None, None, n
+            self._chk(self.lib.qe_pairs_to_host(self.h, C.byref(p), k.ctypes.data, None))
+        return k
+
     def merge_join_counts(self, R: Pairs, S: Pairs) -> int:
         P = C.c_uint64()
         self._chk(self.lib.qe_merge_join_counts(self.h, C.byref(R), C.byref(S), C.byref(P)))

@@ -6,6 +6,8 @@ chain:  R0.c1 = R1.c0, R1.c1 = R2.c0, R2.c1 = R3.c0 with an optional row filter 
 """
 import numpy as np
 
+M64 = (1 << 64) - 1
+
 
 def _bincount_u(keys, weights, domain):
     """exact integer bincount (weights are small non-negative ints; float64 is exact < 2^53)"""
@@ -44,3 +46,23 @@ def pair_sums(R0, R1, domain):
     with np.errstate(over="ignore"):
         return int(np.sum(cs, dtype=np.uint64)), int(np.sum(cs * R0[2], dtype=np.uint64)), \
             int(np.sum(cr * R1[2], dtype=np.uint64))
+
+
+def sharded_pair_sums(kR, vR, kS, vS, domain, shards):
+    """R.key = S.key: (pairs, sum over pairs of vR, sum over pairs of vS) mod 2^64, per key range
+    [lo, hi): counts cR, cS over the range, pairs += sum cR * cS, sums += cS[kR] * vR / cR[kS] * vS
+    (int64 arithmetic wraps: exact mod 2^64)"""
+    import torch
+    pairs = sa = sb = 0
+    for s in range(shards):
+        lo, hi = domain * s // shards, domain * (s + 1) // shards
+        mR = (kR >= lo) & (kR < hi)
+        mS = (kS >= lo) & (kS < hi)
+        r_idx, s_idx = kR[mR] - lo, kS[mS] - lo
+        cR = torch.bincount(r_idx, minlength=hi - lo)
+        cS = torch.bincount(s_idx, minlength=hi - lo)
+        pairs += int((cR * cS).sum().item())
+        sa += int((cS[r_idx] * vR[mR]).sum().item())
+        sb += int((cR[s_idx] * vS[mS]).sum().item())
+        del mR, mS, r_idx, s_idx, cR, cS
+    return pairs & M64, sa & M64, sb & M64

@@ -32,7 +32,8 @@ def agg_worker(rank, world, port, rows, queries, outq):
     import torch
     import torch.distributed as dist
 
-    from qe import c5bench, lib
+    from qe import datagen as dg
+    from qe import lib
     from qe.dist import DistAggJoin, GPUEngine
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -40,7 +41,7 @@ def agg_worker(rank, world, port, rows, queries, outq):
     torch.cuda.set_device(0)
     ctx = lib.Ctx(0)
     try:
-        c5bench.gen_c5(ctx, rows)
+        dg.gen_c5(ctx, rows)
         ex = DistAggJoin(GPUEngine(ctx, rank, world), [rows, rows])
         res = [ex.run(q) for q in queries]
         if rank == 0:

@@ -1,0 +1,250 @@
+"""A numpy (+ torch.distributed gloo) engine for the C partitioned plan (include/qe_plan.h) through
+ctypes, so the plan that drives libqe + RCCL on the GPUs -- the same compiled C -- runs on CPU
+ranks here.  TEST INFRASTRUCTURE ONLY: the product engine is libqe's (qe_run_queries_dist)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import traceback
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SO = os.path.join(ROOT, "query-compiler-executor_amd", "build", "libqeplan.so")
+
+_OPS = {"=": np.equal, ">": np.greater, "<": np.less}
+I, U32, U64, VP, H = C.c_int, C.c_uint32, C.c_uint64, C.c_void_p, C.c_uint64
+P = C.POINTER
+
+FIELDS = [
+    ("rel_count", C.CFUNCTYPE(I, VP, P(U32))),
+    ("rel_shape", C.CFUNCTYPE(I, VP, U32, P(U64), P(U32))),
+    ("scan", C.CFUNCTYPE(I, VP, U32, U32, U64, U64, C.c_char, U64, P(H))),
+    ("iota", C.CFUNCTYPE(I, VP, U64, U64, P(H))),
+    ("refine", C.CFUNCTYPE(I, VP, U32, U32, H, C.c_char, U64, P(H))),
+    ("keys", C.CFUNCTYPE(I, VP, U32, U32, H, P(H))),
+    ("base_side", C.CFUNCTYPE(I, VP, U32, U32, P(H), P(H))),
+    ("exchange_start", C.CFUNCTYPE(I, VP, H, P(H), I, P(H))),
+    ("exchange_finish", C.CFUNCTYPE(I, VP, H, P(H), P(H))),
+    ("join", C.CFUNCTYPE(I, VP, H, H, H, H, P(H), P(H))),
+    ("take", C.CFUNCTYPE(I, VP, H, H, P(H))),
+    ("length", C.CFUNCTYPE(I, VP, H, P(U64))),
+    ("checksums", C.CFUNCTYPE(I, VP, I, P(U32), P(U32), P(H), P(U64))),
+    ("allreduce", C.CFUNCTYPE(I, VP, P(U64), I)),
+    ("release", C.CFUNCTYPE(None, VP, H)),
+    ("fallback", C.CFUNCTYPE(I, VP, VP, VP)),
+]
+
+
+class Engine(C.Structure):
+    _fields_ = [("u", VP), ("rank", U32), ("world", U32)] + FIELDS
+
+
+def part_of(k: np.ndarray, nparts: int) -> np.ndarray:
+    """qe_partition's destination: (hi32((k ^ k >> 29) * 0xbf58476d1ce4e5b9) * nparts) >> 32"""
+    k = np.asarray(k, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        h = (k ^ (k >> np.uint64(29))) * np.uint64(0xbf58476d1ce4e5b9)
+    return ((h >> np.uint64(32)) * np.uint64(nparts)) >> np.uint64(32)
+
+
+def join_local(ka, kb):
+    """every (i, j) with ka[i] == kb[j]: i ascending by key (stable), j in kb's stable key order"""
+    oa = np.argsort(ka, kind="stable")
+    ob = np.argsort(kb, kind="stable")
+    sa, sb = ka[oa], kb[ob]
+    lo = np.searchsorted(sb, sa, "left")
+    hi = np.searchsorted(sb, sa, "right")
+    c = hi - lo
+    ia = np.repeat(oa, c)
+    starts = np.repeat(lo - np.concatenate([[0], np.cumsum(c)[:-1]]).astype(np.int64), c)
+    ib = ob[starts + np.arange(int(c.sum()))]
+    return ia.astype(np.uint32), ib.astype(np.uint32)
+
+
+class NumpyPlanEngine:
+    """one rank: relations replicated as numpy columns; handles index a dict of arrays"""
+
+    def __init__(self, rels, rank=0, world=1, group=None):
+        self.rels, self.rank, self.world, self.group = rels, rank, world, group
+        self.h, self.next, self.borrowed = {}, 1, set()
+        self.exchanges = 0
+        self.lib = C.CDLL(SO)
+        self.lib.qe_plan_run_text.argtypes = [P(Engine), C.c_char_p, P(C.c_void_p), P(C.c_size_t), P(U64), P(U64)]
+        self.lib.qe_plan_check_text.argtypes = [P(Engine), C.c_char_p, P(C.c_uint8), C.c_size_t]
+        self.lib.qe_plan_why.restype = C.c_char_p
+        self.libc = C.CDLL(None)
+        self.libc.free.argtypes = [C.c_void_p]
+        self._cbs = []
+        e = Engine()
+        e.u, e.rank, e.world = None, rank, world
+        for name, ftype in FIELDS:
+            if name == "fallback":
+                setattr(e, name, ftype())            # NULL: refused queries return QE_ENOTSUP
+                continue
+            fn = self._wrap(getattr(self, "cb_" + name), name == "release")
+            cb = ftype(fn)
+            self._cbs.append(cb)
+            setattr(e, name, cb)
+        self.e = e
+
+    # -- plumbing
+    def _wrap(self, f, void):
+        def g(*a):
+            try:
+                r = f(*a)
+                return None if void else (0 if r is None else r)
+            except Exception:
+                traceback.print_exc()
+                return None if void else -1
+        return g
+
+    def put(self, arr, borrowed=False) -> int:
+        k = self.next
+        self.next += 1
+        self.h[k] = arr
+        if borrowed:
+            self.borrowed.add(k)
+        return k
+
+    def get(self, k):
+        return self.h[k]
+
+    # -- the C entry points
+    def run(self, text: str):
+        """(stdout, rc, rows, refused)"""
+        out, n, rows, nref = C.c_void_p(), C.c_size_t(), U64(), U64()
+        rc = self.lib.qe_plan_run_text(C.byref(self.e), text.encode(), C.byref(out), C.byref(n), C.byref(rows),
+                                       C.byref(nref))
+        s = C.string_at(out, n.value).decode("latin-1") if out.value else ""
+        if out.value:
+            self.libc.free(out)
+        return s, rc, rows.value, nref.value
+
+    def check(self, text: str):
+        acc = (C.c_uint8 * 4096)()
+        nq = self.lib.qe_plan_check_text(C.byref(self.e), text.encode(), acc, 4096)
+        return [bool(acc[i]) for i in range(nq)], self.lib.qe_plan_why().decode()
+
+    def live_handles(self) -> int:
+        return len(self.h) - len(self.borrowed)
+
+    # -- engine callbacks
+    def cb_rel_count(self, u, n):
+        n[0] = len(self.rels)
+
+    def cb_rel_shape(self, u, rel, rows, ncols):
+        if rel >= len(self.rels):
+            return -1
+        rows[0] = len(self.rels[rel][0]) if self.rels[rel] else 0
+        ncols[0] = len(self.rels[rel])
+
+    def cb_scan(self, u, rel, col, s, t, op, v, out):
+        c = self.rels[rel][col][s:t]
+        out[0] = self.put((np.nonzero(_OPS[op.decode()](c, np.uint64(v)))[0] + s).astype(np.uint32))
+
+    def cb_iota(self, u, s, n, out):
+        out[0] = self.put(np.arange(s, s + n, dtype=np.uint32))
+
+    def cb_refine(self, u, rel, col, rows, op, v, out):
+        r = self.h.pop(rows)
+        out[0] = self.put(r[_OPS[op.decode()](self.rels[rel][col][r], np.uint64(v))])
+
+    def cb_keys(self, u, rel, col, rows, out):
+        out[0] = self.put(self.rels[rel][col][self.get(rows)])
+
+    def cb_base_side(self, u, rel, col, keys, rowids):
+        c = self.rels[rel][col]
+        if self.world == 1:
+            keys[0] = self.put(c, borrowed=True)
+            rowids[0] = 0
+            return
+        mask = part_of(c, self.world) == np.uint64(self.rank)
+        rows = np.nonzero(mask)[0]
+        # an unordered bucket, like qe_bucket_select's: shuffle so no test depends on its order
+        rows = np.random.default_rng(self.rank + 17).permutation(rows).astype(np.uint32)
+        keys[0] = self.put(c[rows])
+        rowids[0] = self.put(rows)
+
+    def cb_exchange_start(self, u, keys, cols, ncols, ticket):
+        import torch
+        import torch.distributed as dist
+        self.exchanges += 1
+        k = self.h.pop(keys)
+        cs = [self.h.pop(cols[i]) for i in range(ncols)]
+        dest = part_of(k, self.world).astype(np.int64)
+        order = np.argsort(dest, kind="stable")
+        counts = np.bincount(dest, minlength=self.world).astype(np.int64)
+        cnt = torch.from_numpy(counts)
+        rcnt = torch.empty_like(cnt)
+        dist.all_to_all_single(rcnt, cnt, group=self.group)
+        osp, isp = rcnt.tolist(), counts.tolist()
+        outs = []
+        for arr, dt in [(k.view(np.int64), torch.int64)] + [(c.view(np.int32), torch.int32) for c in cs]:
+            s = torch.from_numpy(np.ascontiguousarray(arr[order]))
+            r = torch.empty(sum(osp), dtype=dt)
+            dist.all_to_all_single(r, s, osp, isp, group=self.group)
+            outs.append(r.numpy())
+        ticket[0] = self.put((outs[0].view(np.uint64), [o.view(np.uint32) for o in outs[1:]]))
+
+    def cb_exchange_finish(self, u, ticket, keys, cols):
+        k, cs = self.h.pop(ticket)
+        keys[0] = self.put(k)
+        for i, c in enumerate(cs):
+            cols[i] = self.put(c)
+
+    def cb_join(self, u, ka, va, kb, vb, oa, ob):
+        ia, ib = join_local(self.get(ka), self.get(kb))
+        oa[0] = self.put(self.get(va)[ia] if va else ia)
+        ob[0] = self.put(self.get(vb)[ib] if vb else ib)
+
+    def cb_take(self, u, src, idx, out):
+        out[0] = self.put(self.get(src)[self.get(idx)])
+
+    def cb_length(self, u, h, n):
+        n[0] = len(self.get(h))
+
+    def cb_checksums(self, u, n, rels, cols, rows, sums):
+        for i in range(n):
+            sums[i] = int(np.sum(self.rels[rels[i]][cols[i]][self.get(rows[i])], dtype=np.uint64))
+
+    def cb_allreduce(self, u, v, n):
+        if self.world == 1 or n == 0:
+            return
+        import torch
+        import torch.distributed as dist
+        a = np.array([v[i] for i in range(n)], dtype=np.uint64)
+        t = torch.from_numpy(a.view(np.int64).copy())
+        dist.all_reduce(t, group=self.group)
+        r = t.numpy().view(np.uint64)
+        for i in range(n):
+            v[i] = int(r[i])
+
+    def cb_release(self, u, h):
+        if h in self.borrowed:
+            return
+        self.h.pop(h, None)
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def worker(rank, world, port, rels, queries, outq):
+    """one gloo rank: every query through the C plan, rank 0 reports (stdout, rc, rows, refused)"""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        eng = NumpyPlanEngine(rels, rank, world)
+        res = [eng.run(q) for q in queries]
+        if rank == 0:
+            outq.put((res, eng.exchanges, eng.live_handles()))
+    finally:
+        dist.destroy_process_group()

@@ -35,3 +35,15 @@ def test_chain_truth_small_vs_enumeration():
                 s[0] += a * int(R1[2][r1]); s[1] += a * int(R2[2][r2]); s[2] += a * int(R3[2][r3])
     assert rows == tot
     assert sums == [x % (1 << 64) for x in s]
+
+
+def test_sharded_truth_matches_numpy_small():
+    """the torch key-range-sharded checker (used at 1e9 rows on the GPU) against pair_sums on a
+    small Zipf case, on the CPU"""
+    import torch
+    n = 200_000
+    rels = dg.make_relations(dg.c5_spec(n), dg.C5_SEED)
+    t = [[torch.from_numpy(c.view(np.int64)) for c in r] for r in rels]
+    want = agg_truth.pair_sums(rels[0], rels[1], n)
+    for shards in (1, 3):
+        assert agg_truth.sharded_pair_sums(t[0][1], t[0][2], t[1][0], t[1][2], n, shards) == want

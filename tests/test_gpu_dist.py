@@ -149,12 +149,11 @@ def test_gpu_plan_two_ranks_share_one_gpu(ctx):
 def test_gpu_agg_plan_equals_faithful_executor_on_c5(ctx, world):
     """DistAggJoin (heavy split + local buckets + aggregate merge) on the GPU equals the faithful
     executor's aggregate path on the same Zipf data; world 2 = two gloo ranks on the one GPU"""
-    from qe import c5bench
     from qe.dist import DistAggJoin
     rows = 3_000_000
     queries = ["0 1|0.1=1.0|0.2 1.2", "0 1|0.1=1.0|1.2 0.2 0.0 1.1 0.1", "1 0|0.0=1.1|0.2 1.2"]
     ctx.drop_relations()
-    c5bench.gen_c5(ctx, rows)
+    dg.gen_c5(ctx, rows)
     want = [ctx.run(q + "\n")[0] for q in queries]
     if world == 1:
         res = [DistAggJoin(GPUEngine(ctx, 0, 1), [rows, rows]).run(q) for q in queries]

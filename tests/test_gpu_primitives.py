@@ -340,6 +340,27 @@ def test_join_payloads_short_edit_is_error(ctx):
         ctx.join_payloads(dc.d, 3, L, E)
 
 
+def test_join_payloads_beyond_the_materialisation_limit_is_etoobig(ctx):
+    """an expansion past the limit (the reference's DArray bound, INT32_MAX by default) fails
+    cleanly with QE_ETOOBIG before allocating, as the merge join does -- never a hipMalloc abort"""
+    n = 1000
+    L = ctx.list_from_host(np.arange(n, dtype=np.uint32))
+    E = ctx.list_from_host(np.arange(n, dtype=np.uint32))
+    dc = ctx.list_from_host(np.full(n, 2, dtype=np.uint32))      # P = 2000
+    ctx.set_materialize_limit(1999)
+    try:
+        with pytest.raises(lib.QEError) as e:
+            ctx.join_payloads(dc.d, n, L, E)
+        assert e.value.code == lib.QE_ETOOBIG
+        with pytest.raises(lib.QEError) as e:
+            ctx.join_payloads_multi(dc.d, n, L, [E, E])
+        assert e.value.code == lib.QE_ETOOBIG
+        ctx.set_materialize_limit(2000)
+        assert ctx.join_payloads(dc.d, n, L, E).n == 2000
+    finally:
+        ctx.set_materialize_limit(0x7FFFFFFF)
+
+
 @pytest.mark.parametrize("n", [0, 3, 1_000_001])
 def test_checksum_wraps_mod_2_64(ctx, n):
     a = np.full(2 * n + 1, (1 << 63) + 12345, dtype=np.uint64)

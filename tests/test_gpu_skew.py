@@ -237,10 +237,9 @@ def test_qe_set_zipf_is_deterministic_and_close_to_numpy(ctx):
 def test_c5_shape_100m_against_aggregate_truth(ctx):
     """the C5 query at 1e8 rows per side (P ~ 6.5e12 pairs: far past the limit) through the
     drop-in executor, against numpy aggregate push-down on the same (device-made) columns"""
-    from qe import c5bench
     N = 100_000_000
     ctx.drop_relations()
-    c5bench.gen_c5(ctx, N)
+    dg.gen_c5(ctx, N)
     out, rc = ctx.run(dg.C5_QUERY)
     assert rc == 0
     R0 = [ctx.column_to_host(0, c) for c in range(3)]

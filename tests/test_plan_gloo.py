@@ -1,0 +1,93 @@
+"""The C partitioned plan (include/qe_plan.h, host/qe_plan.c) on CPU: the same compiled plan that
+drives libqe + RCCL on the GPUs, over a numpy engine (tests/plan_engine.py) -- one rank here, and
+world_size 2 and 3 under torch.distributed gloo.
+
+* Domain check: every golden of the real reference either is refused (QE_ENOTSUP, the faithful
+  executor runs it) or comes out byte-identical -- W-class (positional garbage) outputs included.
+* Sharding: N ranks print what one rank prints, and C3 equals the aggregate truth."""
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import goldens
+import plan_engine as pe
+from qe import datagen as dg
+
+QE_ENOTSUP = -6
+C3 = "0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>1000000000&3.2<3000000000|1.2 2.2 3.2\n"
+
+
+def _run_world(rels, queries, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = pe.free_port()
+    procs = [ctx.Process(target=pe.worker, args=(r, world, port, rels, queries, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("fixture", [f.split("/")[-1][:-5] for f in goldens.golden_files()])
+def test_every_golden_is_refused_or_exact(fixture):
+    doc = goldens.load(f"{goldens.GOLDEN_DIR}/{fixture}.json")
+    rels, _ = goldens.dataset(doc["dataset"])
+    eng = pe.NumpyPlanEngine(rels, 0, 1)
+    accepted = {"T": 0, "W": 0}
+    for c in doc["cases"]:
+        out, rc, _, _ = eng.run(c["input"])
+        if rc == QE_ENOTSUP:
+            continue
+        assert rc == 0, (c["input"], rc)
+        assert (out, c["rc"]) == (c["stdout"], 0), c["input"]
+        accepted[c.get("class", "T")] = accepted.get(c.get("class", "T"), 0) + 1
+    assert eng.live_handles() == 0                     # the plan releases every array it made
+    t_cases = sum(c.get("class") == "T" for c in doc["cases"])
+    if fixture in ("c4", "fuzz_a", "fuzz_c", "headline"):
+        assert accepted["T"] >= 0.75 * t_cases, accepted   # the relational class is the plan's domain
+
+
+def test_check_names_the_reason():
+    rels = dg.make_relations(dg.chain_spec(4, 1000), 1)
+    eng = pe.NumpyPlanEngine(rels, 0, 1)
+    acc, why = eng.check("0 1|0.2>5&1.2<7&0.1=1.0|0.2\n")      # two filter lists: positional scan_join
+    assert acc == [False] and "scan_join" in why
+    acc, why = eng.check("0 1|0.1=1.0|0.2 1.2\n0 0|0.1=0.1|0.2\n")
+    assert acc == [True, False] and "DO_NOTHING" in why
+    acc, _ = eng.check(C3)
+    assert acc == [True]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_c3_chain_on_ranks_equals_one_rank_and_truth(world):
+    import agg_truth
+    rows = 60_000
+    rels = dg.make_relations(dg.chain_spec(4, rows), 1)
+    one = pe.NumpyPlanEngine(rels, 0, 1).run(C3)
+    c2 = rels[3][2]
+    mask = (c2 > np.uint64(1000000000)) & (c2 < np.uint64(3000000000))
+    cnt, nrows, sums = agg_truth.chain4_sums(rels, rows, mask)
+    want = f"{cnt}\n" + "".join(f"{s} " for s in sums) + "\n"
+    assert one[:3] == (want, 0, nrows)
+    res, nex, live = _run_world(rels, [C3, "0 1|0.1=1.0|0.2 1.2\n"], world)
+    assert res[0][:3] == (want, 0, nrows)
+    pairs_want = agg_truth.pair_sums(rels[0], rels[1], rows)
+    assert res[1][0] == f"{pairs_want[1]} {pairs_want[2]} \n"
+    # whole base relations are bucketed locally (replicated columns): only derived sides move --
+    # C3 reordered (R2-sigma(R3), then R1, then R0): one exchange per join; the 2-rel query none
+    assert nex == 3
+    assert live == 0
+
+
+def test_two_ranks_match_goldens():
+    doc = goldens.load(f"{goldens.GOLDEN_DIR}/fuzz_a.json")
+    rels, _ = goldens.dataset(doc["dataset"])
+    one = pe.NumpyPlanEngine(rels, 0, 1)
+    cases = [c for c in doc["cases"] if one.run(c["input"])[1] == 0][:60]
+    res, nex, _ = _run_world(rels, [c["input"] for c in cases], 2)
+    assert nex > 0 and len(cases) >= 40
+    for c, (out, rc, _, _) in zip(cases, res):
+        assert (out, rc) == (c["stdout"], 0), c["input"]
