@@ -10,10 +10,15 @@ One step = one full execution of that query: both filters, three sort-merge join
 mid_result payload propagation and the three checksums, printed exactly as the reference
 prints them.  `value` = chain rows produced per second (joined tuples/s), whole job.
 
-N = 1 runs libqe's faithful executor (the drop-in for the reference's execute_query).  N > 1
-runs the key-partitioned plan of qe.dist: every rank owns R rows of every
-relation (weak scaling), rows are hash-partitioned on the join key and exchanged with an RCCL
-all-to-all per join, and the checksums are all-reduced.
+N = 1 runs libqe's faithful executor (qe_run_queries, the drop-in for the reference's
+execute_queries).  N > 1 (and `--plan dist`) runs the key-partitioned plan, host C over an RCCL
+communicator (qe_run_queries_dist, include/qe_plan.h): every rank holds the
+relations, filters its rowid slice, exchanges the derived join sides by key (grouped
+ncclSend/ncclRecv on the communicator's stream), joins its bucket and all-reduces the sums.
+`--scaling strong` (default, the north star's shape): 100 M rows per relation in total, whatever N;
+`--scaling weak`: 100 M rows per relation per GPU.  Rank 0 checks the printed bytes in-run against
+the faithful executor on the same relations (and, for the default workload, against the C3 output
+pinned by tests/test_gpu_fullsize.py::test_c3_chain_100m) and reports `parity`.
 
 The JSON line also carries `roofline` (the dominant kernel's algorithmic GB/s from HIP events on
 the libqe stream, against the 8 TB/s HBM3E peak) and `cpu_baseline` (oracle/cpu_ref, the C
@@ -33,6 +38,9 @@ sys.path.insert(0, os.path.join(ROOT, "query-compiler-executor_amd"))
 sys.path.insert(0, ROOT)
 
 METRIC = "joined tuples/sec + achieved HBM GB/s, 4-rel chain join, 1/2/4/8 MI355X"
+# C3 at 100 M rows/relation, seed 1: the bytes tests/test_gpu_fullsize.py::test_c3_chain_100m pins
+# against the aggregate truth (itself pinned to the reference's G1-G3 goldens)
+C3_100M_STDOUT = "46567055\n100034367840717139 100020175372851973 93168255049607962 \n"
 QUERY = "0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>1000000000&3.2<3000000000|1.2 2.2 3.2\n"
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
@@ -80,57 +88,123 @@ def load_traffic(workload: str = "c3"):
 def cpu_baseline(sample_rows: int, seed: int, gpu_ctx):
     """oracle/cpu_ref (single thread) on a bounded sample of the same workload; the GPU runs
     the same sample so the two outputs are compared bit for bit."""
-    import ctypes as C
-
-    import numpy as np
-
+    from benchmarks.cpuref import CpuRef, cpu_model, pin_one_core
     from qe import datagen as dg
-    so = os.path.join(ROOT, "oracle", "build", "libcpuref.so")
-    if not os.path.exists(so):
-        import subprocess
-        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "cpuref"], check=True)
-    lib = C.CDLL(so)
-    lib.cpuref_create.restype = C.c_void_p
-    lib.cpuref_add_relation.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_void_p)]
-    lib.cpuref_run_str.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
-    lib.cpuref_destroy.argtypes = [C.c_void_p]
-    rels = dg.make_relations(dg.chain_spec(4, sample_rows), seed)
-    h = lib.cpuref_create()
-    keep = []
-    for cols in rels:
-        arr = (C.c_void_p * 3)(*[c.ctypes.data for c in cols])
-        keep.append(arr)
-        lib.cpuref_add_relation(h, sample_rows, 3, arr)
-    out, n = C.c_void_p(), C.c_size_t()
-    try:
-        os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})   # one pinned core
-    except Exception:
-        pass
-    t0 = time.perf_counter()
-    rc = lib.cpuref_run_str(h, QUERY.encode(), C.byref(out), C.byref(n))
-    dt = time.perf_counter() - t0
-    cpu_out = C.string_at(out, n.value).decode()
-    lib.cpuref_destroy(h)
+    cr = CpuRef()
+    for cols in dg.make_relations(dg.chain_spec(4, sample_rows), seed):
+        cr.add_relation(cols)
+    pin_one_core()
+    cpu_out, rc, dt = cr.run(QUERY)
+    cr.close()
     # same sample on the GPU, for a bit-exact comparison
     gpu_ctx.drop_relations()
     gen_chain(gpu_ctx, sample_rows, seed, sample_rows)
     gpu_out, _ = gpu_ctx.run(QUERY)
     rows = gpu_ctx.last_result_rows()
     gpu_ctx.drop_relations()
-    del rels
-    cpu_model = ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu_model = line.split(":", 1)[1].strip()
-                break
-    except Exception:
-        pass
     return {"value": round(rows / dt, 1), "unit": "joined tuples/s", "cores": 1, "kind": "port",
             "sample": f"C3 shape at {sample_rows} rows/rel (seed {seed}); oracle/cpu_ref single-threaded, "
                       f"{dt:.2f} s for {rows} chain rows",
-            "seconds": round(dt, 3), "cpu_model": cpu_model, "nproc": os.cpu_count(),
+            "seconds": round(dt, 3), "cpu_model": cpu_model(), "nproc": os.cpu_count(),
             "parity_with_gpu": cpu_out == gpu_out and rc == 0, "sample_stdout": cpu_out}
+
+
+def pinned_parity(args, out):
+    """the printed bytes against the pinned C3 output (default workload only; None otherwise)"""
+    if args.rows == 100_000_000 and args.seed == 1:
+        return out == C3_100M_STDOUT
+    return None
+
+
+def run_dist(args):
+    """the partitioned plan (C, include/qe_plan.h) on every rank of an RCCL communicator"""
+    import torch
+    import torch.distributed as dist
+
+    from qe import lib
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    torch.cuda.init()
+    multi = world > 1
+    if multi and not dist.is_initialized():
+        dist.init_process_group("gloo")          # control plane only: the bootstrap id, barriers, max time
+    ctx = lib.Ctx(dev)
+    comm = None
+    if multi:
+        box = [lib.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        comm = lib.Comm(ctx, world, rank, box[0])   # the data path: RCCL over xGMI
+    total = args.rows if args.scaling == "strong" else args.rows * world
+    t0 = time.time()
+    gen_chain(ctx, total, args.seed, total)       # replicated on every rank
+    ctx.sync()
+    if rank == 0:
+        log(f"[bench] {world} rank(s): 4 x {total} rows x 3 cols in HBM per GPU in {time.time() - t0:.2f}s")
+    out = None
+    for i in range(args.warmup):
+        out, _, refused = ctx.run_dist(QUERY, comm)
+        if rank == 0:
+            log(f"[bench] warmup {i}: {out.strip()!r} (refused {refused})")
+    ctx.set_profiling(True)
+    ctx.reset_stats()
+    if multi:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out, rc, refused = ctx.run_dist(QUERY, comm)
+    ctx.sync()
+    torch.cuda.synchronize()
+    if multi:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if multi:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    stats = ctx.kernel_stats()
+    ctx.set_profiling(False)
+    rows = ctx.last_result_rows()
+    exchanges, sent = comm.stats() if comm else (0, 0)
+    res = None
+    if rank == 0:
+        faithful, _ = ctx.run(QUERY)              # in-run parity: the drop-in executor, same relations
+        kern = sorted(stats.items(), key=lambda kv: -kv[1]["ms"])
+        res = {
+            "metric": METRIC, "value": round(rows * args.steps / dt, 1), "unit": "joined tuples/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": args.scaling,
+            "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic: splitmix64 relations generated in HBM on every rank (SURVEY.md §9.1), seed %d"
+                    % args.seed,
+            "parity": out == faithful and pinned_parity(args, out) is not False,
+            "parity_detail": {"equals_faithful_executor": out == faithful,
+                              "equals_pinned_c3_100m": pinned_parity(args, out)},
+            "config": {"workload": "C3: 4-relation chain join, 2 filters on R3, %d rows/rel in total" % total,
+                       "query": QUERY.strip(), "rows_per_relation": total, "result_rows": rows, "stdout": out,
+                       "executor": "qe_run_queries_dist: host-C partitioned plan (include/qe_plan.h), "
+                                   "RCCL grouped send/recv per exchange, all-reduced sums",
+                       "refused_queries": refused, "exchanges_per_step": exchanges / max(1, args.steps + args.warmup),
+                       "parallelism": f"hash-partitioned dp{world}" if multi else "partitioned plan, one rank"},
+            "roofline": roofline(stats, None),
+            "kernel_ms_per_step": round(sum(s["ms"] for _, s in kern) / args.steps, 3),
+            "stages": {k: {"ms_per_step": round(s["ms"] / args.steps, 3)} for k, s in kern[:12]},
+        }
+        if not args.no_cpu:
+            res["cpu_baseline"] = cpu_baseline(args.cpu_rows, args.seed, ctx)
+        else:
+            res["cpu_baseline"] = None
+    if multi:
+        dist.barrier()
+    if comm:
+        comm.close()
+    ctx.close()
+    if multi:
+        dist.destroy_process_group()
+    return res
 
 
 def run_single(args):
@@ -181,8 +255,9 @@ def run_single(args):
     res = {
         "metric": METRIC, "value": round(value, 1), "unit": "joined tuples/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "scaling": args.scaling, "vs_baseline": None, "dtype": "u64",
         "data": "synthetic: splitmix64 relations generated in HBM (SURVEY.md §9.1), seed %d" % args.seed,
+        "parity": pinned_parity(args, out),
         "config": {"workload": "C3: 4-relation chain join R0-R1-R2-R3, 2 filters on R3, %d rows/rel" % args.rows,
                    "query": QUERY.strip(), "rows_per_relation": args.rows, "result_rows": rows,
                    "stdout": out, "executor": "libqe faithful state machine (qe_run_queries)",
@@ -220,6 +295,9 @@ def main():
     ap.add_argument("--workload", choices=["c3", "c4", "c5"], default="c3",
                     help="c3 (default): the headline 4-relation chain join; c4: the SIGMOD-style batch; "
                          "c5: the skewed (Zipf 0.9) 2-relation join at 1e9 rows")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="c3 at N > 1: strong = --rows per relation in total (the north star: 100 M), "
+                         "weak = --rows per relation per GPU")
     ap.add_argument("--plan", choices=["auto", "dist"], default="auto",
                     help="auto = faithful executor at N = 1, the partitioned plan (qe.dist) at N > 1; "
                          "dist = the partitioned plan at every N (its per-rank cost at N = 1); c3 and c5")
@@ -240,9 +318,7 @@ def main():
         else:
             res = c4bench.run_single(args, log, roofline_fn=roofline, traffic_fn=lambda: load_traffic("c4"))
     elif world > 1 or args.gpus > 1 or args.plan == "dist":
-        from qe import dist
-        res = dist.bench_main(args, METRIC, QUERY, cpu_baseline_fn=cpu_baseline, roofline_fn=roofline,
-                              traffic_fn=None)
+        res = run_dist(args)
     else:
         res = run_single(args)
     if res is not None:

@@ -211,6 +211,33 @@ int qe_bucket_select(qe_ctx*, qe_col col, uint32_t nparts, uint32_t part, const 
  * wsum = sum of vals[row] * weights[h] over those rows mod 2^64.  counts/wsum nullable. */
 int qe_heavy_stats(qe_ctx*, qe_col keys, uint64_t start, uint64_t end, const uint64_t* heavy, uint32_t nheavy,
                    qe_col vals, const uint64_t* weights, uint64_t* counts, uint64_t* wsum);
+/* ---- multi-GPU: RCCL communicator, exchange, all-reduce, the partitioned executor ------------ */
+/* One rank per GPU (one process each); rank 0 makes the bootstrap id and hands it to every rank
+ * out of band (bench.py: torch.distributed gloo; `queries`: a pipe). */
+typedef struct qe_comm qe_comm;
+/* ncclGetUniqueId: 128 bytes */
+int  qe_comm_unique_id(uint8_t* id);
+/* ncclCommInitRank on the ctx's device; exchanges run on the communicator's own stream */
+int  qe_comm_init(qe_ctx*, int nranks, int rank, const uint8_t* id, qe_comm** out);
+void qe_comm_fini(qe_comm*);
+/* vals[i] = sum over ranks of vals[i] mod 2^64 (host array, n <= 64): ncclAllReduce(ncclUint64,
+ * ncclSum) -- print_sums' checksums (src/utilities.c:216-219) and list lengths across ranks */
+int  qe_allreduce_u64(qe_ctx*, qe_comm*, uint64_t* vals, int n);
+/* Hash-partition n rows (keys + ncols uint32 rowid columns) on the key (qe_partition's dest) and
+ * exchange them: every rank receives its bucket from every rank, one grouped ncclSend/ncclRecv.
+ * Outputs are ctx device buffers (qe_buffer_free); inputs are left untouched. */
+int  qe_shuffle_pairs(qe_ctx*, qe_comm*, const uint64_t* keys, uint64_t n, const uint32_t* const* cols, int ncols,
+                      uint64_t** out_keys, uint32_t** out_cols, uint64_t* out_n);
+void qe_buffer_free(qe_ctx*, void*);
+int  qe_comm_stats(qe_comm*, uint64_t* exchanges, uint64_t* bytes_sent);
+/* execute_queries (src/utilities.c:289-300) on every rank of `comm` (NULL: one rank): each query
+ * whose output is the relational answer (qe_plan.h's replay of the reference's state machine) runs
+ * key-partitioned -- rank slices filtered, derived join sides exchanged, local sort-merge joins,
+ * sums all-reduced; the others run on the faithful executor on rank 0 (relations are replicated on
+ * every rank).  Every rank passes the same text and relations; *out (rank 0) is the reference's
+ * stdout; *refused = queries run the faithful way.  Returns 0, QE_EEXIT or an error. */
+int  qe_run_queries_dist(qe_ctx*, qe_comm*, const char* text, char** out, size_t* outlen, uint64_t* refused);
+
 /* The ctx's HIP stream (hipStream_t), for callers that order their own work against it. */
 int qe_sync_stream_ptr(qe_ctx*, void** stream);
 

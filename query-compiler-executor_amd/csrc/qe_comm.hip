@@ -1,0 +1,538 @@
+// qe_comm.hip -- multi-GPU half of the C ABI: an RCCL communicator per
+// ctx (one process per GPU, xGMI), the key exchange and the all-reduce, and the device engine that
+// runs the partitioned plan of include/qe_plan.h (host/qe_plan.c) on libqe's primitives.
+//
+// The reference has no multi-GPU path; its seam is main/queries_main.c:37 -> execute_queries
+// (src/utilities.c:289-300).  qe_run_queries_dist replaces that seam on N ranks: every rank holds
+// the relations, queries in the relational domain run partitioned by join key, the others run on
+// the faithful executor on rank 0 (qe_exec_query) -- the printed bytes are the reference's either way.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "../../include/qe_plan.h"
+#include "../host/qe_query.h"
+#include "qe_internal.h"
+
+struct qe_comm {
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    hipStream_t stream = nullptr;     // exchanges run here, overlapped with the ctx stream's work
+    uint64_t* d_red = nullptr;        // all-reduce staging (64 words)
+    uint64_t* h_red = nullptr;        // pinned mirror
+    uint64_t exchanges = 0, bytes_sent = 0;
+};
+
+namespace qe {
+namespace {
+
+#define QE_NCCL(call)                                                                                  \
+    do {                                                                                               \
+        ncclResult_t r_ = (call);                                                                      \
+        if (r_ != ncclSuccess) throw ::qe::Error(QE_EHIP, std::string(#call) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+// ---- the device engine: handles are heap objects -------------------------------------------------
+struct Obj {
+    virtual ~Obj() {}
+};
+
+// a device array: rowids (u32) or keys (u64)
+struct DArr : Obj {
+    qe_ctx* c = nullptr;
+    void* d = nullptr;
+    uint64_t n = 0;
+    bool u64 = false, owned = true;
+    bool bits = false;
+    uint64_t kor = 0, kand = 0;
+    ~DArr() override {
+        if (owned && d) {
+            qe_pairs p{};
+            p.key = static_cast<uint64_t*>(d);   // drops a gathered histogram kept for this key buffer
+            if (u64) pairs_drop_deferred(c, &p);
+            dfree(c, d);
+        }
+    }
+};
+
+struct Ticket : Obj {
+    DArr* keys = nullptr;
+    std::vector<DArr*> cols;
+    std::vector<void*> send;          // partitioned send buffers, freed once the exchange is done
+    hipEvent_t done = nullptr;
+};
+
+struct Eng {
+    qe_ctx* c;
+    qe_comm* comm;
+    int world, rank;
+    uint64_t refused = 0;
+};
+
+inline Eng* E(void* u) { return static_cast<Eng*>(u); }
+inline DArr* A(qe_h h) { return reinterpret_cast<DArr*>(h); }
+inline qe_h H(Obj* o) { return reinterpret_cast<qe_h>(o); }
+
+DArr* new_arr(qe_ctx* c, void* d, uint64_t n, bool u64, bool owned = true) {
+    DArr* a = new DArr;
+    a->c = c;
+    a->d = d;
+    a->n = n;
+    a->u64 = u64;
+    a->owned = owned;
+    return a;
+}
+
+qe_list as_list(const DArr* a) {
+    qe_list l{};
+    l.d = static_cast<uint32_t*>(a->d);
+    l.n = a->n;
+    l.cap = a->n;
+    return l;
+}
+
+template <class F>
+int guard(Eng* e, F f) {
+    try {
+        f();
+        return 0;
+    } catch (const Error& x) {
+        e->c->err = x.what();
+        return x.code;
+    } catch (const std::exception& x) {
+        e->c->err = x.what();
+        return QE_EINVAL;
+    }
+}
+
+void ck(int rc, qe_ctx* c) {
+    if (rc != 0) throw Error(rc, c->err);
+}
+
+int e_rel_count(void* u, uint32_t* n) {
+    *n = (uint32_t)E(u)->c->rels.size();
+    return 0;
+}
+
+int e_rel_shape(void* u, uint32_t rel, uint64_t* rows, uint32_t* ncols) {
+    qe_ctx* c = E(u)->c;
+    if (rel >= c->rels.size()) return QE_EINVAL;
+    *rows = c->rels[rel].rows;
+    *ncols = (uint32_t)c->rels[rel].cols.size();
+    return 0;
+}
+
+qe_col column(qe_ctx* c, uint32_t rel, uint32_t col) {
+    qe_col q;
+    ck(qe_relation_column(c, (int)rel, (int)col, &q), c);
+    return q;
+}
+
+int e_scan(void* u, uint32_t rel, uint32_t col, uint64_t s, uint64_t t, char op, uint64_t v, qe_h* out) {
+    Eng* e = E(u);
+    return guard(e, [&] {
+        qe_list l{};
+        ck(qe_filter_scan_range(e->c, column(e->c, rel, col), s, t, op, v, &l), e->c);
+        *out = H(new_arr(e->c, l.d, l.n, false));
+    });
+}
+
+int e_iota(void* u, uint64_t s, uint64_t n, qe_h* out) {
+    Eng* e = E(u);
+    return guard(e, [&] {
+        qe_list l{};
+        ck(qe_iota(e->c, s, n, &l), e->c);
+        *out = H(new_arr(e->c, l.d, l.n, false));
+    });
+}
+
+int e_refine(void* u, uint32_t rel, uint32_t col, qe_h rows, char op, uint64_t v, qe_h* out) {
+    Eng* e = E(u);
+    return guard(e, [&] {
+        DArr* a = A(rows);
+        qe_list l = as_list(a);
+        l.flags = QE_LIST_DISTINCT;
+        ck(qe_filter_refine(e->c, column(e->c, rel, col), op, v, &l), e->c);
+        a->d = l.d;
+        a->n = l.n;
+        *out = rows;
+    });
+}
+
+int e_keys(void* u, uint32_t rel, uint32_t col, qe_h rows, qe_h* out) {
+    Eng* e = E(u);
+    return guard(e, [&] {
+        qe_list l = as_list(A(rows));
+        qe_pairs p{};
+        ck(qe_gather_pairs(e->c, column(e->c, rel, col), &l, &p), e->c);
+        DArr* k = new_arr(e->c, p.key, p.n, true);
+        k->bits = (p.flags & QE_PAIRS_BITS) != 0;
+        k->kor = p.kor;
+        k->kand = p.kand;
+        *out = H(k);
+    });
+}
+
+int e_base_side(void* u, uint32_t rel, uint32_t col, qe_h* keys, qe_h* rowids) {
+    Eng* e = E(u);
+    return guard(e, [&] {
+        qe_ctx* c = e->c;
+        const qe_col q = column(c, rel, col);
+        uint64_t kor = 0, kand = 0;
+        ck(qe_relation_column_bits(c, (int)rel, (int)col, &kor, &kand), c);
+        if (e->world == 1) {                  // the column itself, row i: zero copy
+            DArr* k = new_arr(c, const_cast<uint64_t*>(q.d), q.n, true, false);
+            k->bits = true;
+            k->kor = kor;
+            k->kand = kand;
+            *keys = H(k);
+            *rowids = 0;
+            return;
+        }
+        qe_pairs p{};                          // this rank's hash bucket of the replicated column
+        ck(qe_bucket_select(c, q, (uint32_t)e->world, (uint32_t)e->rank, nullptr, 0, &p), c);
+        DArr* k = new_arr(c, p.key, p.n, true);
+        k->bits = true;
+        k->kor = kor;
+        k->kand = kand;
+        *keys = H(k);
+        *rowids = H(new_arr(c, p.val, p.n, false));
+    });
+}
+
+// partition (ctx stream, no host sync) -> counts all-to-all + the grouped send/recv of every array
+// on the comm stream; the ctx stream carries on with the other join side meanwhile
+int e_exchange_start(void* u, qe_h keys, const qe_h* cols, int ncols, qe_h* ticket) {
+    Eng* e = E(u);
+    return guard(e, [&] {
+        qe_ctx* c = e->c;
+        qe_comm* m = e->comm;
+        const int W = e->world;
+        DArr* k = A(keys);
+        const uint64_t n = k->n;
+        // more than 4 rowid columns: an index rides through the partition, the columns follow it
+        const bool via_idx = ncols > 4;
+        std::vector<const uint32_t*> in;
+        uint32_t* idx = nullptr;
+        if (via_idx) {
+            qe_list l{};
+            ck(qe_iota(c, 0, n, &l), c);
+            idx = l.d;
+            in.push_back(idx);
+        } else {
+            for (int i = 0; i < ncols; i++) in.push_back(static_cast<const uint32_t*>(A(cols[i])->d));
+        }
+        const int np = (int)in.size();
+        uint64_t* sk = dalloc_t<uint64_t>(c, std::max<uint64_t>(n, 1));
+        std::vector<uint32_t*> sc(np);
+        for (int i = 0; i < np; i++) sc[i] = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
+        unsigned long long* cnt = dalloc_t<unsigned long long>(c, 4 * 64);   // [send | cursors | recv | -]
+        partition_dev(c, static_cast<const uint64_t*>(k->d), n, in.data(), np, (uint32_t)W, cnt, sk, sc.data());
+        Ticket* t = new Ticket;
+        t->send.push_back(sk);
+        for (auto* p : sc) t->send.push_back(p);
+        t->send.push_back(cnt);
+        std::vector<uint32_t*> scols;                  // the columns in partitioned order
+        if (via_idx) {
+            for (int i = 0; i < ncols; i++) {
+                qe_list il{};
+                il.d = sc[0];
+                il.n = n;
+                qe_list o{};
+                ck(qe_take_u32(c, static_cast<const uint32_t*>(A(cols[i])->d), &il, &o), c);
+                scols.push_back(o.d);
+                t->send.push_back(o.d);
+            }
+            dfree(c, idx);
+        } else {
+            scols = sc;
+        }
+        hipEvent_t ready;
+        QE_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        QE_HIP(hipEventRecord(ready, c->stream));
+        QE_HIP(hipStreamWaitEvent(m->stream, ready, 0));
+        QE_HIP(hipEventDestroy(ready));
+        QE_NCCL(ncclAllToAll(cnt, cnt + 128, 1, ncclUint64, m->comm, m->stream));
+        uint64_t hc[2 * 64];
+        QE_HIP(hipMemcpyAsync(hc, cnt, 64 * sizeof(uint64_t), hipMemcpyDeviceToHost, m->stream));
+        QE_HIP(hipMemcpyAsync(hc + 64, cnt + 128, 64 * sizeof(uint64_t), hipMemcpyDeviceToHost, m->stream));
+        QE_HIP(hipStreamSynchronize(m->stream));       // the one host round trip: receive sizes
+        uint64_t soff[64], roff[64], total = 0, run = 0;
+        for (int p = 0; p < W; p++) {
+            soff[p] = run;
+            run += hc[p];
+            roff[p] = total;
+            total += hc[64 + p];
+        }
+        if (run != n) throw Error(QE_EINVAL, "internal: partition counts do not add up");
+        DArr* rk = new_arr(c, dalloc_t<uint64_t>(c, std::max<uint64_t>(total, 1)), total, true);
+        rk->bits = k->bits;
+        rk->kor = k->kor;
+        rk->kand = k->kand;
+        t->keys = rk;
+        for (int i = 0; i < ncols; i++)
+            t->cols.push_back(new_arr(c, dalloc_t<uint32_t>(c, std::max<uint64_t>(total, 1)), total, false));
+        QE_NCCL(ncclGroupStart());
+        for (int p = 0; p < W; p++) {
+            QE_NCCL(ncclSend(sk + soff[p], hc[p], ncclUint64, p, m->comm, m->stream));
+            QE_NCCL(ncclRecv(static_cast<uint64_t*>(rk->d) + roff[p], hc[64 + p], ncclUint64, p, m->comm, m->stream));
+            for (int i = 0; i < ncols; i++) {
+                QE_NCCL(ncclSend(scols[i] + soff[p], hc[p], ncclUint32, p, m->comm, m->stream));
+                QE_NCCL(ncclRecv(static_cast<uint32_t*>(t->cols[i]->d) + roff[p], hc[64 + p], ncclUint32, p, m->comm,
+                                 m->stream));
+            }
+        }
+        QE_NCCL(ncclGroupEnd());
+        QE_HIP(hipEventCreateWithFlags(&t->done, hipEventDisableTiming));
+        QE_HIP(hipEventRecord(t->done, m->stream));
+        m->exchanges++;
+        m->bytes_sent += (n - hc[e->rank]) * (8 + 4 * (uint64_t)ncols);
+        delete k;                                      // the inputs are consumed
+        for (int i = 0; i < ncols; i++) delete A(cols[i]);
+        *ticket = H(t);
+    });
+}
+
+int e_exchange_finish(void* u, qe_h ticket, qe_h* keys, qe_h* cols) {
+    Eng* e = E(u);
+    return guard(e, [&] {
+        Ticket* t = reinterpret_cast<Ticket*>(ticket);
+        QE_HIP(hipStreamWaitEvent(e->c->stream, t->done, 0));   // later ctx work sees the bucket
+        QE_HIP(hipEventDestroy(t->done));
+        for (void* p : t->send) dfree(e->c, p);                  // stream-ordered after the wait
+        *keys = H(t->keys);
+        for (size_t i = 0; i < t->cols.size(); i++) cols[i] = H(t->cols[i]);
+        delete t;
+    });
+}
+
+qe_pairs side_pairs(const DArr* k, const DArr* v) {
+    qe_pairs p{};
+    p.key = static_cast<uint64_t*>(k->d);
+    p.val = v ? static_cast<uint32_t*>(v->d) : nullptr;
+    p.n = k->n;
+    if (k->bits) {
+        p.kor = k->kor;
+        p.kand = k->kand;
+        p.flags = QE_PAIRS_BITS;
+    }
+    return p;
+}
+
+int e_join(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, qe_h* oa, qe_h* ob) {
+    Eng* e = E(u);
+    return guard(e, [&] {
+        qe_ctx* c = e->c;
+        qe_pairs P = side_pairs(A(ka), va ? A(va) : nullptr);
+        qe_pairs Q = side_pairs(A(kb), vb ? A(vb) : nullptr);
+        qe_list la{}, lb{};
+        int rc = qe_sort_pairs(c, &P);
+        if (rc == 0) rc = qe_sort_pairs(c, &Q);
+        if (rc == 0) rc = qe_merge_join(c, &P, &Q, &la, &lb);
+        qe_pairs_free(c, &P);
+        qe_pairs_free(c, &Q);
+        ck(rc, c);
+        *oa = H(new_arr(c, la.d, la.n, false));
+        *ob = H(new_arr(c, lb.d, lb.n, false));
+    });
+}
+
+int e_take(void* u, qe_h src, qe_h idx, qe_h* out) {
+    Eng* e = E(u);
+    return guard(e, [&] {
+        qe_list il = as_list(A(idx)), o{};
+        ck(qe_take_u32(e->c, static_cast<const uint32_t*>(A(src)->d), &il, &o), e->c);
+        *out = H(new_arr(e->c, o.d, o.n, false));
+    });
+}
+
+int e_length(void* u, qe_h h, uint64_t* n) {
+    (void)u;
+    *n = A(h)->n;
+    return 0;
+}
+
+int e_checksums(void* u, int n, const uint32_t* rels, const uint32_t* cols, const qe_h* rows, uint64_t* sums) {
+    Eng* e = E(u);
+    return guard(e, [&] {
+        std::vector<qe_col> cs(n);
+        std::vector<qe_list> ls(n);
+        std::vector<const qe_list*> lp(n);
+        for (int i = 0; i < n; i++) {
+            cs[i] = column(e->c, rels[i], cols[i]);
+            ls[i] = as_list(A(rows[i]));
+            lp[i] = &ls[i];
+        }
+        ck(qe_checksums(e->c, n, cs.data(), lp.data(), sums), e->c);
+    });
+}
+
+int e_allreduce(void* u, uint64_t* v, int n) {
+    Eng* e = E(u);
+    if (!e->comm) return 0;
+    return qe_allreduce_u64(e->c, e->comm, v, n);
+}
+
+void e_release(void* u, qe_h h) {
+    (void)u;
+    if (h) delete reinterpret_cast<Obj*>(h);
+}
+
+// a query outside the plan's domain: the faithful executor on rank 0 (relations are replicated);
+// its status reaches every rank so all stop together where the reference exits
+int e_fallback(void* u, void* query, void* out) {
+    Eng* e = E(u);
+    e->refused++;
+    int rc = 0;
+    if (e->rank == 0) rc = qe_exec_query(e->c, static_cast<query_t*>(query), static_cast<FILE*>(out));
+    if (e->comm) {
+        uint64_t v = (uint64_t)(int64_t)rc;
+        int r2 = e_allreduce(u, &v, 1);
+        if (r2) return r2;
+        rc = (int)(int64_t)v;
+    }
+    return rc;
+}
+
+}  // namespace
+}  // namespace qe
+
+using namespace qe;
+
+extern "C" {
+
+int qe_comm_unique_id(uint8_t* id) {
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return QE_EHIP;
+    std::memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+    return 0;
+}
+
+int qe_comm_init(qe_ctx* c, int nranks, int rank, const uint8_t* id, qe_comm** out) {
+    QE_API_BEGIN(c)
+    if (nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks) throw Error(QE_EINVAL, "bad rank / world");
+    QE_HIP(hipSetDevice(c->device));
+    qe_comm* m = new qe_comm;
+    m->nranks = nranks;
+    m->rank = rank;
+    try {
+        ncclUniqueId u;
+        std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+        QE_NCCL(ncclCommInitRank(&m->comm, nranks, u, rank));
+        QE_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+        QE_HIP(hipMalloc(&m->d_red, 64 * sizeof(uint64_t)));
+        QE_HIP(hipHostMalloc(&m->h_red, 64 * sizeof(uint64_t), hipHostMallocDefault));
+    } catch (...) {
+        qe_comm_fini(m);
+        throw;
+    }
+    *out = m;
+    return 0;
+    QE_API_END(c)
+}
+
+void qe_comm_fini(qe_comm* m) {
+    if (!m) return;
+    if (m->stream) (void)hipStreamSynchronize(m->stream);
+    if (m->comm) ncclCommDestroy(m->comm);
+    if (m->stream) (void)hipStreamDestroy(m->stream);
+    if (m->d_red) (void)hipFree(m->d_red);
+    if (m->h_red) (void)hipHostFree(m->h_red);
+    delete m;
+}
+
+int qe_allreduce_u64(qe_ctx* c, qe_comm* m, uint64_t* vals, int n) {
+    QE_API_BEGIN(c)
+    if (n < 0 || n > 64) throw Error(QE_EINVAL, "at most 64 values per all-reduce");
+    if (!m || n == 0) return 0;        // (one rank still goes through RCCL: the tested path)
+    std::memcpy(m->h_red, vals, n * sizeof(uint64_t));
+    // every RCCL call of the communicator goes on its one stream (so no two of them can run in a
+    // different order on two ranks); the values are host numbers, nothing to wait for on the ctx
+    QE_HIP(hipMemcpyAsync(m->d_red, m->h_red, n * sizeof(uint64_t), hipMemcpyHostToDevice, m->stream));
+    QE_NCCL(ncclAllReduce(m->d_red, m->d_red, n, ncclUint64, ncclSum, m->comm, m->stream));
+    QE_HIP(hipMemcpyAsync(m->h_red, m->d_red, n * sizeof(uint64_t), hipMemcpyDeviceToHost, m->stream));
+    QE_HIP(hipStreamSynchronize(m->stream));
+    std::memcpy(vals, m->h_red, n * sizeof(uint64_t));
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_shuffle_pairs(qe_ctx* c, qe_comm* m, const uint64_t* keys, uint64_t n, const uint32_t* const* cols, int ncols,
+                     uint64_t** out_keys, uint32_t** out_cols, uint64_t* out_n) {
+    QE_API_BEGIN(c)
+    if (!m) throw Error(QE_EINVAL, "no communicator");
+    if (ncols < 0 || ncols > 64) throw Error(QE_EINVAL, "at most 64 rowid columns");
+    Eng e{c, m, m->nranks, m->rank, 0};
+    // the engine consumes its inputs: hand it copies it may free, the caller keeps its arrays
+    DArr* k = new_arr(c, dalloc_t<uint64_t>(c, std::max<uint64_t>(n, 1)), n, true);
+    if (n) QE_HIP(hipMemcpyAsync(k->d, keys, n * 8, hipMemcpyDeviceToDevice, c->stream));
+    std::vector<qe_h> hc(ncols);
+    for (int i = 0; i < ncols; i++) {
+        DArr* a = new_arr(c, dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1)), n, false);
+        if (n) QE_HIP(hipMemcpyAsync(a->d, cols[i], n * 4, hipMemcpyDeviceToDevice, c->stream));
+        hc[i] = H(a);
+    }
+    qe_h t = 0, rk = 0;
+    std::vector<qe_h> rc(ncols);
+    ck(e_exchange_start(&e, H(k), hc.data(), ncols, &t), c);
+    ck(e_exchange_finish(&e, t, &rk, rc.data()), c);
+    DArr* K = A(rk);
+    *out_keys = static_cast<uint64_t*>(K->d);
+    *out_n = K->n;
+    K->owned = false;
+    delete K;
+    for (int i = 0; i < ncols; i++) {
+        DArr* a = A(rc[i]);
+        out_cols[i] = static_cast<uint32_t*>(a->d);
+        a->owned = false;
+        delete a;
+    }
+    QE_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+    QE_API_END(c)
+}
+
+void qe_buffer_free(qe_ctx* c, void* p) {
+    if (c && p) dfree(c, p);
+}
+
+int qe_comm_stats(qe_comm* m, uint64_t* exchanges, uint64_t* bytes_sent) {
+    if (!m) return QE_EINVAL;
+    if (exchanges) *exchanges = m->exchanges;
+    if (bytes_sent) *bytes_sent = m->bytes_sent;
+    return 0;
+}
+
+int qe_run_queries_dist(qe_ctx* c, qe_comm* m, const char* text, char** out, size_t* outlen, uint64_t* refused) {
+    if (!c) return QE_EINVAL;
+    Eng e{c, m, m ? m->nranks : 1, m ? m->rank : 0, 0};
+    qe_engine g{};
+    g.u = &e;
+    g.rank = (uint32_t)e.rank;
+    g.world = (uint32_t)e.world;
+    g.rel_count = e_rel_count;
+    g.rel_shape = e_rel_shape;
+    g.scan = e_scan;
+    g.iota = e_iota;
+    g.refine = e_refine;
+    g.keys = e_keys;
+    g.base_side = e_base_side;
+    g.exchange_start = e_exchange_start;
+    g.exchange_finish = e_exchange_finish;
+    g.join = e_join;
+    g.take = e_take;
+    g.length = e_length;
+    g.checksums = e_checksums;
+    g.allreduce = e_allreduce;
+    g.release = e_release;
+    g.fallback = e_fallback;
+    uint64_t rows = c->last_result_rows, nref = 0;
+    int rc = qe_plan_run_text(&g, text, out, outlen, &rows, &nref);
+    if (refused) *refused = nref;
+    c->last_result_rows = rows;
+    return rc;
+}
+
+}  // extern "C"

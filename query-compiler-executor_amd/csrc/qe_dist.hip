@@ -387,45 +387,41 @@ __global__ void __launch_bounds__(BS_B) heavy_stats_kernel(const uint64_t* __res
     }
 }
 
-}  // namespace qe
+// exclusive scan of the (<= 64) destination counts into the scatter cursors, on the device
+__global__ void part_starts_kernel(const unsigned long long* __restrict__ cnt, unsigned long long* __restrict__ cursor,
+                                   uint32_t nparts) {
+    if (threadIdx.x == 0) {
+        unsigned long long run = 0;
+        for (uint32_t p = 0; p < nparts; p++) {
+            cursor[p] = run;
+            run += cnt[p];
+        }
+    }
+}
 
-using namespace qe;
-
-extern "C" {
-
-int qe_partition(qe_ctx* c, const uint64_t* keys, uint64_t n, const uint32_t* const* cols, int ncols,
-                 uint32_t nparts, uint64_t* counts, uint64_t* out_keys, uint32_t* const* out_cols) {
-    QE_API_BEGIN(c)
+void partition_dev(qe_ctx* c, const uint64_t* keys, uint64_t n, const uint32_t* const* cols, int ncols,
+                   uint32_t nparts, unsigned long long* d_cnt, uint64_t* out_keys, uint32_t* const* out_cols) {
     if (nparts < 1 || nparts > (uint32_t)PMAX) throw Error(QE_EINVAL, "nparts must be in [1, 64]");
     if (ncols < 0 || ncols > 4) throw Error(QE_EINVAL, "at most 4 rowid columns per partition call");
     if (n >= 0xFFFFFFFFull) throw Error(QE_EINVAL, "partition input too large");
-    for (uint32_t p = 0; p < nparts; p++) counts[p] = 0;
-    if (n == 0) return 0;
+    QE_HIP(hipMemsetAsync(d_cnt, 0, PMAX * sizeof(uint64_t), c->stream));
+    if (n == 0) return;
     int dbits = 0;
     while ((1u << dbits) < nparts) dbits++;
     const uint32_t nb = (uint32_t)((n + PTILE - 1) / PTILE);
-    unsigned long long* d_cnt = dalloc_t<unsigned long long>(c, 2 * PMAX);   // [counts | cursors]
     PartCols pc{};
     for (int i = 0; i < ncols; i++) {
         pc.in[i] = cols[i];
         pc.out[i] = out_cols[i];
     }
-    QE_HIP(hipMemsetAsync(d_cnt, 0, PMAX * sizeof(uint64_t), c->stream));
     {
         Timed t(c, "partition_count", 8.0 * n);
         hipLaunchKernelGGL(part_count_kernel, dim3(std::min<uint32_t>(nb, 1024)), dim3(PB), 0, c->stream, keys, n,
                            nparts, dbits, d_cnt);
         QE_HIP(hipGetLastError());
     }
-    QE_HIP(hipMemcpyAsync(counts, d_cnt, nparts * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
-    QE_HIP(hipStreamSynchronize(c->stream));
-    uint64_t start[PMAX], run = 0;
-    for (uint32_t p = 0; p < nparts; p++) {
-        start[p] = run;
-        run += counts[p];
-    }
-    if (run != n) throw Error(QE_EINVAL, "internal: partition counts do not add up");
-    QE_HIP(hipMemcpyAsync(d_cnt + PMAX, start, nparts * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(part_starts_kernel, dim3(1), dim3(64), 0, c->stream, d_cnt, d_cnt + PMAX, nparts);
+    QE_HIP(hipGetLastError());
     {
         Timed t(c, "partition", (8.0 + 4.0 * ncols) * 2.0 * n);
         switch (ncols) {
@@ -439,8 +435,25 @@ int qe_partition(qe_ctx* c, const uint64_t* keys, uint64_t n, const uint32_t* co
         }
         QE_HIP(hipGetLastError());
     }
+}
+
+}  // namespace qe
+
+using namespace qe;
+
+extern "C" {
+
+int qe_partition(qe_ctx* c, const uint64_t* keys, uint64_t n, const uint32_t* const* cols, int ncols,
+                 uint32_t nparts, uint64_t* counts, uint64_t* out_keys, uint32_t* const* out_cols) {
+    QE_API_BEGIN(c)
+    unsigned long long* d_cnt = dalloc_t<unsigned long long>(c, 2 * PMAX);   // [counts | cursors]
+    partition_dev(c, keys, n, cols, ncols, nparts, d_cnt, out_keys, out_cols);
+    QE_HIP(hipMemcpyAsync(counts, d_cnt, nparts * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     QE_HIP(hipStreamSynchronize(c->stream));   // the caller hands the buffers to RCCL next
     dfree(c, d_cnt);
+    uint64_t run = 0;
+    for (uint32_t p = 0; p < nparts; p++) run += counts[p];
+    if (run != n) throw Error(QE_EINVAL, "internal: partition counts do not add up");
     return 0;
     QE_API_END(c)
 }

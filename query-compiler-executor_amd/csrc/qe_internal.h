@@ -206,6 +206,11 @@ bool gather_with_hist(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint
 bool tl_join(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS, uint32_t* oflags);
 SortOut radix_sort_u32(qe_ctx* c, const uint32_t* keys, const uint32_t* vals, uint64_t n,
                        const uint64_t* bits = nullptr);
+// multi-GPU (qe_dist.hip): hash-partition rows into per-destination segments of out_keys /
+// out_cols; d_cnt (2 x 64 words, device) receives the per-destination counts (then the cursors).
+// Queued on the ctx stream, no host synchronisation.
+void partition_dev(qe_ctx* c, const uint64_t* keys, uint64_t n, const uint32_t* const* cols, int ncols,
+                   uint32_t nparts, unsigned long long* d_cnt, uint64_t* out_keys, uint32_t* const* out_cols);
 // OR / AND of n keys -> host out[2] (synchronises)
 void key_bits_u64(qe_ctx* c, const uint64_t* keys, uint64_t n, uint64_t* out);
 

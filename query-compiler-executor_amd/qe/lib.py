@@ -15,7 +15,7 @@ PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("QE_LIB_PATH") or os.path.join(PKG, "build", "libqe.so")   # override: ablation builds (tools/)
 HEADER = os.path.join(os.path.dirname(PKG), "include", "qe.h")
 
-QE_EINVAL, QE_EHIP, QE_ENOMEM, QE_EEXIT, QE_ETOOBIG = -1, -2, -3, -4, -5
+QE_EINVAL, QE_EHIP, QE_ENOMEM, QE_EEXIT, QE_ETOOBIG, QE_ENOTSUP = -1, -2, -3, -4, -5, -6
 LIST_DISTINCT = 1
 PAIRS_DISTINCT, PAIRS_SORTED = 1, 2
 
@@ -119,6 +119,16 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "qe_set_profiling": (I, [P, I]),
         "qe_reset_stats": (I, [P]),
         "qe_kernel_stats": (I, [P, C.POINTER(KStat), I]),
+        "qe_comm_unique_id": (I, [C.c_char_p]),
+        "qe_comm_init": (I, [P, I, I, C.c_char_p, C.POINTER(C.c_void_p)]),
+        "qe_comm_fini": (None, [P]),
+        "qe_allreduce_u64": (I, [P, P, C.POINTER(C.c_uint64), I]),
+        "qe_shuffle_pairs": (I, [P, P, C.c_void_p, U64, C.POINTER(C.c_void_p), I, C.POINTER(C.c_void_p),
+                                 C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
+        "qe_buffer_free": (None, [P, C.c_void_p]),
+        "qe_comm_stats": (I, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+        "qe_run_queries_dist": (I, [P, P, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t),
+                                    C.POINTER(C.c_uint64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -209,6 +219,21 @@ class Ctx:
         if rc not in (0, QE_EEXIT):
             raise QEError(rc, self.lib.qe_last_error(self.h).decode())
         return s, (1 if rc == QE_EEXIT else 0)
+
+    def run_dist(self, text: str, comm: "Comm | None" = None) -> tuple[str, int, int]:
+        """qe_run_queries_dist: (stdout on rank 0, exit status, queries run the faithful way)"""
+        out, n, ref = C.c_void_p(), C.c_size_t(), C.c_uint64()
+        rc = self.lib.qe_run_queries_dist(self.h, comm.h if comm else None, text.encode(), C.byref(out), C.byref(n),
+                                          C.byref(ref))
+        s = C.string_at(out, n.value).decode("latin-1") if out.value else ""
+        if out.value:
+            self.lib.qe_free_host(out)
+        if rc not in (0, QE_EEXIT):
+            raise QEError(rc, self.lib.qe_last_error(self.h).decode())
+        return s, (1 if rc == QE_EEXIT else 0), ref.value
+
+    def buffer_free(self, ptr: int) -> None:
+        self.lib.qe_buffer_free(self.h, ptr)
 
     def last_result_rows(self) -> int:
         r = C.c_uint64()
@@ -421,3 +446,48 @@ class Ctx:
         self._chk(self.lib.qe_kernel_stats(self.h, arr, n))
         return {arr[i].name.decode(): {"launches": arr[i].launches, "ms": arr[i].total_ms,
                                        "alg_bytes": arr[i].alg_bytes} for i in range(n)}
+
+
+def comm_unique_id() -> bytes:
+    """rank 0: the RCCL bootstrap id (128 bytes) every rank passes to Comm"""
+    lib = load_library()
+    b = C.create_string_buffer(128)
+    rc = lib.qe_comm_unique_id(b)
+    if rc != 0:
+        raise QEError(rc, "ncclGetUniqueId failed")
+    return b.raw
+
+
+class Comm:
+    """an RCCL communicator on a ctx's device (qe_comm_init): one rank per GPU"""
+
+    def __init__(self, ctx: Ctx, nranks: int, rank: int, uid: bytes):
+        self.ctx, self.lib = ctx, ctx.lib
+        h = C.c_void_p()
+        ctx._chk(self.lib.qe_comm_init(ctx.h, nranks, rank, uid, C.byref(h)))
+        self.h = h
+        self.nranks, self.rank = nranks, rank
+
+    def allreduce(self, vals) -> list[int]:
+        a = (C.c_uint64 * len(vals))(*[int(v) & ((1 << 64) - 1) for v in vals])
+        self.ctx._chk(self.lib.qe_allreduce_u64(self.ctx.h, self.h, a, len(vals)))
+        return list(a)
+
+    def shuffle(self, keys_ptr: int, n: int, col_ptrs: list[int]):
+        """qe_shuffle_pairs -> (keys ptr, [col ptrs], n) in ctx buffers (free with ctx.buffer_free)"""
+        cols = (C.c_void_p * max(1, len(col_ptrs)))(*col_ptrs)
+        ok, oc, on = C.c_void_p(), (C.c_void_p * max(1, len(col_ptrs)))(), C.c_uint64()
+        self.ctx._chk(self.lib.qe_shuffle_pairs(self.ctx.h, self.h, keys_ptr, n, cols, len(col_ptrs), C.byref(ok),
+                                                oc, C.byref(on)))
+        return ok.value, [oc[i] for i in range(len(col_ptrs))], on.value
+
+    def stats(self) -> tuple[int, int]:
+        x, b = C.c_uint64(), C.c_uint64()
+        self.lib.qe_comm_stats(self.h, C.byref(x), C.byref(b))
+        return x.value, b.value
+
+    def close(self):
+        if self.h:
+            self.lib.qe_comm_fini(self.h)
+            self.h = None
+

@@ -1,12 +1,12 @@
-"""A numpy engine for qe.dist.DistExecutor so the multi-GPU plan (partitioning, all-to-all
-exchange, local joins, all-reduced checksums) runs under torch.distributed gloo on CPU.
-TEST INFRASTRUCTURE ONLY: the product engine is qe.dist.GPUEngine (libqe)."""
+"""A numpy engine for qe.dist.DistAggJoin (the C5 skew plan) so it runs under torch.distributed
+gloo on CPU.  TEST INFRASTRUCTURE ONLY: the product engine is qe.dist.GPUEngine (libqe).  (The
+relational plan is C: tests/plan_engine.py drives it.)"""
 import os
 import socket
 
 import numpy as np
 
-from qe.dist import DistExecutor, M64
+from qe.dist import M64
 
 _OPS = {"=": np.equal, ">": np.greater, "<": np.less}
 
@@ -23,49 +23,6 @@ class NumpyEngine:
     def __init__(self, rels, rank, world, group=None):
         self.rels, self.rank, self.world, self.group = rels, rank, world, group
         self.exchanges = 0
-
-    def length(self, a):
-        return len(a)
-
-    def scan(self, rel, col, s, t, op, v):
-        c = self.rels[rel][col][s:t]
-        return (np.nonzero(_OPS[op](c, np.uint64(v)))[0] + s).astype(np.uint32)
-
-    def iota(self, s, n):
-        return np.arange(s, s + n, dtype=np.uint32)
-
-    def refine(self, rel, col, rows, op, v):
-        return rows[_OPS[op](self.rels[rel][col][rows], np.uint64(v))]
-
-    def keys(self, rel, col, rows):
-        return self.rels[rel][col][rows]
-
-    def filter_idx(self, rel, col, rows, op, v):
-        return np.nonzero(_OPS[op](self.rels[rel][col][rows], np.uint64(v)))[0].astype(np.uint32)
-
-    def take(self, rows, idx):
-        return rows[idx]
-
-    def join_local(self, ka, kb):
-        ob = np.argsort(kb, kind="stable")
-        sb = kb[ob]
-        lo = np.searchsorted(sb, ka, "left")
-        hi = np.searchsorted(sb, ka, "right")
-        c = hi - lo
-        ia = np.repeat(np.arange(len(ka)), c)
-        starts = np.repeat(lo - np.concatenate([[0], np.cumsum(c)[:-1]]).astype(np.int64), c)
-        ib = ob[starts + np.arange(int(c.sum()))]
-        return ia.astype(np.uint32), ib.astype(np.uint32)
-
-    def base_side(self, rel, col):
-        c = self.rels[rel][col]
-        if self.world == 1:
-            return c, None
-        mask = part_of(c, self.world) == np.uint64(self.rank)
-        rows = np.nonzero(mask)[0]
-        # an unordered bucket, like qe_bucket_select's: shuffle so no test depends on its order
-        rows = np.random.default_rng(self.rank + 17).permutation(rows).astype(np.uint32)
-        return c[rows], rows
 
     def base_side_light(self, rel, col, heavy):
         c = self.rels[rel][col]
@@ -117,50 +74,6 @@ class NumpyEngine:
         dist.all_reduce(t, group=self.group)
         return t.numpy().view(np.uint64)
 
-    def join_pairs(self, ka, va, kb, vb):
-        ia, ib = self.join_local(ka, kb)
-        return (va[ia] if va is not None else ia), (vb[ib] if vb is not None else ib)
-
-    def keep_equal(self, ka, kb):
-        return np.nonzero(ka == kb)[0].astype(np.uint32)
-
-    def checksum(self, rel, col, rows):
-        return int(np.sum(self.rels[rel][col][rows], dtype=np.uint64))
-
-    def allreduce(self, x):
-        if self.world == 1:
-            return x & M64
-        import torch
-        import torch.distributed as dist
-        t = torch.tensor([x - (1 << 64) if x >= (1 << 63) else x], dtype=torch.int64)
-        dist.all_reduce(t, group=self.group)
-        return int(t.item()) & M64
-
-    def exchange_start(self, keys, cols):
-        return self.exchange(keys, cols)
-
-    def exchange_finish(self, h):
-        return h
-
-    def exchange(self, keys, cols):
-        import torch
-        import torch.distributed as dist
-        self.exchanges += 1
-        dest = part_of(keys, self.world).astype(np.int64)
-        order = np.argsort(dest, kind="stable")
-        counts = np.bincount(dest, minlength=self.world).astype(np.int64)
-        cnt = torch.from_numpy(counts)
-        rcnt = torch.empty_like(cnt)
-        dist.all_to_all_single(rcnt, cnt, group=self.group)
-        osp, isp = rcnt.tolist(), counts.tolist()
-        outs = []
-        for arr, dt in [(keys.view(np.int64), torch.int64)] + [(c.view(np.int32), torch.int32) for c in cols]:
-            s = torch.from_numpy(np.ascontiguousarray(arr[order]))
-            r = torch.empty(sum(osp), dtype=dt)
-            dist.all_to_all_single(r, s, osp, isp, group=self.group)
-            outs.append(r.numpy())
-        return outs[0].view(np.uint64), [o.view(np.uint32) for o in outs[1:]]
-
 
 def free_port():
     s = socket.socket()
@@ -183,26 +96,5 @@ def agg_worker(rank, world, port, rels, queries, outq, sample):
         res = [ex.run(q) for q in queries]
         if rank == 0:
             outq.put((res, 0))
-    finally:
-        dist.destroy_process_group()
-
-
-def worker(rank, world, port, rels, queries, outq):
-    """one gloo rank: run every query with the distributed plan, report rank 0's output"""
-    import torch.distributed as dist
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        eng = NumpyEngine(rels, rank, world)
-        ex = DistExecutor(eng, [len(r[0]) for r in rels])
-        res = []
-        for q in queries:
-            try:
-                res.append(ex.run(q))
-            except Exception as e:     # NotSupported on every rank alike
-                res.append((f"!{type(e).__name__}", -1))
-        if rank == 0:
-            outq.put((res, eng.exchanges))
     finally:
         dist.destroy_process_group()

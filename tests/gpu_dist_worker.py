@@ -1,30 +1,6 @@
-"""Spawned rank for tests/test_gpu_dist.py: the real GPUEngine (libqe) under gloo, two ranks
-sharing the box's one GPU (host-staged all-to-all).  TEST INFRASTRUCTURE."""
+"""Spawned rank for tests/test_gpu_dist.py: the C5 aggregate plan on the real GPUEngine (libqe)
+under gloo, two ranks sharing the box's one GPU (host-staged all-reduce).  TEST INFRASTRUCTURE."""
 import os
-
-
-def worker(rank, world, port, rows, queries, outq):
-    import torch
-    import torch.distributed as dist
-
-    from qe import lib
-    from qe.dist import DistExecutor, GPUEngine
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(0)
-    ctx = lib.Ctx(0)
-    try:
-        kinds = [("mod", rows), ("mod", rows), ("hi32",)]
-        for r in range(4):
-            ctx.gen_relation(rows, kinds, seed=1, gen_rel=r)
-        ex = DistExecutor(GPUEngine(ctx, rank, world), [rows] * 4)
-        res = [ex.run(q) for q in queries]
-        if rank == 0:
-            outq.put(res)
-    finally:
-        ctx.close()
-        dist.destroy_process_group()
 
 
 def agg_worker(rank, world, port, rows, queries, outq):

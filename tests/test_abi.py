@@ -50,3 +50,20 @@ def test_no_gpu_means_loud_failure(built):
         pytest.skip("GPU present")
     with pytest.raises(lib.QEError):
         lib.Ctx(0)
+
+
+def test_plan_header_exports(built):
+    """include/qe_plan.h: the partitioned plan is in libqe and, alone, in libqeplan.so (the CPU
+    tests' build of the same C)"""
+    hdr = os.path.join(ROOT, "include", "qe_plan.h")
+    syms = lib.declared_symbols(hdr)
+    assert {"qe_plan_run_text", "qe_plan_check_text", "qe_plan_why"} <= set(syms)
+    plan = ctypes.CDLL(os.path.join(ROOT, "query-compiler-executor_amd", "build", "libqeplan.so"))
+    for s in syms:
+        assert hasattr(built, s) and hasattr(plan, s), s
+
+
+def test_multi_gpu_abi_declared():
+    """the multi-GPU half of the boundary"""
+    syms = set(lib.declared_symbols())
+    assert {"qe_comm_init", "qe_shuffle_pairs", "qe_allreduce_u64", "qe_run_queries_dist"} <= syms

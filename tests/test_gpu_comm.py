@@ -1,0 +1,105 @@
+"""The multi-GPU half of the C ABI on one MI355X: an RCCL communicator of one rank (qe_comm_init),
+the all-reduce and the exchange through it, and the partitioned executor qe_run_queries_dist on
+every golden of the real reference -- queries in the plan's domain run partitioned, the others on
+the faithful executor, and the bytes must be the reference's either way.  (RCCL refuses two ranks
+on one device, so N > 1 runs on the driver's 8-GPU node; the same C plan runs at world 2 and 3
+under gloo in tests/test_plan_gloo.py.)"""
+import ctypes as C
+import json
+
+import numpy as np
+import pytest
+
+import goldens
+from qe import datagen as dg
+from qe import lib
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def comm(ctx):
+    c = lib.Comm(ctx, 1, 0, lib.comm_unique_id())
+    yield c
+    c.close()
+
+
+def test_allreduce_one_rank_is_exact(ctx, comm):
+    v = [1, (1 << 64) - 1, 5, 1 << 63]
+    assert comm.allreduce(v) == v
+
+
+def test_shuffle_one_rank_keeps_every_row(ctx, comm):
+    rng = np.random.default_rng(7)
+    n = 300_007
+    k = rng.integers(0, 1 << 62, n, dtype=np.uint64)
+    a = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    b = np.arange(n, dtype=np.uint32)
+    P = ctx.pairs_from_host(k, a)
+    L = ctx.list_from_host(b)
+    ok, (oa, ob), on = comm.shuffle(P.key, n, [P.val, L.d])
+    assert on == n
+    kk, aa = np.empty(n, np.uint64), np.empty(n, np.uint32)
+    Q = lib.Pairs()
+    Q.key, Q.val, Q.n = ok, oa, n
+    ctx._chk(ctx.lib.qe_pairs_to_host(ctx.h, C.byref(Q), kk.ctypes.data, aa.ctypes.data))
+    M = lib.List()
+    M.d, M.n = ob, n
+    bb = ctx.list_to_host(M)
+    # the rows travel whole: b is the original position, so (k, a) must be the row it names
+    assert np.array_equal(np.sort(bb), b)
+    assert np.array_equal(kk, k[bb]) and np.array_equal(aa, a[bb])
+    for p in (ok, oa, ob):
+        ctx.buffer_free(p)
+    ctx.pairs_free(P)
+    ctx.list_free(L)
+    x, sent = comm.stats()
+    assert x >= 1 and sent == 0          # one rank: everything stays home
+
+
+_loaded = {"key": None}
+
+
+def _load(ctx, ds):
+    key = json.dumps(ds, sort_keys=True)
+    if _loaded["key"] != key:
+        ctx.drop_relations()
+        rels, _ = goldens.dataset(ds)
+        for cols in rels:
+            ctx.load_relation(cols)
+        _loaded["key"] = key
+
+
+@pytest.mark.parametrize("fixture", [f.split("/")[-1][:-5] for f in goldens.golden_files()])
+def test_dist_executor_matches_every_golden(ctx, comm, fixture):
+    doc = goldens.load(f"{goldens.GOLDEN_DIR}/{fixture}.json")
+    _load(ctx, doc["dataset"])
+    planned = 0
+    for case in doc["cases"]:
+        for cm in (comm, None):
+            out, rc, refused = ctx.run_dist(case["input"], cm)
+            assert (out, rc) == (case["stdout"], case["rc"]), (case["input"], cm is None)
+        planned += refused == 0
+    if fixture in ("c4", "fuzz_a", "headline"):
+        assert planned >= len(doc["cases"]) // 2     # most of them really ran partitioned
+
+
+@pytest.mark.slow
+def test_dist_executor_c3_100m_one_rank(ctx, comm):
+    """the partitioned plan at the headline size through a one-rank RCCL communicator equals the
+    faithful executor (itself pinned to the aggregate truth by test_gpu_fullsize)"""
+    N = 100_000_000
+    q = "0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>1000000000&3.2<3000000000|1.2 2.2 3.2\n"
+    ctx.drop_relations()
+    _loaded["key"] = None
+    try:
+        kinds = [("mod", N), ("mod", N), ("hi32",)]
+        for r in range(4):
+            ctx.gen_relation(N, kinds, seed=1, gen_rel=r)
+        want, _ = ctx.run(q)
+        rows = ctx.last_result_rows()
+        out, rc, refused = ctx.run_dist(q, comm)
+        assert (out, rc, refused) == (want, 0, 0)
+        assert ctx.last_result_rows() == rows
+    finally:
+        ctx.drop_relations()

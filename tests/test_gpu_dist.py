@@ -1,17 +1,17 @@
-"""GPU tests of the multi-GPU plan's primitives and of qe.dist.GPUEngine end to end."""
+"""GPU tests of the multi-GPU plan's primitives (partition, bucket select, heavy stats, slices)
+and of the C5 aggregate plan (qe.dist.DistAggJoin) on qe.dist.GPUEngine.  The relational plan's
+GPU tests are tests/test_gpu_comm.py."""
 import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
 import dist_cpu_engine as dce
 import gpu_dist_worker
+import plan_engine as pe
 from qe import datagen as dg
-from qe.dist import DistExecutor, GPUEngine
+from qe.dist import GPUEngine
 
 pytestmark = pytest.mark.gpu
-
-C3 = "0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>1000000000&3.2<3000000000|1.2 2.2 3.2"
-
 
 @pytest.mark.parametrize("n,parts,ncols", [(0, 2, 1), (1, 8, 2), (100_000, 8, 3), (3_000_001, 5, 1), (4096, 64, 4),
                                            (2_000_000, 1, 0), (777_777, 7, 4)])
@@ -29,7 +29,7 @@ def test_partition_groups_rows_by_destination(ctx, n, parts, ncols):
     torch.cuda.synchronize()
     counts = ctx.partition(dk.data_ptr(), n, [t.data_ptr() for t in dc], parts, ok.data_ptr(),
                            [t.data_ptr() for t in oc])
-    dest = dce.part_of(keys, parts).astype(np.int64)
+    dest = pe.part_of(keys, parts).astype(np.int64)
     assert counts == np.bincount(dest, minlength=parts).tolist()
     gk = ok.cpu().numpy()[:n].view(np.uint64)
     gc = [o.cpu().numpy()[:n].view(np.uint32) for o in oc]
@@ -51,7 +51,7 @@ def test_bucket_select_is_the_hash_bucket(ctx, n, parts, nheavy):
     keys = rng.integers(0, max(1, n // 3), n, dtype=np.uint64) * np.uint64(0x9E3779B1)
     rel = ctx.load_relation([keys])
     heavy = np.unique(keys[:nheavy]) if nheavy else np.zeros(0, np.uint64)
-    dest = dce.part_of(keys, parts).astype(np.int64)
+    dest = pe.part_of(keys, parts).astype(np.int64)
     for part in sorted({0, parts - 1, parts // 2}):
         p = ctx.bucket_select(ctx.column(rel, 0), parts, part, heavy)
         k, v = ctx.pairs_to_host(p)
@@ -103,46 +103,11 @@ def test_join_indices_and_take(ctx):
     ha, hb = ctx.list_to_host(ia), ctx.list_to_host(ib)
     assert np.all(ka[ha] == kb[hb])
     got = sorted(zip(ha.tolist(), hb.tolist()))
-    want = dce.NumpyEngine(None, 0, 1).join_local(ka, kb)
+    want = pe.join_local(ka, kb)
     assert got == sorted(zip(want[0].tolist(), want[1].tolist()))
     src = ctx.list_from_host(np.arange(20_000, dtype=np.uint32) * 3)
     t = ctx.take_u32(src.d, ia)
     np.testing.assert_array_equal(ctx.list_to_host(t), ha * 3)
-
-
-def test_gpu_plan_single_rank_equals_faithful_executor(ctx):
-    rows = 2_000_000
-    ctx.drop_relations()
-    kinds = [("mod", rows), ("mod", rows), ("hi32",)]
-    for r in range(4):
-        ctx.gen_relation(rows, kinds, seed=1, gen_rel=r)
-    faithful, rc = ctx.run(C3 + "\n")
-    out, nrows = DistExecutor(GPUEngine(ctx, 0, 1), [rows] * 4).run(C3)
-    assert rc == 0 and out == faithful
-    assert nrows == ctx.last_result_rows()
-    ctx.drop_relations()
-
-
-def test_gpu_plan_two_ranks_share_one_gpu(ctx):
-    rows = 1_000_000
-    ctx.drop_relations()
-    kinds = [("mod", rows), ("mod", rows), ("hi32",)]
-    for r in range(4):
-        ctx.gen_relation(rows, kinds, seed=1, gen_rel=r)
-    want, _ = ctx.run(C3 + "\n0 1|0.1=1.0|0.2 1.2\n")
-    ctx.drop_relations()
-    mpc = mp.get_context("spawn")
-    q = mpc.Queue()
-    port = dce.free_port()
-    procs = [mpc.Process(target=gpu_dist_worker.worker, args=(r, 2, port, rows, [C3, "0 1|0.1=1.0|0.2 1.2"], q))
-             for r in range(2)]
-    for p in procs:
-        p.start()
-    res = q.get(timeout=600)
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
-    assert res[0][0] + res[1][0] == want
 
 
 @pytest.mark.parametrize("world", [1, 2])
