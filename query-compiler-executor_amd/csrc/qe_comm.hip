@@ -8,6 +8,8 @@
 // the faithful executor on rank 0 (qe_exec_query) -- the printed bytes are the reference's either way.
 #include <rccl/rccl.h>
 
+#include <unistd.h>
+
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -396,6 +398,24 @@ int e_fallback(void* u, void* query, void* out) {
     return rc;
 }
 
+// RCCL prints a version banner on stdout when a communicator is made; stdout is the reference's
+// protocol channel (main/queries_main.c), so library chatter is sent to stderr meanwhile
+struct StdoutToStderr {
+    int saved = -1;
+    StdoutToStderr() {
+        fflush(stdout);
+        saved = dup(1);
+        if (saved >= 0) dup2(2, 1);
+    }
+    ~StdoutToStderr() {
+        fflush(stdout);
+        if (saved >= 0) {
+            dup2(saved, 1);
+            close(saved);
+        }
+    }
+};
+
 }  // namespace
 }  // namespace qe
 
@@ -404,6 +424,7 @@ using namespace qe;
 extern "C" {
 
 int qe_comm_unique_id(uint8_t* id) {
+    StdoutToStderr quiet;
     ncclUniqueId u;
     if (ncclGetUniqueId(&u) != ncclSuccess) return QE_EHIP;
     std::memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
@@ -420,7 +441,10 @@ int qe_comm_init(qe_ctx* c, int nranks, int rank, const uint8_t* id, qe_comm** o
     try {
         ncclUniqueId u;
         std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
-        QE_NCCL(ncclCommInitRank(&m->comm, nranks, u, rank));
+        {
+            StdoutToStderr quiet;
+            QE_NCCL(ncclCommInitRank(&m->comm, nranks, u, rank));
+        }
         QE_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
         QE_HIP(hipMalloc(&m->d_red, 64 * sizeof(uint64_t)));
         QE_HIP(hipHostMalloc(&m->h_red, 64 * sizeof(uint64_t), hipHostMallocDefault));
@@ -436,7 +460,10 @@ int qe_comm_init(qe_ctx* c, int nranks, int rank, const uint8_t* id, qe_comm** o
 void qe_comm_fini(qe_comm* m) {
     if (!m) return;
     if (m->stream) (void)hipStreamSynchronize(m->stream);
-    if (m->comm) ncclCommDestroy(m->comm);
+    if (m->comm) {
+        StdoutToStderr quiet;
+        ncclCommDestroy(m->comm);
+    }
     if (m->stream) (void)hipStreamDestroy(m->stream);
     if (m->d_red) (void)hipFree(m->d_red);
     if (m->h_red) (void)hipHostFree(m->h_red);

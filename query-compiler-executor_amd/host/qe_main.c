@@ -4,78 +4,199 @@
  * stdin: relation file paths, one per line, until "Done"/"done" (src/utilities.c:124-162);
  * then query batches until EOF.  stdout: the reference's bytes.  Relations are mmap'd and
  * copied into HBM once; every query runs on the GPU through libqe.  Exit status 1 where the
- * reference calls exit(EXIT_FAILURE).  QE_DEVICE selects the GPU (default 0).
+ * reference calls exit(EXIT_FAILURE).
+ *
+ *   QE_DEVICE=d   the GPU of a one-GPU run (default 0)
+ *   QE_GPUS=N     (N >= 1) N GPUs of this node, one process per GPU (forked before any GPU is touched):
+ *                 every rank loads the relations, rank 0 makes the RCCL bootstrap id and hands it
+ *                 to the others over pipes, and qe_run_queries_dist runs the batch -- queries in
+ *                 the relational domain key-partitioned across the ranks, the others on rank 0's
+ *                 faithful executor (include/qe_plan.h).  Rank 0 prints; the exit status is its.
+ *   QE_PLAN=1     (one GPU) the partitioned executor on one rank instead of qe_run_queries
  */
 #define _GNU_SOURCE
 #include <fcntl.h>
+#include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include "qe.h"
 
-int main(void) {
-    const char* dev = getenv("QE_DEVICE");
-    qe_ctx* c = qe_init(dev ? atoi(dev) : 0);
-    if (!c) {
-        fprintf(stderr, "[ERROR] no usable GPU (libqe has no CPU path)\n");
-        return EXIT_FAILURE;
-    }
+typedef struct { char** paths; size_t n; char* text; } input_t;
+
+static input_t read_input(void) {
+    input_t in = {NULL, 0, NULL};
+    size_t pcap = 0;
     char* line = NULL;
     size_t cap = 0;
     ssize_t got;
     while ((got = getline(&line, &cap, stdin)) != -1) {
         if (!strncmp(line, "Done\n", 5) || !strncmp(line, "done\n", 5)) break;
-        line[strlen(line) - 1] = '\0';
-        int fd = open(line, O_RDONLY);
+        line[strlen(line) - 1] = '\0';     /* the last character is the newline (src/utilities.c:135) */
+        if (in.n == pcap) {
+            pcap = pcap ? 2 * pcap : 16;
+            in.paths = (char**)realloc(in.paths, pcap * sizeof(char*));
+        }
+        in.paths[in.n++] = strdup(line);
+    }
+    size_t tcap = 1 << 16, tlen = 0;
+    in.text = (char*)malloc(tcap);
+    while ((got = getline(&line, &cap, stdin)) != -1) {
+        while (tlen + (size_t)got + 1 > tcap) {
+            tcap *= 2;
+            in.text = (char*)realloc(in.text, tcap);
+        }
+        memcpy(in.text + tlen, line, (size_t)got);
+        tlen += (size_t)got;
+    }
+    in.text[tlen] = 0;
+    free(line);
+    return in;
+}
+
+static int load_relations(qe_ctx* c, const input_t* in) {
+    for (size_t i = 0; i < in->n; i++) {
+        int fd = open(in->paths[i], O_RDONLY);
         if (fd < 0) {
-            fprintf(stderr, "[ERROR] open failed: %s\n", line);
-            return EXIT_FAILURE;
+            fprintf(stderr, "[ERROR] open failed: %s\n", in->paths[i]);
+            return -1;
         }
         struct stat sb;
-        if (fstat(fd, &sb) < 0) return EXIT_FAILURE;
+        if (fstat(fd, &sb) < 0) return -1;
         const uint64_t* m = (const uint64_t*)mmap(NULL, sb.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
-        if (m == MAP_FAILED) return EXIT_FAILURE;
+        if (m == MAP_FAILED) return -1;
         uint64_t rows = m[0], ncols = m[1];
         const uint64_t** cols = (const uint64_t**)malloc((ncols ? ncols : 1) * sizeof(uint64_t*));
         for (uint64_t j = 0; j < ncols; j++) cols[j] = m + 2 + j * rows;
         if (qe_load_relation(c, rows, ncols, cols) < 0) {
             fprintf(stderr, "[ERROR] load: %s\n", qe_last_error(c));
-            return EXIT_FAILURE;
+            return -1;
         }
         free(cols);
         munmap((void*)m, sb.st_size);
         close(fd);
     }
-    size_t tcap = 1 << 16, tlen = 0;
-    char* text = (char*)malloc(tcap);
-    while ((got = getline(&line, &cap, stdin)) != -1) {
-        while (tlen + (size_t)got + 1 > tcap) {
-            tcap *= 2;
-            text = (char*)realloc(text, tcap);
-        }
-        memcpy(text + tlen, line, (size_t)got);
-        tlen += (size_t)got;
-    }
-    text[tlen] = 0;
-    free(line);
-    char* out = NULL;
-    size_t outlen = 0;
-    int rc = qe_run_queries(c, text, &out, &outlen);
+    return 0;
+}
+
+static int finish(int rc, char* out, size_t outlen, int print) {
     if (out) {
-        fwrite(out, 1, outlen, stdout);
+        if (print) fwrite(out, 1, outlen, stdout);
         qe_free_host(out);
     }
     fflush(stdout);
-    free(text);
-    qe_fini(c);
     if (rc == QE_EEXIT) return EXIT_FAILURE;
     if (rc != 0) {
         fprintf(stderr, "[ERROR] query execution failed (%d)\n", rc);
         return 139;
     }
     return EXIT_SUCCESS;
+}
+
+/* one rank of a QE_GPUS=N run (a forked child; nothing touched the GPU before the fork) */
+static int run_rank(const input_t* in, int rank, int world, int* to_peers, int from_root) {
+    qe_ctx* c = qe_init(rank);
+    if (!c) {
+        fprintf(stderr, "[ERROR] rank %d: no usable GPU %d\n", rank, rank);
+        return EXIT_FAILURE;
+    }
+    uint8_t id[128];
+    if (rank == 0) {
+        if (qe_comm_unique_id(id) != 0) return EXIT_FAILURE;
+        for (int r = 1; r < world; r++)
+            if (write(to_peers[r], id, sizeof id) != (ssize_t)sizeof id) return EXIT_FAILURE;
+    } else if (read(from_root, id, sizeof id) != (ssize_t)sizeof id) {
+        return EXIT_FAILURE;
+    }
+    if (load_relations(c, in) != 0) return EXIT_FAILURE;
+    qe_comm* m = NULL;
+    if (qe_comm_init(c, world, rank, id, &m) != 0) {
+        fprintf(stderr, "[ERROR] rank %d: %s\n", rank, qe_last_error(c));
+        return EXIT_FAILURE;
+    }
+    char* out = NULL;
+    size_t outlen = 0;
+    uint64_t refused = 0;
+    int rc = qe_run_queries_dist(c, m, in->text, &out, &outlen, &refused);
+    int status = finish(rc, out, outlen, rank == 0);
+    qe_comm_fini(m);
+    qe_fini(c);
+    return status;
+}
+
+int main(void) {
+    input_t in = read_input();
+    const char* g = getenv("QE_GPUS");
+    const int world = g ? atoi(g) : 0;
+    if (world >= 1) {                    /* (QE_GPUS=1: one rank through the same launcher) */
+        int fds[64][2];
+        int to_peers[64];
+        if (world > 64) return EXIT_FAILURE;
+        for (int r = 1; r < world; r++) {
+            if (pipe(fds[r]) != 0) return EXIT_FAILURE;
+            to_peers[r] = fds[r][1];
+        }
+        fflush(stdout);
+        pid_t pid[64];
+        for (int r = 0; r < world; r++) {
+            pid[r] = fork();
+            if (pid[r] < 0) return EXIT_FAILURE;
+            if (pid[r] == 0) _exit(run_rank(&in, r, world, to_peers, r ? fds[r][0] : -1));
+        }
+        /* a rank that fails can leave the others blocked in RCCL: when one ends with an error
+         * while rank 0 still runs, rank 0 gets 10 s to finish on its own (a reference exit(1)
+         * ends every rank alike), then every rank still running is killed */
+        int status0 = 139, left = world, done0 = 0;
+        while (left > 0) {
+            int st = 0;
+            pid_t p = waitpid(-1, &st, 0);
+            if (p < 0) break;
+            left--;
+            const int code = WIFEXITED(st) ? WEXITSTATUS(st) : 139;
+            if (p == pid[0]) {
+                status0 = code;
+                done0 = 1;
+            } else if (code != 0 && !done0) {
+                for (int t = 0; t < 100 && !done0; t++) {
+                    if (waitpid(pid[0], &st, WNOHANG) == pid[0]) {
+                        status0 = WIFEXITED(st) ? WEXITSTATUS(st) : 139;
+                        done0 = 1;
+                        left--;
+                    } else {
+                        usleep(100000);
+                    }
+                }
+                if (!done0) {
+                    for (int r = 0; r < world; r++) kill(pid[r], SIGKILL);
+                    status0 = code;
+                }
+            }
+        }
+        return status0;
+    }
+    const char* dev = getenv("QE_DEVICE");
+    qe_ctx* c = qe_init(dev ? atoi(dev) : 0);
+    if (!c) {
+        fprintf(stderr, "[ERROR] no usable GPU (libqe has no CPU path)\n");
+        return EXIT_FAILURE;
+    }
+    if (load_relations(c, &in) != 0) return EXIT_FAILURE;
+    char* out = NULL;
+    size_t outlen = 0;
+    const char* plan = getenv("QE_PLAN");
+    int rc;
+    if (plan && plan[0] == '1') {
+        uint64_t refused = 0;
+        rc = qe_run_queries_dist(c, NULL, in.text, &out, &outlen, &refused);
+    } else {
+        rc = qe_run_queries(c, in.text, &out, &outlen);
+    }
+    int status = finish(rc, out, outlen, 1);
+    qe_fini(c);
+    return status;
 }

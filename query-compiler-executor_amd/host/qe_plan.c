@@ -465,11 +465,13 @@ typedef struct {
     int base;                   /* keys is a whole base column (vals NONE = row i) */
 } side_t;
 
+static int is_whole(const comp_t* c) { return c->n == 1 && c->m[0].whole; }
+
 static int side_start(plan_t* P, int cid, int b, uint32_t col, const uint8_t* need, side_t* s) {
     const qe_engine* e = P->e;
     comp_t* c = &P->C[cid];
     memset(s, 0, sizeof *s);
-    if (c->n == 1 && c->m[0].b == b && c->m[0].whole) {      /* a whole base relation: never exchanged */
+    if (is_whole(c) && c->m[0].b == b) {                     /* a whole base relation: never exchanged */
         ECHK(e->base_side(e->u, P->q->rels[b], col, &s->keys, &s->vals));
         s->base = 1;
         if (need[b]) {
@@ -554,8 +556,7 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need) {
     const int A = component(P, ba), B = component(P, bb);
     side_t sa, sb;
     /* derived sides first, so their exchanges overlap the base side's local bucket scan */
-    const int a_base = P->C[A].n == 1 && P->C[A].m[0].whole;
-    if (a_base) {
+    if (is_whole(&P->C[A])) {
         ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, &sb));
         ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, &sa));
     } else {

@@ -53,28 +53,33 @@ def test_gpu_executor_without_dead_list_elimination(ctx, monkeypatch):
 WELL_FORMED = re.compile(r"[0-9 ]+\|[0-9.=<>&]+\|[0-9. ]+\n")
 
 
-def _binary(paths, queries):
-    r = subprocess.run([QUERIES], input=dg.protocol_input(paths, queries).encode(), capture_output=True, timeout=600)
+def _binary(paths, queries, env=None):
+    r = subprocess.run([QUERIES], input=dg.protocol_input(paths, queries).encode(), capture_output=True, timeout=600,
+                       env=dict(os.environ, **(env or {})))
     return r.stdout.decode("latin-1"), r.returncode
 
 
+@pytest.mark.parametrize("mode", ["faithful", "plan", "ranks1"])
 @pytest.mark.parametrize("fixture", [os.path.basename(f)[:-5] for f in goldens.golden_files()])
-def test_dropin_binary_matches_reference_golden(fixture):
+def test_dropin_binary_matches_reference_golden(fixture, mode):
     """every golden through build/queries (mmap'd relation files, the reference's stdin protocol).
     Well-formed single-line queries that exit 0 run as one batch per fixture -- every line fills
     all three of the parser's scan buffers, so no line sees another's leftovers -- and the batch's
     stdout is the concatenation of theirs; every other case (malformed lines, exit(1), multi-line
     inputs) runs on its own."""
+    # the faithful executor; the partitioned executor on one GPU; the same through the rank
+    # launcher (fork, RCCL bootstrap over a pipe, one-rank communicator)
+    env = {"faithful": {}, "plan": {"QE_PLAN": "1"}, "ranks1": {"QE_GPUS": "1"}}[mode]
     doc = goldens.load(os.path.join(goldens.GOLDEN_DIR, f"{fixture}.json"))
     rels, paths = goldens.dataset(doc["dataset"])
     batch = [c for c in doc["cases"] if c["rc"] == 0 and WELL_FORMED.fullmatch(c["input"])]
     alone = [c for c in doc["cases"] if c not in batch]
     if batch:
-        out, rc = _binary(paths, "".join(c["input"] for c in batch))
+        out, rc = _binary(paths, "".join(c["input"] for c in batch), env)
         want = "".join(c["stdout"] for c in batch)
         if out != want:
             for c in batch:
-                assert _binary(paths, c["input"]) == (c["stdout"], 0), c["input"]
+                assert _binary(paths, c["input"], env) == (c["stdout"], 0), c["input"]
         assert (out, rc) == (want, 0)
     for case in alone:
-        assert _binary(paths, case["input"]) == (case["stdout"], case["rc"]), case["input"]
+        assert _binary(paths, case["input"], env) == (case["stdout"], case["rc"]), case["input"]
