@@ -147,6 +147,13 @@ int qe_is_sorted(qe_ctx*, const qe_pairs*, int* sorted);
  * outR->n = outS->n = the exact pair count, no lists, and R->match filled (the reference's
  * DArray cannot hold such a result either: src/DArray.h:14-15, src/DArray.c:62-65). */
 int qe_merge_join(qe_ctx*, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS);
+/* a8 without the order: every (R.val[i], S.val[j]) with equal keys (row i / j when val is NULL),
+ * aligned in outR / outS in NO particular order -- the partitioned plan's join (include/qe_plan.h),
+ * whose pairs feed only order-free consumers.  Both sides are sorted by their two global radix
+ * passes only; when the two bucket geometries agree, each 15-bit bucket joins in LDS (a counting
+ * sort of R's bucket by its remaining key bits, one bound lookup per S row), else the sorts
+ * complete and the merge runs.  QE_ETOOBIG beyond the materialisation limit. */
+int qe_join_pairs(qe_ctx*, qe_pairs* R, qe_pairs* S, qe_list* outR, qe_list* outS);
 /* Pairs above which qe_merge_join returns QE_ETOOBIG (default INT32_MAX; env QE_MAT_LIMIT). */
 int qe_set_materialize_limit(qe_ctx*, uint64_t pairs);
 /* a8, aggregate form (C5, SURVEY.md §0.7 / §8(e) "aggregate push-down"): for sorted R and S,

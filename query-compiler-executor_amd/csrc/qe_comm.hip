@@ -330,9 +330,16 @@ int e_join(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, qe_h* oa, qe_h* ob) {
         qe_pairs P = side_pairs(A(ka), va ? A(va) : nullptr);
         qe_pairs Q = side_pairs(A(kb), vb ? A(vb) : nullptr);
         qe_list la{}, lb{};
-        int rc = qe_sort_pairs(c, &P);
-        if (rc == 0) rc = qe_sort_pairs(c, &Q);
-        if (rc == 0) rc = qe_merge_join(c, &P, &Q, &la, &lb);
+        // the plan's pairs need no order (their consumers are joins that sort again, takes and sums)
+        static const bool ordered = getenv("QE_PLAN_MERGE") && getenv("QE_PLAN_MERGE")[0] == '1';
+        int rc = 0;
+        if (ordered) {
+            rc = qe_sort_pairs(c, &P);
+            if (rc == 0) rc = qe_sort_pairs(c, &Q);
+            if (rc == 0) rc = qe_merge_join(c, &P, &Q, &la, &lb);
+        } else {
+            rc = qe_join_pairs(c, &P, &Q, &la, &lb);
+        }
         qe_pairs_free(c, &P);
         qe_pairs_free(c, &Q);
         ck(rc, c);

@@ -57,9 +57,9 @@ constexpr int LB_MAX_COUNTERS = 65536;
 enum : uint32_t { MJF_R_FANOUT = 1u, MJF_S_DUP = 2u, MJF_ERR = 4u, MJF_OVF = 8u };
 
 // A two-level sort whose last step (the per-bucket LDS sort) has not run yet: the pairs' key /
-// val buffers are allocated but unfilled, the bucket-partitioned packed words are kept.  A merge
-// of two such sides with the same bucket geometry runs fused (tl_join); anything else that
-// reads the pairs first completes the sort (pairs_need_keys).
+// val buffers are allocated but unfilled, the bucket-partitioned packed words are kept.  An
+// unordered join of two such sides with the same bucket geometry runs per bucket (bucket_join);
+// anything else that reads the pairs first completes the sort (pairs_need_keys).
 struct DeferredSort {
     uint64_t* words = nullptr;    // bucket-partitioned (field << 32 | rowid) words
     uint32_t* bstart = nullptr;   // bucket starts (+ end)
@@ -68,7 +68,6 @@ struct DeferredSort {
     int lo = 0, L = 0;            // field = (key >> lo) & fmask; bucket = field >> L
     uint64_t fmask = 0, kconst = 0;
     int lr_n = 0, lr_bits[4] = {0, 0, 0, 0};
-    bool val_ready = false;       // vout already holds the sorted rowids (written by tl_join)
 };
 
 // The two-level sort's histogram, computed while the keys were gathered (gather_with_hist): the
@@ -189,13 +188,13 @@ struct SortOut {
     bool keys_new, vals_new;
 };
 // bits (nullable): host {OR, AND} of the keys when already known; otherwise one reduction pass
-// defer = true (qe_sort_pairs only): a two-level sort may stop before its per-bucket step (see
-// DeferredSort); the returned buffers are then filled by pairs_need_keys or tl_join
+// defer = true (qe_join_pairs only): a two-level sort may stop before its per-bucket step (see
+// DeferredSort); the returned buffers are then filled by pairs_need_keys, or never (bucket_join)
 SortOut radix_sort_u64(qe_ctx* c, const uint64_t* keys, const uint32_t* vals /*nullable: iota*/, uint64_t n,
                        bool with_vals, const uint64_t* bits = nullptr, bool defer = false);
 // deferred two-level sorts (qe_sort.hip): complete one before its keys (or vals) are read;
-// drop one whose pairs are freed; the fused merge of two deferred sides (false: not applicable
-// or the output outgrew nR + nS -- the caller completes both sorts and merges as usual)
+// drop one whose pairs are freed; the unordered per-bucket join of two deferred sides (false:
+// not applicable -- the caller completes both sorts and merges as usual)
 void pairs_need_keys(qe_ctx* c, const qe_pairs* p);
 void pairs_need_vals(qe_ctx* c, const qe_pairs* p);
 void pairs_drop_deferred(qe_ctx* c, const qe_pairs* p);   // (also drops a gathered histogram)
@@ -203,7 +202,7 @@ void pairs_drop_deferred(qe_ctx* c, const qe_pairs* p);   // (also drops a gathe
 // histogram is built in the same pass (false: not that sort -- the caller gathers plainly)
 bool gather_with_hist(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint64_t n, uint64_t kor, uint64_t kand,
                       uint64_t* keys);
-bool tl_join(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS, uint32_t* oflags);
+bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS);
 SortOut radix_sort_u32(qe_ctx* c, const uint32_t* keys, const uint32_t* vals, uint64_t n,
                        const uint64_t* bits = nullptr);
 // multi-GPU (qe_dist.hip): hash-partition rows into per-destination segments of out_keys /

@@ -1572,12 +1572,47 @@ int qe_gather_pairs(qe_ctx* c, qe_col col, const qe_list* rows, qe_pairs* out) {
     QE_API_END(c)
 }
 
+// qe_sort_pairs' body; defer: a large two-level sort may stop before its per-bucket step
+// (qe_join_pairs hands such sides to bucket_join)
+static void sort_pairs(qe_ctx* c, qe_pairs* p, bool defer) {
+    if (p->flags & PF_SORTED) return;
+    p->flags &= ~QE_PAIRS_MATCHED;
+    uint64_t bits[2] = {p->kor, p->kand};
+    SortOut so = radix_sort_u64(c, p->key, p->val, p->n, true, (p->flags & QE_PAIRS_BITS) ? bits : nullptr, defer);
+    if (so.keys_new) {
+        pairs_drop_deferred(c, p);   // a gathered histogram the sort did not take dies with the keys
+        if (p->owns & 1) dfree(c, p->key);
+        p->key = (uint64_t*)so.keys;
+        p->owns |= 1;
+    }
+    if (so.vals_new) {
+        if (p->owns & 2) dfree(c, p->val);
+        p->val = so.vals;
+        p->owns |= 2;
+    }
+    p->flags |= PF_SORTED;
+}
+
+int qe_join_pairs(qe_ctx* c, qe_pairs* R, qe_pairs* S, qe_list* outR, qe_list* outS) {
+    QE_API_BEGIN(c)
+    sort_pairs(c, R, true);
+    sort_pairs(c, S, true);
+    if (bucket_join(c, R, S, outR, outS)) return 0;
+    pairs_need_keys(c, R);
+    pairs_need_keys(c, S);
+    uint32_t fl = MJF_R_FANOUT | MJF_S_DUP;
+    merge_sorted(c, R, S, outR, outS, &fl);
+    outR->flags = outS->flags = 0;
+    return 0;
+    QE_API_END(c)
+}
+
 int qe_sort_pairs(qe_ctx* c, qe_pairs* p) {
     QE_API_BEGIN(c)
     if (p->flags & PF_SORTED) return 0;
     p->flags &= ~QE_PAIRS_MATCHED;
     uint64_t bits[2] = {p->kor, p->kand};
-    SortOut so = radix_sort_u64(c, p->key, p->val, p->n, true, (p->flags & QE_PAIRS_BITS) ? bits : nullptr, true);
+    SortOut so = radix_sort_u64(c, p->key, p->val, p->n, true, (p->flags & QE_PAIRS_BITS) ? bits : nullptr, false);
     if (so.keys_new) {
         pairs_drop_deferred(c, p);   // a gathered histogram the sort did not take dies with the keys
         if (p->owns & 1) dfree(c, p->key);
@@ -1606,12 +1641,10 @@ int qe_merge_join(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_l
     QE_API_BEGIN(c)
     const bool sorted = pairs_sorted(c, R) && pairs_sorted(c, S);
     uint32_t fl = MJF_R_FANOUT | MJF_S_DUP;
-    if (!(sorted && tl_join(c, R, S, outR, outS, &fl))) {   // fused: both sides' sorts end inside the join
-        pairs_need_keys(c, R);
-        pairs_need_keys(c, S);
-        if (sorted) merge_sorted(c, R, S, outR, outS, &fl);
-        else merge_sequential(c, R, S, outR, outS);
-    }
+    pairs_need_keys(c, R);
+    pairs_need_keys(c, S);
+    if (sorted) merge_sorted(c, R, S, outR, outS, &fl);
+    else merge_sequential(c, R, S, outR, outS);
     outR->flags = ((R->flags & PF_DISTINCT) && sorted && !(fl & MJF_R_FANOUT)) ? QE_LIST_DISTINCT : 0;
     outS->flags = ((S->flags & PF_DISTINCT) && sorted && !(fl & MJF_S_DUP)) ? QE_LIST_DISTINCT : 0;
     return 0;

@@ -935,253 +935,122 @@ __global__ void __launch_bounds__(TL2_NT, 4) tl_pass2_kernel(const uint64_t* __r
     }
 }
 
-// ---- fused per-bucket sort + merge join (tl_join) ------------------------------------------
+// ---- bucket join (the partitioned plan's join: pairs in no particular order) ----------------
 // Both join sides went through the two global passes of the two-level sort with the same bucket
-// geometry, so equal keys share a bucket number and bucket b of R joins bucket b of S only.
-// One workgroup per bucket (taken in order by ticket): both buckets' packed words are sorted in
-// LDS (the per-bucket step of the sort, done here instead of writing sorted key + rowid arrays
-// and reading them back in the merge), each sorted R row finds its S run by binary searches in
-// LDS, a block scan and a lookback over buckets give the output offsets, and the pairs are
-// written in the reference's order (key, then R order, then S order).  Also written: R's match
-// count and rowid per sorted row (what qe_driver_counts reads).
-//
-// lds_sort_words: stable LDS radix sort of m <= NT x ITEMS words held in registers in the
-// wave-contiguous layout (wave w owns jm x 64 consecutive words); on return `stage` holds the
-// sorted words (the same ranking rounds as tl_local_kernel).
-template <int NT, int ITEMS>
-__device__ __forceinline__ void lds_sort_words(uint64_t (&word)[ITEMS], uint32_t m, const LocalRounds& lr,
-                                               uint64_t* stage, uint32_t (*whist)[256], uint32_t* bexcl,
-                                               uint32_t* wsum) {
-    constexpr int NW = NT / 64, BINS = 256;
-    const int w = wave_id(), l = lane_id();
-    const uint64_t lt = lanemask_lt();
-    const uint32_t jm = (m + NW * 64 - 1) / (NW * 64);
-    const uint32_t wbase = (uint32_t)w * jm * 64;
-    if (lr.n == 0) {   // no bits below the bucket: already in order
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const uint32_t i = wbase + (uint32_t)j * 64 + l;
-            if ((uint32_t)j < jm && i < m) stage[i] = word[j];
-        }
-        __syncthreads();
-        return;
-    }
-    int dsh = 32;
-    for (int r = 0; r < lr.n; r++) {
-        const int bits = lr.bits[r];
-        if (r > 0) dsh += lr.bits[r - 1];
-        const uint32_t mask = (1u << bits) - 1u;
-        for (int i = threadIdx.x; i < NW * BINS; i += NT) (&whist[0][0])[i] = 0;
-        __syncthreads();
-        uint32_t pos[ITEMS];
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            pos[j] = 0;
-            if ((uint32_t)j >= jm) continue;   // wave-uniform
-            const uint32_t i = wbase + (uint32_t)j * 64 + l;
-            const bool ok = i < m;
-            const uint32_t d = (uint32_t)(word[j] >> dsh) & mask;
-            uint64_t peers = __ballot(ok);
-#pragma unroll
-            for (int b = 0; b < 8; b++) {
-                if (b >= bits) break;
-                const bool bit = (d >> b) & 1u;
-                const uint64_t mm = __ballot(bit);
-                peers &= bit ? mm : ~mm;
-            }
-            const int leader = peers ? (__ffsll((unsigned long long)peers) - 1) : 0;
-            uint32_t old = 0;
-            if (ok && l == leader) {
-                old = whist[w][d];
-                whist[w][d] = old + (uint32_t)__popcll(peers);
-            }
-            old = (uint32_t)__shfl((int)old, leader, 64);
-            pos[j] = old + (uint32_t)__popcll(peers & lt);
-        }
-        __syncthreads();
-        uint32_t tot = 0;
-        if (threadIdx.x < BINS) {
-#pragma unroll
-            for (int ww = 0; ww < NW; ww++) {
-                const uint32_t cc = whist[ww][threadIdx.x];
-                whist[ww][threadIdx.x] = tot;
-                tot += cc;
-            }
-        }
-        const uint32_t inc = wave_incl_scan_u32(tot);
-        if (l == 63) wsum[w] = inc;
-        __syncthreads();
-        if (threadIdx.x < BINS) {
-            uint32_t ex = inc - tot;
-            for (int ww = 0; ww < w; ww++) ex += wsum[ww];
-            bexcl[threadIdx.x] = ex;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const uint32_t i = wbase + (uint32_t)j * 64 + l;
-            if ((uint32_t)j < jm && i < m) {
-                const uint32_t d = (uint32_t)(word[j] >> dsh) & mask;
-                stage[bexcl[d] + whist[w][d] + pos[j]] = word[j];
-            }
-        }
-        __syncthreads();
-        if (r + 1 < lr.n) {
-#pragma unroll
-            for (int j = 0; j < ITEMS; j++) {
-                const uint32_t i = wbase + (uint32_t)j * 64 + l;
-                word[j] = ((uint32_t)j < jm && i < m) ? stage[i] : 0;
-            }
-            __syncthreads();   // every read of stage before the next round writes it
-        }
-    }
-}
-
-constexpr int TJ_NT = 1024, TJ_ITEMS = (TL_CAP + TJ_NT - 1) / TJ_NT;   // 5 words per thread per side
-static_assert(TJ_NT * TJ_ITEMS >= TL_CAP, "a bucket fits the workgroup's registers");
+// geometry, so equal keys share a bucket and bucket b of R joins bucket b of S only -- and inside
+// a bucket a key is its L low field bits (L <= HJ_DBITS): a dense domain.  One workgroup per
+// bucket (in order, by ticket): R's rowids are grouped by key value with an LDS counting sort
+// (histogram, scan, scatter -- the runs need no order inside), every S row finds its R run by
+// one LDS read of the run bounds, a (row-group, wave) scan gives the offsets inside the bucket and
+// ONE atomic reserves the bucket's output slice (no order between buckets is needed: no lookback
+// chain through 32 K buckets), and consecutive lanes write consecutive pairs.  This replaces, for a join whose
+// pairs need no order, the per-bucket LDS sorts of both sides (12 B/row written and read back)
+// and the merge's searches: words in (8 B/row), pairs out (8 B/pair).  LDS: run bounds (4 B per
+// key value of the bucket) + R rowids (4 B per row) -- four workgroups per CU at L = 12.
+constexpr int HJ_NT = 1024, HJ_NW = HJ_NT / 64;   // 53 VGPRs: two blocks = 32 waves per CU
+constexpr int HJ_I = (TL_CAP + HJ_NT - 1) / HJ_NT;   // rows per thread per side
+constexpr int HJ_DBITS = 13;                          // largest in-bucket key domain (2^13 values)
+static_assert(HJ_I * HJ_NW <= 128, "the (row-group, wave) table is scanned by one wave, two entries per lane");
 
 __device__ __forceinline__ uint32_t fld(uint64_t w) { return (uint32_t)(w >> 32); }   // the key field
 
-__global__ void __launch_bounds__(TJ_NT) tl_join_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict__ bsR,
-                                                        const uint64_t* __restrict__ wS, const uint32_t* __restrict__ bsS,
-                                                        LocalRounds lr, uint32_t* __restrict__ matchR,
-                                                        uint32_t* __restrict__ valR, uint32_t* __restrict__ outR,
-                                                        uint32_t* __restrict__ outS, uint64_t cap,
-                                                        uint32_t* __restrict__ flags, uint64_t* status, uint32_t* ticket,
-                                                        uint32_t epoch, uint32_t nb, uint64_t* total_out) {
-    constexpr int NW = TJ_NT / 64;
-    constexpr uint32_t Q = TJ_ITEMS;          // sorted R rows per thread in the walk (consecutive)
-    __shared__ uint64_t sR[TL_CAP];
-    __shared__ uint64_t sS[TL_CAP];
-    __shared__ uint32_t loc[TL_CAP];          // per sorted R row: S run start | run length << 16
-    __shared__ uint32_t roff[TL_CAP];         // per sorted R row: bucket-relative output offset
-    __shared__ uint32_t whist[NW][256];
-    __shared__ uint32_t bexcl[256];
-    __shared__ uint32_t wsum[NW];
+template <int DBITS>
+__global__ void __launch_bounds__(HJ_NT) tl_hjoin_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict__ bsR,
+                                                         const uint64_t* __restrict__ wS, const uint32_t* __restrict__ bsS,
+                                                         int L, uint32_t* __restrict__ outR, uint32_t* __restrict__ outS,
+                                                         uint64_t cap, uint64_t* total_out) {
+    __shared__ uint32_t bnd[1 << DBITS];   // per key value: count, then run start, then run end
+    __shared__ uint32_t rr[TL_CAP];        // R rowids grouped by key value
+    __shared__ uint32_t tab[HJ_I * HJ_NW];
+    __shared__ uint32_t wsum[HJ_NW];
     __shared__ uint64_t s_excl;
-    __shared__ uint32_t s_flag, s_ticket;
-    const uint32_t b = take_ticket(ticket, &s_ticket);   // buckets in order: the lookback cannot deadlock
+    __shared__ uint32_t s_total;
+    const uint32_t b = blockIdx.x;
     const uint32_t r0 = bsR[b], mR = bsR[b + 1] - r0, s0 = bsS[b], mS = bsS[b + 1] - s0;
-    if (threadIdx.x == 0) s_flag = 0;
+    const uint32_t D = 1u << L, dmask = D - 1u;
     const int w = wave_id(), l = lane_id();
-    {
-        uint64_t wr[TJ_ITEMS], ws[TJ_ITEMS];   // both buckets' loads in flight before any ranking
-        const uint32_t jmR = (mR + NW * 64 - 1) / (NW * 64), jmS = (mS + NW * 64 - 1) / (NW * 64);
+    const uint64_t* __restrict__ bR = wR + r0;
+    const uint64_t* __restrict__ bS = wS + s0;
+    uint64_t wr[HJ_I];   // R's loads in flight first; S's are issued once R's rows are scattered
 #pragma unroll
-        for (int j = 0; j < TJ_ITEMS; j++) {
-            const uint32_t iR = (uint32_t)w * jmR * 64 + (uint32_t)j * 64 + l;
-            const uint32_t iS = (uint32_t)w * jmS * 64 + (uint32_t)j * 64 + l;
-            wr[j] = ((uint32_t)j < jmR && iR < mR) ? wR[r0 + iR] : 0;
-            ws[j] = ((uint32_t)j < jmS && iS < mS) ? wS[s0 + iS] : 0;
-        }
-        lds_sort_words<TJ_NT, TJ_ITEMS>(wr, mR, lr, sR, whist, bexcl, wsum);
-        lds_sort_words<TJ_NT, TJ_ITEMS>(ws, mS, lr, sS, whist, bexcl, wsum);
+    for (int j = 0; j < HJ_I; j++) {
+        const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
+        wr[j] = i < mR ? bR[i] : 0;
     }
-    // walk: thread t owns sorted R rows [t*Q, t*Q + Q); its S range from two searches, then one
-    // lower / upper bound pair per row inside that range
-    const uint32_t e0 = threadIdx.x * Q;
-    const uint32_t nv = mR > e0 ? (mR - e0 < Q ? mR - e0 : Q) : 0u;
-    uint32_t cnt[Q], lo[Q], tsum = 0, myflag = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < Q; j++) cnt[j] = lo[j] = 0;
-    if (nv) {
-        const uint32_t kf = fld(sR[e0]), kl = fld(sR[e0 + nv - 1]);
-        uint32_t a = 0, an = mS;
-        while (an) {   // lower_bound(kf)
-            const uint32_t h = an >> 1;
-            if (fld(sS[a + h]) < kf) {
-                a += h + 1;
-                an -= h + 1;
-            } else {
-                an = h;
-            }
-        }
-        uint32_t e = a, en = mS - a;
-        while (en) {   // upper_bound(kl)
-            const uint32_t h = en >> 1;
-            if (fld(sS[e + h]) <= kl) {
-                e += h + 1;
-                en -= h + 1;
-            } else {
-                en = h;
-            }
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < Q; j++) {
-            if (j >= nv) continue;
-            const uint32_t key = fld(sR[e0 + j]);
-            uint32_t x = a, xn = e - a;
-            while (xn) {
-                const uint32_t h = xn >> 1;
-                if (fld(sS[x + h]) < key) {
-                    x += h + 1;
-                    xn -= h + 1;
-                } else {
-                    xn = h;
-                }
-            }
-            uint32_t y = x, yn = e - x;
-            while (yn) {
-                const uint32_t h = yn >> 1;
-                if (fld(sS[y + h]) <= key) {
-                    y += h + 1;
-                    yn -= h + 1;
-                } else {
-                    yn = h;
-                }
-            }
-            lo[j] = x;
-            cnt[j] = y - x;
-            tsum += y - x;
-            if (y - x > 1) myflag |= MJF_R_FANOUT;
-            if (y > x && e0 + j + 1 < mR && fld(sR[e0 + j + 1]) == key) myflag |= MJF_S_DUP;
-        }
-    }
-    // block scan of the per-thread pair counts (a bucket's pairs < 2^32: <= TL_CAP^2)
-    const uint32_t inc = wave_incl_scan_u32(tsum);
-    if (l == 63) wsum[w] = inc;
+    for (uint32_t v = threadIdx.x; v < D; v += HJ_NT) bnd[v] = 0;
     __syncthreads();
-    uint32_t run = inc - tsum, btotal = 0;
-    for (int ww = 0; ww < NW; ww++) {
-        if (ww < w) run += wsum[ww];
-        btotal += wsum[ww];
-    }
 #pragma unroll
-    for (uint32_t j = 0; j < Q; j++) {
-        if (j >= nv) continue;
-        loc[e0 + j] = lo[j] | (cnt[j] << 16);   // both < TL_CAP < 2^16
-        roff[e0 + j] = run;
-        run += cnt[j];
-    }
-    if (w == 0) {
-        lookback_publish(status, epoch, b, btotal);
-        const uint64_t ex = lookback_wait(status, epoch, b, btotal);
-        if (l == 0) {
-            s_excl = ex;
-            if (b == nb - 1) *total_out = ex + btotal;
-            if (ex + btotal > LB_VAL_MASK) atomicOr(flags, MJF_OVF);
+    for (int j = 0; j < HJ_I; j++)
+        if ((uint32_t)j * HJ_NT + threadIdx.x < mR) atomicAdd(&bnd[fld(wr[j]) & dmask], 1u);
+    __syncthreads();
+    {   // exclusive scan of the D counts: PER consecutive values per thread, then a block scan
+        const uint32_t PER = (D + HJ_NT - 1) / HJ_NT, v0 = threadIdx.x * PER;
+        uint32_t sum = 0;
+        for (uint32_t k = 0; k < PER && v0 + k < D; k++) sum += bnd[v0 + k];
+        const uint32_t inc = wave_incl_scan_u32(sum);
+        if (l == 63) wsum[w] = inc;
+        __syncthreads();
+        uint32_t run = inc - sum;
+        for (int ww = 0; ww < w; ww++) run += wsum[ww];
+        for (uint32_t k = 0; k < PER && v0 + k < D; k++) {
+            const uint32_t cnt = bnd[v0 + k];
+            bnd[v0 + k] = run;
+            run += cnt;
         }
     }
-    if (myflag) atomicOr(&s_flag, myflag);
     __syncthreads();
-    if (threadIdx.x == 0 && s_flag) {
-        const uint32_t seen = __hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (s_flag & ~seen) atomicOr(flags, s_flag);
+#pragma unroll
+    for (int j = 0; j < HJ_I; j++)   // scatter: afterwards bnd[v] is the END of v's run
+        if ((uint32_t)j * HJ_NT + threadIdx.x < mR) rr[atomicAdd(&bnd[fld(wr[j]) & dmask], 1u)] = (uint32_t)wr[j];
+    uint64_t ws[HJ_I];
+#pragma unroll
+    for (int j = 0; j < HJ_I; j++) {
+        const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
+        ws[j] = i < mS ? bS[i] : 0;
     }
+    __syncthreads();
+    uint32_t pre[HJ_I];   // (the runs are looked up again when writing: fewer live registers)
+#pragma unroll
+    for (int j = 0; j < HJ_I; j++) {
+        uint32_t cnt = 0;
+        if ((uint32_t)j * HJ_NT + threadIdx.x < mS) {
+            const uint32_t v = fld(ws[j]) & dmask;
+            cnt = bnd[v] - (v ? bnd[v - 1] : 0u);
+        }
+        const uint32_t inc = wave_incl_scan_u32(cnt);
+        pre[j] = inc - cnt;
+        if (l == 63) tab[j * HJ_NW + w] = inc;
+    }
+    __syncthreads();
+    if (w == 0) {   // (row group, wave) totals in row order -> bucket offsets; bucket total -> lookback
+        constexpr uint32_t E = HJ_I * HJ_NW;
+        const uint32_t a0 = 2u * l < E ? tab[2 * l] : 0u, a1 = 2u * l + 1 < E ? tab[2 * l + 1] : 0u;
+        const uint32_t inc = wave_incl_scan_u32(a0 + a1);
+        const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
+        if (2u * l < E) tab[2 * l] = inc - a0 - a1;
+        if (2u * l + 1 < E) tab[2 * l + 1] = inc - a1;
+        if (l == 0) {   // the pairs need no order: a bucket reserves its output slice with one atomic
+            s_excl = total ? atomicAdd(reinterpret_cast<unsigned long long*>(total_out), (unsigned long long)total)
+                           : 0ull;
+            s_total = total;
+        }
+    }
+    __syncthreads();
     const uint64_t gofs = s_excl;
-    const bool room = gofs + btotal <= cap;
-    // emission: consecutive threads take consecutive sorted R rows, so with fan-out ~1 the
-    // stores of a wave-instruction are consecutive
-    for (uint32_t i = threadIdx.x; i < mR; i += TJ_NT) {
-        const uint32_t v = loc[i], c = v >> 16, s = v & 0xFFFFu;
-        const uint32_t rr = (uint32_t)sR[i];
-        matchR[r0 + i] = c;
-        valR[r0 + i] = rr;
-        if (!room) continue;
-        const uint64_t o = gofs + roff[i];
-        for (uint32_t k = 0; k < c; k++) {
-            outR[o + k] = rr;
-            outS[o + k] = (uint32_t)sS[s + k];
+    if (gofs + s_total > cap) return;   // outgrew the buffers: the host re-runs with the exact size
+#pragma unroll
+    for (int j = 0; j < HJ_I; j++) {
+        if ((uint32_t)j * HJ_NT + threadIdx.x >= mS) continue;
+        const uint32_t v = fld(ws[j]) & dmask;
+        const uint32_t st = v ? bnd[v - 1] : 0u, cnt = bnd[v] - st;
+        const uint64_t o = gofs + tab[j * HJ_NW + w] + pre[j];
+        const uint32_t srow = (uint32_t)ws[j];
+        uint32_t* __restrict__ pR = outR + o;
+        uint32_t* __restrict__ pS = outS + o;
+#pragma nounroll
+        for (uint32_t k = 0; k < cnt; k++) {   // fan-out ~1: a plain loop (unrolled, it was 118 VGPRs)
+            pR[k] = rr[st + k];
+            pS[k] = srow;
         }
     }
 }
@@ -1453,16 +1322,6 @@ static bool prof_split() {   // tuning aid: QE_PROF_SPLIT=1 times the second pas
     return on;
 }
 
-// QE_FUSED_JOIN=1 (read at every sort): leave the per-bucket step of large two-level sorts to a
-// fused merge (tl_join).  Off by default: measured on MI355X it is SLOWER -- 3.35 ms per
-// 1e8 x 1e8 join against 2.2 ms for two per-bucket sorts + the merge -- because its 137 KiB of
-// LDS (both buckets, per-row runs and offsets) leave one workgroup per CU, so the load, ranking,
-// search and store phases of a bucket never overlap another bucket's.
-static bool fused_on() {
-    const char* s = getenv("QE_FUSED_JOIN");
-    return s && s[0] == '1';
-}
-
 static uint64_t sort_pre_min() {   // tuning knob: QE_SORT_PRE_MIN = smallest n for the lookback-free form
     static uint64_t v = [] {
         const char* s = getenv("QE_SORT_PRE_MIN");
@@ -1561,7 +1420,7 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
         return false;
     }
     if constexpr (sizeof(K) == 8) {
-        if (defer && fused_on()) {   // the per-bucket step waits for the consumer (tl_join / pairs_need_keys)
+        if (defer) {   // the per-bucket step waits for the consumer (bucket_join / pairs_need_keys)
             DeferredSort d;
             d.words = w2;
             d.bstart = bstart;
@@ -1660,6 +1519,26 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
                                dim3(R_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, dsh, pmask, f, base1,
                                sl.status, sl.ticket, sl.epoch);
         QE_HIP(hipGetLastError());
+    }
+    if constexpr (sizeof(K) == 8) {
+        if (defer && H == TL_H) {   // the per-bucket step waits for the consumer (bucket_join / pairs_need_keys)
+            DeferredSort d;
+            d.words = w2;
+            d.bstart = bstart;
+            d.kout = (uint64_t*)kout;
+            d.vout = vout;
+            d.lo = f.lo;
+            d.L = L;
+            d.fmask = f.fmask;
+            d.kconst = f.kconst;
+            d.lr_n = lr.n;
+            for (int r = 0; r < 4; r++) d.lr_bits[r] = lr.bits[r];
+            c->deferred[kout] = d;
+            dfree(c, w1);
+            dfree(c, hist);
+            *out = SortOut{kout, vout, true, true};
+            return true;
+        }
     }
     {
         Timed t(c, "sort_local", 8.0 * n + ((double)sizeof(K) + 4) * n);
@@ -1843,12 +1722,7 @@ void pairs_need_keys(qe_ctx* c, const qe_pairs* p) {
     drop(c, d);
 }
 
-void pairs_need_vals(qe_ctx* c, const qe_pairs* p) {
-    if (!p || !p->key) return;
-    auto it = c->deferred.find(p->key);
-    if (it != c->deferred.end() && it->second.val_ready) return;
-    pairs_need_keys(c, p);
-}
+void pairs_need_vals(qe_ctx* c, const qe_pairs* p) { pairs_need_keys(c, p); }
 
 void pairs_drop_deferred(qe_ctx* c, const qe_pairs* p) {
     if (!p || !p->key) return;
@@ -1902,61 +1776,53 @@ bool gather_with_hist(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint
     return true;
 }
 
-bool tl_join(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS, uint32_t* oflags) {
+bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS) {
     auto iR = c->deferred.find(R->key), iS = c->deferred.find(S->key);
     if (iR == c->deferred.end() || iS == c->deferred.end() || R->key == S->key) return false;
-    DeferredSort& dR = iR->second;
+    const DeferredSort& dR = iR->second;
     const DeferredSort& dS = iS->second;
-    if (dR.lo != dS.lo || dR.L != dS.L || dR.fmask != dS.fmask || dR.kconst != dS.kconst ||
-        dR.lr_n != dS.lr_n)
-        return false;   // different bucket geometry
+    if (dR.lo != dS.lo || dR.L != dS.L || dR.fmask != dS.fmask || dR.kconst != dS.kconst || dR.L > HJ_DBITS)
+        return false;   // different bucket geometry, or a bucket domain beyond LDS
     const uint64_t nR = R->n, nS = S->n;
-    if (!R->match) {
-        R->match = dalloc_t<uint32_t>(c, nR);
-        R->owns |= 4;
-    }
-    const uint64_t cap = nR + nS;
-    uint32_t* oR = dalloc_t<uint32_t>(c, cap);
-    uint32_t* oS = dalloc_t<uint32_t>(c, cap);
-    uint32_t* d_flags = (uint32_t*)(c->d_scratch + 16);
-    QE_HIP(hipMemsetAsync(d_flags, 0, 4, c->stream));
-    {
-        LBSlot s = lb_acquire(c, TL_BUCKETS);
-        // algorithmic bytes: both sides' words in, R's match + rowid out (+ 8 B per pair below)
-        Timed t(c, "tl_join", 8.0 * (double)(nR + nS) + 8.0 * (double)nR);
-        hipLaunchKernelGGL(tl_join_kernel, dim3(TL_BUCKETS), dim3(TJ_NT), 0, c->stream, dR.words, dR.bstart, dS.words,
-                           dS.bstart, rounds_of(dR), R->match, dR.vout, oR, oS, cap, d_flags, s.status, s.ticket,
-                           s.epoch, (uint32_t)TL_BUCKETS, c->d_scratch + 17);
-        QE_HIP(hipGetLastError());
-    }
-    uint64_t h[2];
-    read_words(c, c->d_scratch + 16, h, 2);
-    const uint32_t fl = (uint32_t)h[0];
-    const uint64_t P = h[1];
-    if (P > cap || (fl & MJF_OVF)) {   // outgrew the optimistic buffers: the caller merges as usual
+    uint64_t cap = nR + nS;   // optimistic (fan-out ~1); an outgrown launch re-runs with the exact size
+    for (int attempt = 0; attempt < 2; attempt++) {
+        uint32_t* oR = dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1));
+        uint32_t* oS = dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1));
+        QE_HIP(hipMemsetAsync(c->d_scratch + 17, 0, sizeof(uint64_t), c->stream));
+        {
+            // algorithmic bytes: both sides' words in (+ 8 B per pair below)
+            Timed t(c, "bucket_join", 8.0 * (double)(nR + nS));
+            if (dR.L <= 12)
+                hipLaunchKernelGGL(tl_hjoin_kernel<12>, dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream, dR.words, dR.bstart,
+                                   dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17);
+            else
+                hipLaunchKernelGGL(tl_hjoin_kernel<HJ_DBITS>, dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream, dR.words,
+                                   dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17);
+            QE_HIP(hipGetLastError());
+        }
+        const uint64_t P = read_u64(c, c->d_scratch + 17);
+        if (P <= cap) {
+            if (c->prof && !c->pending.empty()) c->pending.back().bytes += 8.0 * (double)P;
+            if (P > c->mat_limit) {   // the reference's DArray cannot hold it either (src/DArray.h:14-15)
+                dfree(c, oR);
+                dfree(c, oS);
+                char msg[160];
+                snprintf(msg, sizeof msg, "join of %llu pairs exceeds the materialisation limit %llu",
+                         (unsigned long long)P, (unsigned long long)c->mat_limit);
+                throw Error(QE_ETOOBIG, msg);
+            }
+            outR->d = oR;
+            outS->d = oS;
+            outR->n = outS->n = P;
+            outR->cap = outS->cap = cap;
+            outR->flags = outS->flags = 0;
+            return true;
+        }
         dfree(c, oR);
         dfree(c, oS);
-        return false;
+        cap = P;
     }
-    if (c->prof && !c->pending.empty()) c->pending.back().bytes += 8.0 * (double)P;
-    dR.val_ready = true;
-    R->flags |= QE_PAIRS_MATCHED;
-    *oflags = fl;
-    outR->n = outS->n = P;
-    if (P > c->mat_limit) {   // R->match stays valid: the caller may take the aggregate form
-        dfree(c, oR);
-        dfree(c, oS);
-        outR->d = outS->d = nullptr;
-        outR->cap = outS->cap = 0;
-        char msg[160];
-        snprintf(msg, sizeof msg, "merge join of %llu pairs exceeds the materialisation limit %llu",
-                 (unsigned long long)P, (unsigned long long)c->mat_limit);
-        throw Error(QE_ETOOBIG, msg);
-    }
-    outR->d = oR;
-    outS->d = oS;
-    outR->cap = outS->cap = cap;
-    return true;
+    throw Error(QE_EINVAL, "internal: bucket join outgrew its exact size");
 }
 
 }  // namespace qe

@@ -80,6 +80,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "qe_sort_pairs": (I, [P, C.POINTER(Pairs)]),
         "qe_is_sorted": (I, [P, C.POINTER(Pairs), C.POINTER(C.c_int)]),
         "qe_merge_join": (I, [P, C.POINTER(Pairs), C.POINTER(Pairs), C.POINTER(List), C.POINTER(List)]),
+        "qe_join_pairs": (I, [P, C.POINTER(Pairs), C.POINTER(Pairs), C.POINTER(List), C.POINTER(List)]),
         "qe_scan_join": (I, [P, C.POINTER(Pairs), C.POINTER(Pairs), C.POINTER(List), C.POINTER(List)]),
         "qe_driver_counts": (I, [P, C.POINTER(Pairs), C.POINTER(Pairs), C.POINTER(List), C.POINTER(List), I, U64,
                                  C.POINTER(C.c_void_p)]),
@@ -297,6 +298,12 @@ class Ctx:
     def merge_join(self, R: Pairs, S: Pairs) -> tuple[List, List]:
         a, b = List(), List()
         self._chk(self.lib.qe_merge_join(self.h, C.byref(R), C.byref(S), C.byref(a), C.byref(b)))
+        return a, b
+
+    def join_pairs(self, R: Pairs, S: Pairs) -> tuple[List, List]:
+        """qe_join_pairs: every matching (R val, S val), aligned, in no particular order"""
+        a, b = List(), List()
+        self._chk(self.lib.qe_join_pairs(self.h, C.byref(R), C.byref(S), C.byref(a), C.byref(b)))
         return a, b
 
     def scan_join(self, R: Pairs, S: Pairs) -> tuple[List, List]:
