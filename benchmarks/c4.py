@@ -69,21 +69,40 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
     t0 = time.time()
     specs = gen_c4(ctx)
     log(f"[c4] {len(specs)} relations in HBM in {time.time() - t0:.2f}s; {len(queries)} gated queries")
+    # the measured line: the batch's queries on concurrent lanes (qe_run_queries_parallel: worker
+    # contexts on this GPU, each its own stream, the relations shared); `--plan faithful` = one lane
+    workers = int(os.environ.get("QE_WORKERS", "8"))
+    if getattr(args, "plan", "auto") == "faithful":
+        workers = 1
+
+    def run_batch():
+        return ctx.run_parallel(text, workers)
+
     out = None
     for _ in range(args.warmup):
-        out, rc = ctx.run(text)
+        out, rc = run_batch()
     ctx.set_profiling(True)
     ctx.reset_stats()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out, rc = ctx.run(text)
+        out, rc = run_batch()
     ctx.sync()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     stats = ctx.kernel_stats()
     ctx.set_profiling(False)
     kern = sorted(stats.items(), key=lambda kv: -kv[1]["ms"])
+
+    def timed(fn):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        o = fn()
+        ctx.sync()
+        d = time.perf_counter() - t1
+        return {"ms_per_step": round(d * 1e3, 3), "value": round(len(queries) / d, 2), "stdout_identical": o == out}
+    others = {"sequential_faithful (qe_run_queries)": timed(lambda: ctx.run(text)[0]),
+              "partitioned_plan (qe_run_queries_dist)": timed(lambda: ctx.run_dist(text)[0])}
     res = {
         "metric": METRIC, "value": round(len(queries) * args.steps / dt, 2), "unit": "queries/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
@@ -92,9 +111,13 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
         "config": {"workload": "C4: 14 relations, %d gated SIGMOD-style queries in batches of %d"
                                % (len(queries), dg.C4_BATCH),
                    "rows_total": sum(s.rows for s in specs), "output_lines": out.count("\n"),
-                   "executor": "libqe faithful state machine (qe_run_queries)", "parallelism": "single GPU"},
+                   "executor": "qe_run_queries_parallel: the faithful executor, %d concurrent lanes (worker "
+                               "contexts = HIP streams on this GPU, relations shared), output in input order"
+                               % workers,
+                   "parallelism": "single GPU, inter-query concurrency x%d" % workers},
+        "other_executors_same_batch": others,
         "roofline": roofline_fn(stats, traffic_fn() if traffic_fn else None) if roofline_fn else None,
-        "stages": {k: {"ms_per_step": round(s["ms"] / args.steps, 3), "launches_per_step": s["launches"] / args.steps}
+        "stages_lane0": {k: {"ms_per_step": round(s["ms"] / args.steps, 3), "launches_per_step": s["launches"] / args.steps}
                    for k, s in kern[:10]},
     }
     if not args.no_cpu:

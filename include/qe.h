@@ -123,6 +123,17 @@ int qe_drop_relations(qe_ctx*);
  * another negative code. */
 int  qe_run_queries(qe_ctx*, const char* text, char** out, size_t* outlen);
 void qe_free_host(void*);
+/* The same batch with its queries run concurrently: `workers` (1..16) contexts on this ctx's GPU --
+ * each its own HIP stream and allocator, this ctx's relations shared -- take queries in turn from
+ * host threads; the outputs are joined in input order and cut after the first query where the
+ * reference exits (QE_EEXIT), so the bytes and the status are qe_run_queries'.  The reference runs
+ * its queries one after another with no state between them but rand() (src/utilities.c:289-300;
+ * the gate excludes rand-dependent outputs), so the order of execution is not observable. */
+int  qe_run_queries_parallel(qe_ctx*, int workers, const char* text, char** out, size_t* outlen);
+/* The worker contexts behind qe_run_queries_parallel (made on first use, freed by qe_fini; the
+ * relations re-shared at every call); qe_bind_thread makes the ctx's GPU the calling thread's. */
+int  qe_workers(qe_ctx*, int n, qe_ctx** out);
+int  qe_bind_thread(qe_ctx*);
 /* Row count of the first selected binding's list in the last query that printed sums (the
  * join's output cardinality for the relational shapes; bench "joined tuples"). */
 int  qe_last_result_rows(qe_ctx*, uint64_t* rows);

@@ -29,6 +29,7 @@ struct Error : std::runtime_error {
 
 struct Relation {
     uint64_t rows = 0;
+    bool owned = true;                 // false: another ctx's columns, shared (qe_workers)
     std::vector<uint64_t*> cols;
     std::vector<uint64_t> kor, kand;   // column statistics: OR / AND of all values (at load)
 };
@@ -124,6 +125,10 @@ struct qe_ctx {
     // two-level sorts awaiting their per-bucket step, by the pairs' key buffer
     std::unordered_map<const void*, qe::DeferredSort> deferred;
     std::unordered_map<const void*, qe::PreHist> prehist;
+
+    // worker contexts on the same device (qe_workers): their own stream and allocator, this ctx's
+    // relations shared -- the concurrent batch executor's lanes
+    std::vector<qe_ctx*> workers;
 
     // profiling
     bool prof = false;

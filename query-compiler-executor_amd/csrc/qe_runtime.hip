@@ -416,10 +416,13 @@ qe_ctx* qe_init(int device) {
 
 void qe_fini(qe_ctx* c) {
     if (!c) return;
+    for (qe_ctx* w : c->workers) qe_fini(w);   // (they borrow this ctx's relations)
+    c->workers.clear();
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     for (auto& r : c->rels)
-        for (auto* p : r.cols) (void)hipFree(p);
+        if (r.owned)
+            for (auto* p : r.cols) (void)hipFree(p);
     for (auto& kv : c->free_blocks) (void)hipFree(kv.second);
     for (auto& kv : c->live) (void)hipFree(kv.first);
     for (auto& p : c->pending) {
@@ -627,12 +630,47 @@ int qe_relation_rows(qe_ctx* c, int rel, uint64_t* rows) {
 
 int qe_drop_relations(qe_ctx* c) {
     QE_API_BEGIN(c)
+    for (qe_ctx* w : c->workers) {             // workers may still read them
+        sync(w);
+        w->rels.clear();
+    }
     sync(c);
     for (auto& r : c->rels)
-        for (auto* p : r.cols) QE_HIP(hipFree(p));
+        if (r.owned)
+            for (auto* p : r.cols) QE_HIP(hipFree(p));
     c->rels.clear();
     return 0;
     QE_API_END(c)
+}
+
+int qe_workers(qe_ctx* c, int n, qe_ctx** out) {
+    QE_API_BEGIN(c)
+    if (n < 1 || n > 16) throw Error(QE_EINVAL, "1..16 workers");
+    while ((int)c->workers.size() < n) {
+        qe_ctx* w = qe_init(c->device);
+        if (!w) throw Error(QE_EHIP, "worker context");
+        c->workers.push_back(w);
+    }
+    sync(c);                                   // the relations are complete before a worker reads them
+    for (int i = 0; i < n; i++) {
+        qe_ctx* w = c->workers[i];
+        w->rels.clear();
+        for (const auto& r : c->rels) {
+            Relation b = r;
+            b.owned = false;
+            w->rels.push_back(b);
+        }
+        w->mat_limit = c->mat_limit;
+        w->prof = c->prof;
+        out[i] = w;
+    }
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_bind_thread(qe_ctx* c) {
+    if (!c) return QE_EINVAL;
+    return hipSetDevice(c->device) == hipSuccess ? 0 : QE_EHIP;
 }
 
 void qe_free_host(void* p) { free(p); }
@@ -761,31 +799,56 @@ int qe_mem_trim(qe_ctx* c) {
     QE_API_END(c)
 }
 
+// profiling covers a ctx and its worker contexts (qe_run_queries_parallel's lanes): statistics
+// of kernels with one name are summed (the lanes' durations overlap in time)
 int qe_set_profiling(qe_ctx* c, int on) {
     QE_API_BEGIN(c)
     drain_events(c);
     c->prof = on != 0;
+    for (qe_ctx* w : c->workers) {
+        drain_events(w);
+        w->prof = c->prof;
+    }
     return 0;
     QE_API_END(c)
 }
 
 int qe_reset_stats(qe_ctx* c) {
     QE_API_BEGIN(c)
-    drain_events(c);
-    for (auto& k : c->kstats) {
-        k.launches = 0;
-        k.ms = 0;
-        k.bytes = 0;
-    }
+    auto reset = [](qe_ctx* x) {
+        drain_events(x);
+        for (auto& k : x->kstats) {
+            k.launches = 0;
+            k.ms = 0;
+            k.bytes = 0;
+        }
+    };
+    reset(c);
+    for (qe_ctx* w : c->workers) reset(w);
     return 0;
     QE_API_END(c)
 }
 
 int qe_kernel_stats(qe_ctx* c, qe_kstat* out, int max) {
     QE_API_BEGIN(c)
-    drain_events(c);
+    std::vector<KStat> all;
+    auto add = [&](qe_ctx* x) {
+        drain_events(x);
+        for (auto& k : x->kstats) {
+            auto it = std::find_if(all.begin(), all.end(), [&](const KStat& a) { return a.name == k.name; });
+            if (it == all.end()) {
+                all.push_back(k);
+            } else {
+                it->launches += k.launches;
+                it->ms += k.ms;
+                it->bytes += k.bytes;
+            }
+        }
+    };
+    add(c);
+    for (qe_ctx* w : c->workers) add(w);
     int n = 0;
-    for (auto& k : c->kstats) {
+    for (auto& k : all) {
         if (n < max && out) {
             memset(&out[n], 0, sizeof(qe_kstat));
             strncpy(out[n].name, k.name.c_str(), sizeof(out[n].name) - 1);

@@ -31,6 +31,13 @@
 
 namespace qe {
 
+// pass outputs: plain or non-temporal stores (tuning knob, A/B: QE_NT_STORE=1)
+#ifdef QE_NT_STORE
+#define QE_ST(ptr, v) __builtin_nontemporal_store((v), (ptr))
+#else
+#define QE_ST(ptr, v) (*(ptr) = (v))
+#endif
+
 constexpr int RB = 256;          // block
 constexpr int RNW = RB / 64;     // waves per block
 #ifndef QE_R_ITEMS
@@ -306,7 +313,7 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
 #endif
             if ((uint64_t)p >= n) continue;   // never taken with consistent offsets; keeps stores in bounds
             if (OUT == OUT_WORD) {
-                wout[p] = wd;
+                QE_ST(&wout[p], wd);
             } else if (PACK) {
                 kout[p] = (K)(f.kconst | ((wd >> 32) << f.lo));
                 vout[p] = (uint32_t)wd;
@@ -840,10 +847,13 @@ __global__ void __launch_bounds__(256) cs_apply_kernel(CSJobs js) {
 #ifndef QE_TL2_ITEMS
 #define QE_TL2_ITEMS 18
 #endif
-constexpr int TL2_NT = 512, TL2_ITEMS = QE_TL2_ITEMS, TL2_TILE = TL2_NT * TL2_ITEMS;   // 9216: mean 8192 + 11 sd
+#ifndef QE_TL2_NT
+#define QE_TL2_NT 512
+#endif
+constexpr int TL2_NT = QE_TL2_NT, TL2_ITEMS = QE_TL2_ITEMS, TL2_TILE = TL2_NT * TL2_ITEMS;   // 9216: mean 8192 + 11 sd
 
 template <typename K>
-__global__ void __launch_bounds__(TL2_NT, 4) tl_pass2_kernel(const uint64_t* __restrict__ win, uint64_t* __restrict__ wout,
+__global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const uint64_t* __restrict__ win, uint64_t* __restrict__ wout,
                                                          uint64_t n, int dsh, const uint32_t* __restrict__ off1,
                                                          const uint32_t* __restrict__ off2, uint32_t G) {
     constexpr int BINS = 128, NW = TL2_NT / 64, WT = 64 * TL2_ITEMS;
@@ -928,7 +938,7 @@ __global__ void __launch_bounds__(TL2_NT, 4) tl_pass2_kernel(const uint64_t* __r
             if (i < m) {
                 const uint64_t wd = stage[i];
                 const uint32_t p = gofs[(uint32_t)(wd >> dsh) & (BINS - 1)] + i;
-                if ((uint64_t)p < n) wout[p] = wd;   // never false with consistent offsets
+                if ((uint64_t)p < n) QE_ST(&wout[p], wd);   // never false with consistent offsets
             }
         }
         __syncthreads();   // stage / whist / gofs are rewritten by the next sub-tile

@@ -10,7 +10,9 @@
  * GPU through qe_* calls; rowid lists stay in HBM as qe_list and never visit the host.
  */
 #define _GNU_SOURCE
+#include <pthread.h>
 #include <setjmp.h>
+#include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -682,3 +684,92 @@ int qe_run_queries(qe_ctx* ctx, const char* text, char** out, size_t* outlen) {
     fclose(x.out);
     return rc;
 }
+
+/* ---- the concurrent batch (qe_run_queries_parallel) ----------------------------------------- */
+
+typedef struct {
+    qe_ctx* ctx;
+    query_t* qs;
+    size_t nq;
+    atomic_size_t* next;
+    char** outs;
+    size_t* lens;
+    int* rcs;
+    atomic_int* stop;          /* the first query index known to end the batch (+1), 0 none */
+} lane_t;
+
+static void* lane_main(void* arg) {
+    lane_t* L = (lane_t*)arg;
+    qe_bind_thread(L->ctx);
+    for (;;) {
+        const size_t i = atomic_fetch_add(L->next, 1);
+        if (i >= L->nq) break;
+        const int st = atomic_load(L->stop);
+        if (st && (size_t)(st - 1) < i) {       /* past a query where the reference exits */
+            L->rcs[i] = 0;
+            continue;
+        }
+        FILE* f = open_memstream(&L->outs[i], &L->lens[i]);
+        if (!f) {
+            L->rcs[i] = QE_ENOMEM;
+        } else {
+            qe_arrange_predicates(&L->qs[i]);
+            L->rcs[i] = qe_exec_query(L->ctx, &L->qs[i], f);
+            fclose(f);
+        }
+        if (L->rcs[i] != 0) {                   /* remember the earliest failing query */
+            int cur = atomic_load(L->stop);
+            while ((cur == 0 || (size_t)(cur - 1) > i) && !atomic_compare_exchange_weak(L->stop, &cur, (int)i + 1)) {
+            }
+        }
+    }
+    return NULL;
+}
+
+int qe_run_queries_parallel(qe_ctx* ctx, int workers, const char* text, char** out, size_t* outlen) {
+    *out = NULL;
+    *outlen = 0;
+    if (workers <= 1) return qe_run_queries(ctx, text, out, outlen);
+    qe_ctx* w[16];
+    int rc = qe_workers(ctx, workers, w);
+    if (rc != 0) return rc;
+    size_t nq = 0;
+    query_t* qs = qe_parse_text(text, &nq);     /* parsed before anything runs (main/queries_main.c:31-37) */
+    char** outs = (char**)calloc(nq ? nq : 1, sizeof(char*));
+    size_t* lens = (size_t*)calloc(nq ? nq : 1, sizeof(size_t));
+    int* rcs = (int*)calloc(nq ? nq : 1, sizeof(int));
+    atomic_size_t next = 0;
+    atomic_int stop = 0;
+    lane_t lanes[16];
+    pthread_t th[16];
+    int started = 0;
+    for (int k = 0; k < workers; k++) {
+        lane_t l = {w[k], qs, nq, &next, outs, lens, rcs, &stop};
+        lanes[k] = l;
+        if (pthread_create(&th[k], NULL, lane_main, &lanes[k]) == 0) started++;
+        else break;
+    }
+    if (started == 0) lane_main(&lanes[0]);      /* no threads: run the batch on one lane */
+    for (int k = 0; k < started; k++) pthread_join(th[k], NULL);
+    for (int k = 0; k < workers; k++) qe_sync(w[k]);
+    /* the reference's bytes: every query in input order, up to and including the first that ends
+     * the batch (its partial output, then its status) */
+    FILE* f = open_memstream(out, outlen);
+    rc = 0;
+    for (size_t i = 0; f && i < nq; i++) {
+        if (outs[i] && lens[i]) fwrite(outs[i], 1, lens[i], f);
+        if (rcs[i] != 0) {
+            rc = rcs[i];
+            break;
+        }
+    }
+    if (f) fclose(f);
+    else rc = QE_ENOMEM;
+    for (size_t i = 0; i < nq; i++) free(outs[i]);
+    free(outs);
+    free(lens);
+    free(rcs);
+    qe_free_queries(qs, nq);
+    return rc;
+}
+

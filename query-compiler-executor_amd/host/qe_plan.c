@@ -566,7 +566,30 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need) {
     ECHK(side_finish(P, &sa));
     ECHK(side_finish(P, &sb));
     qe_h oa = NONE, ob = NONE;
-    ECHK(e->join(e->u, sa.keys, sa.vals, sb.keys, sb.vals, &oa, &ob));
+    const int jr = e->join(e->u, sa.keys, sa.vals, sb.keys, sb.vals, &oa, &ob);
+    if (jr != 0 && jr != QE_ETOOBIG) {
+        P->rc = jr;
+        return jr;
+    }
+    {   /* every rank learns whether any rank's bucket was too large to materialise, so all of them
+         * leave the query together (the fallback then runs it) -- one all-reduce with the size */
+        uint64_t v[2] = {0, jr == QE_ETOOBIG};
+        if (jr == 0) ECHK(e->length(e->u, oa, &v[0]));
+        if (P->e->world > 1) ECHK(P->e->allreduce(P->e->u, v, 2));
+        if (v[1]) {
+            rel(P, oa);
+            rel(P, ob);
+            rel(P, sa.keys);
+            rel(P, sb.keys);
+            rel(P, sa.vals);
+            rel(P, sb.vals);
+            for (int k = 0; k < sa.ncar; k++) rel(P, sa.car_rows[k]);
+            for (int k = 0; k < sb.ncar; k++) rel(P, sb.car_rows[k]);
+            P->rc = QE_ETOOBIG;
+            return QE_ETOOBIG;
+        }
+        P->C[A].size = v[0];    /* the join's global pair count, taken below */
+    }
     /* the merged component: carried bindings, rowids = o (vals rode along) or take(rows, o) */
     member* m = (member*)calloc(P->q->nrels + 1, sizeof(member));
     int n = 0;
@@ -599,9 +622,7 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need) {
     rel(P, sb.vals);
     if (!used[0]) rel(P, oa);
     if (!used[1]) rel(P, ob);
-    uint64_t size = 0;
-    ECHK(e->length(e->u, m[0].rows, &size));
-    ECHK(allreduce1(P, &size));
+    const uint64_t size = P->C[A].size;
     /* A absorbs B */
     free_comp(P, A);
     free_comp(P, B);
@@ -793,9 +814,27 @@ int qe_plan_run_text(const qe_engine* e, const char* text, char** out, size_t* o
             rc = e->fallback ? e->fallback(e->u, &qs[i], f) : QE_ENOTSUP;
             continue;
         }
+        /* the query's bytes are buffered: a join too large to materialise (QE_ETOOBIG, the
+         * reference's DArray bound) sends the whole query to the fallback, whose executor takes
+         * the aggregate form where the reference's output allows it */
+        char* qbuf = NULL;
+        size_t qlen = 0;
+        FILE* qf = open_memstream(&qbuf, &qlen);
+        if (!qf) {
+            rc = QE_ENOMEM;
+            break;
+        }
         uint64_t r = 0;
-        rc = plan_query(e, &qs[i], f, &r);
-        if (rc == 0 && rows) *rows = r;
+        rc = plan_query(e, &qs[i], qf, &r);
+        fclose(qf);
+        if (rc == QE_ETOOBIG && e->fallback) {
+            refused++;
+            rc = e->fallback(e->u, &qs[i], f);
+        } else {
+            if (qlen) fwrite(qbuf, 1, qlen, f);
+            if (rc == 0 && rows) *rows = r;
+        }
+        free(qbuf);
     }
     snprintf(g_why, sizeof g_why, "%s", first);
     qe_free_queries(qs, nq);

@@ -130,6 +130,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "qe_comm_stats": (I, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "qe_run_queries_dist": (I, [P, P, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t),
                                     C.POINTER(C.c_uint64)]),
+        "qe_run_queries_parallel": (I, [P, I, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+        "qe_workers": (I, [P, I, C.POINTER(C.c_void_p)]),
+        "qe_bind_thread": (I, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -214,6 +217,17 @@ class Ctx:
         out = C.c_void_p()
         n = C.c_size_t()
         rc = self.lib.qe_run_queries(self.h, text.encode(), C.byref(out), C.byref(n))
+        s = C.string_at(out, n.value).decode("latin-1") if out.value else ""
+        if out.value:
+            self.lib.qe_free_host(out)
+        if rc not in (0, QE_EEXIT):
+            raise QEError(rc, self.lib.qe_last_error(self.h).decode())
+        return s, (1 if rc == QE_EEXIT else 0)
+
+    def run_parallel(self, text: str, workers: int = 4) -> tuple[str, int]:
+        """qe_run_queries_parallel: the batch's queries on `workers` concurrent lanes, same bytes"""
+        out, n = C.c_void_p(), C.c_size_t()
+        rc = self.lib.qe_run_queries_parallel(self.h, workers, text.encode(), C.byref(out), C.byref(n))
         s = C.string_at(out, n.value).decode("latin-1") if out.value else ""
         if out.value:
             self.lib.qe_free_host(out)

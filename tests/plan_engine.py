@@ -69,6 +69,7 @@ class NumpyPlanEngine:
         self.rels, self.rank, self.world, self.group = rels, rank, world, group
         self.h, self.next, self.borrowed = {}, 1, set()
         self.exchanges = 0
+        self.mat_limit = 1 << 62
         self.lib = C.CDLL(SO)
         self.lib.qe_plan_run_text.argtypes = [P(Engine), C.c_char_p, P(C.c_void_p), P(C.c_size_t), P(U64), P(U64)]
         self.lib.qe_plan_check_text.argtypes = [P(Engine), C.c_char_p, P(C.c_uint8), C.c_size_t]
@@ -195,6 +196,8 @@ class NumpyPlanEngine:
 
     def cb_join(self, u, ka, va, kb, vb, oa, ob):
         ia, ib = join_local(self.get(ka), self.get(kb))
+        if len(ia) > self.mat_limit:          # like qe_join_pairs: QE_ETOOBIG past the limit
+            return -5
         oa[0] = self.put(self.get(va)[ia] if va else ia)
         ob[0] = self.put(self.get(vb)[ib] if vb else ib)
 
@@ -235,14 +238,17 @@ def free_port():
     return p
 
 
-def worker(rank, world, port, rels, queries, outq):
-    """one gloo rank: every query through the C plan, rank 0 reports (stdout, rc, rows, refused)"""
+def worker(rank, world, port, rels, queries, outq, limits=None):
+    """one gloo rank: every query through the C plan, rank 0 reports (stdout, rc, rows, refused);
+    limits[rank] (optional): that rank's materialisation limit"""
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         eng = NumpyPlanEngine(rels, rank, world)
+        if limits:
+            eng.mat_limit = limits[rank]
         res = [eng.run(q) for q in queries]
         if rank == 0:
             outq.put((res, eng.exchanges, eng.live_handles()))

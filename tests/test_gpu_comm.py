@@ -84,6 +84,29 @@ def test_dist_executor_matches_every_golden(ctx, comm, fixture):
         assert planned >= len(doc["cases"]) // 2     # most of them really ran partitioned
 
 
+def test_dist_executor_aggregate_fallback_on_every_golden(ctx, comm):
+    """materialisation limit 0: a planned join too large to materialise (QE_ETOOBIG) sends its query
+    to the faithful executor, which takes the aggregate form where the reference's output allows
+    it and fails loudly where it does not -- never a different answer (C5's shape at 1e9 rows)"""
+    ctx.set_materialize_limit(0)
+    ran = 0
+    try:
+        for name, idx, ds, case in goldens.all_cases(include_headline=False):
+            _load(ctx, ds)
+            try:
+                out, rc, _ = ctx.run_dist(case["input"], comm)
+            except lib.QEError as e:
+                assert e.code == lib.QE_ETOOBIG, (name, idx, str(e))
+                continue
+            assert (out, rc) == (case["stdout"], case["rc"]), (name, idx, case["input"])
+            ran += 1
+    finally:
+        ctx.set_materialize_limit(0x7FFFFFFF)
+        ctx.drop_relations()
+        _loaded["key"] = None
+    assert ran > 100
+
+
 @pytest.mark.slow
 def test_dist_executor_c3_100m_one_rank(ctx, comm):
     """the partitioned plan at the headline size through a one-rank RCCL communicator equals the

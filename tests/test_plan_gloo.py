@@ -17,11 +17,11 @@ QE_ENOTSUP = -6
 C3 = "0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>1000000000&3.2<3000000000|1.2 2.2 3.2\n"
 
 
-def _run_world(rels, queries, world):
+def _run_world(rels, queries, world, limits=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = pe.free_port()
-    procs = [ctx.Process(target=pe.worker, args=(r, world, port, rels, queries, q)) for r in range(world)]
+    procs = [ctx.Process(target=pe.worker, args=(r, world, port, rels, queries, q, limits)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=600)
@@ -91,3 +91,12 @@ def test_two_ranks_match_goldens():
     assert nex > 0 and len(cases) >= 40
     for c, (out, rc, _, _) in zip(cases, res):
         assert (out, rc) == (c["stdout"], 0), c["input"]
+
+
+def test_one_rank_too_large_stops_every_rank():
+    """a join whose bucket is past the materialisation limit on ONE rank only: every rank leaves
+    the query with QE_ETOOBIG together (one all-reduce), none waits forever in the next exchange"""
+    rows = 20_000
+    rels = dg.make_relations(dg.chain_spec(4, rows), 1)
+    res, _, _ = _run_world(rels, [C3, "0 1|0.1=1.0|0.2 1.2\n"], 2, limits=[1 << 62, 100])
+    assert res[0][1] == -5 and res[1][1] == -5

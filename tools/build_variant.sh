@@ -6,5 +6,5 @@ out=build/diag/$1; rm -rf $out; mkdir -p $out
 pids=()
 for f in csrc/*.hip; do /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result -I../include -munsafe-fp-atomics $2 -c $f -o $out/$(basename $f .hip).o & pids+=($!); done
 for p in "${pids[@]}"; do wait $p; done   # any failed compile fails the script
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,--no-undefined -o build/diag/libqe_$1.so $out/*.o build/qe_exec.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,--no-undefined -o build/diag/libqe_$1.so $out/*.o build/qe_exec.o build/qe_query.o build/qe_plan.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo built build/diag/libqe_$1.so
