@@ -22,6 +22,7 @@ from .cpuref import CpuRef, cpu_model, pin_one_core
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden", "c4.json")
+GOLDEN_FULL = os.path.join(ROOT, "tests", "golden", "full", "c4_full.json")   # cpu_ref at full size
 METRIC = "queries/sec, SIGMOD-2018-style batch (C4: 14 relations, gated query set)"
 
 
@@ -108,6 +109,8 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u64",
         "data": "synthetic: qe.datagen.c4_spec(1.0) relations generated in HBM (seed 4)",
+        "parity": out == "".join(c["stdout"] for c in json.load(open(GOLDEN_FULL))["cases"])
+                  if os.path.exists(GOLDEN_FULL) else None,
         "config": {"workload": "C4: 14 relations, %d gated SIGMOD-style queries in batches of %d"
                                % (len(queries), dg.C4_BATCH),
                    "rows_total": sum(s.rows for s in specs), "output_lines": out.count("\n"),
@@ -127,7 +130,10 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
 
 
 def run_dist(args, log) -> dict | None:
-    """replicas-style: rank r runs queries r, r+N, ...; outputs gathered to rank 0 in order"""
+    """replicas-style: rank r runs the r-th contiguous share of the batch on its own GPU (relations
+    replicated), its queries on concurrent lanes (qe_run_queries_parallel); rank 0 joins the shares
+    in rank order -- input order -- cut after the first share where the reference exits.
+    torch.distributed (gloo) is the control plane only: barriers, the max time, the gather."""
     import torch
     import torch.distributed as dist
 
@@ -135,49 +141,53 @@ def run_dist(args, log) -> dict | None:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    backend = os.environ.get("QE_DIST_BACKEND", "nccl")
     dev = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev)
     if not dist.is_initialized():
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group("gloo")
+    workers = int(os.environ.get("QE_WORKERS", "8"))
     ctx = lib.Ctx(dev)
     queries = load_queries()
-    mine = [q for i, q in enumerate(queries) if i % world == rank]
+    lo, hi = len(queries) * rank // world, len(queries) * (rank + 1) // world
+    mine = "".join(queries[lo:hi])               # no F lines needed: one batch per rank
     gen_c4(ctx)
-    outs = None
+    res_mine = ("", 0)
     for _ in range(args.warmup):
-        outs = [ctx.run(q)[0] for q in mine]
+        res_mine = ctx.run_parallel(mine, workers)
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        outs = [ctx.run(q)[0] for q in mine]
+        res_mine = ctx.run_parallel(mine, workers)
     ctx.sync()
     torch.cuda.synchronize()
     dist.barrier()
     dt = time.perf_counter() - t0
-    tmax = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}" if backend == "nccl" else "cpu")
+    tmax = torch.tensor([dt], dtype=torch.float64)
     dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     dt = float(tmax.item())
     gathered = [None] * world
-    dist.all_gather_object(gathered, outs)
+    dist.all_gather_object(gathered, res_mine)
     ctx.close()
     if rank != 0:
         return None
-    ordered = []
-    for i in range(len(queries)):
-        ordered.append(gathered[i % world][i // world])
-    text = "".join(ordered)
+    text, rc = "", 0
+    for out, r in gathered:
+        text += out
+        if r:
+            rc = r
+            break
+    want = "".join(c["stdout"] for c in json.load(open(GOLDEN_FULL))["cases"]) if os.path.exists(GOLDEN_FULL) else None
     return {
         "metric": METRIC, "value": round(len(queries) * args.steps / dt, 2), "unit": "queries/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u64",
         "data": "synthetic: qe.datagen.c4_spec(1.0) relations generated in HBM (seed 4), replicated on every rank",
+        "parity": (text == want and rc == 0) if want is not None else None,
         "config": {"workload": "C4: 14 relations, %d gated SIGMOD-style queries" % len(queries),
-                   "output_lines": text.count("\n"), "executor": "libqe faithful state machine, one query per rank",
+                   "output_lines": text.count("\n"),
+                   "executor": "qe_run_queries_parallel per rank (%d lanes), a contiguous share of the batch "
+                               "per rank" % workers,
                    "parallelism": f"query-parallel replicas x{world}"},
         "roofline": None, "cpu_baseline": None,
     }

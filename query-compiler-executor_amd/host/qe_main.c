@@ -13,6 +13,7 @@
  *                 the relational domain key-partitioned across the ranks, the others on rank 0's
  *                 faithful executor (include/qe_plan.h).  Rank 0 prints; the exit status is its.
  *   QE_PLAN=1     (one GPU) the partitioned executor on one rank instead of qe_run_queries
+ *   QE_WORKERS=k  (one GPU) the batch's queries on k concurrent lanes (qe_run_queries_parallel)
  */
 #define _GNU_SOURCE
 #include <fcntl.h>
@@ -194,7 +195,8 @@ int main(void) {
         uint64_t refused = 0;
         rc = qe_run_queries_dist(c, NULL, in.text, &out, &outlen, &refused);
     } else {
-        rc = qe_run_queries(c, in.text, &out, &outlen);
+        const char* wk = getenv("QE_WORKERS");
+        rc = qe_run_queries_parallel(c, wk ? atoi(wk) : 1, in.text, &out, &outlen);
     }
     int status = finish(rc, out, outlen, 1);
     qe_fini(c);

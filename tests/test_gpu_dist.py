@@ -138,3 +138,19 @@ def test_gpu_agg_plan_equals_faithful_executor_on_c5(ctx, world):
             assert p.exitcode == 0
         assert all(nheavy > 0 for _, _, nheavy in res)
     assert [r[0] for r in res] == want
+
+
+def test_c4_replicas_two_ranks_share_one_gpu():
+    """bench.py --workload c4 at N = 2 (contiguous shares, concurrent lanes per rank, gloo control
+    plane) on the one GPU: the joined output is the full-size fixture's, byte for byte"""
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = dce.free_port()
+    procs = [mpc.Process(target=gpu_dist_worker.c4_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert res["parity"] is True and res["n_gpus"] == 2
