@@ -173,6 +173,20 @@ def run_dist(args):
     ctx.set_profiling(False)
     rows = ctx.last_result_rows()
     exchanges, sent = comm.stats() if comm else (0, 0)
+    # the same steps without the per-kernel HIP events (the value stays the profiled region's)
+    if multi:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.run_dist(QUERY, comm)
+    ctx.sync()
+    torch.cuda.synchronize()
+    dt_np = time.perf_counter() - t0
+    if multi:
+        t = torch.tensor([dt_np], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt_np = float(t.item())
     res = None
     faithful_line = None
     faithful = None
@@ -211,6 +225,8 @@ def run_dist(args):
             "faithful_executor": faithful_line,
             "roofline": roofline(stats, load_traffic("c3_plan")),
             "kernel_ms_per_step": round(sum(s["ms"] for _, s in kern) / args.steps, 3),
+            "host_round_trips_per_step": stats.get("host_round_trip", {}).get("launches", 0) / args.steps,
+            "unprofiled_ms_per_step": round(dt_np / args.steps * 1e3, 3),
             "stages": {k: {"ms_per_step": round(s["ms"] / args.steps, 3)} for k, s in kern[:12]},
         }
         if not args.no_cpu:

@@ -64,6 +64,7 @@ enum : uint32_t { MJF_R_FANOUT = 1u, MJF_S_DUP = 2u, MJF_ERR = 4u, MJF_OVF = 8u 
 struct DeferredSort {
     uint64_t* words = nullptr;    // bucket-partitioned (field << 32 | rowid) words
     uint32_t* bstart = nullptr;   // bucket starts (+ end)
+    uint64_t* d_max = nullptr;    // largest bucket (device word: > TL_CAP = skew, not yet checked)
     uint64_t* kout = nullptr;
     uint32_t* vout = nullptr;
     int lo = 0, L = 0;            // field = (key >> lo) & fmask; bucket = field >> L

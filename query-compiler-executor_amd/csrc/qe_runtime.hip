@@ -152,13 +152,35 @@ Timed::~Timed() {
     }
 }
 
-void sync(qe_ctx* c) { QE_HIP(hipStreamSynchronize(c->stream)); }
+// profiling: a host round trip (the host waits for the GPU) counts as one "launch" of the
+// zero-time stage host_round_trip, so bench.py reports round trips per query beside the kernels
+static void count_round_trip(qe_ctx* c) {
+    if (!c->prof) return;
+    auto it = c->kindex.find("host_round_trip");
+    int k;
+    if (it == c->kindex.end()) {
+        k = (int)c->kstats.size();
+        c->kindex["host_round_trip"] = k;
+        KStat s;
+        s.name = "host_round_trip";
+        c->kstats.push_back(s);
+    } else {
+        k = it->second;
+    }
+    c->kstats[k].launches++;
+}
+
+void sync(qe_ctx* c) {
+    count_round_trip(c);
+    QE_HIP(hipStreamSynchronize(c->stream));
+}
 
 // Wait for a scalar result the host needs to go on (a list length, a pair count, a sum): the
 // host polls an event instead of sleeping in hipStreamSynchronize, so the next launches follow
 // the result by a few microseconds (the trace showed ~22 us between such a read and the next
 // kernel, ~16 of them per C3 query).  QE_SPIN_WAIT=0 restores the blocking wait.
 static void wait_result(qe_ctx* c) {
+    count_round_trip(c);
     static const bool spin = [] {
         const char* s = getenv("QE_SPIN_WAIT");
         return !(s && s[0] == '0');

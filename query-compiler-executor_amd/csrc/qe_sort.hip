@@ -977,6 +977,10 @@ __global__ void __launch_bounds__(HJ_NT) tl_hjoin_kernel(const uint64_t* __restr
     __shared__ uint32_t s_total;
     const uint32_t b = blockIdx.x;
     const uint32_t r0 = bsR[b], mR = bsR[b + 1] - r0, s0 = bsS[b], mS = bsS[b + 1] - s0;
+    if (mR > (uint32_t)TL_CAP || mS > (uint32_t)TL_CAP) {   // beyond LDS (the sorts were not checked): flag it
+        if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(total_out + 1), 1ull);
+        return;
+    }
     const uint32_t D = 1u << L, dmask = D - 1u;
     const int w = wave_id(), l = lane_id();
     const uint64_t* __restrict__ bR = wR + r0;
@@ -1362,7 +1366,10 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     uint32_t* gcnt = dalloc_t<uint32_t>(c, (size_t)nseg * 128);
     uint32_t* hist = dalloc_t<uint32_t>(c, TL_BUCKETS);
     uint32_t* bstart = dalloc_t<uint32_t>(c, TL_BUCKETS + 1);
-    uint64_t* d_max = c->d_scratch + 34;
+    // a deferred sort keeps its largest bucket on the device: the consumer checks it there
+    // (bucket_join) or reads it when it completes the sort (pairs_need_keys) -- no round trip here
+    const bool dfr = defer && sizeof(K) == 8;
+    uint64_t* d_max = dfr ? dalloc_t<uint64_t>(c, 1) : c->d_scratch + 34;
     auto release = [&] {
         dfree(c, tcnt);
         dfree(c, gcnt);
@@ -1421,7 +1428,7 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     }
     // the two passes are valid whatever the bucket sizes, so they are queued before the host
     // reads the largest bucket: the GPU stays busy through that round trip
-    if (read_u64(c, d_max) > (uint64_t)TL_CAP) {   // a bucket beyond LDS (skew): plain LSD passes
+    if (!dfr && read_u64(c, d_max) > (uint64_t)TL_CAP) {   // a bucket beyond LDS (skew): plain LSD passes
         dfree(c, w1);
         dfree(c, w2);
         dfree(c, kout);
@@ -1430,10 +1437,11 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
         return false;
     }
     if constexpr (sizeof(K) == 8) {
-        if (defer) {   // the per-bucket step waits for the consumer (bucket_join / pairs_need_keys)
+        if (dfr) {   // the per-bucket step waits for the consumer (bucket_join / pairs_need_keys)
             DeferredSort d;
             d.words = w2;
             d.bstart = bstart;
+            d.d_max = d_max;
             d.kout = (uint64_t*)kout;
             d.vout = vout;
             d.lo = f.lo;
@@ -1481,7 +1489,8 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
     uint32_t* bstart = dalloc_t<uint32_t>(c, TL_BUCKETS + 1 + 512);
     uint32_t* base1 = bstart + TL_BUCKETS + 1;
     uint32_t* base2 = base1 + 256;
-    uint64_t* d_max = c->d_scratch + 34;
+    const bool dfr = defer && H == TL_H && sizeof(K) == 8;   // largest bucket checked by the consumer
+    uint64_t* d_max = dfr ? dalloc_t<uint64_t>(c, 1) : c->d_scratch + 34;
     if (H == 8) {
         base1 = bstart;   // one pass: its digit IS the bucket
         QE_HIP(hipMemsetAsync(hist, 0, 256 * sizeof(uint32_t), c->stream));
@@ -1500,8 +1509,7 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
         hipLaunchKernelGGL(tl_scan_kernel, dim3(1), dim3(1024), 0, c->stream, hist, bstart, base1, base2, d_max);
         QE_HIP(hipGetLastError());
     }
-    uint64_t mx = read_u64(c, d_max);
-    if (mx > (uint64_t)TL_CAP) {
+    if (!dfr && read_u64(c, d_max) > (uint64_t)TL_CAP) {
         dfree(c, hist);
         dfree(c, bstart);
         return false;
@@ -1531,10 +1539,11 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
         QE_HIP(hipGetLastError());
     }
     if constexpr (sizeof(K) == 8) {
-        if (defer && H == TL_H) {   // the per-bucket step waits for the consumer (bucket_join / pairs_need_keys)
+        if (dfr) {   // the per-bucket step waits for the consumer (bucket_join / pairs_need_keys)
             DeferredSort d;
             d.words = w2;
             d.bstart = bstart;
+            d.d_max = d_max;
             d.kout = (uint64_t*)kout;
             d.vout = vout;
             d.lo = f.lo;
@@ -1714,6 +1723,46 @@ static LocalRounds rounds_of(const DeferredSort& d) {
 static void drop(qe_ctx* c, const DeferredSort& d) {
     dfree(c, d.words);
     dfree(c, d.bstart);
+    dfree(c, d.d_max);
+}
+
+// A deferred sort with a bucket beyond LDS (skew) completes by plain LSD passes over the packed
+// words' whole field, the last one unpacking into the pairs' key / rowid buffers.  The words are
+// bucket-partitioned and stable, so ties keep their input order, as in every other sort path.
+static void complete_lsd(qe_ctx* c, const DeferredSort& d, uint64_t n) {
+    const int nb = d.L + TL_H;
+    PassDesc pd{};
+    pd.npass = (nb + 7) / 8;
+    const int width = (nb + pd.npass - 1) / pd.npass;
+    for (int p = 0; p < pd.npass; p++) {
+        pd.shift[p] = 32 + p * width;
+        pd.mask[p] = (1u << std::min(width, nb - p * width)) - 1u;
+    }
+    constexpr int BINS = 256;
+    uint32_t* hist = dalloc_t<uint32_t>(c, (size_t)MAX_PASS * BINS);
+    hist_and_scan<uint64_t, 8>(c, d.words, n, pd, hist);
+    const uint64_t nt = (n + RTILE - 1) / RTILE;
+    uint64_t* buf[2] = {dalloc_t<uint64_t>(c, n), pd.npass > 2 ? dalloc_t<uint64_t>(c, n) : nullptr};
+    const Field f{d.lo, d.fmask, d.kconst};
+    const uint64_t* in = d.words;
+    for (int p = 0; p < pd.npass; p++) {
+        const bool last = p == pd.npass - 1;
+        LBSlot s = lb_acquire(c, nt * BINS);
+        Timed t(c, "sort_pass_skew", last ? 8.0 * n + 12.0 * n : 16.0 * n);
+        if (last)
+            hipLaunchKernelGGL((radix_pass_kernel<uint64_t, IN_WORD, OUT_KV, true, 8, R_ITEMS, R_NT>), dim3((unsigned)nt),
+                               dim3(R_NT), 0, c->stream, nullptr, in, nullptr, d.kout, nullptr, d.vout, n, pd.shift[p],
+                               pd.mask[p], f, hist + p * BINS, s.status, s.ticket, s.epoch);
+        else
+            hipLaunchKernelGGL((radix_pass_kernel<uint64_t, IN_WORD, OUT_WORD, true, 8, R_ITEMS, R_NT>),
+                               dim3((unsigned)nt), dim3(R_NT), 0, c->stream, nullptr, in, nullptr, nullptr, buf[p & 1],
+                               nullptr, n, pd.shift[p], pd.mask[p], f, hist + p * BINS, s.status, s.ticket, s.epoch);
+        QE_HIP(hipGetLastError());
+        if (!last) in = buf[p & 1];
+    }
+    dfree(c, hist);
+    dfree(c, buf[0]);
+    if (buf[1]) dfree(c, buf[1]);
 }
 
 void pairs_need_keys(qe_ctx* c, const qe_pairs* p) {
@@ -1723,7 +1772,9 @@ void pairs_need_keys(qe_ctx* c, const qe_pairs* p) {
     const DeferredSort d = it->second;
     c->deferred.erase(it);
     const Field f{d.lo, d.fmask, d.kconst};
-    {
+    if (read_u64(c, d.d_max) > (uint64_t)TL_CAP) {
+        complete_lsd(c, d, p->n);
+    } else {
         Timed t(c, "sort_local", 8.0 * p->n + 12.0 * p->n);
         hipLaunchKernelGGL((tl_local_kernel<uint64_t, IN_WORD>), dim3(TL_BUCKETS), dim3(TL_NT), 0, c->stream, d.words,
                            nullptr, nullptr, d.kout, d.vout, d.bstart, 0u, f, rounds_of(d));
@@ -1798,7 +1849,7 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
     for (int attempt = 0; attempt < 2; attempt++) {
         uint32_t* oR = dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1));
         uint32_t* oS = dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1));
-        QE_HIP(hipMemsetAsync(c->d_scratch + 17, 0, sizeof(uint64_t), c->stream));
+        QE_HIP(hipMemsetAsync(c->d_scratch + 17, 0, 2 * sizeof(uint64_t), c->stream));   // [pairs, oversize]
         {
             // algorithmic bytes: both sides' words in (+ 8 B per pair below)
             Timed t(c, "bucket_join", 8.0 * (double)(nR + nS));
@@ -1810,7 +1861,14 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
                                    dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17);
             QE_HIP(hipGetLastError());
         }
-        const uint64_t P = read_u64(c, c->d_scratch + 17);
+        uint64_t h[2];
+        read_words(c, c->d_scratch + 17, h, 2);   // the ONE round trip of the join
+        const uint64_t P = h[0];
+        if (h[1]) {   // a bucket beyond LDS (skew): the sides complete their sorts, the merge joins them
+            dfree(c, oR);
+            dfree(c, oS);
+            return false;
+        }
         if (P <= cap) {
             if (c->prof && !c->pending.empty()) c->pending.back().bytes += 8.0 * (double)P;
             if (P > c->mat_limit) {   // the reference's DArray cannot hold it either (src/DArray.h:14-15)

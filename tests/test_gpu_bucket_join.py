@@ -28,7 +28,7 @@ def _ref(rk, rv, sk, sv):
     return np.sort((r << np.uint64(32)) | s)
 
 
-def _check(ctx, rk, sk, gathered=True, expect=None):
+def _check(ctx, rk, sk, gathered=True, expect=None, stage=None):
     n_r, n_s = len(rk), len(sk)
     ctx.drop_relations()
     relR = ctx.load_relation([rk])
@@ -40,7 +40,8 @@ def _check(ctx, rk, sk, gathered=True, expect=None):
     ctx.set_profiling(True)
     ctx.reset_stats()
     a, b = ctx.join_pairs(R, S)
-    launched = ctx.kernel_stats().get("bucket_join", {}).get("launches", 0)
+    stats = ctx.kernel_stats()
+    launched = stats.get("bucket_join", {}).get("launches", 0)
     ctx.set_profiling(False)
     got = np.sort((ctx.list_to_host(a).astype(np.uint64) << np.uint64(32)) | ctx.list_to_host(b).astype(np.uint64))
     rv = rows if gathered else np.arange(n_r, dtype=np.uint32)
@@ -54,6 +55,8 @@ def _check(ctx, rk, sk, gathered=True, expect=None):
     ctx.drop_relations()
     if expect is not None:
         assert (launched > 0) == expect, launched
+    if stage is not None:
+        assert stats.get(stage, {}).get("launches", 0) > 0, sorted(stats)
     return len(want)
 
 
@@ -87,7 +90,7 @@ def test_bucket_join_fallbacks(ctx, shape):
     elif shape == "wide_domain":          # 30 varying bits: 15 left inside a bucket, beyond LDS
         rk = rng.integers(0, 1 << 30, n, dtype=np.uint64)
         sk = np.concatenate([rk[: n // 2], rng.integers(0, 1 << 30, n // 2, dtype=np.uint64)])
-    elif shape == "skewed":               # one key holds a third of the rows: no two-level sort
+    elif shape == "skewed":               # one key holds a third of the rows: its bucket is beyond LDS
         rk = rng.integers(0, 1 << 24, n, dtype=np.uint64)
         rk[: n // 3] = 12345
         sk = rng.integers(0, 1 << 24, n, dtype=np.uint64)
@@ -95,7 +98,10 @@ def test_bucket_join_fallbacks(ctx, shape):
     else:
         rk = rng.integers(0, 5000, 4000, dtype=np.uint64)
         sk = rng.integers(0, 5000, 3000, dtype=np.uint64)
-    _check(ctx, rk, sk, gathered=True, expect=False)
+    if shape == "skewed":   # the join launches, flags the bucket, and the sides complete by LSD passes
+        _check(ctx, rk, sk, gathered=True, expect=True, stage="sort_pass_skew")
+    else:
+        _check(ctx, rk, sk, gathered=True, expect=False)
 
 
 def test_bucket_join_materialisation_limit(ctx):

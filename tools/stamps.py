@@ -63,6 +63,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=100_000_000)
     ap.add_argument("--what", default="sort,mj")
+    ap.add_argument("--cp-tile", type=int, default=8192, help="compact tile rows (CB x FS_ITEMS x 2)")
     a = ap.parse_args()
     ctx = lib.Ctx(0)
     n = a.n
@@ -72,7 +73,7 @@ def main():
     if "cp" in a.what:
         l1 = ctx.filter_scan(ctx.column(r0, 2), ">", 1_000_000_000)
         ctx.sync()
-        report(ctx, "cp", (n + 8191) // 8192)
+        report(ctx, "cp", (n + a.cp_tile - 1) // a.cp_tile)
         ctx.list_free(l1)
     if "sort" not in a.what and "mj" not in a.what:
         ctx.close()
