@@ -96,8 +96,9 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
         "config": {"workload": "C5: 2-relation join, %d rows/side, Zipf theta=%.1f keys, query %s"
                                % (rows, dg.C5_THETA, dg.C5_QUERY.strip()),
                    "pairs": pairs, "materialised": False,
-                   "path": "libqe faithful executor: sort both sides, qe_merge_join_counts (aggregate form: "
-                           "P > INT32_MAX), qe_checksum_weighted",
+                   "path": "libqe faithful executor; its last join of two base columns whose lists only the "
+                           "checksums read runs as qe_join_aggregate (csrc/qe_agg.hip): each side sorted once "
+                           "as (key, select value) words, one merge-path pass counting both sides' partners",
                    "pairs_counted_per_s": round(pairs * args.steps / dt, 1),
                    "stdout": out, "parallelism": "single GPU"},
         "roofline": roofline_fn(stats, traffic_fn() if traffic_fn else None) if roofline_fn else None,

@@ -201,6 +201,15 @@ int qe_checksums(qe_ctx*, int n, const qe_col* cols, const qe_list* const* rows,
  * qe_checksum over the list qe_merge_join would have produced for that side
  * (sum_pairs col(pR) = sum_k (sum_{r in R_k} col(r)) * |S_k|). */
 int qe_checksum_weighted(qe_ctx*, qe_col col, const qe_pairs* p, uint64_t* sum);
+/* a8 + print_sums, aggregate form for two BASE columns (C5: the query's last join, each side's
+ * selects on at most one column): with c_i = #S rows whose key equals R.key[i] (and symmetric),
+ * out[0] = sum_i c_i = the join's pair count P, out[1] = sum_i valR[i] * c_i and out[2] =
+ * sum_j valS[j] * c_j (mod 2^64) -- the checksums qe_checksum computes over the two P-row lists
+ * the reference would build (src/join.c:325-392, src/utilities.c:197-224).  Each side is sorted
+ * once with its value column in the word, then one merge-path pass counts both sides: no rowid,
+ * no gather, no pair.  valR.d / valS.d may be NULL (that sum is 0).  QE_ENOTSUP when a value
+ * column holds values >= 2^32, the keys vary in more than 32 bits or a side has >= 2^32 rows. */
+int qe_join_aggregate(qe_ctx*, qe_col keyR, qe_col valR, qe_col keyS, qe_col valS, uint64_t* out);
 
 /* ---- multi-GPU plan; the exchange itself is an RCCL all-to-all -------------- */
 /* Hash-partition n rows on their key: dest = (hi32((key ^ key >> 29) * 0xbf58476d1ce4e5b9) * nparts) >> 32.  Rows go

@@ -1,0 +1,381 @@
+// qe_agg.hip -- the aggregate join of two base columns (C5).
+//
+// The query's last join, whose two lists only print_sums reads (src/utilities.c:197-224), is
+// never materialised: for R row i with c_i partners in S, the R list holds rowid i exactly c_i
+// times, so its checksum over column V is sum_i V[i] * c_i (mod 2^64), and the list length is
+// P = sum_i c_i.  The reference builds the lists (src/join.c:325-392, its DArray caps them at
+// INT32_MAX: src/DArray.h:14-15); the faithful executor's merge path computes the same numbers
+// from sorted (key, rowid) pairs and then gathers V by rowid (random 8-B reads).  Here each
+// side is sorted once as (key field << 32 | V[i]) words -- the select column rides where the
+// rowid would -- and ONE merge-path pass over both sorted sides yields c_i for every row of both
+// sides and the three sums, all streaming:
+//
+//   * the merged order of R and S (R first on equal keys) is cut into tiles of AG_T elements
+//     (merge path: a binary search per boundary); a key whose merged run crosses a tile boundary
+//     gets its global counts there (galloping searches around the boundary, both sides);
+//   * a tile loads its R and S ranges (coalesced words) and keeps the key fields in LDS; every
+//     other key's run lies wholly inside the tile, and two merge walks of the tile (R first, then
+//     S first on equal keys; one stretch of AG_ITEMS merged elements per thread) give each row
+//     the lower and upper bound of its key in the other range: the partner count;
+//   * per-tile partial sums, then one small reduction: one host read of (P, sumR, sumS).
+//
+// HBM traffic: the sorted words once (8 B per row of both sides) + the split table.
+#include "qe_device.h"
+#include "qe_internal.h"
+
+namespace qe {
+
+#ifndef QE_AG_NT
+#define QE_AG_NT 256
+#endif
+#ifndef QE_AG_ITEMS
+#define QE_AG_ITEMS 16
+#endif
+constexpr int AG_NT = QE_AG_NT;
+constexpr int AG_ITEMS = QE_AG_ITEMS;
+constexpr int AG_T = AG_NT * AG_ITEMS;   // merged elements per tile
+
+__device__ __forceinline__ uint32_t kf(uint64_t w) { return (uint32_t)(w >> 32); }
+
+// the run of key k in sorted a[0..n) that contains (or starts at) position p, where every key
+// before p is <= k and every key from p on is >= k: [first, end), by galloping outwards from p
+__device__ __forceinline__ void g_run(const uint64_t* __restrict__ a, uint64_t n, uint64_t p, uint32_t k, uint64_t* first,
+                                      uint64_t* end) {
+    // backwards: smallest i <= p with a[i..p) all == k
+    uint64_t lo = p, step = 1;
+    while (lo > 0 && kf(a[lo - 1]) == k) {
+        const uint64_t nl = lo >= step ? lo - step : 0;
+        if (kf(a[nl]) == k) {
+            lo = nl;
+            step <<= 1;
+        } else {   // a[nl] < k <= a[lo-1] = k: the run starts in (nl, lo)
+            uint64_t l2 = nl + 1, h2 = lo;
+            while (l2 < h2) {
+                const uint64_t mid = l2 + (h2 - l2) / 2;
+                if (kf(a[mid]) < k) l2 = mid + 1;
+                else h2 = mid;
+            }
+            lo = l2;
+            break;
+        }
+    }
+    // forwards: first i >= p with a[i] > k
+    uint64_t hi = p;
+    step = 1;
+    while (hi < n && kf(a[hi]) == k) {
+        const uint64_t nh = hi + step < n ? hi + step : n;
+        if (nh < n && kf(a[nh]) == k) {
+            hi = nh + 1;
+            step <<= 1;
+        } else {   // a[hi] == k, a[nh] > k (or nh == n): the run ends in (hi, nh]
+            uint64_t l2 = hi + 1, h2 = nh;
+            while (l2 < h2) {
+                const uint64_t mid = l2 + (h2 - l2) / 2;
+                if (kf(a[mid]) <= k) l2 = mid + 1;
+                else h2 = mid;
+            }
+            hi = l2;
+            break;
+        }
+    }
+    *first = lo;
+    *end = hi;
+}
+
+// boundary t (0..nt): ra[t] = number of R rows among the first d = min(t * AG_T, nR + nS) merged
+// elements (R first on equal keys); for 0 < t < nt also the key of merged element d and its
+// global run lengths in R and S
+__global__ void __launch_bounds__(256) ag_split_kernel(const uint64_t* __restrict__ R, uint64_t nR,
+                                                       const uint64_t* __restrict__ S, uint64_t nS, uint32_t nt,
+                                                       uint64_t* __restrict__ ra, uint32_t* __restrict__ bkey,
+                                                       uint32_t* __restrict__ bcR, uint32_t* __restrict__ bcS) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t > nt) return;
+    const uint64_t m = nR + nS;
+    const uint64_t d = (uint64_t)t * AG_T < m ? (uint64_t)t * AG_T : m;
+    // largest a with R[a-1] <= S[d-a]: binary search over a in [max(0, d - nS), min(d, nR)]
+    uint64_t lo = d > nS ? d - nS : 0, hi = d < nR ? d : nR;
+    while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;   // take R[mid] before S[d - mid - 1]?
+        if (kf(R[mid]) <= kf(S[d - mid - 1])) lo = mid + 1;
+        else hi = mid;
+    }
+    const uint64_t a = lo, b = d - a;
+    ra[t] = a;
+    if (t == 0 || t == nt) return;
+    uint32_t k;
+    if (a < nR && (b >= nS || kf(R[a]) <= kf(S[b]))) k = kf(R[a]);
+    else k = kf(S[b]);
+    uint64_t f0, e0, f1, e1;
+    g_run(R, nR, a, k, &f0, &e0);
+    g_run(S, nS, b, k, &f1, &e1);
+    bkey[t] = k;
+    bcR[t] = (uint32_t)(e0 - f0);
+    bcS[t] = (uint32_t)(e1 - f1);
+}
+
+// LDS index with one pad word per 32: the walks' threads start ~8-16 words apart, which without
+// padding lands a wave's accesses on a few banks
+__device__ __forceinline__ uint32_t pd(uint32_t i) { return i + (i >> 5); }
+
+// One thread's stretch [d, e) of the tile's merged order, walked twice at once: R first on
+// equal keys (chain A) and S first (chain B), each chain placed by its own merge-path search in
+// LDS.  Every element taken learns how many elements of the other side precede it -- chain A: an
+// R row #S < k, an S row #R <= k; chain B: an R row #S <= k, an S row #R < k -- so the two give
+// each row the lower and upper bound of its key in the other range.  The chains are independent
+// (16-bit bounds, lo[] and hi[]): their LDS latencies overlap.
+// keys[] holds the R range at [0, na) and the S range at [na, na + nb) (padded indices).
+__device__ __forceinline__ void merge_walks(const uint32_t* keys, uint32_t na, uint32_t nb, uint32_t d, uint32_t e,
+                                            uint16_t* blo, uint16_t* bhi) {
+    uint32_t la = d > nb ? d - nb : 0, ha = d < na ? d : na;
+    uint32_t lb = la, hb = ha;
+#pragma unroll
+    for (int it = 0; it < 13; it++) {   // 13 halvings cover AG_T <= 4096 (static_assert below)
+        if (la < ha) {
+            const uint32_t mid = (la + ha) >> 1;
+            if (keys[pd(mid)] <= keys[pd(na + d - mid - 1)]) la = mid + 1;
+            else ha = mid;
+        }
+        if (lb < hb) {
+            const uint32_t mid = (lb + hb) >> 1;
+            if (keys[pd(mid)] < keys[pd(na + d - mid - 1)]) lb = mid + 1;
+            else hb = mid;
+        }
+    }
+    uint32_t aA = la, bA = d - la, aB = lb, bB = d - lb;
+    uint32_t kaA = aA < na ? keys[pd(aA)] : 0, kbA = bA < nb ? keys[pd(na + bA)] : 0;
+    uint32_t kaB = aB < na ? keys[pd(aB)] : 0, kbB = bB < nb ? keys[pd(na + bB)] : 0;
+    for (uint32_t p = d; p < e; p++) {
+        const bool tA = aA < na && (bA >= nb || kaA <= kbA);
+        const bool tB = aB < na && (bB >= nb || kaB < kbB);
+        blo[pd(tA ? aA : na + bA)] = (uint16_t)(tA ? bA : aA);   // R: #S < k; S: #R <= k
+        bhi[pd(tB ? aB : na + bB)] = (uint16_t)(tB ? bB : aB);   // R: #S <= k; S: #R < k
+        aA += tA ? 1u : 0u;
+        bA += tA ? 0u : 1u;
+        aB += tB ? 1u : 0u;
+        bB += tB ? 0u : 1u;
+        const uint32_t nA = tA ? aA : na + bA, nB = tB ? aB : na + bB;
+        const uint32_t kA = (tA ? aA < na : bA < nb) ? keys[pd(nA)] : 0;
+        const uint32_t kB = (tB ? aB < na : bB < nb) ? keys[pd(nB)] : 0;
+        kaA = tA ? kA : kaA;
+        kbA = tA ? kbA : kA;
+        kaB = tB ? kB : kaB;
+        kbB = tB ? kbB : kB;
+    }
+}
+
+#ifdef QE_DIAG_STAMPS
+__device__ uint64_t g_ag_stamps[STAMP_TILES * STAMP_SLOTS];
+#endif
+
+// the words of tile t (its R range, then its S range) into registers, striped over the block
+__device__ __forceinline__ void ag_load(const uint64_t* __restrict__ R, const uint64_t* __restrict__ S, uint64_t m,
+                                        const uint64_t* __restrict__ ra, uint32_t t, uint64_t* w, uint32_t* na_out,
+                                        uint32_t* tot_out) {
+    const uint64_t d0 = (uint64_t)t * AG_T, d1 = d0 + AG_T < m ? d0 + AG_T : m;
+    const uint64_t a0 = ra[t], a1 = ra[t + 1];
+    const uint64_t b0 = d0 - a0;
+    const uint32_t na = (uint32_t)(a1 - a0), tot = (uint32_t)(d1 - d0);
+#pragma unroll
+    for (int j = 0; j < AG_ITEMS; j++) {
+        const uint32_t i = (uint32_t)j * AG_NT + threadIdx.x;
+        w[j] = i < na ? R[a0 + i] : (i < tot ? S[b0 + (i - na)] : 0);
+    }
+    *na_out = na;
+    *tot_out = tot;
+}
+
+// Persistent: each workgroup takes tiles blockIdx.x, + gridDim.x, ...; the next tile's words are
+// loaded while the current tile is walked and summed (its HBM latency hides behind LDS work),
+// and the sums stay in registers until the last tile: partial[block] = (pairs, sum of R vals x
+// S counts, sum of S vals x R counts)
+__global__ void __launch_bounds__(AG_NT) ag_tile_kernel(const uint64_t* __restrict__ R, uint64_t nR,
+                                                        const uint64_t* __restrict__ S, uint64_t nS, uint32_t nt,
+                                                        const uint64_t* __restrict__ ra, const uint32_t* __restrict__ bkey,
+                                                        const uint32_t* __restrict__ bcR, const uint32_t* __restrict__ bcS,
+                                                        uint64_t* __restrict__ partial) {
+    static_assert(AG_T <= 4096, "13 merge-path halvings, 16-bit in-tile bounds");
+    __shared__ uint32_t keys[AG_T + AG_T / 32];   // R range then S range (padded indices, pd)
+    __shared__ uint16_t blo[AG_T + AG_T / 32];    // per element: bounds of its key in the other range
+    __shared__ uint16_t bhi[AG_T + AG_T / 32];
+    __shared__ uint64_t red[3][AG_NT / 64];
+    const uint64_t m = nR + nS;
+    uint64_t pairs = 0, sr = 0, ss = 0;
+    uint64_t w[AG_ITEMS], wn[AG_ITEMS];
+    uint32_t na = 0, tot = 0, nan = 0, totn = 0;
+    uint32_t t = blockIdx.x;
+    if (t < nt) ag_load(R, S, m, ra, t, w, &na, &tot);
+    for (; t < nt; t += gridDim.x) {
+        QE_STAMP(g_ag_stamps, t, 0);
+        const uint32_t nb = tot - na;
+#pragma unroll
+        for (int j = 0; j < AG_ITEMS; j++) {
+            const uint32_t i = (uint32_t)j * AG_NT + threadIdx.x;
+            if (i < tot) keys[pd(i)] = kf(w[j]);
+        }
+        __syncthreads();
+        QE_STAMP(g_ag_stamps, t, 1);
+        const uint32_t tn = t + gridDim.x;
+        if (tn < nt) ag_load(R, S, m, ra, tn, wn, &nan, &totn);   // in flight during the walks
+        // boundary keys: a key equal to one of these may run past the tile -- global counts;
+        // every other key's run lies wholly inside the tile and the walks count its partners
+        const bool hasL = t > 0, hasR = t + 1 < nt;
+        const uint32_t kL = hasL ? bkey[t] : 0, kR = hasR ? bkey[t + 1] : 0;
+        const uint32_t lR = hasL ? bcR[t] : 0, lS = hasL ? bcS[t] : 0;
+        const uint32_t rR = hasR ? bcR[t + 1] : 0, rS = hasR ? bcS[t + 1] : 0;
+        const uint32_t e0 = threadIdx.x * AG_ITEMS < tot ? threadIdx.x * AG_ITEMS : tot;
+        const uint32_t e1 = e0 + AG_ITEMS < tot ? e0 + AG_ITEMS : tot;
+        merge_walks(keys, na, nb, e0, e1, blo, bhi);
+        __syncthreads();
+        QE_STAMP(g_ag_stamps, t, 2);
+#pragma unroll
+        for (int j = 0; j < AG_ITEMS; j++) {
+            const uint32_t i = (uint32_t)j * AG_NT + threadIdx.x;
+            if (i >= tot) continue;
+            const uint32_t k = kf(w[j]);
+            const uint32_t v = (uint32_t)w[j];
+            const bool isR = i < na;
+            const uint32_t lo = blo[pd(i)], hi = bhi[pd(i)];
+            uint32_t c = isR ? hi - lo : lo - hi;   // partners in the other side
+            if (hasL && k == kL) c = isR ? lS : lR;
+            else if (hasR && k == kR) c = isR ? rS : rR;
+            if (isR) {
+                pairs += c;
+                sr += (uint64_t)v * c;
+            } else {
+                ss += (uint64_t)v * c;
+            }
+        }
+        __syncthreads();   // keys / bounds are rewritten for the next tile
+        QE_STAMP(g_ag_stamps, t, 3);
+#pragma unroll
+        for (int j = 0; j < AG_ITEMS; j++) w[j] = wn[j];
+        na = nan;
+        tot = totn;
+    }
+    pairs = wave_sum_u64(pairs);
+    sr = wave_sum_u64(sr);
+    ss = wave_sum_u64(ss);
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[0][wv] = pairs;
+        red[1][wv] = sr;
+        red[2][wv] = ss;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        uint64_t sum = 0;
+#pragma unroll
+        for (int q = 0; q < AG_NT / 64; q++) sum += red[threadIdx.x][q];
+        partial[(uint64_t)blockIdx.x * 3 + threadIdx.x] = sum;
+    }
+}
+
+__global__ void __launch_bounds__(1024) ag_reduce_kernel(const uint64_t* __restrict__ partial, uint32_t nt,
+                                                         uint64_t* __restrict__ out) {
+    __shared__ uint64_t red[3][16];
+    uint64_t s[3] = {0, 0, 0};
+    for (uint32_t t = threadIdx.x; t < nt; t += 1024)
+#pragma unroll
+        for (int q = 0; q < 3; q++) s[q] += partial[(uint64_t)t * 3 + q];
+#pragma unroll
+    for (int q = 0; q < 3; q++) s[q] = wave_sum_u64(s[q]);
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int q = 0; q < 3; q++) red[q][threadIdx.x >> 6] = s[q];
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        uint64_t v = 0;
+        for (int q = 0; q < 16; q++) v += red[threadIdx.x][q];
+        out[threadIdx.x] = v;
+    }
+}
+
+// OR / AND of a column: the load-time statistics of a relation column, else one pass
+static void col_bits(qe_ctx* c, const uint64_t* d, uint64_t n, uint64_t kb[2]) {
+    for (const Relation& r : c->rels)
+        for (size_t j = 0; j < r.cols.size(); j++)
+            if (r.cols[j] == d && r.rows == n && j < r.kor.size()) {
+                kb[0] = r.kor[j];
+                kb[1] = r.kand[j];
+                return;
+            }
+    key_bits_u64(c, d, n, kb);
+}
+
+}  // namespace qe
+
+#ifdef QE_DIAG_STAMPS
+extern "C" int qe_diag_stamps_ag(uint64_t* out, uint64_t n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(qe::g_ag_stamps), n * 8) == hipSuccess ? 0 : -2;
+}
+#endif
+
+using namespace qe;
+
+extern "C" int qe_join_aggregate(qe_ctx* c, qe_col keyR, qe_col valR, qe_col keyS, qe_col valS, uint64_t* out) {
+    QE_API_BEGIN(c)
+    if (!out) throw Error(QE_EINVAL, "null output");
+    if (!keyR.d || !keyS.d) throw Error(QE_EINVAL, "null key column");
+    if ((valR.d && valR.n != keyR.n) || (valS.d && valS.n != keyS.n))
+        throw Error(QE_EINVAL, "value column length differs from its key column");
+    const uint64_t nR = keyR.n, nS = keyS.n;
+    out[0] = out[1] = out[2] = 0;
+    if (nR == 0 || nS == 0) return 0;
+    if (nR >= 0xFFFFFFFFull || nS >= 0xFFFFFFFFull) throw Error(QE_ENOTSUP, "aggregate join side beyond 2^32 rows");
+    uint64_t kr[2], ks[2];
+    col_bits(c, keyR.d, nR, kr);
+    col_bits(c, keyS.d, nS, ks);
+    for (const qe_col* v : {&valR, &valS}) {
+        if (!v->d) continue;
+        uint64_t vb[2];
+        col_bits(c, v->d, v->n, vb);
+        if (vb[0] >> 32) throw Error(QE_ENOTSUP, "aggregate join value column beyond 32 bits");
+    }
+    const uint64_t vary = (kr[0] | ks[0]) & ~(kr[1] & ks[1]);
+    int lo = 0, nb = 0;
+    if (vary) {
+        lo = __builtin_ctzll(vary);
+        nb = 64 - __builtin_clzll(vary) - lo;
+    }
+    // (bits outside the field are equal in every key of both sides: comparing fields is exact)
+    if (nb > 32) throw Error(QE_ENOTSUP, "aggregate join keys vary in more than 32 bits");
+    uint64_t* wR = sort_words_kv64(c, keyR.d, valR.d, nR, lo, nb);
+    uint64_t* wS = sort_words_kv64(c, keyS.d, valS.d, nS, lo, nb);
+    const uint64_t m = nR + nS;
+    const uint32_t nt = (uint32_t)((m + AG_T - 1) / AG_T);
+    uint64_t* ra = dalloc_t<uint64_t>(c, (uint64_t)nt + 1);
+    uint32_t* bk = dalloc_t<uint32_t>(c, (uint64_t)nt + 1);
+    uint32_t* bcR = dalloc_t<uint32_t>(c, (uint64_t)nt + 1);
+    uint32_t* bcS = dalloc_t<uint32_t>(c, (uint64_t)nt + 1);
+    // persistent tile kernel: as many workgroups as stay resident
+    static int resident = [&] {
+        int ncu = 0, per = 0;
+        QE_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
+        QE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ag_tile_kernel, AG_NT, 0));
+        return std::max(ncu, 1) * std::max(per, 1);
+    }();
+    const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(nt, (uint32_t)resident));
+    uint64_t* partial = dalloc_t<uint64_t>(c, (uint64_t)grid * 3);
+    uint64_t* d_out = c->d_scratch + 48;   // [pairs, sum R, sum S]
+    {
+        Timed t(c, "agg_split", 0);
+        hipLaunchKernelGGL(ag_split_kernel, dim3((nt + 1 + 255) / 256), dim3(256), 0, c->stream, wR, nR, wS, nS, nt, ra, bk,
+                           bcR, bcS);
+        QE_HIP(hipGetLastError());
+    }
+    {
+        Timed t(c, "agg_count", 8.0 * (double)m);
+        hipLaunchKernelGGL(ag_tile_kernel, dim3(grid), dim3(AG_NT), 0, c->stream, wR, nR, wS, nS, nt, ra, bk, bcR, bcS,
+                           partial);
+        QE_HIP(hipGetLastError());
+        hipLaunchKernelGGL(ag_reduce_kernel, dim3(1), dim3(1024), 0, c->stream, partial, grid, d_out);
+        QE_HIP(hipGetLastError());
+    }
+    read_words(c, d_out, out, 3);
+    if (!valR.d) out[1] = 0;   // (the words carried row indices)
+    if (!valS.d) out[2] = 0;
+    for (void* p : {(void*)wR, (void*)wS, (void*)ra, (void*)bk, (void*)bcR, (void*)bcS, (void*)partial}) dfree(c, p);
+    return 0;
+    QE_API_END(c)
+}

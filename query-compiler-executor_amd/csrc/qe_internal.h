@@ -218,6 +218,9 @@ void partition_dev(qe_ctx* c, const uint64_t* keys, uint64_t n, const uint32_t* 
                    uint32_t nparts, unsigned long long* d_cnt, uint64_t* out_keys, uint32_t* const* out_cols);
 // OR / AND of n keys -> host out[2] (synchronises)
 void key_bits_u64(qe_ctx* c, const uint64_t* keys, uint64_t n, uint64_t* out);
+// (key field << 32 | (uint32_t) val) words of a base column, stable-sorted by the field
+// (key >> lo) & (2^nb - 1), nb <= 32 (qe_join_aggregate); vals == null packs the row index
+uint64_t* sort_words_kv64(qe_ctx* c, const uint64_t* keys, const uint64_t* vals, uint64_t n, int lo, int nb);
 
 }  // namespace qe
 

@@ -1879,11 +1879,13 @@ int qe_checksums(qe_ctx* c, int n, const qe_col* cols, const qe_list* const* row
 #ifdef QE_DIAG_STAMPS
 extern "C" int qe_diag_stamps_sort(const char* which, uint64_t* out, uint64_t n);
 extern "C" int qe_diag_stamps_cp(uint64_t* out, uint64_t n);
+extern "C" int qe_diag_stamps_ag(uint64_t* out, uint64_t n);
 // tuning builds only (not part of qe.h): copy the last launch's phase stamps out
 extern "C" int qe_diag_stamps(const char* which, uint64_t* out, uint64_t n) {
     (void)hipDeviceSynchronize();
     if (!strcmp(which, "mj")) return hipMemcpyFromSymbol(out, HIP_SYMBOL(qe::g_mj_stamps), n * 8) == hipSuccess ? 0 : -2;
     if (!strcmp(which, "cp")) return qe_diag_stamps_cp(out, n);
+    if (!strcmp(which, "ag")) return qe_diag_stamps_ag(out, n);
     return qe_diag_stamps_sort(which, out, n);
 }
 #endif

@@ -133,7 +133,7 @@ __global__ void __launch_bounds__(256) digit_scan_kernel(uint32_t* hist) {
 }
 
 // input / output formats of a pass
-enum { IN_WORD = 0, IN_KV = 1, IN_KIOTA = 2 };
+enum { IN_WORD = 0, IN_KV = 1, IN_KIOTA = 2, IN_KV64 = 3 };   // IN_KV64: `vin` is a u64 column, low 32 bits packed
 enum { OUT_WORD = 0, OUT_KV = 1 };
 
 // word <-> (key, rowid).  PACK: word = ((key >> lo) & fmask) << 32 | rowid, key restored as
@@ -203,7 +203,9 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
         } else {
             uint64_t k = ok ? (uint64_t)kin[i] : 0;
             if (PACK) {
-                uint32_t v = IN == IN_KV ? (ok ? vin[i] : 0u) : (uint32_t)i;
+                uint32_t v = IN == IN_KV     ? (ok ? vin[i] : 0u)
+                             : IN == IN_KV64 ? (ok ? (uint32_t)reinterpret_cast<const uint64_t*>(vin)[i] : 0u)
+                                             : (uint32_t)i;
                 word[j] = (((k >> f.lo) & f.fmask) << 32) | v;
             } else {
                 word[j] = k;
@@ -1763,6 +1765,59 @@ static void complete_lsd(qe_ctx* c, const DeferredSort& d, uint64_t n) {
     dfree(c, hist);
     dfree(c, buf[0]);
     if (buf[1]) dfree(c, buf[1]);
+}
+
+// (field << 32 | (uint32_t) val[i]) words of a base column, stable-sorted by the key field
+// (key >> lo) & (2^nb - 1): the aggregate join's sides (qe_join_aggregate), whose select column
+// rides in the word where the other sorts carry the rowid.  vals == null packs the row index.
+uint64_t* sort_words_kv64(qe_ctx* c, const uint64_t* keys, const uint64_t* vals, uint64_t n, int lo, int nb) {
+    if (n >= 0xFFFFFFFFull) throw Error(QE_EINVAL, "sort input too large");
+    PassDesc pd{};
+    const uint64_t fmask = nb >= 32 ? 0xFFFFFFFFull : (1ull << nb) - 1;
+    if (nb == 0) {   // every key equal: one pass packs the words (digit 0 everywhere, order kept)
+        pd.npass = 1;
+        pd.shift[0] = lo;
+        pd.mask[0] = 0;
+    } else {
+        pd.npass = (nb + 7) / 8;
+        const int width = (nb + pd.npass - 1) / pd.npass;
+        for (int p = 0; p < pd.npass; p++) {
+            pd.shift[p] = lo + p * width;
+            pd.mask[p] = (1u << std::min(width, nb - p * width)) - 1u;
+        }
+    }
+    const Field f{lo, fmask, 0};
+    constexpr int BINS = 256;
+    uint32_t* hist = dalloc_t<uint32_t>(c, (size_t)MAX_PASS * BINS);
+    hist_and_scan<uint64_t, 8>(c, keys, n, pd, hist);
+    const uint64_t nt = (n + RTILE - 1) / RTILE;
+    uint64_t* buf[2] = {dalloc_t<uint64_t>(c, std::max<uint64_t>(n, 1)),
+                        pd.npass > 1 ? dalloc_t<uint64_t>(c, n) : nullptr};
+    const uint64_t* win = nullptr;
+    for (int p = 0; p < pd.npass; p++) {
+        uint64_t* wo = buf[p & 1];
+        const int dsh = 32 + pd.shift[p] - lo;
+        LBSlot s = lb_acquire(c, nt * BINS);
+        Timed t(c, "sort_pass_agg", (p == 0 ? (vals ? 16.0 : 8.0) : 8.0) * n + 8.0 * n);
+        if (p > 0)
+            hipLaunchKernelGGL((radix_pass_kernel<uint64_t, IN_WORD, OUT_WORD, true, 8, R_ITEMS, R_NT>), dim3((unsigned)nt),
+                               dim3(R_NT), 0, c->stream, keys, win, nullptr, nullptr, wo, nullptr, n, dsh, pd.mask[p], f,
+                               hist + p * BINS, s.status, s.ticket, s.epoch);
+        else if (vals)
+            hipLaunchKernelGGL((radix_pass_kernel<uint64_t, IN_KV64, OUT_WORD, true, 8, R_ITEMS, R_NT>), dim3((unsigned)nt),
+                               dim3(R_NT), 0, c->stream, keys, nullptr, reinterpret_cast<const uint32_t*>(vals), nullptr,
+                               wo, nullptr, n, dsh, pd.mask[p], f, hist + p * BINS, s.status, s.ticket, s.epoch);
+        else
+            hipLaunchKernelGGL((radix_pass_kernel<uint64_t, IN_KIOTA, OUT_WORD, true, 8, R_ITEMS, R_NT>), dim3((unsigned)nt),
+                               dim3(R_NT), 0, c->stream, keys, nullptr, nullptr, nullptr, wo, nullptr, n, dsh, pd.mask[p],
+                               f, hist + p * BINS, s.status, s.ticket, s.epoch);
+        QE_HIP(hipGetLastError());
+        win = wo;
+    }
+    dfree(c, hist);
+    const int last = (pd.npass - 1) & 1;
+    if (buf[last ^ 1]) dfree(c, buf[last ^ 1]);
+    return buf[last];
 }
 
 void pairs_need_keys(qe_ctx* c, const qe_pairs* p) {

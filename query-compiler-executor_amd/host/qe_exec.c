@@ -49,6 +49,9 @@ typedef struct {
     const uint8_t* pred_live;    /* pred_live[b]: binding b is read by a later predicate */
     struct agg_side { const qe_list* l; qe_pairs p; } *aggs;   /* unmaterialised join sides */
     size_t naggs, capaggs;
+    int last_pred;               /* the predicate running is the query's last */
+    struct agg_sum { const qe_list* l; uint64_t col; uint64_t sum; } sums[2];   /* qe_join_aggregate */
+    size_t nsums;
 } exec_t;
 
 /* Dead-list elimination.  fix_all re-materialises every other entry of the entity
@@ -98,6 +101,7 @@ static qe_list* new_list(exec_t* x) {
 static void free_lists(exec_t* x) {
     for (size_t i = 0; i < x->naggs; i++) qe_pairs_free(x->q, &x->aggs[i].p);
     x->naggs = 0;
+    x->nsums = 0;
     for (size_t i = 0; i < x->nlists; i++) {
         qe_list_free(x->q, x->lists[i]);
         free(x->lists[i]);
@@ -430,6 +434,72 @@ static void merge(exec_t* x, const query_t* q, const pred_t* p, const mra_t* M, 
     keep_agg(x, jr->res[1], &rel[1], P);
 }
 
+/* The query's last join, of two base columns, whose lists only print_sums reads and whose
+ * bindings' selects each name one column with values < 2^32: qe_join_aggregate computes the
+ * pair count and both checksums from value-carrying sorts and one counting pass -- the numbers
+ * print_sums would compute over the materialised lists, whatever their size.  Joins of fewer
+ * than QE_AGG_MIN rows (both sides; default 2^24) keep the merge path. */
+static uint64_t agg_min(void) {
+    static uint64_t v = (uint64_t)-1;
+    if (v == (uint64_t)-1) {
+        const char* e = getenv("QE_AGG_MIN");
+        v = e ? strtoull(e, NULL, 10) : (1ull << 24);
+    }
+    return v;
+}
+
+/* the one column the selects read from binding b (1), none (0), or several / invalid (-1) */
+static int select_col(exec_t* x, const query_t* q, uint64_t b, uint64_t* col) {
+    int found = 0;
+    for (size_t i = 0; i < q->nsel; i++) {
+        if (q->sel[2 * i] != b) continue;
+        if (found && q->sel[2 * i + 1] != *col) return -1;
+        *col = q->sel[2 * i + 1];
+        found = 1;
+    }
+    if (!found) return 0;
+    qe_col c;
+    uint64_t kor = 0, kand = 0;
+    if (qe_relation_column(x->q, (int)q->rels[b], (int)*col, &c) != 0) return -1;
+    if (qe_relation_column_bits(x->q, (int)q->rels[b], (int)*col, &kor, &kand) != 0 || (kor >> 32)) return -1;
+    return 1;
+}
+
+static int join_aggregate(exec_t* x, const query_t* q, const pred_t* p, const mra_t* M, int v, const qe_pairs rel[2],
+                          const qe_list* src[2], jres_t* jr) {
+    if (!x->last_pred || v != CLASSIC_JOIN || src[0] || src[1]) return 0;
+    if (rel[0].n + rel[1].n < agg_min() || !aggregate_ok(x, q, p, M, v)) return 0;
+    uint64_t cR = 0, cS = 0, kb[4];
+    const int hR = select_col(x, q, p->frel, &cR), hS = select_col(x, q, p->srel, &cS);
+    if (hR < 0 || hS < 0) return 0;
+    if (qe_relation_column_bits(x->q, (int)q->rels[p->frel], (int)p->fcol, &kb[0], &kb[1]) != 0 ||
+        qe_relation_column_bits(x->q, (int)q->rels[p->srel], (int)p->scol, &kb[2], &kb[3]) != 0)
+        return 0;
+    const uint64_t vary = (kb[0] | kb[2]) & ~(kb[1] & kb[3]);
+    if (vary && 64 - __builtin_clzll(vary) - __builtin_ctzll(vary) > 32) return 0;
+    qe_col vR = {NULL, 0}, vS = {NULL, 0};
+    if (hR) vR = column(x, q->rels[p->frel], cR);
+    if (hS) vS = column(x, q->rels[p->srel], cS);
+    uint64_t out[3];
+    chk(x, qe_join_aggregate(x->q, column(x, q->rels[p->frel], p->fcol), vR, column(x, q->rels[p->srel], p->scol), vS,
+                             out));
+    x->nsums = 0;
+    for (int side = 0; side < 2; side++) {
+        qe_list* l = jr->res[side];
+        l->d = NULL;
+        l->n = out[0];
+        l->cap = 0;
+        l->flags = QE_LIST_AGG;
+        if (side == 0 ? hR : hS) {
+            x->sums[x->nsums].l = l;
+            x->sums[x->nsums].col = side == 0 ? cR : cS;
+            x->sums[x->nsums].sum = out[1 + side];
+            x->nsums++;
+        }
+    }
+    return 1;
+}
+
 /* execute_join (src/join.c:630-679) */
 static int execute_join(exec_t* x, const query_t* q, const pred_t* p, mra_t* M) {
     qe_pairs rel[2];
@@ -444,7 +514,9 @@ static int execute_join(exec_t* x, const query_t* q, const pred_t* p, mra_t* M) 
     jr.src[1] = src[1];
     jr.R = &rel[0];
     jr.S = &rel[1];
-    switch (v) {
+    switch (join_aggregate(x, q, p, M, v, rel, src, &jr) ? -2 : v) {
+    case -2:
+        break;
     case CLASSIC_JOIN:
         chk(x, qe_sort_pairs(x->q, &rel[0]));
         chk(x, qe_sort_pairs(x->q, &rel[1]));
@@ -554,7 +626,13 @@ static void print_sums(exec_t* x, const query_t* q, const mra_t* M) {
             const qe_pairs* agg = NULL;
             for (size_t a = 0; a < x->naggs && (l->flags & QE_LIST_AGG); a++)
                 if (x->aggs[a].l == l) agg = &x->aggs[a].p;
-            if (agg) {
+            const struct agg_sum* as = NULL;
+            for (size_t a = 0; a < x->nsums && (l->flags & QE_LIST_AGG); a++)
+                if (x->sums[a].l == l && x->sums[a].col == colno) as = &x->sums[a];
+            if (as) {
+                (void)column(x, relation, colno);   /* the same validation, at its place in the line */
+                s = as->sum;
+            } else if (agg) {
                 chk(x, qe_checksum_weighted(x->q, column(x, relation, colno), agg, &s));
             } else if (!(l->flags & (QE_LIST_AGG | QE_LIST_DEAD)) && k < nb) {
                 (void)column(x, relation, colno);   /* the same validation, at its place in the line */
@@ -615,10 +693,12 @@ static void execute_query(exec_t* x, query_t* q) {
         x->live = live;
         x->pred_live = pred_live;
         const pred_t* p = &q->preds[i];
+        x->last_pred = i + 1 == q->npreds;
         int r = p->type == 1 ? execute_filter(x, q, p, &M) : execute_join(x, q, p, &M);
         if (r == -1) ok = 0;
     }
     x->live = x->pred_live = NULL;
+    x->last_pred = 0;
     free(live);
     free(pred_live);
     if (ok) print_sums(x, q, &M);

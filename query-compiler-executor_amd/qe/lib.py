@@ -92,6 +92,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "qe_checksums": (I, [P, I, C.POINTER(Col), C.POINTER(C.POINTER(List)), C.POINTER(C.c_uint64)]),
         "qe_checksum_weighted": (I, [P, Col, C.POINTER(Pairs), C.POINTER(C.c_uint64)]),
         "qe_merge_join_counts": (I, [P, C.POINTER(Pairs), C.POINTER(Pairs), C.POINTER(C.c_uint64)]),
+        "qe_join_aggregate": (I, [P, Col, Col, Col, Col, C.POINTER(C.c_uint64)]),
         "qe_set_materialize_limit": (I, [P, U64]),
         "qe_set_zipf_table": (I, [P, C.c_void_p, U64, U64]),
         "qe_set_zipf": (I, [P, U64, C.c_double, U64]),
@@ -377,6 +378,13 @@ class Ctx:
         P = C.c_uint64()
         self._chk(self.lib.qe_merge_join_counts(self.h, C.byref(R), C.byref(S), C.byref(P)))
         return P.value
+
+    def join_aggregate(self, keyR: Col, valR: Col | None, keyS: Col, valS: Col | None) -> tuple[int, int, int]:
+        """(pairs, sum of valR x S partners, sum of valS x R partners) of two base columns"""
+        out = (C.c_uint64 * 3)()
+        self._chk(self.lib.qe_join_aggregate(self.h, keyR, valR if valR is not None else Col(None, 0), keyS,
+                                             valS if valS is not None else Col(None, 0), out))
+        return out[0], out[1], out[2]
 
     def checksum_weighted(self, col: Col, p: Pairs) -> int:
         s = C.c_uint64()

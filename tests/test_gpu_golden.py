@@ -59,7 +59,7 @@ def _binary(paths, queries, env=None):
     return r.stdout.decode("latin-1"), r.returncode
 
 
-@pytest.mark.parametrize("mode", ["faithful", "plan", "ranks1", "lanes4"])
+@pytest.mark.parametrize("mode", ["faithful", "plan", "ranks1", "lanes4", "agg0"])
 @pytest.mark.parametrize("fixture", [os.path.basename(f)[:-5] for f in goldens.golden_files()])
 def test_dropin_binary_matches_reference_golden(fixture, mode):
     """every golden through build/queries (mmap'd relation files, the reference's stdin protocol).
@@ -69,7 +69,8 @@ def test_dropin_binary_matches_reference_golden(fixture, mode):
     inputs) runs on its own."""
     # the faithful executor; the partitioned executor on one GPU; the same through the rank
     # launcher (fork, RCCL bootstrap over a pipe, one-rank communicator); four concurrent lanes
-    env = {"faithful": {}, "plan": {"QE_PLAN": "1"}, "ranks1": {"QE_GPUS": "1"}, "lanes4": {"QE_WORKERS": "4"}}[mode]
+    env = {"faithful": {}, "plan": {"QE_PLAN": "1"}, "ranks1": {"QE_GPUS": "1"}, "lanes4": {"QE_WORKERS": "4"},
+           "agg0": {"QE_AGG_MIN": "0"}}[mode]
     doc = goldens.load(os.path.join(goldens.GOLDEN_DIR, f"{fixture}.json"))
     rels, paths = goldens.dataset(doc["dataset"])
     batch = [c for c in doc["cases"] if c["rc"] == 0 and WELL_FORMED.fullmatch(c["input"])]

@@ -22,6 +22,7 @@ PHASES = {
     "mj": ["ticket+win", "stage", "walk+annot+scan", "lookback+flags", "emit"],
     "sort": ["ticket+zero", "load+rank", "totals+publish+scan", "stage+lookback(t0)", "lookback wait", "write"],
     "cp": ["ticket", "load+ballots", "scan+lookback", "stage", "write"],
+    "ag": ["load+keys", "walks", "sums"],
 }
 
 
@@ -67,6 +68,13 @@ def main():
     a = ap.parse_args()
     ctx = lib.Ctx(0)
     n = a.n
+    if "ag" in a.what:   # the aggregate join's tile kernel on C5-shaped data (first 65536 tiles)
+        from qe import datagen as dg
+        dg.gen_c5(ctx, n)
+        ctx.run(dg.C5_QUERY)
+        report(ctx, "ag", min(65536, (2 * n + 4095) // 4096))
+        ctx.close()
+        return
     kinds = [("mod", n), ("mod", n), ("hi32",)]
     r0 = ctx.gen_relation(n, kinds, seed=1, gen_rel=0)
     r1 = ctx.gen_relation(n, kinds, seed=1, gen_rel=1)
