@@ -220,6 +220,12 @@ int qe_partition(qe_ctx*, const uint64_t* keys, uint64_t n, const uint32_t* cons
                  uint32_t nparts, uint64_t* counts, uint64_t* out_keys, uint32_t* const* out_cols);
 /* a1 on a row range [start, end) of a column, rowids numbered globally (a rank's slice). */
 int qe_filter_scan_range(qe_ctx*, qe_col col, uint64_t start, uint64_t end, char op, uint64_t v, qe_list* out);
+/* a1 + a2 fused: rowids r in [start, end) with col1[r] op1 v1 AND col2[r] op2 v2, ascending --
+ * exec_filter_rel_no_exists followed by exec_filter_rel_exists on the same binding
+ * (src/filter.c:37-64, 3-35); the refine's list is never built.  col1 and col2 may be the same
+ * column (read once). */
+int qe_filter_scan2_range(qe_ctx*, qe_col col1, char op1, uint64_t v1, qe_col col2, char op2, uint64_t v2,
+                          uint64_t start, uint64_t end, qe_list* out);
 /* rowids start .. start+n-1 (an unfiltered slice). */
 int qe_iota(qe_ctx*, uint64_t start, uint64_t n, qe_list* out);
 /* out[i] = src[idx[i]] (carry a rowid column through a join's index lists). */

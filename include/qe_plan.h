@@ -71,6 +71,11 @@ typedef struct qe_engine {
      * host/qe_query.h, `out` the FILE* the batch prints to (rank 0's matters); returns 0 or the
      * reference's exit code path (QE_EEXIT) -- identical on every rank */
     int (*fallback)(void* u, void* query, void* out);
+    /* a1 then a2 on the same binding, fused (nullable): rowids r in [start, end) with
+     * col1[r] op1 v1 and col2[r] op2 v2, ascending -- one pass over the column(s) instead of a
+     * scan and a refine gathering through its list */
+    int (*scan2)(void* u, uint32_t rel, uint32_t col1, char op1, uint64_t v1, uint32_t col2, char op2, uint64_t v2,
+                 uint64_t start, uint64_t end, qe_h* out);
 } qe_engine;
 
 /* Replay the reference's variant choice and list bookkeeping for every query of `text` on the

@@ -141,6 +141,17 @@ int e_scan(void* u, uint32_t rel, uint32_t col, uint64_t s, uint64_t t, char op,
     });
 }
 
+int e_scan2(void* u, uint32_t rel, uint32_t col1, char op1, uint64_t v1, uint32_t col2, char op2, uint64_t v2,
+            uint64_t s, uint64_t t, qe_h* out) {
+    Eng* e = E(u);
+    return guard(e, [&] {
+        qe_list l{};
+        ck(qe_filter_scan2_range(e->c, column(e->c, rel, col1), op1, v1, column(e->c, rel, col2), op2, v2, s, t, &l),
+           e->c);
+        *out = H(new_arr(e->c, l.d, l.n, false));
+    });
+}
+
 int e_iota(void* u, uint64_t s, uint64_t n, qe_h* out) {
     Eng* e = E(u);
     return guard(e, [&] {
@@ -551,6 +562,7 @@ int qe_run_queries_dist(qe_ctx* c, qe_comm* m, const char* text, char** out, siz
     g.scan = e_scan;
     g.iota = e_iota;
     g.refine = e_refine;
+    g.scan2 = e_scan2;
     g.keys = e_keys;
     g.base_side = e_base_side;
     g.exchange_start = e_exchange_start;

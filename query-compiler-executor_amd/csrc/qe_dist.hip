@@ -476,6 +476,24 @@ int qe_filter_scan_range(qe_ctx* c, qe_col col, uint64_t start, uint64_t end, ch
     QE_API_END(c)
 }
 
+int qe_filter_scan2_range(qe_ctx* c, qe_col col1, char op1, uint64_t v1, qe_col col2, char op2, uint64_t v2,
+                          uint64_t start, uint64_t end, qe_list* out) {
+    QE_API_BEGIN(c)
+    if (end > col1.n || end > col2.n || start > end) throw Error(QE_EINVAL, "bad row range");
+    const uint64_t n = end - start;
+    out->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
+    out->cap = n;
+    out->n = filter_scan2(c, col1.d + start, op1, v1, col2.d + start, op2, v2, n, out->d);
+    if (start && out->n) {
+        hipLaunchKernelGGL(add_u32_kernel, dim3(grid_for(out->n, 256)), dim3(256), 0, c->stream, out->d, out->n,
+                           (uint32_t)start);
+        QE_HIP(hipGetLastError());
+    }
+    out->flags = QE_LIST_DISTINCT;
+    return 0;
+    QE_API_END(c)
+}
+
 int qe_iota(qe_ctx* c, uint64_t start, uint64_t n, qe_list* out) {
     QE_API_BEGIN(c)
     out->d = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));

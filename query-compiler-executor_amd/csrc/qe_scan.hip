@@ -64,6 +64,30 @@ struct FilterScanOp {          // exec_filter_rel_no_exists: rowid i if col[i] o
     }
 };
 
+__device__ __forceinline__ bool cmp_rt(uint32_t op, uint64_t k, uint64_t v) {
+    return op == OP_EQ ? k == v : (op == OP_GT ? k > v : k < v);
+}
+
+struct FilterScan2Op {         // a scan and a refine of the same binding: rowid i if both hold
+    static constexpr int VEC = 2;
+    const uint64_t *c1, *c2;
+    uint64_t v1, v2;
+    uint32_t o1, o2;
+    __device__ __forceinline__ void load(uint64_t base, uint64_t n, bool* f, uint32_t* v0, uint32_t*) const {
+        if (base + 1 < n) {
+            const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(c1 + base);
+            const ulonglong2 y = c2 == c1 ? x : *reinterpret_cast<const ulonglong2*>(c2 + base);
+            f[0] = cmp_rt(o1, x.x, v1) && cmp_rt(o2, y.x, v2);
+            f[1] = cmp_rt(o1, x.y, v1) && cmp_rt(o2, y.y, v2);
+        } else {
+            f[0] = base < n && cmp_rt(o1, c1[base], v1) && cmp_rt(o2, c2[base], v2);
+            f[1] = false;
+        }
+        v0[0] = (uint32_t)base;
+        v0[1] = (uint32_t)(base + 1);
+    }
+};
+
 template <int OP>
 struct FilterRefineOp {        // exec_filter_rel_exists: keep rowid r if col[r] op v, in order
     static constexpr int VEC = 4;
@@ -250,6 +274,123 @@ __global__ void __launch_bounds__(CB) compact_kernel(Op op, uint64_t n, uint32_t
     QE_STAMP(g_cp_stamps, tile, 5);
 }
 
+// Persistent, software-pipelined form of compact_kernel: a resident grid of workgroups loops
+// over tiles taken by ticket.  Per tile: rank, scan the (step, wave) counts, PUBLISH the tile's
+// aggregate, stage the survivors in LDS with tile-local offsets, and only then wait for the
+// lookback -- meanwhile waves 1.. already load the next tile (its ticket was taken at the top of
+// the iteration), wave 0 after its wait (a wave's loads complete in order, so its polls must not
+// queue behind a tile of loads).  The lookback latency, the whole "scan+lookback" phase of the
+// one-tile-per-workgroup form (7 of its ~22 us per tile, tools/stamps.py), overlaps HBM loads.
+// Deadlock-free by ticket order: a workgroup holds its current tile and the next one, the
+// current one taken first, so the smallest unfinished tile is always some workgroup's current
+// tile whose predecessors are all complete.
+template <int ITEMS, int NOUT, class Op>
+__global__ void __launch_bounds__(CB) compact_pipe_kernel(Op op, uint64_t n, uint32_t ntiles, uint64_t* status,
+                                                          uint32_t* ticket, uint32_t epoch, uint32_t* __restrict__ out0,
+                                                          uint32_t* __restrict__ out1, uint64_t* total_out) {
+    constexpr int VEC = Op::VEC;
+    constexpr int TILE = CB * ITEMS * VEC;
+    static_assert(ITEMS * CNW <= 128, "one wave scans the (step, wave) table, two entries per lane");
+    __shared__ uint32_t s_vals[NOUT][TILE];
+    __shared__ uint32_t s_cnt[ITEMS * CNW];
+    __shared__ uint32_t s_tk[2];
+    __shared__ uint64_t s_excl;
+    __shared__ uint32_t s_total;
+    const int w = wave_id(), l = lane_id();
+    const uint64_t lt = lanemask_lt();
+    if (threadIdx.x == 0) s_tk[0] = atomicAdd(ticket, 1u);
+    __syncthreads();
+    uint32_t tile = s_tk[0];
+    bool f[ITEMS][VEC];
+    uint32_t v0[ITEMS][VEC], v1[ITEMS][VEC];
+    auto load_tile = [&](uint32_t t) {
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t base = (uint64_t)t * TILE + (uint64_t)j * (CB * VEC) + (uint64_t)threadIdx.x * VEC;
+            op.load(base, n, f[j], v0[j], v1[j]);
+        }
+    };
+    if (tile < ntiles) load_tile(tile);
+    int par = 0;
+    while (tile < ntiles) {
+        QE_STAMP(g_cp_stamps, tile, 0);
+        if (threadIdx.x == 0) s_tk[par ^ 1] = atomicAdd(ticket, 1u);   // the next tile, taken early
+        uint32_t rank[ITEMS][VEC];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            uint32_t pre = 0, tot = 0;
+#pragma unroll
+            for (int k = 0; k < VEC; k++) {
+                const uint64_t m = __ballot(f[j][k]);
+                pre += (uint32_t)__popcll(m & lt);
+                tot += (uint32_t)__popcll(m);
+            }
+            uint32_t r = pre;
+#pragma unroll
+            for (int k = 0; k < VEC; k++) {
+                rank[j][k] = r;
+                r += f[j][k] ? 1u : 0u;
+            }
+            if (l == 0) s_cnt[j * CNW + w] = tot;
+        }
+        __syncthreads();   // s_cnt complete, s_tk[par ^ 1] visible
+        QE_STAMP(g_cp_stamps, tile, 1);
+        if (w == 0) {
+            constexpr uint32_t E = ITEMS * CNW;
+            const uint32_t c0 = 2u * l < E ? s_cnt[2 * l] : 0u, c1 = 2u * l + 1 < E ? s_cnt[2 * l + 1] : 0u;
+            const uint32_t inc = wave_incl_scan_u32(c0 + c1);
+            const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
+            if (2u * l < E) s_cnt[2 * l] = inc - c0 - c1;
+            if (2u * l + 1 < E) s_cnt[2 * l + 1] = inc - c1;
+            lookback_publish(status, epoch, tile, total);
+            if (l == 0) s_total = total;
+        }
+        __syncthreads();   // tile-local offsets visible
+        QE_STAMP(g_cp_stamps, tile, 2);
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint32_t b = s_cnt[j * CNW + w];
+#pragma unroll
+            for (int k = 0; k < VEC; k++) {
+                if (f[j][k]) {
+                    s_vals[0][b + rank[j][k]] = v0[j][k];
+                    if (NOUT == 2) s_vals[NOUT - 1][b + rank[j][k]] = v1[j][k];
+                }
+            }
+        }
+        const uint32_t total = s_total;
+        const uint32_t next = s_tk[par ^ 1];
+        if (w != 0 && next < ntiles) load_tile(next);   // in flight during the lookback
+        if (w == 0) {
+            const uint64_t excl = lookback_wait(status, epoch, tile, total);
+            if (l == 0) {
+                s_excl = excl;
+                if (tile == ntiles - 1) *total_out = excl + total;
+            }
+            if (next < ntiles) load_tile(next);
+        }
+        __syncthreads();   // staged values and the tile's offset visible
+        QE_STAMP(g_cp_stamps, tile, 3);
+        const uint64_t off = s_excl;
+        for (uint32_t i = threadIdx.x; i < total; i += CB) {
+            out0[off + i] = s_vals[0][i];
+            if (NOUT == 2) out1[off + i] = s_vals[NOUT - 1][i];
+        }
+        __syncthreads();   // s_vals / s_cnt / s_tk[par] are rewritten by the next iteration
+        QE_STAMP(g_cp_stamps, tile, 4);
+        tile = next;
+        par ^= 1;
+    }
+}
+
+static bool cp_pipe_on() {
+    static bool on = [] {   // tuning knob: QE_CP_PIPE=0 keeps one tile per workgroup
+        const char* s = getenv("QE_CP_PIPE");
+        return !(s && s[0] == '0');
+    }();
+    return on;
+}
+
 #ifdef QE_DIAG_STAMPS
 extern "C" int qe_diag_stamps_cp(uint64_t* out, uint64_t n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(qe::g_cp_stamps), n * 8) == hipSuccess ? 0 : -2;
@@ -267,7 +408,19 @@ static uint64_t run_compact(qe_ctx* c, const char* name, double bytes, const Op&
     if (nt >= (1ull << 31)) throw Error(QE_EINVAL, "input too large");
     LBSlot s = lb_acquire(c, nt);
     uint64_t* d_total = c->d_scratch;
-    {
+    if (cp_pipe_on()) {
+        static const uint32_t resident = [&] {
+            int ncu = 0, per = 0;
+            QE_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
+            QE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, compact_pipe_kernel<ITEMS, NOUT, Op>, CB, 0));
+            return (uint32_t)(std::max(ncu, 1) * std::max(per, 1));
+        }();
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(nt, resident);
+        Timed t(c, name, bytes);
+        hipLaunchKernelGGL((compact_pipe_kernel<ITEMS, NOUT, Op>), dim3(grid), dim3(CB), 0, c->stream, op, n,
+                           (uint32_t)nt, s.status, s.ticket, s.epoch, out0, out1, d_total);
+        QE_HIP(hipGetLastError());
+    } else {
         Timed t(c, name, bytes);
         hipLaunchKernelGGL((compact_kernel<ITEMS, NOUT, Op>), dim3((unsigned)nt), dim3(CB), 0, c->stream, op, n,
                            (uint32_t)nt, s.status, s.ticket, s.epoch, out0, out1, d_total);
@@ -289,6 +442,20 @@ uint64_t filter_scan(qe_ctx* c, const uint64_t* col, uint64_t n, char op, uint64
     default: throw Error(QE_EINVAL, "Wrong operator");
     }
     return m;
+}
+
+static uint32_t op_code(char op) {
+    if (op == '=') return OP_EQ;
+    if (op == '>') return OP_GT;
+    if (op == '<') return OP_LT;
+    throw Error(QE_EINVAL, "Wrong operator");
+}
+
+uint64_t filter_scan2(qe_ctx* c, const uint64_t* c1, char op1, uint64_t v1, const uint64_t* c2, char op2, uint64_t v2,
+                      uint64_t n, uint32_t* out) {
+    // read 8 B/row per distinct column; 4 B/survivor added below
+    const FilterScan2Op o{c1, c2, v1, v2, op_code(op1), op_code(op2)};
+    return run_compact<FS_ITEMS, 1>(c, "filter_scan", (c1 == c2 ? 8.0 : 16.0) * n, o, n, out, nullptr);
 }
 
 uint64_t filter_refine(qe_ctx* c, const uint64_t* col, const uint32_t* in, uint64_t n, char op, uint64_t v,

@@ -678,6 +678,19 @@ static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t*
                 if (!rc) rc = allreduce1(P, &n);
                 P->list_size[b] = n;
                 if (!rc) fprintf(out, "%d\n", (int)(uint32_t)n);        /* src/filter.c:32 */
+            } else if (e->scan2 && k + 1 < q->npreds && q->preds[k + 1].type == 1 && (int)q->preds[k + 1].frel == b) {
+                /* the scan and the refine after it, in one pass (only the refine prints a count) */
+                const pred_t* p2 = &q->preds[k + 1];
+                uint64_t s, t;
+                owned_range(P, rel_rows(P, relid), &s, &t);
+                rc = e->scan2(e->u, relid, (uint32_t)p->fcol, p->op, p->cval, (uint32_t)p2->fcol, p2->op, p2->cval, s,
+                              t, &P->list[b]);
+                uint64_t n = 0;
+                if (!rc) rc = e->length(e->u, P->list[b], &n);
+                if (!rc) rc = allreduce1(P, &n);
+                P->list_size[b] = n;
+                if (!rc) fprintf(out, "%d\n", (int)(uint32_t)n);        /* src/filter.c:32 */
+                k++;
             } else {
                 uint64_t s, t;
                 owned_range(P, rel_rows(P, relid), &s, &t);

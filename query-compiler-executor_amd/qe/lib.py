@@ -99,6 +99,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "qe_partition": (I, [P, C.c_void_p, U64, C.POINTER(C.c_void_p), I, C.c_uint32, C.POINTER(C.c_uint64),
                              C.c_void_p, C.POINTER(C.c_void_p)]),
         "qe_filter_scan_range": (I, [P, Col, U64, U64, C.c_char, U64, C.POINTER(List)]),
+        "qe_filter_scan2_range": (I, [P, Col, C.c_char, U64, Col, C.c_char, U64, U64, U64, C.POINTER(List)]),
         "qe_iota": (I, [P, U64, U64, C.POINTER(List)]),
         "qe_take_u32": (I, [P, C.c_void_p, C.POINTER(List), C.POINTER(List)]),
         "qe_join_indices": (I, [P, C.c_void_p, U64, C.c_void_p, U64, C.POINTER(List), C.POINTER(List)]),
@@ -412,6 +413,13 @@ class Ctx:
     def filter_scan_range(self, col: Col, start: int, end: int, op: str, v: int) -> List:
         l = List()
         self._chk(self.lib.qe_filter_scan_range(self.h, col, start, end, op.encode(), v, C.byref(l)))
+        return l
+
+    def filter_scan2_range(self, col1: Col, op1: str, v1: int, col2: Col, op2: str, v2: int, start: int,
+                           end: int) -> List:
+        l = List()
+        self._chk(self.lib.qe_filter_scan2_range(self.h, col1, op1.encode(), v1, col2, op2.encode(), v2, start, end,
+                                                 C.byref(l)))
         return l
 
     def iota(self, start: int, n: int) -> List:

@@ -33,6 +33,7 @@ FIELDS = [
     ("allreduce", C.CFUNCTYPE(I, VP, P(U64), I)),
     ("release", C.CFUNCTYPE(None, VP, H)),
     ("fallback", C.CFUNCTYPE(I, VP, VP, VP)),
+    ("scan2", C.CFUNCTYPE(I, VP, U32, U32, C.c_char, U64, U32, C.c_char, U64, U64, U64, P(H))),
 ]
 
 
@@ -65,7 +66,7 @@ def join_local(ka, kb):
 class NumpyPlanEngine:
     """one rank: relations replicated as numpy columns; handles index a dict of arrays"""
 
-    def __init__(self, rels, rank=0, world=1, group=None):
+    def __init__(self, rels, rank=0, world=1, group=None, fused_scan=True):
         self.rels, self.rank, self.world, self.group = rels, rank, world, group
         self.h, self.next, self.borrowed = {}, 1, set()
         self.exchanges = 0
@@ -80,8 +81,8 @@ class NumpyPlanEngine:
         e = Engine()
         e.u, e.rank, e.world = None, rank, world
         for name, ftype in FIELDS:
-            if name == "fallback":
-                setattr(e, name, ftype())            # NULL: refused queries return QE_ENOTSUP
+            if name == "fallback" or (name == "scan2" and not fused_scan):
+                setattr(e, name, ftype())            # NULL: refused queries return QE_ENOTSUP; no fused scan
                 continue
             fn = self._wrap(getattr(self, "cb_" + name), name == "release")
             cb = ftype(fn)
@@ -143,6 +144,12 @@ class NumpyPlanEngine:
     def cb_scan(self, u, rel, col, s, t, op, v, out):
         c = self.rels[rel][col][s:t]
         out[0] = self.put((np.nonzero(_OPS[op.decode()](c, np.uint64(v)))[0] + s).astype(np.uint32))
+
+    def cb_scan2(self, u, rel, c1, op1, v1, c2, op2, v2, s, t, out):
+        a = self.rels[rel][c1][s:t]
+        b = self.rels[rel][c2][s:t]
+        m = _OPS[op1.decode()](a, np.uint64(v1)) & _OPS[op2.decode()](b, np.uint64(v2))
+        out[0] = self.put((np.nonzero(m)[0] + s).astype(np.uint32))
 
     def cb_iota(self, u, s, n, out):
         out[0] = self.put(np.arange(s, s + n, dtype=np.uint32))

@@ -76,6 +76,24 @@ def test_filter_scan(ctx, n, op):
     ctx.list_free(l)
 
 
+@pytest.mark.parametrize("same", [True, False], ids=["one_column", "two_columns"])
+@pytest.mark.parametrize("n,start", [(1, 0), (5, 2), (24_577, 0), (3_000_001, 1_234_567)])
+def test_filter_scan2_is_scan_then_refine(ctx, n, start, same):
+    """the plan's fused scan + refine of one binding: rowids r in [start, n) with both predicates,
+    ascending -- what a scan and a refine of its list give"""
+    rng = np.random.default_rng(n + start)
+    a = rng.integers(0, 1 << 32, n, dtype=np.uint64)
+    b = a if same else rng.integers(0, 1000, n, dtype=np.uint64)
+    ca = _col(ctx, a)
+    cb = ca if same else _col(ctx, b)
+    for (o1, v1), (o2, v2) in (((">", 1 << 30), ("<", 3 << 30)), (("=", int(a[-1])), (">", 0)), (("<", 5), ("=", 7))):
+        l = ctx.filter_scan2_range(ca, o1, v1, cb, o2, v2, start, n)
+        r = np.arange(start, n)
+        want = r[OPS[o1](a[start:], np.uint64(v1)) & OPS[o2](b[start:], np.uint64(v2))].astype(np.uint32)
+        np.testing.assert_array_equal(ctx.list_to_host(l), want)
+        ctx.list_free(l)
+
+
 @pytest.mark.parametrize("n", [1, 5, 8191, 500_000])
 def test_filter_refine_keeps_order(ctx, n):
     rng = np.random.default_rng(n)

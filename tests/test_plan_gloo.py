@@ -31,11 +31,13 @@ def _run_world(rels, queries, world, limits=None):
     return res
 
 
+@pytest.mark.parametrize("fused_scan", [True, False], ids=["scan2", "scan_refine"])
 @pytest.mark.parametrize("fixture", [f.split("/")[-1][:-5] for f in goldens.golden_files()])
-def test_every_golden_is_refused_or_exact(fixture):
+def test_every_golden_is_refused_or_exact(fixture, fused_scan):
+    """with the engine's fused scan + refine (scan2) and without it (a scan, then a refine)"""
     doc = goldens.load(f"{goldens.GOLDEN_DIR}/{fixture}.json")
     rels, _ = goldens.dataset(doc["dataset"])
-    eng = pe.NumpyPlanEngine(rels, 0, 1)
+    eng = pe.NumpyPlanEngine(rels, 0, 1, fused_scan=fused_scan)
     accepted = {"T": 0, "W": 0}
     for c in doc["cases"]:
         out, rc, _, _ = eng.run(c["input"])

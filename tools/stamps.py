@@ -23,6 +23,7 @@ PHASES = {
     "sort": ["ticket+zero", "load+rank", "totals+publish+scan", "stage+lookback(t0)", "lookback wait", "write"],
     "cp": ["ticket", "load+ballots", "scan+lookback", "stage", "write"],
     "ag": ["load+keys", "walks", "sums"],
+    "cpp": ["ballots (data wait)", "scan+publish", "stage+prefetch+lookback", "write"],
 }
 
 
@@ -30,7 +31,7 @@ def report(ctx, which, ntiles):
     buf = np.zeros(ntiles * SLOTS, dtype=np.uint64)
     fn = ctx.lib.qe_diag_stamps
     fn.argtypes = [C.c_char_p, C.c_void_p, C.c_uint64]
-    rc = fn(which.encode(), buf.ctypes.data, buf.size)
+    rc = fn(("cp" if which == "cpp" else which).encode(), buf.ctypes.data, buf.size)
     assert rc == 0, rc
     st = buf.reshape(ntiles, SLOTS).astype(np.int64)
     names = PHASES[which]
@@ -81,7 +82,7 @@ def main():
     if "cp" in a.what:
         l1 = ctx.filter_scan(ctx.column(r0, 2), ">", 1_000_000_000)
         ctx.sync()
-        report(ctx, "cp", (n + a.cp_tile - 1) // a.cp_tile)
+        report(ctx, "cpp" if os.environ.get("QE_CP_PIPE", "1") != "0" else "cp", (n + a.cp_tile - 1) // a.cp_tile)
         ctx.list_free(l1)
     if "sort" not in a.what and "mj" not in a.what:
         ctx.close()
