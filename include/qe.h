@@ -293,6 +293,9 @@ int  qe_mem_trim(qe_ctx*);
 
 /* ---- profiling ----------------------------------------------------------------------------- */
 int qe_set_profiling(qe_ctx*, int on);
+/* time only the launches of one stage (NULL or "": all): two HIP events per launch cost host
+ * time, so the bench's timed region measures its roofline kernel alone (bench.py) */
+int qe_set_profiling_only(qe_ctx*, const char* stage);
 int qe_reset_stats(qe_ctx*);
 /* fills up to `max` entries, returns the number of kernels with statistics */
 int qe_kernel_stats(qe_ctx*, qe_kstat* out, int max);

@@ -582,7 +582,7 @@ int qe_bucket_select(qe_ctx* c, qe_col col, uint32_t nparts, uint32_t part, cons
         if (attempt == 1) throw Error(QE_EINVAL, "internal: bucket larger than its column");
         cap = n;
     }
-    if (c->prof && !c->pending.empty()) c->pending.back().bytes += 12.0 * out->n;
+    add_bytes(c, "bucket_select", 12.0 * out->n);
     out->owns = 3;
     out->flags = QE_PAIRS_DISTINCT;
     if (d_heavy) dfree(c, d_heavy);

@@ -133,6 +133,7 @@ struct qe_ctx {
 
     // profiling
     bool prof = false;
+    std::string prof_only;           // non-empty: only this stage is timed (qe_set_profiling_only)
     std::vector<qe::PendingEvent> pending;
     std::vector<hipEvent_t> event_pool;
     std::vector<qe::KStat> kstats;
@@ -155,6 +156,8 @@ struct LBSlot {
 LBSlot lb_acquire(qe_ctx* c, size_t words);
 
 // profiling-aware launch bracket
+void add_bytes(qe_ctx* c, const char* stage, double bytes);
+
 struct Timed {
     qe_ctx* c;
     int k = -1;

@@ -1177,7 +1177,7 @@ void emit_deferred(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const uint64
         }
         bytes += 12.0 * tot[k];
     }
-    if (c->prof && !c->pending.empty()) c->pending.back().bytes += bytes;
+    add_bytes(c, "mj_heavy", bytes);
     uint32_t* d_ck = dalloc_t<uint32_t>(c, ck.size());
     uint64_t* d_cs = dalloc_t<uint64_t>(c, cs.size());
     QE_HIP(hipMemcpyAsync(d_ck, ck.data(), ck.size() * 4, hipMemcpyHostToDevice, c->stream));
@@ -1254,7 +1254,7 @@ void merge_sorted(qe_ctx* c, qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_l
     *oflags = (uint32_t)h[0];
     const uint32_t nheavy = (uint32_t)h[3];
     const bool exact = P <= cap && !(h[0] & MJF_OVF);
-    if (c->prof && !c->pending.empty() && exact) c->pending.back().bytes += 8.0 * P;
+    if (exact) add_bytes(c, "mj_fused", 8.0 * P);
     if (!exact || nheavy) {   // exact u64 offsets (and total) from the per-tile counts
         hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, c->stream, tc, (uint64_t)nt, c->d_scratch + 18);
         QE_HIP(hipGetLastError());

@@ -123,8 +123,16 @@ static void drain_events(qe_ctx* c) {
     c->pending.clear();
 }
 
+// bytes known only after a launch (its output size) go to that launch's pending record -- only
+// if the last one recorded IS that stage (a stage filter may have skipped it)
+void add_bytes(qe_ctx* c, const char* stage, double bytes) {
+    if (!c->prof || c->pending.empty()) return;
+    PendingEvent& p = c->pending.back();
+    if (p.kernel >= 0 && (size_t)p.kernel < c->kstats.size() && c->kstats[p.kernel].name == stage) p.bytes += bytes;
+}
+
 Timed::Timed(qe_ctx* c_, const char* name, double alg_bytes) : c(c_), bytes(alg_bytes) {
-    if (!c->prof) return;
+    if (!c->prof || (!c->prof_only.empty() && c->prof_only != name)) return;
     auto it = c->kindex.find(name);
     if (it == c->kindex.end()) {
         k = (int)c->kstats.size();
@@ -830,6 +838,19 @@ int qe_set_profiling(qe_ctx* c, int on) {
     for (qe_ctx* w : c->workers) {
         drain_events(w);
         w->prof = c->prof;
+    }
+    return 0;
+    QE_API_END(c)
+}
+
+
+int qe_set_profiling_only(qe_ctx* c, const char* stage) {
+    QE_API_BEGIN(c)
+    drain_events(c);
+    c->prof_only = stage ? stage : "";
+    for (qe_ctx* w : c->workers) {
+        drain_events(w);
+        w->prof_only = c->prof_only;
     }
     return 0;
     QE_API_END(c)

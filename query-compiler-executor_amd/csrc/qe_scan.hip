@@ -427,7 +427,7 @@ static uint64_t run_compact(qe_ctx* c, const char* name, double bytes, const Op&
         QE_HIP(hipGetLastError());
     }
     uint64_t m = read_u64(c, d_total);
-    if (c->prof && !c->pending.empty()) c->pending.back().bytes += 4.0 * NOUT * m;
+    add_bytes(c, name, 4.0 * NOUT * m);
     return m;
 }
 

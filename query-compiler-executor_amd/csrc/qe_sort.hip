@@ -1925,7 +1925,7 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
             return false;
         }
         if (P <= cap) {
-            if (c->prof && !c->pending.empty()) c->pending.back().bytes += 8.0 * (double)P;
+            add_bytes(c, "bucket_join", 8.0 * (double)P);
             if (P > c->mat_limit) {   // the reference's DArray cannot hold it either (src/DArray.h:14-15)
                 dfree(c, oR);
                 dfree(c, oS);

@@ -120,6 +120,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "qe_load_stats": (I, [P, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
         "qe_mem_trim": (I, [P]),
         "qe_set_profiling": (I, [P, I]),
+        "qe_set_profiling_only": (I, [P, C.c_char_p]),
         "qe_reset_stats": (I, [P]),
         "qe_kernel_stats": (I, [P, C.POINTER(KStat), I]),
         "qe_comm_unique_id": (I, [C.c_char_p]),
@@ -473,6 +474,9 @@ class Ctx:
     # ---- profiling ----
     def set_profiling(self, on: bool):
         self._chk(self.lib.qe_set_profiling(self.h, 1 if on else 0))
+
+    def set_profiling_only(self, stage: str | None):
+        self._chk(self.lib.qe_set_profiling_only(self.h, stage.encode() if stage else None))
 
     def reset_stats(self):
         self._chk(self.lib.qe_reset_stats(self.h))
