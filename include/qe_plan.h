@@ -76,6 +76,11 @@ typedef struct qe_engine {
      * scan and a refine gathering through its list */
     int (*scan2)(void* u, uint32_t rel, uint32_t col1, char op1, uint64_t v1, uint32_t col2, char op2, uint64_t v2,
                  uint64_t start, uint64_t end, qe_h* out);
+    /* join, with side b's carried rowid columns cb[0..nb) delivered beside the pairs (nullable):
+     * outb[k][i] = cb[k][ib] for pair i's b row.  The engine may carry them through its sort
+     * and join instead of taking them through the pairs afterwards.  Inputs are borrowed. */
+    int (*join_carry)(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h* cb, qe_h* oa, qe_h* ob,
+                      qe_h* outb);
 } qe_engine;
 
 /* Replay the reference's variant choice and list bookkeeping for every query of `text` on the

@@ -359,6 +359,48 @@ int e_join(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, qe_h* oa, qe_h* ob) {
     });
 }
 
+// the join with b's carried columns: up to two ride through b's sort and the bucket join (S =
+// b); otherwise (or on a bucket beyond LDS) the join runs on b's positions and every column,
+// b's vals included, is taken through them
+int e_join_carry(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h* cb, qe_h* oa, qe_h* ob, qe_h* outb) {
+    Eng* e = E(u);
+    return guard(e, [&] {
+        qe_ctx* c = e->c;
+        qe_pairs P = side_pairs(A(ka), va ? A(va) : nullptr);
+        qe_pairs Q = side_pairs(A(kb), vb ? A(vb) : nullptr);
+        qe_list la{}, lb{}, lx0{}, lx1{};
+        if (nb >= 1 && nb <= 2 &&
+            join_pairs_carry(c, &P, &Q, static_cast<const uint32_t*>(A(cb[0])->d),
+                             nb == 2 ? static_cast<const uint32_t*>(A(cb[1])->d) : nullptr, &la, &lb, &lx0, &lx1)) {
+            qe_pairs_free(c, &P);
+            qe_pairs_free(c, &Q);
+            *oa = H(new_arr(c, la.d, la.n, false));
+            *ob = H(new_arr(c, lb.d, lb.n, false));
+            outb[0] = H(new_arr(c, lx0.d, lx0.n, false));
+            if (nb == 2) outb[1] = H(new_arr(c, lx1.d, lx1.n, false));
+            return;
+        }
+        qe_pairs Qp = side_pairs(A(kb), nullptr);   // b's positions
+        const int rc = qe_join_pairs(c, &P, &Qp, &la, &lb);
+        qe_pairs_free(c, &P);
+        qe_pairs_free(c, &Qp);
+        ck(rc, c);
+        *oa = H(new_arr(c, la.d, la.n, false));
+        auto take = [&](const DArr* src) {
+            qe_list o{};
+            ck(qe_take_u32(c, static_cast<const uint32_t*>(src->d), &lb, &o), c);
+            return H(new_arr(c, o.d, o.n, false));
+        };
+        for (int k = 0; k < nb; k++) outb[k] = take(A(cb[k]));
+        if (vb) {
+            *ob = take(A(vb));
+            dfree(c, lb.d);
+        } else {
+            *ob = H(new_arr(c, lb.d, lb.n, false));
+        }
+    });
+}
+
 int e_take(void* u, qe_h src, qe_h idx, qe_h* out) {
     Eng* e = E(u);
     return guard(e, [&] {
@@ -569,6 +611,7 @@ int qe_run_queries_dist(qe_ctx* c, qe_comm* m, const char* text, char** out, siz
     g.exchange_finish = e_exchange_finish;
     g.join = e_join;
     g.take = e_take;
+    g.join_carry = e_join_carry;
     g.length = e_length;
     g.checksums = e_checksums;
     g.allreduce = e_allreduce;

@@ -65,6 +65,7 @@ struct DeferredSort {
     uint64_t* words = nullptr;    // bucket-partitioned (field << 32 | rowid) words
     uint32_t* bstart = nullptr;   // bucket starts (+ end)
     uint64_t* d_max = nullptr;    // largest bucket (device word: > TL_CAP = skew, not yet checked)
+    uint64_t* x = nullptr;        // carried payloads, in the words' order (qe_join_carry), or null
     uint64_t* kout = nullptr;
     uint32_t* vout = nullptr;
     int lo = 0, L = 0;            // field = (key >> lo) & fmask; bucket = field >> L
@@ -134,6 +135,9 @@ struct qe_ctx {
     // profiling
     bool prof = false;
     std::string prof_only;           // non-empty: only this stage is timed (qe_set_profiling_only)
+    // a payload for the next deferred lookback-free two-level sort to carry (join_pairs_carry)
+    const uint32_t* carry_xa = nullptr;
+    const uint32_t* carry_xb = nullptr;
     std::vector<qe::PendingEvent> pending;
     std::vector<hipEvent_t> event_pool;
     std::vector<qe::KStat> kstats;
@@ -213,7 +217,16 @@ void pairs_drop_deferred(qe_ctx* c, const qe_pairs* p);   // (also drops a gathe
 // histogram is built in the same pass (false: not that sort -- the caller gathers plainly)
 bool gather_with_hist(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint64_t n, uint64_t kor, uint64_t kand,
                       uint64_t* keys);
-bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS);
+bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS,
+                 qe_list* outX0 = nullptr, qe_list* outX1 = nullptr);
+// the payload carry of join_pairs_carry applies: both sides' sorts will be deferred two-level
+// ones with one bucket geometry, S's in the lookback-free form
+bool carry_eligible(const qe_pairs* R, const qe_pairs* S);
+// qe_join_pairs with S carrying one or two u32 payload columns (xa, xb nullable) through its sort
+// and the bucket join: outX0 / outX1 aligned with the pairs.  False: nothing was produced and the
+// inputs are as they were (ineligible, or a bucket beyond LDS) -- the caller joins without it.
+bool join_pairs_carry(qe_ctx* c, qe_pairs* R, qe_pairs* S, const uint32_t* xa, const uint32_t* xb, qe_list* outR,
+                      qe_list* outS, qe_list* outX0, qe_list* outX1);
 SortOut radix_sort_u32(qe_ctx* c, const uint32_t* keys, const uint32_t* vals, uint64_t n,
                        const uint64_t* bits = nullptr);
 // multi-GPU (qe_dist.hip): hash-partition rows into per-destination segments of out_keys /

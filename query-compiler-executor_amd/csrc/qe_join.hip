@@ -1607,6 +1607,31 @@ int qe_join_pairs(qe_ctx* c, qe_pairs* R, qe_pairs* S, qe_list* outR, qe_list* o
     QE_API_END(c)
 }
 
+}  // extern "C"
+
+namespace qe {
+bool join_pairs_carry(qe_ctx* c, qe_pairs* R, qe_pairs* S, const uint32_t* xa, const uint32_t* xb, qe_list* outR,
+                      qe_list* outS, qe_list* outX0, qe_list* outX1) {
+    if (!xa || !carry_eligible(R, S)) return false;
+    const qe_pairs R0 = *R, S0 = *S;   // views of the caller's arrays (nothing owned)
+    if ((R0.owns | S0.owns) & 7) return false;
+    sort_pairs(c, R, true);
+    c->carry_xa = xa;
+    c->carry_xb = xb;
+    sort_pairs(c, S, true);
+    c->carry_xa = c->carry_xb = nullptr;   // (consumed by S's sort; cleared in any case)
+    if (bucket_join(c, R, S, outR, outS, outX0, xb ? outX1 : nullptr)) return true;
+    // a bucket beyond LDS: drop both deferred sorts, give the caller its inputs back
+    qe_pairs_free(c, R);
+    qe_pairs_free(c, S);
+    *R = R0;
+    *S = S0;
+    return false;
+}
+}  // namespace qe
+
+extern "C" {
+
 int qe_sort_pairs(qe_ctx* c, qe_pairs* p) {
     QE_API_BEGIN(c)
     if (p->flags & PF_SORTED) return 0;

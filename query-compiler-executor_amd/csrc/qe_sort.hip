@@ -160,13 +160,21 @@ __device__ uint64_t g_sort_stamps[STAMP_TILES * STAMP_SLOTS];
 // PRE = true: the tile's global digit offsets were computed before the launch (the two-level
 // sort's first pass, whose per-tile counts come out of the histogram read it does anyway,
 // tl_hist_tiles_kernel) -- `offs` is a table of BINS offsets per tile; no ticket, no lookback.
-template <typename K, int IN, int OUT, bool PACK, int RBITS, int ITEMS, int NT, bool PRE = false>
+// CARRY (PRE, OUT_WORD only): a 64-bit payload per element rides along -- xa[i] | xb[i] << 32 in
+// input order (xb nullable), written to xout at the element's output position.  The words are
+// written first; the same LDS stage then takes the payloads in the words' slots, so they leave
+// in the same runs (the partitioned plan's carried bindings, qe_join_carry).
+template <typename K, int IN, int OUT, bool PACK, int RBITS, int ITEMS, int NT, bool PRE = false, bool CARRY = false>
 __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ kin, const uint64_t* __restrict__ win,
                                                         const uint32_t* __restrict__ vin, K* __restrict__ kout,
                                                         uint64_t* __restrict__ wout, uint32_t* __restrict__ vout,
                                                         uint64_t n, int dsh, uint32_t mask, Field f,
                                                         const uint32_t* __restrict__ offs, uint64_t* status,
-                                                        uint32_t* ticket, uint32_t epoch) {
+                                                        uint32_t* ticket, uint32_t epoch,
+                                                        const uint32_t* __restrict__ xa = nullptr,
+                                                        const uint32_t* __restrict__ xb = nullptr,
+                                                        uint64_t* __restrict__ xout = nullptr) {
+    static_assert(!CARRY || (PRE && OUT == OUT_WORD), "payload carry: the lookback-free first pass only");
     constexpr int BINS = 1 << RBITS, DPT = BINS >= NT ? BINS / NT : 1;   // digits per thread
     constexpr int NW = NT / 64;
     constexpr int TILE = NT * ITEMS, WT = 64 * ITEMS;
@@ -303,9 +311,11 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
     QE_STAMP(g_sort_stamps, tile, 5);
     const uint64_t tbase = (uint64_t)tile * TILE;
     const uint32_t tn = (uint32_t)((n - tbase) < (uint64_t)TILE ? (n - tbase) : (uint64_t)TILE);
+    uint32_t pk[CARRY ? ITEMS : 1];
 #pragma unroll
     for (int k = 0; k < ITEMS; k++) {
         uint32_t i = (uint32_t)k * NT + threadIdx.x;
+        if (CARRY) pk[k] = 0xFFFFFFFFu;
         if (i < tn) {
             uint64_t wd = stage[i];
 #ifdef QE_DIAG_SORT_LINEAR   // ablation only: contiguous output instead of the digit scatter
@@ -314,6 +324,7 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
             uint32_t p = gofs[(uint32_t)(wd >> dsh) & mask] + i;
 #endif
             if ((uint64_t)p >= n) continue;   // never taken with consistent offsets; keeps stores in bounds
+            if constexpr (CARRY) pk[k] = p;
             if (OUT == OUT_WORD) {
                 QE_ST(&wout[p], wd);
             } else if (PACK) {
@@ -322,6 +333,24 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
             } else {
                 kout[p] = (K)wd;
             }
+        }
+    }
+    if constexpr (CARRY) {
+        __syncthreads();   // every word is out of the stage
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t i = wave_base + (uint64_t)j * 64 + l;
+            if (i < n) {
+                const uint32_t dd = (uint32_t)(word[j] >> dsh) & mask;
+                const uint64_t x = (uint64_t)xa[i] | (xb ? (uint64_t)xb[i] << 32 : 0ull);
+                stage[bexcl[dd] + whist[w][dd] + pos[j]] = x;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < ITEMS; k++) {
+            const uint32_t i = (uint32_t)k * NT + threadIdx.x;
+            if (i < tn && pk[k] != 0xFFFFFFFFu) QE_ST(&xout[pk[k]], stage[i]);
         }
     }
     QE_STAMP(g_sort_stamps, tile, 6);
@@ -854,10 +883,14 @@ __global__ void __launch_bounds__(256) cs_apply_kernel(CSJobs js) {
 #endif
 constexpr int TL2_NT = QE_TL2_NT, TL2_ITEMS = QE_TL2_ITEMS, TL2_TILE = TL2_NT * TL2_ITEMS;   // 9216: mean 8192 + 11 sd
 
-template <typename K>
+// CARRY: the 64-bit payloads of pass 1 (xin, in pass-1 order) follow the words to xout, staged
+// in the words' LDS slots after the words have left (as in radix_pass_kernel).
+template <typename K, bool CARRY = false>
 __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const uint64_t* __restrict__ win, uint64_t* __restrict__ wout,
                                                          uint64_t n, int dsh, const uint32_t* __restrict__ off1,
-                                                         const uint32_t* __restrict__ off2, uint32_t G) {
+                                                         const uint32_t* __restrict__ off2, uint32_t G,
+                                                         const uint64_t* __restrict__ xin = nullptr,
+                                                         uint64_t* __restrict__ xout = nullptr) {
     constexpr int BINS = 128, NW = TL2_NT / 64, WT = 64 * TL2_ITEMS;
     __shared__ uint64_t stage[TL2_TILE];
     __shared__ uint32_t whist[NW][BINS];
@@ -934,13 +967,43 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
             }
         }
         __syncthreads();
+        if constexpr (CARRY) {
+            // the payloads: each slot's destination is read back from its word before the slot
+            // is reused (one u32 per slot in the LDS word itself: high half = destination)
+#pragma unroll 6
+            for (int k = 0; k < TL2_ITEMS; k++) {
+                const uint32_t i = (uint32_t)k * TL2_NT + threadIdx.x;
+                if (i < m) {
+                    const uint64_t wd = stage[i];
+                    const uint32_t p = gofs[(uint32_t)(wd >> dsh) & (BINS - 1)] + i;
+                    if ((uint64_t)p < n) QE_ST(&wout[p], wd);
+                    reinterpret_cast<uint32_t*>(stage)[2 * i] = p;   // slot i now holds its destination
+                }
+            }
+            __syncthreads();
+            uint32_t dst[TL2_ITEMS];
+#pragma unroll
+            for (int j = 0; j < TL2_ITEMS; j++) {   // each element's slot -> its destination
+                dst[j] = 0xFFFFFFFFu;
+                if (j * 64 < lim) {
+                    const uint32_t dd = (uint32_t)(word[j] >> dsh) & (BINS - 1);
+                    const uint32_t r = (pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                    dst[j] = reinterpret_cast<const uint32_t*>(stage)[2 * (bexcl[dd] + whist[w][dd] + r)];
+                }
+            }
+            const uint64_t* xsrc = xin + base + (uint32_t)w * WT + l;
+#pragma unroll
+            for (int j = 0; j < TL2_ITEMS; j++)   // payload j goes straight to its destination
+                if (j * 64 < lim && (uint64_t)dst[j] < n) QE_ST(&xout[dst[j]], xsrc[j * 64]);
+        } else {
 #pragma unroll 6   // (fully unrolled, every LDS read is hoisted and the kernel spills)
-        for (int k = 0; k < TL2_ITEMS; k++) {
-            const uint32_t i = (uint32_t)k * TL2_NT + threadIdx.x;
-            if (i < m) {
-                const uint64_t wd = stage[i];
-                const uint32_t p = gofs[(uint32_t)(wd >> dsh) & (BINS - 1)] + i;
-                if ((uint64_t)p < n) QE_ST(&wout[p], wd);   // never false with consistent offsets
+            for (int k = 0; k < TL2_ITEMS; k++) {
+                const uint32_t i = (uint32_t)k * TL2_NT + threadIdx.x;
+                if (i < m) {
+                    const uint64_t wd = stage[i];
+                    const uint32_t p = gofs[(uint32_t)(wd >> dsh) & (BINS - 1)] + i;
+                    if ((uint64_t)p < n) QE_ST(&wout[p], wd);   // never false with consistent offsets
+                }
             }
         }
         __syncthreads();   // stage / whist / gofs are rewritten by the next sub-tile
@@ -966,11 +1029,16 @@ static_assert(HJ_I * HJ_NW <= 128, "the (row-group, wave) table is scanned by on
 
 __device__ __forceinline__ uint32_t fld(uint64_t w) { return (uint32_t)(w >> 32); }   // the key field
 
-template <int DBITS>
-__global__ void __launch_bounds__(HJ_NT) tl_hjoin_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict__ bsR,
+// CARRY: S's rows carry a 64-bit payload (xS, in S's word order): its low half goes to outX0 and
+// its high half to outX1 (nullable) beside every pair
+template <int DBITS, bool CARRY = false>
+__global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8))) tl_hjoin_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict__ bsR,
                                                          const uint64_t* __restrict__ wS, const uint32_t* __restrict__ bsS,
                                                          int L, uint32_t* __restrict__ outR, uint32_t* __restrict__ outS,
-                                                         uint64_t cap, uint64_t* total_out) {
+                                                         uint64_t cap, uint64_t* total_out,
+                                                         const uint64_t* __restrict__ xS = nullptr,
+                                                         uint32_t* __restrict__ outX0 = nullptr,
+                                                         uint32_t* __restrict__ outX1 = nullptr) {
     __shared__ uint32_t bnd[1 << DBITS];   // per key value: count, then run start, then run end
     __shared__ uint32_t rr[TL_CAP];        // R rowids grouped by key value
     __shared__ uint32_t tab[HJ_I * HJ_NW];
@@ -1054,6 +1122,14 @@ __global__ void __launch_bounds__(HJ_NT) tl_hjoin_kernel(const uint64_t* __restr
     __syncthreads();
     const uint64_t gofs = s_excl;
     if (gofs + s_total > cap) return;   // outgrew the buffers: the host re-runs with the exact size
+    uint64_t xv[CARRY ? HJ_I : 1];      // S's payloads: every load in flight before the first pair
+    if constexpr (CARRY) {
+#pragma unroll
+        for (int j = 0; j < HJ_I; j++) {
+            const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
+            xv[j] = i < mS ? xS[s0 + i] : 0ull;
+        }
+    }
 #pragma unroll
     for (int j = 0; j < HJ_I; j++) {
         if ((uint32_t)j * HJ_NT + threadIdx.x >= mS) continue;
@@ -1063,6 +1139,18 @@ __global__ void __launch_bounds__(HJ_NT) tl_hjoin_kernel(const uint64_t* __restr
         const uint32_t srow = (uint32_t)ws[j];
         uint32_t* __restrict__ pR = outR + o;
         uint32_t* __restrict__ pS = outS + o;
+        if constexpr (CARRY) {
+            const uint64_t x = xv[j];
+            uint32_t* __restrict__ p0 = outX0 + o;
+#pragma nounroll
+            for (uint32_t k = 0; k < cnt; k++) {
+                pR[k] = rr[st + k];
+                pS[k] = srow;
+                p0[k] = (uint32_t)x;
+                if (outX1) outX1[o + k] = (uint32_t)(x >> 32);
+            }
+            continue;
+        }
 #pragma nounroll
         for (uint32_t k = 0; k < cnt; k++) {   // fan-out ~1: a plain loop (unrolled, it was 118 VGPRs)
             pR[k] = rr[st + k];
@@ -1409,7 +1497,25 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     uint64_t* w2 = dalloc_t<uint64_t>(c, n);
     K* kout = dalloc_t<K>(c, n);
     uint32_t* vout = dalloc_t<uint32_t>(c, n);
-    {
+    // a payload to carry (join_pairs_carry asked for it on this deferred sort)
+    const uint32_t* cxa = dfr ? c->carry_xa : nullptr;
+    const uint32_t* cxb = dfr ? c->carry_xb : nullptr;
+    c->carry_xa = c->carry_xb = nullptr;
+    uint64_t* x1 = cxa ? dalloc_t<uint64_t>(c, n) : nullptr;
+    uint64_t* x2 = cxa ? dalloc_t<uint64_t>(c, n) : nullptr;
+    if (cxa) {
+        const double xb = cxb ? 8.0 : 4.0;
+        Timed t(c, "sort_pass_carry", ((double)sizeof(K) + (vals ? 4.0 : 0.0) + 8.0 + xb + 8.0) * n);
+        if (vals)
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, true>),
+                               dim3(nt), dim3(PRE_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, 255u,
+                               f, tcnt, nullptr, nullptr, 0u, cxa, cxb, x1);
+        else
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KIOTA, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, true>),
+                               dim3(nt), dim3(PRE_NT), 0, c->stream, keys, nullptr, nullptr, kout, w1, vout, n, 32 + L,
+                               255u, f, tcnt, nullptr, nullptr, 0u, cxa, cxb, x1);
+        QE_HIP(hipGetLastError());
+    } else {
         // algorithmic bytes: key (+ rowid when given; generated otherwise) in, packed word out
         Timed t(c, name, ((double)sizeof(K) + (vals ? 4.0 : 0.0) + 8.0) * n);
         if (vals)
@@ -1422,7 +1528,13 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
                                tcnt, nullptr, nullptr, 0u);
         QE_HIP(hipGetLastError());
     }
-    {
+    if (cxa) {
+        Timed t(c, "sort_pass_carry", 32.0 * n);
+        hipLaunchKernelGGL((tl_pass2_kernel<K, true>), dim3(nseg), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8,
+                           tcnt, gcnt, G, x1, x2);
+        QE_HIP(hipGetLastError());
+        dfree(c, x1);
+    } else {
         Timed t(c, prof_split() ? "sort_pass2" : name, 16.0 * n);
         hipLaunchKernelGGL((tl_pass2_kernel<K>), dim3(nseg), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8, tcnt,
                            gcnt, G);
@@ -1444,6 +1556,7 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
             d.words = w2;
             d.bstart = bstart;
             d.d_max = d_max;
+            d.x = x2;
             d.kout = (uint64_t*)kout;
             d.vout = vout;
             d.lo = f.lo;
@@ -1726,6 +1839,7 @@ static void drop(qe_ctx* c, const DeferredSort& d) {
     dfree(c, d.words);
     dfree(c, d.bstart);
     dfree(c, d.d_max);
+    dfree(c, d.x);
 }
 
 // A deferred sort with a bucket beyond LDS (skew) completes by plain LSD passes over the packed
@@ -1892,23 +2006,62 @@ bool gather_with_hist(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint
     return true;
 }
 
-bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS) {
+// the bucket geometry radix_sort_impl would give a deferred sort of p (its pass plan, from the
+// key bounds), or false when p's sort would not be a deferred two-level one (need_pre: the
+// lookback-free form, the only one that carries a payload)
+static bool deferred_geometry(const qe_pairs* p, bool need_pre, int* lo, int* nb, uint64_t* kconst) {
+    const uint64_t n = p->n;
+    if (!(p->flags & QE_PAIRS_BITS) || n < 2 || n >= 0xFFFFFFFFull || !two_level_on() || n <= (uint64_t)TL_CAP)
+        return false;
+    const uint64_t vary = p->kor & ~p->kand;
+    if (!vary) return false;
+    *lo = __builtin_ctzll(vary);
+    *nb = 64 - __builtin_clzll(vary) - *lo;
+    if (*nb > 32) return false;
+    if (*nb >= 12 && *nb <= 8 + 24 && n <= 700000) return false;   // the one-pass form
+    if (!(*nb >= 20 && *nb <= TL_H + 16 && n >= (1u << 20) && n <= 4000ull * TL_BUCKETS)) return false;
+    if (need_pre && !(sort_pre_on() && n >= sort_pre_min())) return false;
+    const uint64_t fmask = (1ull << *nb) - 1;
+    *kconst = p->kand & ~(fmask << *lo);
+    return true;
+}
+
+bool carry_eligible(const qe_pairs* R, const qe_pairs* S) {
+    int loR, nbR, loS, nbS;
+    uint64_t kcR, kcS;
+    if (!deferred_geometry(R, false, &loR, &nbR, &kcR) || !deferred_geometry(S, true, &loS, &nbS, &kcS)) return false;
+    return loR == loS && nbR == nbS && kcR == kcS && nbR - TL_H <= HJ_DBITS;
+}
+
+bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS, qe_list* outX0,
+                 qe_list* outX1) {
     auto iR = c->deferred.find(R->key), iS = c->deferred.find(S->key);
     if (iR == c->deferred.end() || iS == c->deferred.end() || R->key == S->key) return false;
     const DeferredSort& dR = iR->second;
     const DeferredSort& dS = iS->second;
     if (dR.lo != dS.lo || dR.L != dS.L || dR.fmask != dS.fmask || dR.kconst != dS.kconst || dR.L > HJ_DBITS)
         return false;   // different bucket geometry, or a bucket domain beyond LDS
+    const bool carry = outX0 != nullptr;
+    if (carry && !dS.x) return false;   // S's sort did not carry the payload
     const uint64_t nR = R->n, nS = S->n;
     uint64_t cap = nR + nS;   // optimistic (fan-out ~1); an outgrown launch re-runs with the exact size
     for (int attempt = 0; attempt < 2; attempt++) {
         uint32_t* oR = dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1));
         uint32_t* oS = dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1));
+        uint32_t* x0 = carry ? dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1)) : nullptr;
+        uint32_t* x1 = carry && outX1 ? dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1)) : nullptr;
         QE_HIP(hipMemsetAsync(c->d_scratch + 17, 0, 2 * sizeof(uint64_t), c->stream));   // [pairs, oversize]
         {
-            // algorithmic bytes: both sides' words in (+ 8 B per pair below)
-            Timed t(c, "bucket_join", 8.0 * (double)(nR + nS));
-            if (dR.L <= 12)
+            // algorithmic bytes: both sides' words in (+ 8 B per pair below; + S's payloads)
+            Timed t(c, "bucket_join", 8.0 * (double)(nR + nS) + (carry ? 8.0 * (double)nS : 0.0));
+            if (carry && dR.L <= 12)
+                hipLaunchKernelGGL((tl_hjoin_kernel<12, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream, dR.words,
+                                   dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17, dS.x, x0, x1);
+            else if (carry)
+                hipLaunchKernelGGL((tl_hjoin_kernel<HJ_DBITS, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream,
+                                   dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17, dS.x,
+                                   x0, x1);
+            else if (dR.L <= 12)
                 hipLaunchKernelGGL(tl_hjoin_kernel<12>, dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream, dR.words, dR.bstart,
                                    dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17);
             else
@@ -1922,6 +2075,8 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
         if (h[1]) {   // a bucket beyond LDS (skew): the sides complete their sorts, the merge joins them
             dfree(c, oR);
             dfree(c, oS);
+            dfree(c, x0);
+            dfree(c, x1);
             return false;
         }
         if (P <= cap) {
@@ -1929,6 +2084,8 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
             if (P > c->mat_limit) {   // the reference's DArray cannot hold it either (src/DArray.h:14-15)
                 dfree(c, oR);
                 dfree(c, oS);
+                dfree(c, x0);
+                dfree(c, x1);
                 char msg[160];
                 snprintf(msg, sizeof msg, "join of %llu pairs exceeds the materialisation limit %llu",
                          (unsigned long long)P, (unsigned long long)c->mat_limit);
@@ -1939,10 +2096,19 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
             outR->n = outS->n = P;
             outR->cap = outS->cap = cap;
             outR->flags = outS->flags = 0;
+            for (auto [ol, xd] : {std::pair<qe_list*, uint32_t*>{outX0, x0}, {outX1, x1}})
+                if (ol) {
+                    ol->d = xd;
+                    ol->n = P;
+                    ol->cap = cap;
+                    ol->flags = 0;
+                }
             return true;
         }
         dfree(c, oR);
         dfree(c, oS);
+        dfree(c, x0);
+        dfree(c, x1);
         cap = P;
     }
     throw Error(QE_EINVAL, "internal: bucket join outgrew its exact size");

@@ -566,7 +566,35 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need) {
     ECHK(side_finish(P, &sa));
     ECHK(side_finish(P, &sb));
     qe_h oa = NONE, ob = NONE;
-    const int jr = e->join(e->u, sa.keys, sa.vals, sb.keys, sb.vals, &oa, &ob);
+    /* a side carrying several bindings: its first rides as the join's vals, the others (up to two)
+     * ride through the engine's join beside the pairs (join_carry) instead of being taken after */
+    qe_h made[2][64];
+    for (int k = 0; k < 2; k++)
+        for (int i = 0; i < 64; i++) made[k][i] = NONE;
+    int cs = -1;
+    if (e->join_carry) {
+        if (sb.ncar >= 2 && sb.ncar <= 3 && sb.vals == NONE) cs = 1;
+        else if (sa.ncar >= 2 && sa.ncar <= 3 && sa.vals == NONE) cs = 0;
+    }
+    int jr;
+    if (cs >= 0) {
+        side_t* C = cs ? &sb : &sa;
+        side_t* O = cs ? &sa : &sb;
+        C->vals = C->car_rows[0];
+        C->car_rows[0] = NONE;                              /* now rides as vals */
+        qe_h oo = NONE, oc = NONE, ox[2] = {NONE, NONE};
+        jr = e->join_carry(e->u, O->keys, O->vals, C->keys, C->vals, C->ncar - 1, &C->car_rows[1], &oo, &oc, ox);
+        for (int i = 1; i < C->ncar && jr == 0; i++) made[cs][i] = ox[i - 1];
+        if (cs) {
+            oa = oo;
+            ob = oc;
+        } else {
+            oa = oc;
+            ob = oo;
+        }
+    } else {
+        jr = e->join(e->u, sa.keys, sa.vals, sb.keys, sb.vals, &oa, &ob);
+    }
     if (jr != 0 && jr != QE_ETOOBIG) {
         P->rc = jr;
         return jr;
@@ -579,6 +607,8 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need) {
         if (v[1]) {
             rel(P, oa);
             rel(P, ob);
+            for (int k = 0; k < 2; k++)
+                for (int i = 0; i < 64; i++) rel(P, made[k][i]);
             rel(P, sa.keys);
             rel(P, sb.keys);
             rel(P, sa.vals);
@@ -600,7 +630,10 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need) {
         side_t* s = sides[k];
         for (int i = 0; i < s->ncar; i++) {
             m[n].b = s->car_b[i];
-            if (s->car_rows[i] == NONE) {
+            if (made[k][i] != NONE) {                        /* delivered by join_carry */
+                m[n].rows = made[k][i];
+                rel(P, s->car_rows[i]);
+            } else if (s->car_rows[i] == NONE) {
                 m[n].rows = outs[k];
                 used[k] = 1;
             } else {

@@ -34,6 +34,7 @@ FIELDS = [
     ("release", C.CFUNCTYPE(None, VP, H)),
     ("fallback", C.CFUNCTYPE(I, VP, VP, VP)),
     ("scan2", C.CFUNCTYPE(I, VP, U32, U32, C.c_char, U64, U32, C.c_char, U64, U64, U64, P(H))),
+    ("join_carry", C.CFUNCTYPE(I, VP, H, H, H, H, I, P(H), P(H), P(H), P(H))),
 ]
 
 
@@ -66,7 +67,7 @@ def join_local(ka, kb):
 class NumpyPlanEngine:
     """one rank: relations replicated as numpy columns; handles index a dict of arrays"""
 
-    def __init__(self, rels, rank=0, world=1, group=None, fused_scan=True):
+    def __init__(self, rels, rank=0, world=1, group=None, fused_scan=True, join_carry=True):
         self.rels, self.rank, self.world, self.group = rels, rank, world, group
         self.h, self.next, self.borrowed = {}, 1, set()
         self.exchanges = 0
@@ -81,7 +82,7 @@ class NumpyPlanEngine:
         e = Engine()
         e.u, e.rank, e.world = None, rank, world
         for name, ftype in FIELDS:
-            if name == "fallback" or (name == "scan2" and not fused_scan):
+            if name == "fallback" or (name == "scan2" and not fused_scan) or (name == "join_carry" and not join_carry):
                 setattr(e, name, ftype())            # NULL: refused queries return QE_ENOTSUP; no fused scan
                 continue
             fn = self._wrap(getattr(self, "cb_" + name), name == "release")
@@ -207,6 +208,15 @@ class NumpyPlanEngine:
             return -5
         oa[0] = self.put(self.get(va)[ia] if va else ia)
         ob[0] = self.put(self.get(vb)[ib] if vb else ib)
+
+    def cb_join_carry(self, u, ka, va, kb, vb, nb, cb, oa, ob, outb):
+        ia, ib = join_local(self.get(ka), self.get(kb))
+        if len(ia) > self.mat_limit:
+            return -5
+        oa[0] = self.put(self.get(va)[ia] if va else ia)
+        ob[0] = self.put(self.get(vb)[ib] if vb else ib)
+        for k in range(nb):
+            outb[k] = self.put(self.get(cb[k])[ib])
 
     def cb_take(self, u, src, idx, out):
         out[0] = self.put(self.get(src)[self.get(idx)])

@@ -126,3 +126,67 @@ def test_dist_executor_c3_100m_one_rank(ctx, comm):
         assert ctx.last_result_rows() == rows
     finally:
         ctx.drop_relations()
+
+
+def _carry_launches(ctx, q, comm):
+    ctx.set_profiling(True)
+    ctx.reset_stats()
+    out, rc, refused = ctx.run_dist(q, comm)
+    n = ctx.kernel_stats().get("sort_pass_carry", {}).get("launches", 0)
+    ctx.set_profiling(False)
+    return out, rc, refused, n
+
+
+@pytest.mark.slow
+def test_dist_executor_carries_bindings_through_the_join(ctx, comm):
+    """joins whose derived side carries two and three bindings (C3's chain) at 75 M rows, where that
+    side (> 2^25 rows after the filter) is sorted by the lookback-free two-level sort: its extra
+    bindings ride through the sort and the bucket join (sort_pass_carry launches), and the printed
+    bytes equal the faithful executor's"""
+    N = 75_000_001
+    ctx.drop_relations()
+    _loaded["key"] = None
+    try:
+        kinds = [("mod", N), ("mod", N), ("hi32",)]
+        for r in range(4):
+            ctx.gen_relation(N, kinds, seed=3, gen_rel=r)
+        qs = ("0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>1000000000&3.2<3000000000|1.2 2.2 3.2\n",
+              "0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>2000000000|3.0 1.2 2.1\n",
+              "3 2 1 0|0.0=1.1&1.0=2.1&2.0=3.1&0.2<3000000000|0.2 1.2 2.2\n",
+              "0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>1000000000|0.2 1.2 2.2 3.2\n")
+        planned = 0
+        for q in qs:
+            want, _ = ctx.run(q)
+            out, rc, refused, carried = _carry_launches(ctx, q, comm)
+            assert (out, rc) == (want, 0), q
+            if refused == 0:                  # planned (the last one's binding 0 list is not relational)
+                planned += 1
+                assert carried > 0, q
+        assert planned >= 2
+    finally:
+        ctx.drop_relations()
+
+
+@pytest.mark.slow
+def test_dist_executor_carry_falls_back_on_a_skewed_bucket(ctx, comm):
+    """a derived side whose key has one heavy value (a bucket beyond LDS): the carry join gives the
+    inputs back and the join runs on positions with takes -- same bytes as the faithful executor"""
+    N = 50_000_003
+    rng = np.random.default_rng(11)
+    ctx.drop_relations()
+    _loaded["key"] = None
+    try:
+        rels = []
+        for r in range(4):
+            c0 = rng.integers(0, N, N, dtype=np.uint64)
+            if r == 1:
+                c0[rng.random(N) < 0.05] = 12345           # ~1.7 M rows share one key
+            rels.append([c0, rng.integers(0, N, N, dtype=np.uint64), rng.integers(0, 1 << 32, N, dtype=np.uint64)])
+        for cols in rels:
+            ctx.load_relation(cols)
+        q = "0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>1000000000|1.2 2.2 3.2\n"
+        want, _ = ctx.run(q)
+        out, rc, refused, _ = _carry_launches(ctx, q, comm)
+        assert (out, rc, refused) == (want, 0, 0)
+    finally:
+        ctx.drop_relations()

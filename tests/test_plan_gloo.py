@@ -31,13 +31,15 @@ def _run_world(rels, queries, world, limits=None):
     return res
 
 
-@pytest.mark.parametrize("fused_scan", [True, False], ids=["scan2", "scan_refine"])
+@pytest.mark.parametrize("optional", ["all", "none"])
 @pytest.mark.parametrize("fixture", [f.split("/")[-1][:-5] for f in goldens.golden_files()])
-def test_every_golden_is_refused_or_exact(fixture, fused_scan):
-    """with the engine's fused scan + refine (scan2) and without it (a scan, then a refine)"""
+def test_every_golden_is_refused_or_exact(fixture, optional):
+    """with the engine's optional entries (scan2: a fused scan + refine; join_carry: a side's
+    extra bindings delivered by the join) and without them (a scan then a refine; takes)"""
     doc = goldens.load(f"{goldens.GOLDEN_DIR}/{fixture}.json")
     rels, _ = goldens.dataset(doc["dataset"])
-    eng = pe.NumpyPlanEngine(rels, 0, 1, fused_scan=fused_scan)
+    on = optional == "all"
+    eng = pe.NumpyPlanEngine(rels, 0, 1, fused_scan=on, join_carry=on)
     accepted = {"T": 0, "W": 0}
     for c in doc["cases"]:
         out, rc, _, _ = eng.run(c["input"])
