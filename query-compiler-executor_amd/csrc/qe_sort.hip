@@ -1130,6 +1130,51 @@ __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
             xv[j] = i < mS ? xS[s0 + i] : 0ull;
         }
     }
+#ifndef QE_HJ_LANE_EMIT
+    // wave-cooperative emission: item j's pairs of this wave are one contiguous range; lane l
+    // writes pairs q0 + l, q0 + 64 + l, ... -- every store instruction covers 64 consecutive
+    // pairs (whole lines), where a per-lane loop over its own row's partners left partial lines
+    // (PMC: ~2 GB written per C3 bucket join against ~0.6 GB of pairs).  The pair's S row is the
+    // last lane whose exclusive prefix is <= q (found by a 6-step shuffle search).
+#pragma unroll
+    for (int j = 0; j < HJ_I; j++) {
+        const bool live = (uint32_t)j * HJ_NT + threadIdx.x < mS;
+        const uint32_t v = live ? fld(ws[j]) & dmask : 0u;
+        const uint32_t st = live ? (v ? bnd[v - 1] : 0u) : 0u;
+        const uint32_t cnt = live ? bnd[v] - st : 0u;
+        const uint32_t pj = pre[j];
+        const uint32_t tot = (uint32_t)__shfl((int)(pj + cnt), 63, 64);
+        const uint64_t ob = gofs + tab[j * HJ_NW + w];
+        const uint32_t srow = (uint32_t)ws[j];
+        for (uint32_t q0 = 0; q0 < tot; q0 += 64) {   // wave-uniform
+            const uint32_t q = q0 + (uint32_t)l;
+            int owner = 0;
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1) {
+                const int cand = owner + step;
+                const uint32_t pc = (uint32_t)__shfl((int)pj, cand < 64 ? cand : 63, 64);
+                if (cand < 64 && pc <= q) owner = cand;
+            }
+            const uint32_t k = q - (uint32_t)__shfl((int)pj, owner, 64);
+            const uint32_t so = (uint32_t)__shfl((int)st, owner, 64);
+            const uint32_t sr = (uint32_t)__shfl((int)srow, owner, 64);
+            uint32_t x0 = 0, x1 = 0;
+            if constexpr (CARRY) {
+                x0 = (uint32_t)__shfl((int)(uint32_t)xv[j], owner, 64);
+                x1 = (uint32_t)__shfl((int)(uint32_t)(xv[j] >> 32), owner, 64);
+            }
+            if (q < tot) {
+                outR[ob + q] = rr[so + k];
+                outS[ob + q] = sr;
+                if constexpr (CARRY) {
+                    outX0[ob + q] = x0;
+                    if (outX1) outX1[ob + q] = x1;
+                }
+            }
+        }
+    }
+    return;
+#endif
 #pragma unroll
     for (int j = 0; j < HJ_I; j++) {
         if ((uint32_t)j * HJ_NT + threadIdx.x >= mS) continue;
