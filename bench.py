@@ -195,7 +195,8 @@ def run_dist(args):
     faithful = None
     if rank == 0 and not args.no_faithful:
         faithful, _ = ctx.run(QUERY)              # in-run parity: the drop-in executor, same relations
-        if not multi:                             # N = 1: the faithful executor timed too, for the record
+    if rank == 0:
+        if faithful is not None and not multi:   # N = 1: the faithful executor timed too, for the record
             torch.cuda.synchronize()
             t1 = time.perf_counter()
             for _ in range(args.steps):

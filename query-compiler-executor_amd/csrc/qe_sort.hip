@@ -148,6 +148,21 @@ struct Field {
 __device__ uint64_t g_sort_stamps[STAMP_TILES * STAMP_SLOTS];
 #endif
 
+// XCD-contiguous work items for the lookback-free passes: a grid of 8 * per blocks, block b takes
+// item (b % 8) * per + b / 8, so the blocks that share an XCD (b % 8 equal under the observed
+// round-robin placement -- speed only) walk one contiguous range of tiles in dispatch order, and
+// the digit runs that neighbouring tiles write side by side mostly meet in the same L2, which
+// merges their shared boundary lines.  QE_XCD_TILES=0 (build knob) keeps item = b.
+#ifndef QE_XCD_TILES
+#define QE_XCD_TILES 1
+#endif
+__device__ __forceinline__ uint32_t xcd_item(uint32_t b) {
+    return QE_XCD_TILES ? (b & 7u) * (gridDim.x >> 3) + (b >> 3) : b;
+}
+static inline uint32_t xcd_grid(uint64_t items) {
+    return QE_XCD_TILES ? (uint32_t)(8 * ((items + 7) / 8)) : (uint32_t)items;
+}
+
 // One pass over a tile of NT x ITEMS words: rank in registers (RBITS ballots per element = wave
 // match-any, per-wave LDS counters), stage the tile in LDS in digit order, then write it as runs
 // of equal digits.  The tile's global digit offsets come from a per-digit decoupled lookback
@@ -189,7 +204,8 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
 #ifdef QE_DIAG_STAMPS
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-    const uint32_t tile = PRE ? blockIdx.x : take_ticket(ticket, &s_ticket);
+    const uint32_t tile = PRE ? xcd_item(blockIdx.x) : take_ticket(ticket, &s_ticket);
+    if (PRE && (uint64_t)tile * TILE >= n) return;   // the XCD grid's padding blocks (block-uniform)
 #ifdef QE_DIAG_STAMPS
     if (threadIdx.x == 0 && tile < STAMP_TILES) g_sort_stamps[(uint64_t)tile * STAMP_SLOTS] = t_start;
 #endif
@@ -897,7 +913,8 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
     __shared__ uint32_t bexcl[BINS];
     __shared__ uint32_t gofs[BINS];
     __shared__ uint32_t wsum[NW];
-    const uint32_t s = blockIdx.x, d1 = s / G, g = s % G;
+    const uint32_t s = xcd_item(blockIdx.x), d1 = s / G, g = s % G;
+    if (s >= 256u * G) return;   // the XCD grid's padding blocks (block-uniform)
     const uint32_t start = off1[(uint64_t)g * TL_TPG * 256 + d1];
     const uint32_t end = g + 1 < G ? off1[(uint64_t)(g + 1) * TL_TPG * 256 + d1]
                                    : (d1 < 255 ? off1[d1 + 1] : (uint32_t)n);   // tile 0's row = digit starts
@@ -1553,35 +1570,35 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
         Timed t(c, "sort_pass_carry", ((double)sizeof(K) + (vals ? 4.0 : 0.0) + 8.0 + xb + 8.0) * n);
         if (vals)
             hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, true>),
-                               dim3(nt), dim3(PRE_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, 255u,
+                               dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, 255u,
                                f, tcnt, nullptr, nullptr, 0u, cxa, cxb, x1);
         else
             hipLaunchKernelGGL((radix_pass_kernel<K, IN_KIOTA, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, true>),
-                               dim3(nt), dim3(PRE_NT), 0, c->stream, keys, nullptr, nullptr, kout, w1, vout, n, 32 + L,
+                               dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, nullptr, kout, w1, vout, n, 32 + L,
                                255u, f, tcnt, nullptr, nullptr, 0u, cxa, cxb, x1);
         QE_HIP(hipGetLastError());
     } else {
         // algorithmic bytes: key (+ rowid when given; generated otherwise) in, packed word out
         Timed t(c, name, ((double)sizeof(K) + (vals ? 4.0 : 0.0) + 8.0) * n);
         if (vals)
-            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true>), dim3(nt),
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true>), dim3(xcd_grid(nt)),
                                dim3(PRE_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, 255u, f, tcnt,
                                nullptr, nullptr, 0u);
         else
-            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KIOTA, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true>), dim3(nt),
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KIOTA, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true>), dim3(xcd_grid(nt)),
                                dim3(PRE_NT), 0, c->stream, keys, nullptr, nullptr, kout, w1, vout, n, 32 + L, 255u, f,
                                tcnt, nullptr, nullptr, 0u);
         QE_HIP(hipGetLastError());
     }
     if (cxa) {
         Timed t(c, "sort_pass_carry", 32.0 * n);
-        hipLaunchKernelGGL((tl_pass2_kernel<K, true>), dim3(nseg), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8,
+        hipLaunchKernelGGL((tl_pass2_kernel<K, true>), dim3(xcd_grid(nseg)), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8,
                            tcnt, gcnt, G, x1, x2);
         QE_HIP(hipGetLastError());
         dfree(c, x1);
     } else {
         Timed t(c, prof_split() ? "sort_pass2" : name, 16.0 * n);
-        hipLaunchKernelGGL((tl_pass2_kernel<K>), dim3(nseg), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8, tcnt,
+        hipLaunchKernelGGL((tl_pass2_kernel<K>), dim3(xcd_grid(nseg)), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8, tcnt,
                            gcnt, G);
         QE_HIP(hipGetLastError());
     }
