@@ -819,6 +819,10 @@ struct CSJob {
     uint32_t* m;
     uint32_t* part;
     uint32_t rows, C, nb;   // nb = chunks of CS_CH rows
+    // (the tile-count job of a two-level sort, nullable) the second pass's segment starts:
+    // seg[d1 * G + g] = the scanned count of group g's first tile, seg[256 * G] = ntot
+    uint32_t* seg;
+    uint32_t G, ntot;
 };
 struct CSJobs {
     CSJob j[2];
@@ -890,9 +894,13 @@ __global__ void __launch_bounds__(256) cs_apply_kernel(CSJobs js) {
     for (uint32_t r = 0; r < CS_CH; r++) v[r] = r0 + r < J.rows ? J.m[(uint64_t)(r0 + r) * J.C + c] : 0u;
 #pragma unroll
     for (uint32_t r = 0; r < CS_CH; r++) {
-        if (r0 + r < J.rows) J.m[(uint64_t)(r0 + r) * J.C + c] = run;
+        if (r0 + r < J.rows) {
+            J.m[(uint64_t)(r0 + r) * J.C + c] = run;
+            if (J.seg && (r0 + r) % TL_TPG == 0) J.seg[c * J.G + (r0 + r) / TL_TPG] = run;
+        }
         run += v[r];
     }
+    if (J.seg && blk == 0 && c == 0) J.seg[J.C * J.G] = J.ntot;
 }
 
 // pass 2: one workgroup per segment s = d1 * G + g (the run of group g's keys with first-pass
@@ -913,7 +921,7 @@ constexpr int TL2_NT = QE_TL2_NT, TL2_ITEMS = QE_TL2_ITEMS, TL2_TILE = TL2_NT * 
 // in the words' LDS slots after the words have left (as in radix_pass_kernel).
 template <typename K, bool CARRY = false>
 __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const uint64_t* __restrict__ win, uint64_t* __restrict__ wout,
-                                                         uint64_t n, int dsh, const uint32_t* __restrict__ off1,
+                                                         uint64_t n, int dsh, const uint32_t* __restrict__ seg,
                                                          const uint32_t* __restrict__ off2, uint32_t G,
                                                          const uint64_t* __restrict__ xin = nullptr,
                                                          uint64_t* __restrict__ xout = nullptr) {
@@ -923,11 +931,11 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
     __shared__ uint32_t bexcl[BINS];
     __shared__ uint32_t gofs[BINS];
     __shared__ uint32_t wsum[NW];
-    const uint32_t s = xcd_item(blockIdx.x), d1 = s / G, g = s % G;
+    const uint32_t s = xcd_item(blockIdx.x);
     if (s >= 256u * G) return;   // the XCD grid's padding blocks (block-uniform)
-    const uint32_t start = off1[(uint64_t)g * TL_TPG * 256 + d1];
-    const uint32_t end = g + 1 < G ? off1[(uint64_t)(g + 1) * TL_TPG * 256 + d1]
-                                   : (d1 < 255 ? off1[d1 + 1] : (uint32_t)n);   // tile 0's row = digit starts
+    // the segment's bounds from the compact table column_scans wrote (48 KB at 1e8 keys, L2-hot):
+    // reading them from the 12.5 MB tile-count matrix put a far dependent load before every word load
+    const uint32_t start = seg[s], end = seg[s + 1];
     const int w = wave_id(), l = lane_id();
     const uint64_t lt = lanemask_lt();
     const uint32_t d = threadIdx.x;   // threads 0..127 own one digit each
@@ -1474,10 +1482,11 @@ static LocalRounds local_rounds(int L) {   // L low bits in rounds of <= 8
 }
 
 // both column scans of a two-level sort: m0 (rows0 x 256), m1 (rows1 x 128)
-static void column_scans(qe_ctx* c, uint32_t* m0, uint32_t rows0, uint32_t* m1, uint32_t rows1) {
+static void column_scans(qe_ctx* c, uint32_t* m0, uint32_t rows0, uint32_t* m1, uint32_t rows1, uint32_t* seg,
+                         uint32_t G, uint32_t ntot) {
     CSJobs js;
-    js.j[0] = CSJob{m0, nullptr, rows0, 256u, (rows0 + CS_CH - 1) / CS_CH};
-    js.j[1] = CSJob{m1, nullptr, rows1, 128u, (rows1 + CS_CH - 1) / CS_CH};
+    js.j[0] = CSJob{m0, nullptr, rows0, 256u, (rows0 + CS_CH - 1) / CS_CH, seg, G, ntot};
+    js.j[1] = CSJob{m1, nullptr, rows1, 128u, (rows1 + CS_CH - 1) / CS_CH, nullptr, 0u, 0u};
     uint32_t* part = dalloc_t<uint32_t>(c, (size_t)js.j[0].nb * 256 + (size_t)js.j[1].nb * 128);
     js.j[0].part = part;
     js.j[1].part = part + (size_t)js.j[0].nb * 256;
@@ -1536,6 +1545,7 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     uint32_t* gcnt = dalloc_t<uint32_t>(c, (size_t)nseg * 128);
     uint32_t* hist = dalloc_t<uint32_t>(c, TL_BUCKETS);
     uint32_t* bstart = dalloc_t<uint32_t>(c, TL_BUCKETS + 1);
+    uint32_t* seg = dalloc_t<uint32_t>(c, (size_t)nseg + 1);   // the second pass's segment starts
     // a deferred sort keeps its largest bucket on the device: the consumer checks it there
     // (bucket_join) or reads it when it completes the sort (pairs_need_keys) -- no round trip here
     const bool dfr = defer && sizeof(K) == 8;
@@ -1545,6 +1555,7 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
         dfree(c, gcnt);
         dfree(c, hist);
         dfree(c, bstart);
+        dfree(c, seg);
     };
     auto ph = c->prehist.find(keys);   // counted while the keys were gathered?
     const bool have = ph != c->prehist.end() && ph->second.lo == f.lo && ph->second.L == L &&
@@ -1571,7 +1582,7 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     }
     {
         Timed t(c, "sort_scan", 8.0 * ((double)nt * 256 + (double)nseg * 128));
-        column_scans(c, tcnt, nt, gcnt, nseg);
+        column_scans(c, tcnt, nt, gcnt, nseg, seg, G, (uint32_t)n);
     }
     uint64_t* w1 = dalloc_t<uint64_t>(c, n);
     uint64_t* w2 = dalloc_t<uint64_t>(c, n);
@@ -1611,12 +1622,12 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     if (cxa) {
         Timed t(c, "sort_pass_carry", 32.0 * n);
         hipLaunchKernelGGL((tl_pass2_kernel<K, true>), dim3(xcd_grid(nseg)), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8,
-                           tcnt, gcnt, G, x1, x2);
+                           seg, gcnt, G, x1, x2);
         QE_HIP(hipGetLastError());
         dfree(c, x1);
     } else {
         Timed t(c, prof_split() ? "sort_pass2" : name, 16.0 * n);
-        hipLaunchKernelGGL((tl_pass2_kernel<K>), dim3(xcd_grid(nseg)), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8, tcnt,
+        hipLaunchKernelGGL((tl_pass2_kernel<K>), dim3(xcd_grid(nseg)), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8, seg,
                            gcnt, G);
         QE_HIP(hipGetLastError());
     }
@@ -1650,6 +1661,7 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
             dfree(c, tcnt);
             dfree(c, gcnt);
             dfree(c, hist);
+            dfree(c, seg);
             *out = SortOut{kout, vout, true, true};
             return true;
         }
