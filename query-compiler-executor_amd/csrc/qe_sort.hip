@@ -179,7 +179,11 @@ static inline uint32_t xcd_grid(uint64_t items) {
 // input order (xb nullable), written to xout at the element's output position.  The words are
 // written first; the same LDS stage then takes the payloads in the words' slots, so they leave
 // in the same runs (the partitioned plan's carried bindings, qe_join_carry).
-template <typename K, int IN, int OUT, bool PACK, int RBITS, int ITEMS, int NT, bool PRE = false, bool CARRY = false>
+// UNSTABLE (PRE only): ranks from per-wave LDS counters (one ds_add_rtn per element) instead of the
+// 8-ballot match-any -- equal digits keep no order.  For the partitioned plan's deferred sorts:
+// their consumer (bucket_join) needs the buckets, not an order inside them.
+template <typename K, int IN, int OUT, bool PACK, int RBITS, int ITEMS, int NT, bool PRE = false, bool CARRY = false,
+          bool UNSTABLE = false>
 __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ kin, const uint64_t* __restrict__ win,
                                                         const uint32_t* __restrict__ vin, K* __restrict__ kout,
                                                         uint64_t* __restrict__ wout, uint32_t* __restrict__ vout,
@@ -242,6 +246,10 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
         uint64_t i = wave_base + (uint64_t)j * 64 + l;
         bool ok = i < n;
         uint32_t d = (uint32_t)(word[j] >> dsh) & mask;
+        if constexpr (UNSTABLE) {
+            pos[j] = ok ? atomicAdd(&whist[w][d], 1u) : 0u;
+            continue;
+        }
 #ifdef QE_DIAG_SORT_NORANK   // ablation only: LDS-atomic ranks instead of match-any (unstable, in range)
         (void)lt;
         pos[j] = ok ? atomicAdd(&whist[w][d], 1u) : 0u;
@@ -919,7 +927,7 @@ constexpr int TL2_NT = QE_TL2_NT, TL2_ITEMS = QE_TL2_ITEMS, TL2_TILE = TL2_NT * 
 
 // CARRY: the 64-bit payloads of pass 1 (xin, in pass-1 order) follow the words to xout, staged
 // in the words' LDS slots after the words have left (as in radix_pass_kernel).
-template <typename K, bool CARRY = false>
+template <typename K, bool CARRY = false, bool UNSTABLE = false>
 __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const uint64_t* __restrict__ win, uint64_t* __restrict__ wout,
                                                          uint64_t n, int dsh, const uint32_t* __restrict__ seg,
                                                          const uint32_t* __restrict__ off2, uint32_t G,
@@ -959,21 +967,26 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
         for (int j = 0; j < TL2_ITEMS; j++) {   // stable rank inside the wave: (j, lane) order
             const bool ok = j * 64 < lim;
             const uint32_t dd = (uint32_t)(word[j] >> dsh) & (BINS - 1);
-            uint64_t peers = __ballot(ok);
+            uint32_t r;
+            if constexpr (UNSTABLE) {
+                r = ok ? atomicAdd(&whist[w][dd], 1u) : 0u;
+            } else {
+                uint64_t peers = __ballot(ok);
 #pragma unroll
-            for (int b = 0; b < 7; b++) {
-                const bool bit = (dd >> b) & 1u;
-                const uint64_t mm = __ballot(bit);
-                peers &= bit ? mm : ~mm;
+                for (int b = 0; b < 7; b++) {
+                    const bool bit = (dd >> b) & 1u;
+                    const uint64_t mm = __ballot(bit);
+                    peers &= bit ? mm : ~mm;
+                }
+                const int leader = peers ? (__ffsll((unsigned long long)peers) - 1) : 0;
+                uint32_t old = 0;
+                if (ok && l == leader) {
+                    old = whist[w][dd];
+                    whist[w][dd] = old + (uint32_t)__popcll(peers);
+                }
+                old = (uint32_t)__shfl((int)old, leader, 64);
+                r = old + (uint32_t)__popcll(peers & lt);
             }
-            const int leader = peers ? (__ffsll((unsigned long long)peers) - 1) : 0;
-            uint32_t old = 0;
-            if (ok && l == leader) {
-                old = whist[w][dd];
-                whist[w][dd] = old + (uint32_t)__popcll(peers);
-            }
-            old = (uint32_t)__shfl((int)old, leader, 64);
-            const uint32_t r = old + (uint32_t)__popcll(peers & lt);
             if (j & 1) pos2[j >> 1] |= r << 16;
             else pos2[j >> 1] = r;
         }
@@ -1523,6 +1536,14 @@ static uint64_t sort_pre_min() {   // tuning knob: QE_SORT_PRE_MIN = smallest n 
     return v;
 }
 
+static bool sort_unstable_on() {
+    static bool on = [] {   // tuning knob: QE_SORT_UNSTABLE=0 keeps the stable ranks in deferred sorts too
+        const char* s = getenv("QE_SORT_UNSTABLE");
+        return !(s && s[0] == '0');
+    }();
+    return on;
+}
+
 static bool sort_pre_on() {
     static bool on = [] {   // tuning knob: QE_SORT_PRE=0 keeps the lookback form of the two passes
         const char* s = getenv("QE_SORT_PRE");
@@ -1594,42 +1615,38 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     c->carry_xa = c->carry_xb = nullptr;
     uint64_t* x1 = cxa ? dalloc_t<uint64_t>(c, n) : nullptr;
     uint64_t* x2 = cxa ? dalloc_t<uint64_t>(c, n) : nullptr;
+    // a deferred sort's consumer needs its buckets, not an order inside them: unstable ranks
+    const bool uns = dfr && sort_unstable_on();
+#define QE_P1(IN, CR, UN, XA, XB, XO)                                                                                   \
+    hipLaunchKernelGGL((radix_pass_kernel<K, IN, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, CR, UN>),            \
+                       dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, \
+                       255u, f, tcnt, nullptr, nullptr, 0u, XA, XB, XO)
     if (cxa) {
         const double xb = cxb ? 8.0 : 4.0;
         Timed t(c, "sort_pass_carry", ((double)sizeof(K) + (vals ? 4.0 : 0.0) + 8.0 + xb + 8.0) * n);
-        if (vals)
-            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, true>),
-                               dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, 255u,
-                               f, tcnt, nullptr, nullptr, 0u, cxa, cxb, x1);
-        else
-            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KIOTA, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, true>),
-                               dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, nullptr, kout, w1, vout, n, 32 + L,
-                               255u, f, tcnt, nullptr, nullptr, 0u, cxa, cxb, x1);
+        if (vals && uns) QE_P1(IN_KV, true, true, cxa, cxb, x1);
+        else if (vals) QE_P1(IN_KV, true, false, cxa, cxb, x1);
+        else if (uns) QE_P1(IN_KIOTA, true, true, cxa, cxb, x1);
+        else QE_P1(IN_KIOTA, true, false, cxa, cxb, x1);
         QE_HIP(hipGetLastError());
     } else {
         // algorithmic bytes: key (+ rowid when given; generated otherwise) in, packed word out
         Timed t(c, name, ((double)sizeof(K) + (vals ? 4.0 : 0.0) + 8.0) * n);
-        if (vals)
-            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true>), dim3(xcd_grid(nt)),
-                               dim3(PRE_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, 255u, f, tcnt,
-                               nullptr, nullptr, 0u);
-        else
-            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KIOTA, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true>), dim3(xcd_grid(nt)),
-                               dim3(PRE_NT), 0, c->stream, keys, nullptr, nullptr, kout, w1, vout, n, 32 + L, 255u, f,
-                               tcnt, nullptr, nullptr, 0u);
+        if (vals && uns) QE_P1(IN_KV, false, true, nullptr, nullptr, nullptr);
+        else if (vals) QE_P1(IN_KV, false, false, nullptr, nullptr, nullptr);
+        else if (uns) QE_P1(IN_KIOTA, false, true, nullptr, nullptr, nullptr);
+        else QE_P1(IN_KIOTA, false, false, nullptr, nullptr, nullptr);
         QE_HIP(hipGetLastError());
     }
-    if (cxa) {
-        Timed t(c, "sort_pass_carry", 32.0 * n);
-        hipLaunchKernelGGL((tl_pass2_kernel<K, true>), dim3(xcd_grid(nseg)), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8,
-                           seg, gcnt, G, x1, x2);
+#undef QE_P1
+    {
+        Timed t(c, cxa ? "sort_pass_carry" : prof_split() ? "sort_pass2" : name, (cxa ? 32.0 : 16.0) * n);
+        auto kern = cxa ? (uns ? tl_pass2_kernel<K, true, true> : tl_pass2_kernel<K, true, false>)
+                        : (uns ? tl_pass2_kernel<K, false, true> : tl_pass2_kernel<K, false, false>);
+        hipLaunchKernelGGL(kern, dim3(xcd_grid(nseg)), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8, seg, gcnt, G,
+                           x1, x2);
         QE_HIP(hipGetLastError());
-        dfree(c, x1);
-    } else {
-        Timed t(c, prof_split() ? "sort_pass2" : name, 16.0 * n);
-        hipLaunchKernelGGL((tl_pass2_kernel<K>), dim3(xcd_grid(nseg)), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8, seg,
-                           gcnt, G);
-        QE_HIP(hipGetLastError());
+        if (cxa) dfree(c, x1);
     }
     // the two passes are valid whatever the bucket sizes, so they are queued before the host
     // reads the largest bucket: the GPU stays busy through that round trip
