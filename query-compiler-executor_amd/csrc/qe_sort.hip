@@ -179,9 +179,10 @@ static inline uint32_t xcd_grid(uint64_t items) {
 // input order (xb nullable), written to xout at the element's output position.  The words are
 // written first; the same LDS stage then takes the payloads in the words' slots, so they leave
 // in the same runs (the partitioned plan's carried bindings, qe_join_carry).
-// UNSTABLE (PRE only): ranks from per-wave LDS counters (one ds_add_rtn per element) instead of the
-// 8-ballot match-any -- equal digits keep no order.  For the partitioned plan's deferred sorts:
-// their consumer (bucket_join) needs the buckets, not an order inside them.
+// UNSTABLE: ranks from per-wave LDS counters (one ds_add_rtn per element) instead of the 8-ballot
+// match-any -- equal digits keep no order.  For the partitioned plan's deferred sorts (their
+// consumer, bucket_join, needs the buckets, not an order inside them) and the first LSD pass of
+// the aggregate join's sorts (no earlier order to keep, none needed among equal keys).
 template <typename K, int IN, int OUT, bool PACK, int RBITS, int ITEMS, int NT, bool PRE = false, bool CARRY = false,
           bool UNSTABLE = false>
 __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ kin, const uint64_t* __restrict__ win,
@@ -1990,7 +1991,7 @@ static void complete_lsd(qe_ctx* c, const DeferredSort& d, uint64_t n) {
     if (buf[1]) dfree(c, buf[1]);
 }
 
-// (field << 32 | (uint32_t) val[i]) words of a base column, stable-sorted by the key field
+// (field << 32 | (uint32_t) val[i]) words of a base column, sorted by the key field
 // (key >> lo) & (2^nb - 1): the aggregate join's sides (qe_join_aggregate), whose select column
 // rides in the word where the other sorts carry the rowid.  vals == null packs the row index.
 uint64_t* sort_words_kv64(qe_ctx* c, const uint64_t* keys, const uint64_t* vals, uint64_t n, int lo, int nb) {
@@ -2026,14 +2027,17 @@ uint64_t* sort_words_kv64(qe_ctx* c, const uint64_t* keys, const uint64_t* vals,
             hipLaunchKernelGGL((radix_pass_kernel<uint64_t, IN_WORD, OUT_WORD, true, 8, R_ITEMS, R_NT>), dim3((unsigned)nt),
                                dim3(R_NT), 0, c->stream, keys, win, nullptr, nullptr, wo, nullptr, n, dsh, pd.mask[p], f,
                                hist + p * BINS, s.status, s.ticket, s.epoch);
+        // the first pass has no earlier order to keep, and the aggregate join needs none among
+        // equal keys: unstable ranks there (the later LSD passes must keep theirs)
         else if (vals)
-            hipLaunchKernelGGL((radix_pass_kernel<uint64_t, IN_KV64, OUT_WORD, true, 8, R_ITEMS, R_NT>), dim3((unsigned)nt),
-                               dim3(R_NT), 0, c->stream, keys, nullptr, reinterpret_cast<const uint32_t*>(vals), nullptr,
-                               wo, nullptr, n, dsh, pd.mask[p], f, hist + p * BINS, s.status, s.ticket, s.epoch);
+            hipLaunchKernelGGL((radix_pass_kernel<uint64_t, IN_KV64, OUT_WORD, true, 8, R_ITEMS, R_NT, false, false, true>),
+                               dim3((unsigned)nt), dim3(R_NT), 0, c->stream, keys, nullptr,
+                               reinterpret_cast<const uint32_t*>(vals), nullptr, wo, nullptr, n, dsh, pd.mask[p], f,
+                               hist + p * BINS, s.status, s.ticket, s.epoch);
         else
-            hipLaunchKernelGGL((radix_pass_kernel<uint64_t, IN_KIOTA, OUT_WORD, true, 8, R_ITEMS, R_NT>), dim3((unsigned)nt),
-                               dim3(R_NT), 0, c->stream, keys, nullptr, nullptr, nullptr, wo, nullptr, n, dsh, pd.mask[p],
-                               f, hist + p * BINS, s.status, s.ticket, s.epoch);
+            hipLaunchKernelGGL((radix_pass_kernel<uint64_t, IN_KIOTA, OUT_WORD, true, 8, R_ITEMS, R_NT, false, false, true>),
+                               dim3((unsigned)nt), dim3(R_NT), 0, c->stream, keys, nullptr, nullptr, nullptr, wo, nullptr, n,
+                               dsh, pd.mask[p], f, hist + p * BINS, s.status, s.ticket, s.epoch);
         QE_HIP(hipGetLastError());
         win = wo;
     }
