@@ -310,7 +310,16 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
         uint64_t i = wave_base + (uint64_t)j * 64 + l;
         if (i < n) {
             uint32_t dd = (uint32_t)(word[j] >> dsh) & mask;
-            stage[bexcl[dd] + whist[w][dd] + pos[j]] = word[j];
+            const uint32_t slot = bexcl[dd] + whist[w][dd] + pos[j];
+            stage[slot] = word[j];
+            if constexpr (CARRY) pos[j] = slot;   // the payload takes the same slot later
+        }
+    }
+    if constexpr (CARRY) {   // the payloads load into the words' registers, in flight during the write-out
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t i = wave_base + (uint64_t)j * 64 + l;
+            word[j] = i < n ? ((uint64_t)xa[i] | (xb ? (uint64_t)xb[i] << 32 : 0ull)) : 0ull;
         }
     }
 #pragma unroll
@@ -363,14 +372,8 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
     if constexpr (CARRY) {
         __syncthreads();   // every word is out of the stage
 #pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const uint64_t i = wave_base + (uint64_t)j * 64 + l;
-            if (i < n) {
-                const uint32_t dd = (uint32_t)(word[j] >> dsh) & mask;
-                const uint64_t x = (uint64_t)xa[i] | (xb ? (uint64_t)xb[i] << 32 : 0ull);
-                stage[bexcl[dd] + whist[w][dd] + pos[j]] = x;
-            }
-        }
+        for (int j = 0; j < ITEMS; j++)
+            if (wave_base + (uint64_t)j * 64 + l < n) stage[pos[j]] = word[j];
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < ITEMS; k++) {
@@ -1017,8 +1020,17 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
             if (j * 64 < lim) {
                 const uint32_t dd = (uint32_t)(word[j] >> dsh) & (BINS - 1);
                 const uint32_t r = (pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-                stage[bexcl[dd] + whist[w][dd] + r] = word[j];
+                const uint32_t sl = bexcl[dd] + whist[w][dd] + r;
+                stage[sl] = word[j];
+                if constexpr (CARRY)   // pos2 becomes the slot (< TL2_TILE: still 16 bits)
+                    pos2[j >> 1] = (j & 1) ? ((pos2[j >> 1] & 0xFFFFu) | (sl << 16)) : ((pos2[j >> 1] & 0xFFFF0000u) | sl);
             }
+        }
+        if constexpr (CARRY) {   // the payloads load into the words' registers, in flight during the write-out
+            const uint64_t* xsrc = xin + base;
+            const uint32_t o0 = (uint32_t)w * WT + l;
+#pragma unroll
+            for (int j = 0; j < TL2_ITEMS; j++) word[j] = xsrc[std::min(o0 + (uint32_t)j * 64, m - 1)];
         }
         __syncthreads();
         if constexpr (CARRY) {
@@ -1035,20 +1047,14 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
                 }
             }
             __syncthreads();
-            uint32_t dst[TL2_ITEMS];
 #pragma unroll
-            for (int j = 0; j < TL2_ITEMS; j++) {   // each element's slot -> its destination
-                dst[j] = 0xFFFFFFFFu;
+            for (int j = 0; j < TL2_ITEMS; j++) {   // payload j goes straight to its slot's destination
                 if (j * 64 < lim) {
-                    const uint32_t dd = (uint32_t)(word[j] >> dsh) & (BINS - 1);
-                    const uint32_t r = (pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-                    dst[j] = reinterpret_cast<const uint32_t*>(stage)[2 * (bexcl[dd] + whist[w][dd] + r)];
+                    const uint32_t sl = (pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                    const uint32_t dst = reinterpret_cast<const uint32_t*>(stage)[2 * sl];
+                    if ((uint64_t)dst < n) QE_ST(&xout[dst], word[j]);
                 }
             }
-            const uint64_t* xsrc = xin + base + (uint32_t)w * WT + l;
-#pragma unroll
-            for (int j = 0; j < TL2_ITEMS; j++)   // payload j goes straight to its destination
-                if (j * 64 < lim && (uint64_t)dst[j] < n) QE_ST(&xout[dst[j]], xsrc[j * 64]);
         } else {
 #pragma unroll 6   // (fully unrolled, every LDS read is hoisted and the kernel spills)
             for (int k = 0; k < TL2_ITEMS; k++) {
