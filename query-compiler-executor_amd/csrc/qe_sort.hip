@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include "qe_device.h"
 #include "qe_internal.h"
@@ -146,6 +147,7 @@ struct Field {
 
 #ifdef QE_DIAG_STAMPS
 __device__ uint64_t g_sort_stamps[STAMP_TILES * STAMP_SLOTS];
+__device__ uint64_t g_hj_stamps[STAMP_TILES * STAMP_SLOTS];
 #endif
 
 // XCD-contiguous work items for the lookback-free passes: a grid of 8 * per blocks, block b takes
@@ -1105,7 +1107,13 @@ __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
     __shared__ uint32_t wsum[HJ_NW];
     __shared__ uint64_t s_excl;
     __shared__ uint32_t s_total;
+#ifdef QE_DIAG_STAMPS
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint32_t b = blockIdx.x;   // (XCD-contiguous buckets measured slower: 2.23 -> 2.35 ms per C3 query)
+#ifdef QE_DIAG_STAMPS
+    if (threadIdx.x == 0 && b < STAMP_TILES) g_hj_stamps[(uint64_t)b * STAMP_SLOTS] = t_start;
+#endif
     const uint32_t r0 = bsR[b], mR = bsR[b + 1] - r0, s0 = bsS[b], mS = bsS[b + 1] - s0;
     if (mR > (uint32_t)TL_CAP || mS > (uint32_t)TL_CAP) {   // beyond LDS (the sorts were not checked): flag it
         if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(total_out + 1), 1ull);
@@ -1140,10 +1148,12 @@ __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
     }
     for (uint32_t v = threadIdx.x; v < D; v += HJ_NT) bnd[v] = 0;
     __syncthreads();
+    QE_STAMP(g_hj_stamps, b, 1);
 #pragma unroll
     for (int j = 0; j < HJ_I; j++)
         if ((uint32_t)j * HJ_NT + threadIdx.x < mR) atomicAdd(&bnd[fld(wr[j]) & dmask], 1u);
     __syncthreads();
+    QE_STAMP(g_hj_stamps, b, 2);
     {   // exclusive scan of the D counts: PER consecutive values per thread, then a block scan
         const uint32_t PER = (D + HJ_NT - 1) / HJ_NT, v0 = threadIdx.x * PER;
         uint32_t sum = 0;
@@ -1164,6 +1174,7 @@ __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
     for (int j = 0; j < HJ_I; j++)   // scatter: afterwards bnd[v] is the END of v's run
         if ((uint32_t)j * HJ_NT + threadIdx.x < mR) rr[atomicAdd(&bnd[fld(wr[j]) & dmask], 1u)] = (uint32_t)wr[j];
     __syncthreads();
+    QE_STAMP(g_hj_stamps, b, 3);
     uint32_t pre[HJ_I];   // (the runs are looked up again when writing: fewer live registers)
 #pragma unroll
     for (int j = 0; j < HJ_I; j++) {
@@ -1177,6 +1188,7 @@ __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
         if (l == 63) tab[j * HJ_NW + w] = inc;
     }
     __syncthreads();
+    QE_STAMP(g_hj_stamps, b, 4);
     if (w == 0) {   // (row group, wave) totals in row order -> bucket offsets; bucket total -> lookback
         constexpr uint32_t E = HJ_I * HJ_NW;
         const uint32_t a0 = 2u * l < E ? tab[2 * l] : 0u, a1 = 2u * l + 1 < E ? tab[2 * l + 1] : 0u;
@@ -1191,6 +1203,7 @@ __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
         }
     }
     __syncthreads();
+    QE_STAMP(g_hj_stamps, b, 5);
     const uint64_t gofs = s_excl;
     if (gofs + s_total > cap) return;   // outgrew the buffers: the host re-runs with the exact size
 #ifndef QE_HJ_LANE_EMIT
@@ -1236,6 +1249,7 @@ __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
             }
         }
     }
+    QE_STAMP(g_hj_stamps, b, 6);
     return;
 #endif
 #pragma unroll
@@ -2237,7 +2251,7 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
 
 #ifdef QE_DIAG_STAMPS
 extern "C" int qe_diag_stamps_sort(const char* which, uint64_t* out, uint64_t n) {
-    (void)which;
+    if (!strcmp(which, "hj")) return hipMemcpyFromSymbol(out, HIP_SYMBOL(qe::g_hj_stamps), n * 8) == hipSuccess ? 0 : -2;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(qe::g_sort_stamps), n * 8) == hipSuccess ? 0 : -2;
 }
 #endif

@@ -24,6 +24,7 @@ PHASES = {
     "cp": ["ticket", "load+ballots", "scan+lookback", "stage", "write"],
     "ag": ["load+keys", "walks", "sums"],
     "cpp": ["ballots (data wait)", "scan+publish", "stage+prefetch+lookback", "write"],
+    "hj": ["bounds+loads issued", "R loaded+hist", "scan+scatter", "S counts+wave scans", "slice atomic", "emit (t0)"],
 }
 
 
@@ -31,7 +32,7 @@ def report(ctx, which, ntiles):
     buf = np.zeros(ntiles * SLOTS, dtype=np.uint64)
     fn = ctx.lib.qe_diag_stamps
     fn.argtypes = [C.c_char_p, C.c_void_p, C.c_uint64]
-    rc = fn(("cp" if which == "cpp" else which).encode(), buf.ctypes.data, buf.size)
+    rc = fn(("cp" if which == "cpp" else which).encode(), buf.ctypes.data, buf.size)   # "hj": the sort file
     assert rc == 0, rc
     st = buf.reshape(ntiles, SLOTS).astype(np.int64)
     names = PHASES[which]
@@ -74,6 +75,18 @@ def main():
         dg.gen_c5(ctx, n)
         ctx.run(dg.C5_QUERY)
         report(ctx, "ag", min(65536, (2 * n + 4095) // 4096))
+        ctx.close()
+        return
+    if "hj" in a.what:   # the bucket join of the last C3 join (the partitioned plan at N = 1)
+        kinds = [("mod", n), ("mod", n), ("hi32",)]
+        for r in range(4):
+            ctx.gen_relation(n, kinds, seed=1, gen_rel=r)
+        ctx.sync()
+        q = "0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>1000000000&3.2<3000000000|1.2 2.2 3.2\n"
+        for _ in range(2):
+            ctx.run_dist(q, None)
+        ctx.sync()
+        report(ctx, "hj", 32768)
         ctx.close()
         return
     kinds = [("mod", n), ("mod", n), ("hi32",)]
