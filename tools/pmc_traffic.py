@@ -22,15 +22,15 @@ from collections import defaultdict
 
 # demangled kernel name -> bench stage (first match wins)
 STAGES = [
-    (r"radix_pass_kernel<unsigned long, \d, \d, true, \d+, \d+, \d+, true, true>", "sort_pass_carry"),
-    (r"tl_pass2_kernel<unsigned long, true>", "sort_pass_carry"),
+    (r"radix_pass_kernel<unsigned long, \d, \d, true, \d+, \d+, \d+, true, true\b", "sort_pass_carry"),
+    (r"tl_pass2_kernel<unsigned long, true\b", "sort_pass_carry"),
     (r"radix_pass_kernel<unsigned long, \d, \d, true", "sort_pass_k64v32"),
     (r"radix_pass_kernel<unsigned int, \d, \d, true", "sort_pass_k32v32"),
     (r"radix_pass_kernel<unsigned long, \d, \d, false", "sort_pass_k64"),
     (r"radix_pass_kv_kernel<unsigned long", "sort_pass_k64v32"),
     (r"radix_pass_kv_kernel<unsigned int", "sort_pass_k32v32"),
-    (r"tl_pass2_kernel<unsigned long(, false)?>", "sort_pass_k64v32"),
-    (r"tl_pass2_kernel<unsigned int(, false)?>", "sort_pass_k32v32"),
+    (r"tl_pass2_kernel<unsigned long(, false\b[^>]*)?>", "sort_pass_k64v32"),
+    (r"tl_pass2_kernel<unsigned int(, false\b[^>]*)?>", "sort_pass_k32v32"),
     (r"digit_hist_kernel|digit_scan_kernel|tl_hist_kernel|tl_hist8_kernel|tl_hist_tiles_kernel|tl_gsum_kernel|tl_scan_kernel|tl_scan8_kernel", "sort_hist"),
     (r"cs_reduce_kernel|cs_top_kernel|cs_apply_kernel", "sort_scan"),
     (r"tl_local_kernel", "sort_local"),
