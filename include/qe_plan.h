@@ -81,6 +81,14 @@ typedef struct qe_engine {
      * and join instead of taking them through the pairs afterwards.  Inputs are borrowed. */
     int (*join_carry)(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h* cb, qe_h* oa, qe_h* ob,
                       qe_h* outb);
+    /* the last join of a query when only the checksums read its lists and side a carries no
+     * binding (nullable): *pairs = the local pair count, sums[s] = the local sum mod 2^64 of
+     * col_s (relation rels[s], column cols[s]) over the pairs' b rows, through b's vals (src[s]
+     * = 0; its positions when vb == 0) or cb[src[s] - 1] -- the numbers print_sums would
+     * compute from the materialised lists (src/utilities.c:197-224); the engine may skip
+     * materialising them.  Inputs are borrowed. */
+    int (*join_sums)(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h* cb, int nsel, const int* src,
+                     const uint32_t* rels, const uint32_t* cols, uint64_t* pairs, uint64_t* sums);
 } qe_engine;
 
 /* Replay the reference's variant choice and list bookkeeping for every query of `text` on the

@@ -401,6 +401,55 @@ int e_join_carry(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h
     });
 }
 
+int e_checksums(void* u, int n, const uint32_t* rels, const uint32_t* cols, const qe_h* rows, uint64_t* sums);
+void e_release(void* u, qe_h h);
+
+// the last join, read only by the checksums: its pair count and the sums of the selected columns
+// over b's bindings (src 0: b's vals, k: cb[k - 1]) without materialising the pairs
+// (bucket_join_sums); otherwise join_carry + the checksums of its lists, released here
+int e_join_sums(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h* cb, int nsel, const int* src,
+                const uint32_t* rels, const uint32_t* cols, uint64_t* pairs, uint64_t* sums) {
+    Eng* e = E(u);
+    if (nb >= 0 && nb <= 2 && nsel >= 1 && nsel <= HJ_SUMS) {
+        bool done = false;
+        const int rc = guard(e, [&] {
+            qe_ctx* c = e->c;
+            HjSums sc{};
+            sc.n = nsel;
+            for (int s = 0; s < nsel; s++) {
+                sc.col[s] = column(c, rels[s], cols[s]).d;
+                sc.src[s] = src[s];
+            }
+            qe_pairs P = side_pairs(A(ka), va ? A(va) : nullptr);
+            qe_pairs Q = side_pairs(A(kb), vb ? A(vb) : nullptr);
+            done = join_pairs_sums(c, &P, &Q, nb >= 1 ? static_cast<const uint32_t*>(A(cb[0])->d) : nullptr,
+                                   nb == 2 ? static_cast<const uint32_t*>(A(cb[1])->d) : nullptr, sc, pairs, sums);
+            qe_pairs_free(c, &P);
+            qe_pairs_free(c, &Q);
+            if (done && *pairs > c->mat_limit) {   // the same limit the materialising join keeps
+                char msg[160];
+                snprintf(msg, sizeof msg, "join of %llu pairs exceeds the materialisation limit %llu",
+                         (unsigned long long)*pairs, (unsigned long long)c->mat_limit);
+                throw Error(QE_ETOOBIG, msg);
+            }
+        });
+        if (rc != 0 || done) return rc;
+    }
+    qe_h oa = 0, ob = 0, outb[2] = {0, 0};
+    int rc = nb >= 1 ? e_join_carry(u, ka, va, kb, vb, nb, cb, &oa, &ob, outb) : e_join(u, ka, va, kb, vb, &oa, &ob);
+    if (rc == 0) {
+        *pairs = A(oa)->n;
+        std::vector<qe_h> rows(nsel);
+        for (int s = 0; s < nsel; s++) rows[s] = src[s] == 0 ? ob : outb[src[s] - 1];
+        if (*pairs) rc = e_checksums(u, nsel, rels, cols, rows.data(), sums);
+        else
+            for (int s = 0; s < nsel; s++) sums[s] = 0;
+    }
+    for (qe_h h : {oa, ob, outb[0], outb[1]})
+        if (h) e_release(u, h);
+    return rc;
+}
+
 int e_take(void* u, qe_h src, qe_h idx, qe_h* out) {
     Eng* e = E(u);
     return guard(e, [&] {
@@ -612,6 +661,8 @@ int qe_run_queries_dist(qe_ctx* c, qe_comm* m, const char* text, char** out, siz
     g.join = e_join;
     g.take = e_take;
     g.join_carry = e_join_carry;
+    // the last join in aggregate form (QE_PLAN_AGG=0: materialised, then summed -- A/B)
+    g.join_sums = getenv("QE_PLAN_AGG") && getenv("QE_PLAN_AGG")[0] == '0' ? nullptr : e_join_sums;
     g.length = e_length;
     g.checksums = e_checksums;
     g.allreduce = e_allreduce;

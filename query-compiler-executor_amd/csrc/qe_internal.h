@@ -227,6 +227,21 @@ bool carry_eligible(const qe_pairs* R, const qe_pairs* S);
 // inputs are as they were (ineligible, or a bucket beyond LDS) -- the caller joins without it.
 bool join_pairs_carry(qe_ctx* c, qe_pairs* R, qe_pairs* S, const uint32_t* xa, const uint32_t* xb, qe_list* outR,
                       qe_list* outS, qe_list* outX0, qe_list* outX1);
+// the join's checksums without its pairs (the plan's last join): sums[k] = sum over pairs of
+// col_k[S-side rowid], the rowid being S's val (src 0) or the low / high half of its carried
+// payload (src 1 / 2); *pairs = the pair count.  False: not applicable (geometry, a bucket
+// beyond LDS) -- nothing was produced.
+constexpr int HJ_SUMS = 4;
+struct HjSums {
+    const uint64_t* col[HJ_SUMS];
+    int src[HJ_SUMS];
+    int n;
+};
+bool bucket_join_sums(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const HjSums& sc, uint64_t* pairs,
+                      uint64_t* sums);
+// join_pairs_carry's sort + bucket_join_sums (xa null: S carries no payload); false: as there
+bool join_pairs_sums(qe_ctx* c, qe_pairs* R, qe_pairs* S, const uint32_t* xa, const uint32_t* xb, const HjSums& sc,
+                     uint64_t* pairs, uint64_t* sums);
 SortOut radix_sort_u32(qe_ctx* c, const uint32_t* keys, const uint32_t* vals, uint64_t n,
                        const uint64_t* bits = nullptr);
 // multi-GPU (qe_dist.hip): hash-partition rows into per-destination segments of out_keys /

@@ -1628,6 +1628,24 @@ bool join_pairs_carry(qe_ctx* c, qe_pairs* R, qe_pairs* S, const uint32_t* xa, c
     *S = S0;
     return false;
 }
+
+bool join_pairs_sums(qe_ctx* c, qe_pairs* R, qe_pairs* S, const uint32_t* xa, const uint32_t* xb, const HjSums& sc,
+                     uint64_t* pairs, uint64_t* sums) {
+    if (!carry_eligible(R, S)) return false;
+    const qe_pairs R0 = *R, S0 = *S;
+    if ((R0.owns | S0.owns) & 7) return false;
+    sort_pairs(c, R, true);
+    c->carry_xa = xa;   // (null: no payload)
+    c->carry_xb = xb;
+    sort_pairs(c, S, true);
+    c->carry_xa = c->carry_xb = nullptr;
+    if (bucket_join_sums(c, R, S, sc, pairs, sums)) return true;
+    qe_pairs_free(c, R);
+    qe_pairs_free(c, S);
+    *R = R0;
+    *S = S0;
+    return false;
+}
 }  // namespace qe
 
 extern "C" {

@@ -2247,6 +2247,129 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
     throw Error(QE_EINVAL, "internal: bucket join outgrew its exact size");
 }
 
+// ---- the bucket join in aggregate form (the plan's last join, read only by the checksums) ----
+// print_sums (src/utilities.c:197-224) reads a finished query's lists only through sums mod 2^64,
+// and each S row appears in the join's output once per R partner: so the output's checksum over
+// column V of one of S's bindings is sum_s cnt_R(key_s) * V[rowid_s], and its length sum_s cnt_R.
+// Per bucket: R's key values counted in LDS (no scan, no scatter of R's rowids), every S row
+// looks up its count and gathers its selected values once -- no pairs, no payloads written, no
+// checksum pass reading them back.  Each block writes its partial sums (plain stores); a second
+// launch adds them up (one atomic per block on one word would serialise at the memory side).
+__global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
+tl_hjoin_sums_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict__ bsR,
+                     const uint64_t* __restrict__ wS, const uint32_t* __restrict__ bsS, int L,
+                     const uint64_t* __restrict__ xS, HjSums sc, uint64_t* __restrict__ part,
+                     unsigned long long* __restrict__ flag) {
+    __shared__ uint32_t cnt[1 << HJ_DBITS];
+    __shared__ uint64_t red[HJ_NW][HJ_SUMS + 1];
+    const uint32_t b = blockIdx.x;
+    const uint32_t r0 = bsR[b], mR = bsR[b + 1] - r0, s0 = bsS[b], mS = bsS[b + 1] - s0;
+    if (mR > (uint32_t)TL_CAP || mS > (uint32_t)TL_CAP) {   // beyond LDS: the host takes the other path
+        if (threadIdx.x == 0) atomicOr(flag, 1ull);
+        return;
+    }
+    const uint32_t D = 1u << L, dmask = D - 1u;
+    const int w = wave_id(), l = lane_id();
+    uint64_t wr[HJ_I], ws[HJ_I], xv[HJ_I];
+#pragma unroll
+    for (int j = 0; j < HJ_I; j++) {
+        const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
+        wr[j] = i < mR ? wR[r0 + i] : 0;
+        ws[j] = i < mS ? wS[s0 + i] : 0;
+        xv[j] = xS && i < mS ? xS[s0 + i] : 0ull;
+    }
+    for (uint32_t v = threadIdx.x; v < D; v += HJ_NT) cnt[v] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < HJ_I; j++)
+        if ((uint32_t)j * HJ_NT + threadIdx.x < mR) atomicAdd(&cnt[fld(wr[j]) & dmask], 1u);
+    __syncthreads();
+    uint32_t c[HJ_I];
+    uint64_t acc[HJ_SUMS + 1];
+    acc[HJ_SUMS] = 0;
+#pragma unroll
+    for (int j = 0; j < HJ_I; j++) {
+        c[j] = (uint32_t)j * HJ_NT + threadIdx.x < mS ? cnt[fld(ws[j]) & dmask] : 0u;
+        acc[HJ_SUMS] += c[j];
+    }
+#pragma unroll
+    for (int s = 0; s < HJ_SUMS; s++) {
+        acc[s] = 0;
+        if (s < sc.n) {   // block-uniform
+            const uint64_t* __restrict__ col = sc.col[s];
+            const int src = sc.src[s];
+            uint64_t v[HJ_I];
+#pragma unroll
+            for (int j = 0; j < HJ_I; j++) {   // every gather of the select in flight together
+                const uint32_t id = src == 0 ? (uint32_t)ws[j] : src == 1 ? (uint32_t)xv[j] : (uint32_t)(xv[j] >> 32);
+                v[j] = c[j] ? col[id] : 0ull;
+            }
+#pragma unroll
+            for (int j = 0; j < HJ_I; j++) acc[s] += (uint64_t)c[j] * v[j];
+        }
+    }
+#pragma unroll
+    for (int s = 0; s <= HJ_SUMS; s++) {
+        const uint64_t t = wave_sum_u64(acc[s]);
+        if (l == 0) red[w][s] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x <= HJ_SUMS) {
+        uint64_t t = 0;
+        for (int ww = 0; ww < HJ_NW; ww++) t += red[ww][threadIdx.x];
+        part[(uint64_t)b * (HJ_SUMS + 1) + threadIdx.x] = t;
+    }
+}
+
+// out[k] = sum over blocks of part[b][k] (mod 2^64), one workgroup per k
+__global__ void __launch_bounds__(256) hjoin_sums_reduce_kernel(const uint64_t* __restrict__ part, uint32_t nb,
+                                                                uint64_t* __restrict__ out) {
+    const uint32_t k = blockIdx.x;
+    uint64_t t = 0;
+    for (uint32_t b = threadIdx.x; b < nb; b += 256) t += part[(uint64_t)b * (HJ_SUMS + 1) + k];
+    t = wave_sum_u64(t);
+    __shared__ uint64_t red[4];
+    if (lane_id() == 0) red[wave_id()] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) out[k] = red[0] + red[1] + red[2] + red[3];
+}
+
+bool bucket_join_sums(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const HjSums& sc, uint64_t* pairs,
+                      uint64_t* sums) {
+    auto iR = c->deferred.find(R->key), iS = c->deferred.find(S->key);
+    if (iR == c->deferred.end() || iS == c->deferred.end() || R->key == S->key) return false;
+    const DeferredSort& dR = iR->second;
+    const DeferredSort& dS = iS->second;
+    if (dR.lo != dS.lo || dR.L != dS.L || dR.fmask != dS.fmask || dR.kconst != dS.kconst || dR.L > HJ_DBITS)
+        return false;
+    if (sc.n < 0 || sc.n > HJ_SUMS) return false;
+    bool carry = false;
+    for (int s = 0; s < sc.n; s++) carry |= sc.src[s] != 0;
+    if (carry && !dS.x) return false;   // S's sort did not carry the payload
+    uint64_t* part = dalloc_t<uint64_t>(c, (size_t)TL_BUCKETS * (HJ_SUMS + 1));
+    uint64_t* out = dalloc_t<uint64_t>(c, 8);   // [pairs-free sums..., pairs, oversize]
+    QE_HIP(hipMemsetAsync(out, 0, 8 * sizeof(uint64_t), c->stream));
+    {
+        Timed t(c, "bucket_join_sums", 8.0 * (double)(R->n + S->n) + (carry ? 8.0 * (double)S->n : 0.0));
+        hipLaunchKernelGGL(tl_hjoin_sums_kernel, dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream, dR.words, dR.bstart,
+                           dS.words, dS.bstart, dR.L, carry ? dS.x : nullptr, sc, part,
+                           reinterpret_cast<unsigned long long*>(out + HJ_SUMS + 1));
+        QE_HIP(hipGetLastError());
+        hipLaunchKernelGGL(hjoin_sums_reduce_kernel, dim3(HJ_SUMS + 1), dim3(256), 0, c->stream, part,
+                           (uint32_t)TL_BUCKETS, out);
+        QE_HIP(hipGetLastError());
+    }
+    uint64_t h[HJ_SUMS + 2];
+    read_words(c, out, h, HJ_SUMS + 2);   // the ONE round trip of the join and its sums
+    dfree(c, part);
+    dfree(c, out);
+    if (h[HJ_SUMS + 1]) return false;     // a bucket beyond LDS (skew)
+    *pairs = h[HJ_SUMS];
+    for (int s = 0; s < sc.n; s++) sums[s] = h[s];
+    add_bytes(c, "bucket_join_sums", 8.0 * (double)sc.n * (double)h[HJ_SUMS]);   // ~ the gathered values
+    return true;
+}
+
 }  // namespace qe
 
 #ifdef QE_DIAG_STAMPS

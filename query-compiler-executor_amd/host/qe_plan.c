@@ -388,6 +388,11 @@ typedef struct {
     qe_h* list;                 /* filtered, not yet joined bindings */
     uint64_t* list_size;
     int rc;
+    /* the last join ran in aggregate form (engine join_sums): its global pair count and the
+     * selects' local sums, in select order */
+    int agg;
+    uint64_t agg_size;
+    uint64_t agg_sums[64];
 } plan_t;
 
 #define ECHK(call)                                   \
@@ -550,7 +555,7 @@ static void free_comp(plan_t* P, int cid) {
     c->alive = 0;
 }
 
-static int do_join(plan_t* P, const pred_t* p, const uint8_t* need) {
+static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, int last) {
     const qe_engine* e = P->e;
     const int ba = (int)p->frel, bb = (int)p->srel;
     const int A = component(P, ba), B = component(P, bb);
@@ -565,6 +570,55 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need) {
     }
     ECHK(side_finish(P, &sa));
     ECHK(side_finish(P, &sb));
+    if (last && e->join_sums) {
+        /* the query's last join, read only by the selects: one side carries every selected
+         * binding, the other none -- the engine returns the pair count and the sums */
+        side_t* O = sa.ncar == 0 ? &sa : sb.ncar == 0 ? &sb : NULL;
+        side_t* C = O == &sa ? &sb : &sa;
+        const query_t* q = P->q;
+        int src[64], ok = O && C->ncar >= 1 && C->ncar <= 3 && q->nsel >= 1 && q->nsel <= 4;
+        for (size_t s = 0; ok && s < q->nsel; s++) {
+            src[s] = -1;
+            for (int i = 0; i < C->ncar; i++)
+                if (C->car_b[i] == (int)q->sel[2 * s]) src[s] = i;
+            ok = src[s] >= 0;
+        }
+        if (ok) {
+            uint32_t srel[64], scol[64];
+            for (size_t s = 0; s < q->nsel; s++) {
+                srel[s] = q->rels[q->sel[2 * s]];
+                scol[s] = (uint32_t)q->sel[2 * s + 1];
+            }
+            if (C->ncar >= 2) {                                  /* its first binding rides as vals */
+                C->vals = C->car_rows[0];
+                C->car_rows[0] = NONE;
+            }
+            uint64_t v[2] = {0, 0};
+            const int jr = e->join_sums(e->u, O->keys, O->vals, C->keys, C->vals, C->ncar - 1, &C->car_rows[1],
+                                        (int)q->nsel, src, srel, scol, &v[0], P->agg_sums);
+            if (jr != 0 && jr != QE_ETOOBIG) {
+                P->rc = jr;
+                return jr;
+            }
+            v[1] = jr == QE_ETOOBIG;
+            if (P->e->world > 1) ECHK(P->e->allreduce(P->e->u, v, 2));   /* every rank takes one branch */
+            rel(P, sa.keys);
+            rel(P, sb.keys);
+            rel(P, sa.vals);
+            rel(P, sb.vals);
+            for (int k = 0; k < sa.ncar; k++) rel(P, sa.car_rows[k]);
+            for (int k = 0; k < sb.ncar; k++) rel(P, sb.car_rows[k]);
+            free_comp(P, A);
+            free_comp(P, B);
+            if (v[1]) {
+                P->rc = QE_ETOOBIG;
+                return QE_ETOOBIG;
+            }
+            P->agg = 1;
+            P->agg_size = v[0];
+            return 0;
+        }
+    }
     qe_h oa = NONE, ob = NONE;
     /* a side carrying several bindings: its first rides as the join's vals, the others (up to two)
      * ride through the engine's join beside the pairs (join_carry) instead of being taken after */
@@ -763,7 +817,7 @@ static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t*
                 need[q->preds[i].frel] = 1;
                 if (q->preds[i].type == 0) need[q->preds[i].srel] = 1;
             }
-            rc = do_join(P, jp, need);
+            rc = do_join(P, jp, need, np == 0 && end == q->npreds);
         }
         k = end;
     }
@@ -774,7 +828,11 @@ static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t*
     qe_h* srows = (qe_h*)calloc(q->nsel + 1, sizeof(qe_h));
     uint64_t* ssize = (uint64_t*)calloc(q->nsel + 1, sizeof(uint64_t));
     int ns = 0;
-    for (size_t s = 0; rc == 0 && s < q->nsel; s++) {
+    for (size_t s = 0; rc == 0 && P->agg && s < q->nsel; s++) {   /* the aggregate last join's sums */
+        ssize[s] = P->agg_size;
+        if (P->agg_size) sums[ns++] = P->agg_sums[s];
+    }
+    for (size_t s = 0; rc == 0 && !P->agg && s < q->nsel; s++) {
         const int b = (int)q->sel[2 * s];
         uint64_t size;
         qe_h rows;
@@ -794,7 +852,7 @@ static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t*
         scol[ns] = (uint32_t)q->sel[2 * s + 1];
         srows[ns++] = rows;
     }
-    if (rc == 0 && ns) rc = e->checksums(e->u, ns, srel, scol, srows, sums);
+    if (rc == 0 && ns && !P->agg) rc = e->checksums(e->u, ns, srel, scol, srows, sums);
     if (rc == 0 && ns && e->world > 1) rc = e->allreduce(e->u, sums, ns);
     if (rc == 0) {
         int j = 0;

@@ -35,6 +35,7 @@ FIELDS = [
     ("fallback", C.CFUNCTYPE(I, VP, VP, VP)),
     ("scan2", C.CFUNCTYPE(I, VP, U32, U32, C.c_char, U64, U32, C.c_char, U64, U64, U64, P(H))),
     ("join_carry", C.CFUNCTYPE(I, VP, H, H, H, H, I, P(H), P(H), P(H), P(H))),
+    ("join_sums", C.CFUNCTYPE(I, VP, H, H, H, H, I, P(H), I, P(I), P(U32), P(U32), P(U64), P(U64))),
 ]
 
 
@@ -67,10 +68,11 @@ def join_local(ka, kb):
 class NumpyPlanEngine:
     """one rank: relations replicated as numpy columns; handles index a dict of arrays"""
 
-    def __init__(self, rels, rank=0, world=1, group=None, fused_scan=True, join_carry=True):
+    def __init__(self, rels, rank=0, world=1, group=None, fused_scan=True, join_carry=True, join_sums=True):
         self.rels, self.rank, self.world, self.group = rels, rank, world, group
         self.h, self.next, self.borrowed = {}, 1, set()
         self.exchanges = 0
+        self.sums_calls = 0                      # last joins run in aggregate form (join_sums)
         self.mat_limit = 1 << 62
         self.lib = C.CDLL(SO)
         self.lib.qe_plan_run_text.argtypes = [P(Engine), C.c_char_p, P(C.c_void_p), P(C.c_size_t), P(U64), P(U64)]
@@ -82,7 +84,8 @@ class NumpyPlanEngine:
         e = Engine()
         e.u, e.rank, e.world = None, rank, world
         for name, ftype in FIELDS:
-            if name == "fallback" or (name == "scan2" and not fused_scan) or (name == "join_carry" and not join_carry):
+            if (name == "fallback" or (name == "scan2" and not fused_scan) or (name == "join_carry" and not join_carry)
+                    or (name == "join_sums" and not join_sums)):
                 setattr(e, name, ftype())            # NULL: refused queries return QE_ENOTSUP; no fused scan
                 continue
             fn = self._wrap(getattr(self, "cb_" + name), name == "release")
@@ -217,6 +220,22 @@ class NumpyPlanEngine:
         ob[0] = self.put(self.get(vb)[ib] if vb else ib)
         for k in range(nb):
             outb[k] = self.put(self.get(cb[k])[ib])
+
+    def cb_join_sums(self, u, ka, va, kb, vb, nb, cb, nsel, src, rels, cols, pairs, sums):
+        """aggregate form, computed independently of the join: each b row counts its a partners"""
+        self.sums_calls += 1
+        a, b = self.get(ka), self.get(kb)
+        sa = np.sort(a, kind="stable")
+        cnt = (np.searchsorted(sa, b, "right") - np.searchsorted(sa, b, "left")).astype(np.uint64)
+        total = int(cnt.sum())
+        if total > self.mat_limit:
+            return -5
+        pairs[0] = total
+        for s in range(nsel):
+            rows = (self.get(vb) if vb else np.arange(len(b), dtype=np.uint32)) if src[s] == 0 \
+                else self.get(cb[src[s] - 1])
+            with np.errstate(over="ignore"):
+                sums[s] = int(np.sum(cnt * self.rels[rels[s]][cols[s]][rows], dtype=np.uint64))
 
     def cb_take(self, u, src, idx, out):
         out[0] = self.put(self.get(src)[self.get(idx)])

@@ -190,3 +190,37 @@ def test_dist_executor_carry_falls_back_on_a_skewed_bucket(ctx, comm):
         assert (out, rc, refused) == (want, 0, 0)
     finally:
         ctx.drop_relations()
+
+
+@pytest.mark.slow
+def test_dist_executor_last_join_in_aggregate_form(ctx, comm, monkeypatch):
+    """C3's last join only feeds the checksums: the engine's join_sums returns its pair count and
+    the selects' sums without materialising the pairs (bucket_join_sums) -- the same bytes as the
+    faithful executor and as the materialised last join (QE_PLAN_AGG=0), and the same row count"""
+    N = 75_000_001
+    ctx.drop_relations()
+    _loaded["key"] = None
+    try:
+        kinds = [("mod", N), ("mod", N), ("hi32",)]
+        for r in range(4):
+            ctx.gen_relation(N, kinds, seed=5, gen_rel=r)
+        qs = ("0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>1000000000&3.2<3000000000|1.2 2.2 3.2\n",
+              "0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>2000000000|3.2 3.2 1.0 2.1\n",
+              "0 1|0.1=1.0&1.2>3000000000|1.2 1.0\n")
+        for q, want_agg in zip(qs, (1, 1, None)):   # (the last one's side is below the carry sort's size)
+            want, _ = ctx.run(q)
+            rows = ctx.last_result_rows()
+            ctx.set_profiling(True)
+            ctx.reset_stats()
+            out, rc, refused = ctx.run_dist(q, comm)
+            agg = ctx.kernel_stats().get("bucket_join_sums", {}).get("launches", 0)
+            ctx.set_profiling(False)
+            assert (out, rc, refused) == (want, 0, 0), q
+            assert ctx.last_result_rows() == rows, q
+            assert want_agg is None or agg == want_agg, q
+            monkeypatch.setenv("QE_PLAN_AGG", "0")
+            out0, rc0, _ = ctx.run_dist(q, comm)
+            monkeypatch.delenv("QE_PLAN_AGG")
+            assert (out0, rc0) == (want, 0), q
+    finally:
+        ctx.drop_relations()

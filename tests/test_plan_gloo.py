@@ -35,11 +35,12 @@ def _run_world(rels, queries, world, limits=None):
 @pytest.mark.parametrize("fixture", [f.split("/")[-1][:-5] for f in goldens.golden_files()])
 def test_every_golden_is_refused_or_exact(fixture, optional):
     """with the engine's optional entries (scan2: a fused scan + refine; join_carry: a side's
-    extra bindings delivered by the join) and without them (a scan then a refine; takes)"""
+    extra bindings delivered by the join; join_sums: the last join's checksums without its
+    pairs) and without them (a scan then a refine; takes; a materialised last join)"""
     doc = goldens.load(f"{goldens.GOLDEN_DIR}/{fixture}.json")
     rels, _ = goldens.dataset(doc["dataset"])
     on = optional == "all"
-    eng = pe.NumpyPlanEngine(rels, 0, 1, fused_scan=on, join_carry=on)
+    eng = pe.NumpyPlanEngine(rels, 0, 1, fused_scan=on, join_carry=on, join_sums=on)
     accepted = {"T": 0, "W": 0}
     for c in doc["cases"]:
         out, rc, _, _ = eng.run(c["input"])
@@ -52,6 +53,7 @@ def test_every_golden_is_refused_or_exact(fixture, optional):
     t_cases = sum(c.get("class") == "T" for c in doc["cases"])
     if fixture in ("c4", "fuzz_a", "fuzz_c", "headline"):
         assert accepted["T"] >= 0.75 * t_cases, accepted   # the relational class is the plan's domain
+        assert (eng.sums_calls > 0) == on                  # and its last joins take the aggregate form
 
 
 def test_check_names_the_reason():

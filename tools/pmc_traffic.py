@@ -40,6 +40,7 @@ STAGES = [
     (r"take_u32_kernel", "take_u32"),
     (r"heavy_stats_kernel", "heavy_stats"),
     (r"key_bits_kernel", "sort_keybits"),
+    (r"tl_hjoin_sums_kernel|hjoin_sums_reduce_kernel", "bucket_join_sums"),
     (r"tl_hjoin_kernel", "bucket_join"),
     (r"mj_fused", "mj_fused"),
     (r"mj_partition", "mj_partition"),
