@@ -34,6 +34,9 @@ extern "C" {
  * Handles given to the plan are released by it (release) unless noted. */
 typedef uint64_t qe_h;
 
+#define QE_PLAN_VALUES 0xFFFFFFFFu   /* checksums: rows_k holds the values themselves */
+#define QE_PLAN_VALUES_SRC 4        /* join_sums: src[s] | this -- the carried list holds values */
+
 typedef struct qe_engine {
     void* u;                    /* the engine's state, passed back to every call */
     uint32_t rank, world;
@@ -89,6 +92,12 @@ typedef struct qe_engine {
      * materialising them.  Inputs are borrowed. */
     int (*join_sums)(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h* cb, int nsel, const int* src,
                      const uint32_t* rels, const uint32_t* cols, uint64_t* pairs, uint64_t* sums);
+    /* a binding read later only by selects of one column (nullable): out[i] = col[rows[i]] as
+     * uint32 when every value of the column is below 2^32, QE_ENOTSUP otherwise (`rows` is
+     * borrowed).  The plan then carries the values instead of the rowids: a list of values is
+     * passed to checksums with rels[k] = QE_PLAN_VALUES (its own sum) and to join_sums with
+     * src[s] | QE_PLAN_VALUES_SRC (summed, not gathered). */
+    int (*values)(void* u, uint32_t rel, uint32_t col, qe_h rows, qe_h* out);
 } qe_engine;
 
 /* Replay the reference's variant choice and list bookkeeping for every query of `text` on the

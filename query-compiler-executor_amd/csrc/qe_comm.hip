@@ -16,6 +16,7 @@
 
 #include "../../include/qe_plan.h"
 #include "../host/qe_query.h"
+#include "qe_device.h"
 #include "qe_internal.h"
 
 struct qe_comm {
@@ -29,6 +30,46 @@ struct qe_comm {
 
 namespace qe {
 namespace {
+
+// a select column's values in a list's order, as u32 (the column's values are below 2^32)
+__global__ void __launch_bounds__(256) gather_u32_kernel(const uint64_t* __restrict__ col,
+                                                         const uint32_t* __restrict__ rows, uint64_t n,
+                                                         uint32_t* __restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * 4;
+    for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += stride) {
+        if (i + 3 < n) {
+            const uint4 r = *reinterpret_cast<const uint4*>(rows + i);
+            uint4 v;
+            v.x = (uint32_t)col[r.x];
+            v.y = (uint32_t)col[r.y];
+            v.z = (uint32_t)col[r.z];
+            v.w = (uint32_t)col[r.w];
+            *reinterpret_cast<uint4*>(out + i) = v;
+        } else {
+            for (uint64_t k = i; k < n; k++) out[k] = (uint32_t)col[rows[k]];
+        }
+    }
+}
+
+// sum of a list's own u32 values mod 2^64 (a binding that carries its select's values)
+__global__ void __launch_bounds__(256) sum_u32_kernel(const uint32_t* __restrict__ v, uint64_t n,
+                                                      unsigned long long* __restrict__ out) {
+    uint64_t t = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * 4;
+    for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += stride) {
+        if (i + 3 < n) {
+            const uint4 a = *reinterpret_cast<const uint4*>(v + i);
+            t += (uint64_t)a.x + a.y + a.z + a.w;
+        } else {
+            for (uint64_t k = i; k < n; k++) t += v[k];
+        }
+    }
+    t = wave_sum_u64(t);
+    __shared__ uint64_t red[4];
+    if (lane_id() == 0) red[wave_id()] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(out, (unsigned long long)(red[0] + red[1] + red[2] + red[3]));
+}
 
 #define QE_NCCL(call)                                                                                  \
     do {                                                                                               \
@@ -416,8 +457,8 @@ int e_join_sums(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h*
             qe_ctx* c = e->c;
             HjSums sc{};
             sc.n = nsel;
-            for (int s = 0; s < nsel; s++) {
-                sc.col[s] = column(c, rels[s], cols[s]).d;
+            for (int s = 0; s < nsel; s++) {   // a value-carrying list is summed, not gathered through
+                sc.col[s] = (src[s] & QE_PLAN_VALUES_SRC) ? nullptr : column(c, rels[s], cols[s]).d;
                 sc.src[s] = src[s];
             }
             qe_pairs P = side_pairs(A(ka), va ? A(va) : nullptr);
@@ -440,8 +481,13 @@ int e_join_sums(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h*
     if (rc == 0) {
         *pairs = A(oa)->n;
         std::vector<qe_h> rows(nsel);
-        for (int s = 0; s < nsel; s++) rows[s] = src[s] == 0 ? ob : outb[src[s] - 1];
-        if (*pairs) rc = e_checksums(u, nsel, rels, cols, rows.data(), sums);
+        std::vector<uint32_t> rl(nsel);
+        for (int s = 0; s < nsel; s++) {
+            const int k = src[s] & 3;
+            rows[s] = k == 0 ? ob : outb[k - 1];
+            rl[s] = (src[s] & QE_PLAN_VALUES_SRC) ? QE_PLAN_VALUES : rels[s];
+        }
+        if (*pairs) rc = e_checksums(u, nsel, rl.data(), cols, rows.data(), sums);
         else
             for (int s = 0; s < nsel; s++) sums[s] = 0;
     }
@@ -468,15 +514,61 @@ int e_length(void* u, qe_h h, uint64_t* n) {
 int e_checksums(void* u, int n, const uint32_t* rels, const uint32_t* cols, const qe_h* rows, uint64_t* sums) {
     Eng* e = E(u);
     return guard(e, [&] {
-        std::vector<qe_col> cs(n);
+        qe_ctx* c = e->c;
+        std::vector<qe_col> cs;
         std::vector<qe_list> ls(n);
-        std::vector<const qe_list*> lp(n);
+        std::vector<const qe_list*> lp;
+        std::vector<int> at, vat;
         for (int i = 0; i < n; i++) {
-            cs[i] = column(e->c, rels[i], cols[i]);
             ls[i] = as_list(A(rows[i]));
-            lp[i] = &ls[i];
+            if (rels[i] == QE_PLAN_VALUES) {   // the list holds the select's values: its own sum
+                vat.push_back(i);
+                continue;
+            }
+            cs.push_back(column(c, rels[i], cols[i]));
+            lp.push_back(&ls[i]);
+            at.push_back(i);
         }
-        ck(qe_checksums(e->c, n, cs.data(), lp.data(), sums), e->c);
+        if (!vat.empty()) {
+            unsigned long long* d = (unsigned long long*)dalloc_t<uint64_t>(c, vat.size());
+            QE_HIP(hipMemsetAsync(d, 0, vat.size() * 8, c->stream));
+            for (size_t k = 0; k < vat.size(); k++) {
+                const qe_list& l = ls[vat[k]];
+                if (!l.n) continue;
+                Timed t(c, "checksum", 4.0 * l.n);
+                hipLaunchKernelGGL(sum_u32_kernel, dim3(grid_for(l.n, 256 * 16, 4096)), dim3(256), 0, c->stream, l.d,
+                                   l.n, d + k);
+                QE_HIP(hipGetLastError());
+            }
+            std::vector<uint64_t> h(vat.size());
+            read_words(c, (const uint64_t*)d, h.data(), (int)vat.size());
+            dfree(c, d);
+            for (size_t k = 0; k < vat.size(); k++) sums[vat[k]] = h[k];
+        }
+        if (!at.empty()) {
+            std::vector<uint64_t> h(at.size());
+            ck(qe_checksums(c, (int)at.size(), cs.data(), lp.data(), h.data()), c);
+            for (size_t k = 0; k < at.size(); k++) sums[at[k]] = h[k];
+        }
+    });
+}
+
+int e_values(void* u, uint32_t rel, uint32_t col, qe_h rows, qe_h* out) {
+    Eng* e = E(u);
+    qe_ctx* c = e->c;
+    uint64_t kor = 0, kand = 0;
+    if (qe_relation_column_bits(c, (int)rel, (int)col, &kor, &kand) != 0 || (kor >> 32)) return QE_ENOTSUP;
+    return guard(e, [&] {
+        const qe_col q = column(c, rel, col);
+        const DArr* r = A(rows);
+        uint32_t* d = dalloc_t<uint32_t>(c, std::max<uint64_t>(r->n, 1));
+        if (r->n) {
+            Timed t(c, "gather_values", 12.0 * r->n);
+            hipLaunchKernelGGL(gather_u32_kernel, dim3(grid_for(r->n, 256 * 16, 8192)), dim3(256), 0, c->stream, q.d,
+                               static_cast<const uint32_t*>(r->d), r->n, d);
+            QE_HIP(hipGetLastError());
+        }
+        *out = H(new_arr(c, d, r->n, false));
     });
 }
 
@@ -663,6 +755,8 @@ int qe_run_queries_dist(qe_ctx* c, qe_comm* m, const char* text, char** out, siz
     g.join_carry = e_join_carry;
     // the last join in aggregate form (QE_PLAN_AGG=0: materialised, then summed -- A/B)
     g.join_sums = getenv("QE_PLAN_AGG") && getenv("QE_PLAN_AGG")[0] == '0' ? nullptr : e_join_sums;
+    // select values carried instead of rowids (QE_PLAN_VALUES=0: rowids -- A/B)
+    g.values = getenv("QE_PLAN_VALUES") && getenv("QE_PLAN_VALUES")[0] == '0' ? nullptr : e_values;
     g.length = e_length;
     g.checksums = e_checksums;
     g.allreduce = e_allreduce;

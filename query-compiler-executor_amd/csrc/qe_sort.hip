@@ -2297,12 +2297,13 @@ tl_hjoin_sums_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict
         acc[s] = 0;
         if (s < sc.n) {   // block-uniform
             const uint64_t* __restrict__ col = sc.col[s];
-            const int src = sc.src[s];
+            const int src = sc.src[s] & 3;
+            const bool own = (sc.src[s] & 4) != 0;   // the carried list holds the values (QE_PLAN_VALUES_SRC)
             uint64_t v[HJ_I];
 #pragma unroll
             for (int j = 0; j < HJ_I; j++) {   // every gather of the select in flight together
                 const uint32_t id = src == 0 ? (uint32_t)ws[j] : src == 1 ? (uint32_t)xv[j] : (uint32_t)(xv[j] >> 32);
-                v[j] = c[j] ? col[id] : 0ull;
+                v[j] = own ? (uint64_t)id : c[j] ? col[id] : 0ull;
             }
 #pragma unroll
             for (int j = 0; j < HJ_I; j++) acc[s] += (uint64_t)c[j] * v[j];
@@ -2344,7 +2345,7 @@ bool bucket_join_sums(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const HjS
         return false;
     if (sc.n < 0 || sc.n > HJ_SUMS) return false;
     bool carry = false;
-    for (int s = 0; s < sc.n; s++) carry |= sc.src[s] != 0;
+    for (int s = 0; s < sc.n; s++) carry |= (sc.src[s] & 3) != 0;
     if (carry && !dS.x) return false;   // S's sort did not carry the payload
     uint64_t* part = dalloc_t<uint64_t>(c, (size_t)TL_BUCKETS * (HJ_SUMS + 1));
     uint64_t* out = dalloc_t<uint64_t>(c, 8);   // [pairs-free sums..., pairs, oversize]

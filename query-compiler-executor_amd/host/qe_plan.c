@@ -377,7 +377,8 @@ static int plan_check(const qe_engine* e, const query_t* q) {
 
 #define NONE ((qe_h)0)
 
-typedef struct { int b; qe_h rows; int whole; } member;          /* whole: every row of the relation */
+typedef struct { int b; qe_h rows; int whole; int vcol; } member;  /* whole: every row of the relation;
+                                                                     vcol = c + 1: rows holds column c's values */
 typedef struct { member* m; int n; uint64_t size; int alive; } comp_t;
 
 typedef struct {
@@ -464,15 +465,17 @@ typedef struct {
     int ncar;
     int car_b[64];
     qe_h car_rows[64];          /* NONE: the binding's rowids are `vals` */
+    int car_v[64];              /* the member's vcol (values instead of rowids) */
     qe_h ticket;                /* an exchange in flight */
     int keep_n;
     int keep_b[64];
+    int keep_v[64];
     int base;                   /* keys is a whole base column (vals NONE = row i) */
 } side_t;
 
 static int is_whole(const comp_t* c) { return c->n == 1 && c->m[0].whole; }
 
-static int side_start(plan_t* P, int cid, int b, uint32_t col, const uint8_t* need, side_t* s) {
+static int side_start(plan_t* P, int cid, int b, uint32_t col, const uint8_t* need, const int* sel1, side_t* s) {
     const qe_engine* e = P->e;
     comp_t* c = &P->C[cid];
     memset(s, 0, sizeof *s);
@@ -489,6 +492,20 @@ static int side_start(plan_t* P, int cid, int b, uint32_t col, const uint8_t* ne
     member* mb = &c->m[member_idx(c, b)];
     ECHK(rows_of(P, mb));
     ECHK(e->keys(e->u, P->q->rels[b], col, mb->rows, &s->keys));
+    if (e->values && sel1[b] && c->n == 1 && mb->vcol == 0) {
+        /* a filtered list (ascending rowids) read after this join only by selects of one column:
+         * its values ride instead of its rowids (gathered here in order, not at random later) */
+        qe_h v = NONE;
+        const int r = e->values(e->u, P->q->rels[b], (uint32_t)(sel1[b] - 1), mb->rows, &v);
+        if (r == 0) {
+            rel(P, mb->rows);
+            mb->rows = v;
+            mb->vcol = sel1[b];
+        } else if (r != QE_ENOTSUP) {
+            P->rc = r;
+            return r;
+        }
+    }
     qe_h cols[64];
     int nk = 0;
     for (size_t x = 0; x <= P->q->nrels; x++) {               /* carried: the bindings read later */
@@ -496,6 +513,7 @@ static int side_start(plan_t* P, int cid, int b, uint32_t col, const uint8_t* ne
         if (mi < 0 || !need[x]) continue;
         ECHK(rows_of(P, &c->m[mi]));
         s->keep_b[nk] = (int)x;
+        s->keep_v[nk] = c->m[mi].vcol;
         cols[nk++] = c->m[mi].rows;
     }
     s->keep_n = nk;
@@ -513,6 +531,7 @@ static int side_start(plan_t* P, int cid, int b, uint32_t col, const uint8_t* ne
     }
     for (int k = 0; k < nk; k++) {
         s->car_b[k] = s->keep_b[k];
+        s->car_v[k] = s->keep_v[k];
         s->car_rows[k] = cols[k];
     }
     s->ncar = nk;
@@ -537,6 +556,7 @@ static int side_finish(plan_t* P, side_t* s) {
     s->ncar = s->keep_n;
     for (int k = 0; k < s->keep_n; k++) {
         s->car_b[k] = s->keep_b[k];
+        s->car_v[k] = s->keep_v[k];
         s->car_rows[k] = cols[k];
     }
     if (s->keep_n == 1) {
@@ -555,18 +575,18 @@ static void free_comp(plan_t* P, int cid) {
     c->alive = 0;
 }
 
-static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, int last) {
+static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* sel1, int last) {
     const qe_engine* e = P->e;
     const int ba = (int)p->frel, bb = (int)p->srel;
     const int A = component(P, ba), B = component(P, bb);
     side_t sa, sb;
     /* derived sides first, so their exchanges overlap the base side's local bucket scan */
     if (is_whole(&P->C[A])) {
-        ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, &sb));
-        ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, &sa));
+        ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, sel1, &sb));
+        ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, sel1, &sa));
     } else {
-        ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, &sa));
-        ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, &sb));
+        ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, sel1, &sa));
+        ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, sel1, &sb));
     }
     ECHK(side_finish(P, &sa));
     ECHK(side_finish(P, &sb));
@@ -580,7 +600,7 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, int last) {
         for (size_t s = 0; ok && s < q->nsel; s++) {
             src[s] = -1;
             for (int i = 0; i < C->ncar; i++)
-                if (C->car_b[i] == (int)q->sel[2 * s]) src[s] = i;
+                if (C->car_b[i] == (int)q->sel[2 * s]) src[s] = i | (C->car_v[i] ? QE_PLAN_VALUES_SRC : 0);
             ok = src[s] >= 0;
         }
         if (ok) {
@@ -684,6 +704,7 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, int last) {
         side_t* s = sides[k];
         for (int i = 0; i < s->ncar; i++) {
             m[n].b = s->car_b[i];
+            m[n].vcol = s->car_v[i];
             if (made[k][i] != NONE) {                        /* delivered by join_carry */
                 m[n].rows = made[k][i];
                 rel(P, s->car_rows[i]);
@@ -748,6 +769,7 @@ static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t*
     for (size_t i = 0; i < nb; i++) P->comp_of[i] = -1;
     const int reorder = !(getenv("QE_DIST_REORDER") && getenv("QE_DIST_REORDER")[0] == '0');
     uint8_t* need = (uint8_t*)calloc(nb, 1);
+    int* sel1 = (int*)calloc(nb, sizeof(int));
     int* pending = (int*)malloc((q->npreds + 1) * sizeof(int));
     size_t k = 0;
     int rc = 0;
@@ -817,7 +839,24 @@ static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t*
                 need[q->preds[i].frel] = 1;
                 if (q->preds[i].type == 0) need[q->preds[i].srel] = 1;
             }
-            rc = do_join(P, jp, need, np == 0 && end == q->npreds);
+            /* sel1[b] = c + 1: after this join, binding b is read only by selects, all of column c */
+            for (size_t x = 0; x < nb; x++) sel1[x] = 0;
+            for (size_t s = 0; s < q->nsel; s++) {
+                const size_t x = q->sel[2 * s];
+                const int cv = (int)q->sel[2 * s + 1] + 1;
+                sel1[x] = sel1[x] == 0 ? cv : sel1[x] == cv ? cv : -1;
+            }
+            for (size_t i = 0; i < np; i++) {
+                sel1[q->preds[pending[i]].frel] = -1;
+                sel1[q->preds[pending[i]].srel] = -1;
+            }
+            for (size_t i = end; i < q->npreds; i++) {
+                sel1[q->preds[i].frel] = -1;
+                if (q->preds[i].type == 0) sel1[q->preds[i].srel] = -1;
+            }
+            for (size_t x = 0; x < nb; x++)
+                if (sel1[x] < 0) sel1[x] = 0;
+            rc = do_join(P, jp, need, sel1, np == 0 && end == q->npreds);
         }
         k = end;
     }
@@ -836,11 +875,13 @@ static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t*
         const int b = (int)q->sel[2 * s];
         uint64_t size;
         qe_h rows;
+        int vcol = 0;
         if (P->comp_of[b] >= 0) {
             comp_t* c = &P->C[P->comp_of[b]];
             member* m = &c->m[member_idx(c, b)];
             rc = rows_of(P, m);
             rows = m->rows;
+            vcol = m->vcol;
             size = c->size;
         } else {
             rows = P->list[b];
@@ -848,7 +889,7 @@ static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t*
         }
         ssize[s] = size;
         if (size == 0 || rc) continue;
-        srel[ns] = q->rels[b];
+        srel[ns] = vcol ? QE_PLAN_VALUES : q->rels[b];
         scol[ns] = (uint32_t)q->sel[2 * s + 1];
         srows[ns++] = rows;
     }
@@ -876,6 +917,7 @@ static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t*
     free(P->list);
     free(P->list_size);
     free(need);
+    free(sel1);
     free(pending);
     return rc ? rc : P->rc;
 }

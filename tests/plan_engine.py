@@ -36,7 +36,9 @@ FIELDS = [
     ("scan2", C.CFUNCTYPE(I, VP, U32, U32, C.c_char, U64, U32, C.c_char, U64, U64, U64, P(H))),
     ("join_carry", C.CFUNCTYPE(I, VP, H, H, H, H, I, P(H), P(H), P(H), P(H))),
     ("join_sums", C.CFUNCTYPE(I, VP, H, H, H, H, I, P(H), I, P(I), P(U32), P(U32), P(U64), P(U64))),
+    ("values", C.CFUNCTYPE(I, VP, U32, U32, H, P(H))),
 ]
+VALUES, VALUES_SRC = 0xFFFFFFFF, 4   # include/qe_plan.h: QE_PLAN_VALUES, QE_PLAN_VALUES_SRC
 
 
 class Engine(C.Structure):
@@ -68,11 +70,12 @@ def join_local(ka, kb):
 class NumpyPlanEngine:
     """one rank: relations replicated as numpy columns; handles index a dict of arrays"""
 
-    def __init__(self, rels, rank=0, world=1, group=None, fused_scan=True, join_carry=True, join_sums=True):
+    def __init__(self, rels, rank=0, world=1, group=None, fused_scan=True, join_carry=True, join_sums=True, values=True):
         self.rels, self.rank, self.world, self.group = rels, rank, world, group
         self.h, self.next, self.borrowed = {}, 1, set()
         self.exchanges = 0
         self.sums_calls = 0                      # last joins run in aggregate form (join_sums)
+        self.values_calls = 0                    # bindings whose select values ride instead of rowids
         self.mat_limit = 1 << 62
         self.lib = C.CDLL(SO)
         self.lib.qe_plan_run_text.argtypes = [P(Engine), C.c_char_p, P(C.c_void_p), P(C.c_size_t), P(U64), P(U64)]
@@ -85,7 +88,7 @@ class NumpyPlanEngine:
         e.u, e.rank, e.world = None, rank, world
         for name, ftype in FIELDS:
             if (name == "fallback" or (name == "scan2" and not fused_scan) or (name == "join_carry" and not join_carry)
-                    or (name == "join_sums" and not join_sums)):
+                    or (name == "join_sums" and not join_sums) or (name == "values" and not values)):
                 setattr(e, name, ftype())            # NULL: refused queries return QE_ENOTSUP; no fused scan
                 continue
             fn = self._wrap(getattr(self, "cb_" + name), name == "release")
@@ -232,10 +235,18 @@ class NumpyPlanEngine:
             return -5
         pairs[0] = total
         for s in range(nsel):
-            rows = (self.get(vb) if vb else np.arange(len(b), dtype=np.uint32)) if src[s] == 0 \
-                else self.get(cb[src[s] - 1])
+            k = src[s] & 3
+            rows = (self.get(vb) if vb else np.arange(len(b), dtype=np.uint32)) if k == 0 else self.get(cb[k - 1])
+            vals = rows.astype(np.uint64) if src[s] & VALUES_SRC else self.rels[rels[s]][cols[s]][rows]
             with np.errstate(over="ignore"):
-                sums[s] = int(np.sum(cnt * self.rels[rels[s]][cols[s]][rows], dtype=np.uint64))
+                sums[s] = int(np.sum(cnt * vals, dtype=np.uint64))
+
+    def cb_values(self, u, rel, col, rows, out):
+        c = self.rels[rel][col]
+        if len(c) and int(c.max()) >> 32:
+            return -6                            # QE_ENOTSUP: the rowids stay
+        self.values_calls += 1
+        out[0] = self.put(c[self.get(rows)].astype(np.uint32))
 
     def cb_take(self, u, src, idx, out):
         out[0] = self.put(self.get(src)[self.get(idx)])
@@ -245,7 +256,9 @@ class NumpyPlanEngine:
 
     def cb_checksums(self, u, n, rels, cols, rows, sums):
         for i in range(n):
-            sums[i] = int(np.sum(self.rels[rels[i]][cols[i]][self.get(rows[i])], dtype=np.uint64))
+            r = self.get(rows[i])
+            v = r.astype(np.uint64) if rels[i] == VALUES else self.rels[rels[i]][cols[i]][r]
+            sums[i] = int(np.sum(v, dtype=np.uint64))
 
     def cb_allreduce(self, u, v, n):
         if self.world == 1 or n == 0:

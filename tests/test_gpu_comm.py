@@ -195,8 +195,10 @@ def test_dist_executor_carry_falls_back_on_a_skewed_bucket(ctx, comm):
 @pytest.mark.slow
 def test_dist_executor_last_join_in_aggregate_form(ctx, comm, monkeypatch):
     """C3's last join only feeds the checksums: the engine's join_sums returns its pair count and
-    the selects' sums without materialising the pairs (bucket_join_sums) -- the same bytes as the
-    faithful executor and as the materialised last join (QE_PLAN_AGG=0), and the same row count"""
+    the selects' sums without materialising the pairs (bucket_join_sums), and a filtered binding
+    read only by selects of one column carries that column's values instead of its rowids --
+    the same bytes as the faithful executor, as the materialised last join (QE_PLAN_AGG=0) and as
+    rowids throughout (QE_PLAN_VALUES=0), and the same row count"""
     N = 75_000_001
     ctx.drop_relations()
     _loaded["key"] = None
@@ -218,9 +220,10 @@ def test_dist_executor_last_join_in_aggregate_form(ctx, comm, monkeypatch):
             assert (out, rc, refused) == (want, 0, 0), q
             assert ctx.last_result_rows() == rows, q
             assert want_agg is None or agg == want_agg, q
-            monkeypatch.setenv("QE_PLAN_AGG", "0")
-            out0, rc0, _ = ctx.run_dist(q, comm)
-            monkeypatch.delenv("QE_PLAN_AGG")
-            assert (out0, rc0) == (want, 0), q
+            for knob in ("QE_PLAN_AGG", "QE_PLAN_VALUES"):   # materialised last join; rowids, not values
+                monkeypatch.setenv(knob, "0")
+                out0, rc0, _ = ctx.run_dist(q, comm)
+                monkeypatch.delenv(knob)
+                assert (out0, rc0) == (want, 0), (q, knob)
     finally:
         ctx.drop_relations()

@@ -40,7 +40,7 @@ def test_every_golden_is_refused_or_exact(fixture, optional):
     doc = goldens.load(f"{goldens.GOLDEN_DIR}/{fixture}.json")
     rels, _ = goldens.dataset(doc["dataset"])
     on = optional == "all"
-    eng = pe.NumpyPlanEngine(rels, 0, 1, fused_scan=on, join_carry=on, join_sums=on)
+    eng = pe.NumpyPlanEngine(rels, 0, 1, fused_scan=on, join_carry=on, join_sums=on, values=on)
     accepted = {"T": 0, "W": 0}
     for c in doc["cases"]:
         out, rc, _, _ = eng.run(c["input"])
@@ -54,6 +54,7 @@ def test_every_golden_is_refused_or_exact(fixture, optional):
     if fixture in ("c4", "fuzz_a", "fuzz_c", "headline"):
         assert accepted["T"] >= 0.75 * t_cases, accepted   # the relational class is the plan's domain
         assert (eng.sums_calls > 0) == on                  # and its last joins take the aggregate form
+        assert (eng.values_calls > 0) == on                # and select values ride instead of rowids
 
 
 def test_check_names_the_reason():
