@@ -41,6 +41,8 @@ STAGES = [
     (r"heavy_stats_kernel", "heavy_stats"),
     (r"key_bits_kernel", "sort_keybits"),
     (r"tl_hjoin_sums_kernel|hjoin_sums_reduce_kernel", "bucket_join_sums"),
+    (r"gather_u32_kernel", "gather_values"),
+    (r"sum_u32_kernel", "checksum"),
     (r"tl_hjoin_kernel", "bucket_join"),
     (r"mj_fused", "mj_fused"),
     (r"mj_partition", "mj_partition"),
