@@ -51,6 +51,11 @@ __global__ void __launch_bounds__(256) gather_u32_kernel(const uint64_t* __restr
     }
 }
 
+__global__ void __launch_bounds__(256) shift_u32_kernel(uint32_t* __restrict__ a, uint64_t n, uint32_t add) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) a[i] += add;
+}
+
 // sum of a list's own u32 values mod 2^64 (a binding that carries its select's values)
 __global__ void __launch_bounds__(256) sum_u32_kernel(const uint32_t* __restrict__ v, uint64_t n,
                                                       unsigned long long* __restrict__ out) {
@@ -90,7 +95,11 @@ struct DArr : Obj {
     bool u64 = false, owned = true;
     bool bits = false;
     uint64_t kor = 0, kand = 0;
+    // a fused scan's survivors' values of (vrel, vcol) as u32, kept for a later `values` request
+    uint32_t* vcache = nullptr;
+    uint32_t vrel = 0, vcol = 0;
     ~DArr() override {
+        if (vcache) dfree(c, vcache);
         if (owned && d) {
             qe_pairs p{};
             p.key = static_cast<uint64_t*>(d);   // drops a gathered histogram kept for this key buffer
@@ -186,10 +195,31 @@ int e_scan2(void* u, uint32_t rel, uint32_t col1, char op1, uint64_t v1, uint32_
             uint64_t s, uint64_t t, qe_h* out) {
     Eng* e = E(u);
     return guard(e, [&] {
+        qe_ctx* c = e->c;
+        uint64_t kor = 0, kand = 0;
+        const bool vals_on = !(getenv("QE_SCAN_VALUES") && getenv("QE_SCAN_VALUES")[0] == '0');
+        if (vals_on && qe_relation_column_bits(c, (int)rel, (int)col1, &kor, &kand) == 0 && !(kor >> 32)) {
+            // the survivors' col1 values come out of the same pass (the plan may ask for them)
+            const qe_col q1 = column(c, rel, col1), q2 = column(c, rel, col2);
+            if (t > q1.n || t > q2.n || s > t) throw Error(QE_EINVAL, "bad row range");
+            const uint64_t n = t - s;
+            uint32_t* d = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
+            uint32_t* dv = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
+            const uint64_t m = filter_scan2_vals(c, q1.d + s, op1, v1, q2.d + s, op2, v2, n, d, dv);
+            if (s && m) {   // rowids in the relation's numbering (this rank's slice starts at s)
+                hipLaunchKernelGGL(shift_u32_kernel, dim3(grid_for(m, 256)), dim3(256), 0, c->stream, d, m, (uint32_t)s);
+                QE_HIP(hipGetLastError());
+            }
+            DArr* a = new_arr(c, d, m, false);
+            a->vcache = dv;
+            a->vrel = rel;
+            a->vcol = col1;
+            *out = H(a);
+            return;
+        }
         qe_list l{};
-        ck(qe_filter_scan2_range(e->c, column(e->c, rel, col1), op1, v1, column(e->c, rel, col2), op2, v2, s, t, &l),
-           e->c);
-        *out = H(new_arr(e->c, l.d, l.n, false));
+        ck(qe_filter_scan2_range(c, column(c, rel, col1), op1, v1, column(c, rel, col2), op2, v2, s, t, &l), c);
+        *out = H(new_arr(c, l.d, l.n, false));
     });
 }
 
@@ -206,6 +236,10 @@ int e_refine(void* u, uint32_t rel, uint32_t col, qe_h rows, char op, uint64_t v
     Eng* e = E(u);
     return guard(e, [&] {
         DArr* a = A(rows);
+        if (a->vcache) {   // the refined list is a different one: its cached values are stale
+            dfree(e->c, a->vcache);
+            a->vcache = nullptr;
+        }
         qe_list l = as_list(a);
         l.flags = QE_LIST_DISTINCT;
         ck(qe_filter_refine(e->c, column(e->c, rel, col), op, v, &l), e->c);
@@ -559,8 +593,13 @@ int e_values(void* u, uint32_t rel, uint32_t col, qe_h rows, qe_h* out) {
     uint64_t kor = 0, kand = 0;
     if (qe_relation_column_bits(c, (int)rel, (int)col, &kor, &kand) != 0 || (kor >> 32)) return QE_ENOTSUP;
     return guard(e, [&] {
+        DArr* r = A(rows);
+        if (r->vcache && r->vrel == rel && r->vcol == col) {   // made by the scan that made the list
+            *out = H(new_arr(c, r->vcache, r->n, false));
+            r->vcache = nullptr;
+            return;
+        }
         const qe_col q = column(c, rel, col);
-        const DArr* r = A(rows);
         uint32_t* d = dalloc_t<uint32_t>(c, std::max<uint64_t>(r->n, 1));
         if (r->n) {
             Timed t(c, "gather_values", 12.0 * r->n);

@@ -186,6 +186,8 @@ inline unsigned grid_for(uint64_t n, unsigned per_block, unsigned cap = 0x7fffff
 uint64_t filter_scan(qe_ctx* c, const uint64_t* col, uint64_t n, char op, uint64_t v, uint32_t* out);
 uint64_t filter_scan2(qe_ctx* c, const uint64_t* c1, char op1, uint64_t v1, const uint64_t* c2, char op2, uint64_t v2,
                       uint64_t n, uint32_t* out);
+uint64_t filter_scan2_vals(qe_ctx* c, const uint64_t* c1, char op1, uint64_t v1, const uint64_t* c2, char op2,
+                           uint64_t v2, uint64_t n, uint32_t* out, uint32_t* outv);
 uint64_t filter_refine(qe_ctx* c, const uint64_t* col, const uint32_t* in, uint64_t n, char op, uint64_t v,
                        uint32_t* out);
 uint64_t scan_join_k(qe_ctx* c, const uint64_t* rk, const uint32_t* rv, const uint64_t* sk, const uint32_t* sv,

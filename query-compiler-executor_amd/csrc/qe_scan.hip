@@ -73,15 +73,22 @@ struct FilterScan2Op {         // a scan and a refine of the same binding: rowid
     const uint64_t *c1, *c2;
     uint64_t v1, v2;
     uint32_t o1, o2;
-    __device__ __forceinline__ void load(uint64_t base, uint64_t n, bool* f, uint32_t* v0, uint32_t*) const {
+    // (second output, when the launch has one: the survivor's c1 value as u32 -- the values a
+    // binding read only by selects of c1 carries instead of its rowids, engine `values`)
+    __device__ __forceinline__ void load(uint64_t base, uint64_t n, bool* f, uint32_t* v0, uint32_t* vv) const {
         if (base + 1 < n) {
             const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(c1 + base);
             const ulonglong2 y = c2 == c1 ? x : *reinterpret_cast<const ulonglong2*>(c2 + base);
             f[0] = cmp_rt(o1, x.x, v1) && cmp_rt(o2, y.x, v2);
             f[1] = cmp_rt(o1, x.y, v1) && cmp_rt(o2, y.y, v2);
+            vv[0] = (uint32_t)x.x;
+            vv[1] = (uint32_t)x.y;
         } else {
-            f[0] = base < n && cmp_rt(o1, c1[base], v1) && cmp_rt(o2, c2[base], v2);
+            const uint64_t x0 = base < n ? c1[base] : 0;
+            f[0] = base < n && cmp_rt(o1, x0, v1) && cmp_rt(o2, c2[base], v2);
             f[1] = false;
+            vv[0] = (uint32_t)x0;
+            vv[1] = 0;
         }
         v0[0] = (uint32_t)base;
         v0[1] = (uint32_t)(base + 1);
@@ -456,6 +463,14 @@ uint64_t filter_scan2(qe_ctx* c, const uint64_t* c1, char op1, uint64_t v1, cons
     // read 8 B/row per distinct column; 4 B/survivor added below
     const FilterScan2Op o{c1, c2, v1, v2, op_code(op1), op_code(op2)};
     return run_compact<FS_ITEMS, 1>(c, "filter_scan", (c1 == c2 ? 8.0 : 16.0) * n, o, n, out, nullptr);
+}
+
+// the same, with the survivors' c1 values (u32) as a second output; half the tile (two staged
+// outputs in the LDS of one)
+uint64_t filter_scan2_vals(qe_ctx* c, const uint64_t* c1, char op1, uint64_t v1, const uint64_t* c2, char op2,
+                           uint64_t v2, uint64_t n, uint32_t* out, uint32_t* outv) {
+    const FilterScan2Op o{c1, c2, v1, v2, op_code(op1), op_code(op2)};
+    return run_compact<FS_ITEMS / 2, 2>(c, "filter_scan", (c1 == c2 ? 8.0 : 16.0) * n, o, n, out, outv);
 }
 
 uint64_t filter_refine(qe_ctx* c, const uint64_t* col, const uint32_t* in, uint64_t n, char op, uint64_t v,

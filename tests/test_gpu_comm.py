@@ -220,7 +220,8 @@ def test_dist_executor_last_join_in_aggregate_form(ctx, comm, monkeypatch):
             assert (out, rc, refused) == (want, 0, 0), q
             assert ctx.last_result_rows() == rows, q
             assert want_agg is None or agg == want_agg, q
-            for knob in ("QE_PLAN_AGG", "QE_PLAN_VALUES"):   # materialised last join; rowids, not values
+            for knob in ("QE_PLAN_AGG", "QE_PLAN_VALUES", "QE_SCAN_VALUES"):   # materialised last join;
+                # rowids, not values; values gathered after the scan, not emitted by it
                 monkeypatch.setenv(knob, "0")
                 out0, rc0, _ = ctx.run_dist(q, comm)
                 monkeypatch.delenv(knob)
