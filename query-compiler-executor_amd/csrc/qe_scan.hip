@@ -467,10 +467,13 @@ uint64_t filter_scan2(qe_ctx* c, const uint64_t* c1, char op1, uint64_t v1, cons
 
 // the same, with the survivors' c1 values (u32) as a second output; half the tile (two staged
 // outputs in the LDS of one)
+#ifndef QE_FSV_ITEMS
+#define QE_FSV_ITEMS (QE_FS_ITEMS / 2)
+#endif
 uint64_t filter_scan2_vals(qe_ctx* c, const uint64_t* c1, char op1, uint64_t v1, const uint64_t* c2, char op2,
                            uint64_t v2, uint64_t n, uint32_t* out, uint32_t* outv) {
     const FilterScan2Op o{c1, c2, v1, v2, op_code(op1), op_code(op2)};
-    return run_compact<FS_ITEMS / 2, 2>(c, "filter_scan", (c1 == c2 ? 8.0 : 16.0) * n, o, n, out, outv);
+    return run_compact<QE_FSV_ITEMS, 2>(c, "filter_scan", (c1 == c2 ? 8.0 : 16.0) * n, o, n, out, outv);
 }
 
 uint64_t filter_refine(qe_ctx* c, const uint64_t* col, const uint32_t* in, uint64_t n, char op, uint64_t v,
