@@ -130,6 +130,13 @@ void qe_free_host(void*);
  * its queries one after another with no state between them but rand() (src/utilities.c:289-300;
  * the gate excludes rand-dependent outputs), so the order of execution is not observable. */
 int  qe_run_queries_parallel(qe_ctx*, int workers, const char* text, char** out, size_t* outlen);
+/* The concurrent batch with a choice of executor per query: QE_EXEC_FAITHFUL (qe_run_queries'
+ * state machine; = qe_run_queries_parallel) or QE_EXEC_PLAN (each query through the partitioned
+ * plan on its lane's ctx as one rank, the faithful executor for the queries the plan refuses --
+ * qe_run_queries_dist's bytes).  workers <= 1 runs the batch on this ctx. */
+#define QE_EXEC_FAITHFUL 0
+#define QE_EXEC_PLAN 1
+int  qe_run_queries_lanes(qe_ctx*, int workers, int executor, const char* text, char** out, size_t* outlen);
 /* The worker contexts behind qe_run_queries_parallel (made on first use, freed by qe_fini; the
  * relations re-shared at every call); qe_bind_thread makes the ctx's GPU the calling thread's. */
 int  qe_workers(qe_ctx*, int n, qe_ctx** out);
@@ -270,6 +277,21 @@ int  qe_comm_stats(qe_comm*, uint64_t* exchanges, uint64_t* bytes_sent);
  * every rank).  Every rank passes the same text and relations; *out (rank 0) is the reference's
  * stdout; *refused = queries run the faithful way.  Returns 0, QE_EEXIT or an error. */
 int  qe_run_queries_dist(qe_ctx*, qe_comm*, const char* text, char** out, size_t* outlen, uint64_t* refused);
+/* The in-process transport: nranks communicators over ctxs[0..nranks) (contexts of this process --
+ * typically qe_workers of one ctx on ONE GPU, where RCCL refuses a second rank), each rank driven by
+ * its own host thread.  Only the transport differs from qe_comm_init's: the counts all-to-all and the
+ * grouped send/recv become host barriers + device-to-device copies pulled by each receiver, the
+ * all-reduce a host sum; the partitioning, the plan and every kernel are the same code.  A rank that
+ * fails outside a collective breaks the group (its peers return QE_EHIP instead of waiting); a peer
+ * that never arrives times out after QE_LOCAL_TIMEOUT_S seconds (default 600).  Release each with
+ * qe_comm_fini. */
+int  qe_comm_init_local(qe_ctx* const* ctxs, int nranks, qe_comm** out);
+/* qe_run_queries_dist on nranks (1..16) in-process ranks over qe_workers(ctx, nranks) and
+ * qe_comm_init_local, one host thread each: rank 0's bytes and status, *refused = rank 0's
+ * fallback count, *bytes_sent (nullable) = every rank's exchanged bytes (key + carried columns
+ * sent to other ranks).  `queries` runs it with QE_LOCAL_RANKS=N. */
+int  qe_run_queries_local(qe_ctx*, int nranks, const char* text, char** out, size_t* outlen, uint64_t* refused,
+                          uint64_t* bytes_sent);
 
 /* The ctx's HIP stream (hipStream_t), for callers that order their own work against it. */
 int qe_sync_stream_ptr(qe_ctx*, void** stream);

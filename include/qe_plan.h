@@ -98,6 +98,12 @@ typedef struct qe_engine {
      * passed to checksums with rels[k] = QE_PLAN_VALUES (its own sum) and to join_sums with
      * src[s] | QE_PLAN_VALUES_SRC (summed, not gathered). */
     int (*values)(void* u, uint32_t rel, uint32_t col, qe_h rows, qe_h* out);
+    /* the materialisation limit (nullable: none): a join whose pair count summed over every rank
+     * exceeds *mat_limit ends the query with QE_ETOOBIG on every rank (then e->fallback) -- the
+     * reference's DArray bound is on the whole result (src/DArray.h:14-15), so the same query
+     * takes the same branch at any rank count.  (An engine may also refuse a join whose LOCAL
+     * share exceeds it: that share is a lower bound of the global count.) */
+    const uint64_t* mat_limit;
 } qe_engine;
 
 /* Replay the reference's variant choice and list bookkeeping for every query of `text` on the
@@ -114,6 +120,10 @@ const char* qe_plan_why(void);
  * of the last printed query's first select.  *nrefused (nullable): queries sent to the fallback. */
 int qe_plan_run_text(const qe_engine* e, const char* text, char** out, size_t* outlen, uint64_t* rows,
                      uint64_t* nrefused);
+/* One parsed, arranged query (a host/qe_query.h query_t) the same way, printing to the FILE* `out`:
+ * planned when accepted, else (or on QE_ETOOBIG) through e->fallback; *refused = 1 then.  *rows
+ * (nullable) as above.  (The concurrent batch runs its lanes' queries through this.) */
+int qe_plan_run_query(const qe_engine* e, void* query, void* out, uint64_t* rows, int* refused);
 
 #ifdef __cplusplus
 }

@@ -11,7 +11,12 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/qe_plan.h"
@@ -19,8 +24,54 @@
 #include "qe_device.h"
 #include "qe_internal.h"
 
+namespace qe {
+// The in-process transport (qe_comm_init_local): the ranks are host threads of one process, each
+// driving its own ctx -- on a one-GPU box, worker contexts of one device (RCCL refuses two ranks on
+// one device).  It replaces exactly the communicator's three RCCL operations: the all-to-all of
+// the per-destination counts, the grouped send/recv of the partitioned segments (here: each
+// receiver pulls its segment from every sender's partitioned buffer with a device-to-device copy)
+// and the all-reduce (host sums).  Partitioning, offsets, the plan and every kernel are the
+// production code.  Two barriers per operation: the second keeps a sender's posted buffers alive
+// and its posted numbers unchanged until every peer has read them.
+struct LocalGroup {
+    int n = 0, refs = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    bool broken = false;
+    double timeout_s = 600;
+    std::vector<std::array<uint64_t, 64>> red, cnt;
+    std::vector<const uint64_t*> keys;
+    std::vector<std::vector<const uint32_t*>> cols;
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        if (broken) throw Error(QE_EHIP, "local transport: the group is broken (a peer rank failed)");
+        const uint64_t g = gen;
+        if (++arrived == n) {
+            arrived = 0;
+            gen++;
+            cv.notify_all();
+            return;
+        }
+        // a peer that never arrives (it failed outside the transport) must not hang the others
+        if (!cv.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] { return gen != g || broken; }) || broken) {
+            broken = true;
+            cv.notify_all();
+            throw Error(QE_EHIP, "local transport: a peer rank did not reach the exchange (timeout or failure)");
+        }
+    }
+    void fail() {
+        std::lock_guard<std::mutex> lk(mu);
+        broken = true;
+        cv.notify_all();
+    }
+};
+}  // namespace qe
+
 struct qe_comm {
     ncclComm_t comm = nullptr;
+    qe::LocalGroup* local = nullptr;  // in-process transport instead of RCCL (qe_comm_init_local)
     int nranks = 1, rank = 0;
     hipStream_t stream = nullptr;     // exchanges run here, overlapped with the ctx stream's work
     uint64_t* d_red = nullptr;        // all-reduce staging (64 words)
@@ -145,6 +196,12 @@ qe_list as_list(const DArr* a) {
     return l;
 }
 
+// a rank that fails outside the plan's agreed outcomes (ETOOBIG and ENOTSUP are all-reduced by the
+// plan) will not reach its peers' next collective: an in-process group is told so at once
+inline void peer_failed(Eng* e, int code) {
+    if (code != QE_ETOOBIG && code != QE_ENOTSUP && e->comm && e->comm->local) e->comm->local->fail();
+}
+
 template <class F>
 int guard(Eng* e, F f) {
     try {
@@ -152,9 +209,11 @@ int guard(Eng* e, F f) {
         return 0;
     } catch (const Error& x) {
         e->c->err = x.what();
+        peer_failed(e, x.code);
         return x.code;
     } catch (const std::exception& x) {
         e->c->err = x.what();
+        peer_failed(e, QE_EINVAL);
         return QE_EINVAL;
     }
 }
@@ -342,11 +401,25 @@ int e_exchange_start(void* u, qe_h keys, const qe_h* cols, int ncols, qe_h* tick
         QE_HIP(hipEventRecord(ready, c->stream));
         QE_HIP(hipStreamWaitEvent(m->stream, ready, 0));
         QE_HIP(hipEventDestroy(ready));
-        QE_NCCL(ncclAllToAll(cnt, cnt + 128, 1, ncclUint64, m->comm, m->stream));
         uint64_t hc[2 * 64];
-        QE_HIP(hipMemcpyAsync(hc, cnt, 64 * sizeof(uint64_t), hipMemcpyDeviceToHost, m->stream));
-        QE_HIP(hipMemcpyAsync(hc + 64, cnt + 128, 64 * sizeof(uint64_t), hipMemcpyDeviceToHost, m->stream));
-        QE_HIP(hipStreamSynchronize(m->stream));       // the one host round trip: receive sizes
+        LocalGroup* g = m->local;
+        if (g) {   // counts all-to-all: post this rank's send counts and segments, read the peers'
+            QE_HIP(hipMemcpyAsync(hc, cnt, 64 * sizeof(uint64_t), hipMemcpyDeviceToHost, m->stream));
+            QE_HIP(hipStreamSynchronize(m->stream));   // (the partitioned segments are complete too)
+            std::copy(hc, hc + W, g->cnt[e->rank].begin());
+            g->keys[e->rank] = sk;
+            g->cols[e->rank].assign(scols.begin(), scols.end());
+            g->barrier();
+            for (int p = 0; p < W; p++) {
+                if ((int)g->cols[p].size() != ncols) throw Error(QE_EINVAL, "internal: ranks exchange different columns");
+                hc[64 + p] = g->cnt[p][e->rank];
+            }
+        } else {
+            QE_NCCL(ncclAllToAll(cnt, cnt + 128, 1, ncclUint64, m->comm, m->stream));
+            QE_HIP(hipMemcpyAsync(hc, cnt, 64 * sizeof(uint64_t), hipMemcpyDeviceToHost, m->stream));
+            QE_HIP(hipMemcpyAsync(hc + 64, cnt + 128, 64 * sizeof(uint64_t), hipMemcpyDeviceToHost, m->stream));
+            QE_HIP(hipStreamSynchronize(m->stream));   // the one host round trip: receive sizes
+        }
         uint64_t soff[64], roff[64], total = 0, run = 0;
         for (int p = 0; p < W; p++) {
             soff[p] = run;
@@ -362,17 +435,34 @@ int e_exchange_start(void* u, qe_h keys, const qe_h* cols, int ncols, qe_h* tick
         t->keys = rk;
         for (int i = 0; i < ncols; i++)
             t->cols.push_back(new_arr(c, dalloc_t<uint32_t>(c, std::max<uint64_t>(total, 1)), total, false));
-        QE_NCCL(ncclGroupStart());
-        for (int p = 0; p < W; p++) {
-            QE_NCCL(ncclSend(sk + soff[p], hc[p], ncclUint64, p, m->comm, m->stream));
-            QE_NCCL(ncclRecv(static_cast<uint64_t*>(rk->d) + roff[p], hc[64 + p], ncclUint64, p, m->comm, m->stream));
-            for (int i = 0; i < ncols; i++) {
-                QE_NCCL(ncclSend(scols[i] + soff[p], hc[p], ncclUint32, p, m->comm, m->stream));
-                QE_NCCL(ncclRecv(static_cast<uint32_t*>(t->cols[i]->d) + roff[p], hc[64 + p], ncclUint32, p, m->comm,
-                                 m->stream));
+        if (g) {   // the grouped send/recv: pull segment `rank` of every sender
+            for (int p = 0; p < W; p++) {
+                const uint64_t nr = hc[64 + p];
+                if (!nr) continue;
+                uint64_t so = 0;                       // the sender's segment offset for this rank
+                for (int q = 0; q < e->rank; q++) so += g->cnt[p][q];
+                QE_HIP(hipMemcpyAsync(static_cast<uint64_t*>(rk->d) + roff[p], g->keys[p] + so, nr * 8,
+                                      hipMemcpyDeviceToDevice, m->stream));
+                for (int i = 0; i < ncols; i++)
+                    QE_HIP(hipMemcpyAsync(static_cast<uint32_t*>(t->cols[i]->d) + roff[p], g->cols[p][i] + so, nr * 4,
+                                          hipMemcpyDeviceToDevice, m->stream));
             }
+            QE_HIP(hipStreamSynchronize(m->stream));
+            g->barrier();                              // every peer has its segments: sends may be freed
+        } else {
+            QE_NCCL(ncclGroupStart());
+            for (int p = 0; p < W; p++) {
+                QE_NCCL(ncclSend(sk + soff[p], hc[p], ncclUint64, p, m->comm, m->stream));
+                QE_NCCL(ncclRecv(static_cast<uint64_t*>(rk->d) + roff[p], hc[64 + p], ncclUint64, p, m->comm,
+                                 m->stream));
+                for (int i = 0; i < ncols; i++) {
+                    QE_NCCL(ncclSend(scols[i] + soff[p], hc[p], ncclUint32, p, m->comm, m->stream));
+                    QE_NCCL(ncclRecv(static_cast<uint32_t*>(t->cols[i]->d) + roff[p], hc[64 + p], ncclUint32, p,
+                                     m->comm, m->stream));
+                }
+            }
+            QE_NCCL(ncclGroupEnd());
         }
-        QE_NCCL(ncclGroupEnd());
         QE_HIP(hipEventCreateWithFlags(&t->done, hipEventDisableTiming));
         QE_HIP(hipEventRecord(t->done, m->stream));
         m->exchanges++;
@@ -497,16 +587,17 @@ int e_join_sums(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h*
             }
             qe_pairs P = side_pairs(A(ka), va ? A(va) : nullptr);
             qe_pairs Q = side_pairs(A(kb), vb ? A(vb) : nullptr);
+            // the sort may replace P / Q by buffers of its own: released on every exit, a throw included
+            struct Release {
+                qe_ctx* c;
+                qe_pairs *p, *q;
+                ~Release() {
+                    qe_pairs_free(c, p);
+                    qe_pairs_free(c, q);
+                }
+            } release{c, &P, &Q};
             done = join_pairs_sums(c, &P, &Q, nb >= 1 ? static_cast<const uint32_t*>(A(cb[0])->d) : nullptr,
                                    nb == 2 ? static_cast<const uint32_t*>(A(cb[1])->d) : nullptr, sc, pairs, sums);
-            qe_pairs_free(c, &P);
-            qe_pairs_free(c, &Q);
-            if (done && *pairs > c->mat_limit) {   // the same limit the materialising join keeps
-                char msg[160];
-                snprintf(msg, sizeof msg, "join of %llu pairs exceeds the materialisation limit %llu",
-                         (unsigned long long)*pairs, (unsigned long long)c->mat_limit);
-                throw Error(QE_ETOOBIG, msg);
-            }
         });
         if (rc != 0 || done) return rc;
     }
@@ -656,6 +747,38 @@ struct StdoutToStderr {
     }
 };
 
+// libqe's engine for the partitioned plan (include/qe_plan.h)
+qe_engine make_engine(Eng* e) {
+    qe_engine g{};
+    g.u = e;
+    g.rank = (uint32_t)e->rank;
+    g.world = (uint32_t)e->world;
+    g.rel_count = e_rel_count;
+    g.rel_shape = e_rel_shape;
+    g.scan = e_scan;
+    g.iota = e_iota;
+    g.refine = e_refine;
+    g.scan2 = e_scan2;
+    g.keys = e_keys;
+    g.base_side = e_base_side;
+    g.exchange_start = e_exchange_start;
+    g.exchange_finish = e_exchange_finish;
+    g.join = e_join;
+    g.take = e_take;
+    g.join_carry = e_join_carry;
+    // the last join in aggregate form (QE_PLAN_AGG=0: materialised, then summed -- A/B)
+    g.join_sums = getenv("QE_PLAN_AGG") && getenv("QE_PLAN_AGG")[0] == '0' ? nullptr : e_join_sums;
+    // select values carried instead of rowids (QE_PLAN_VALUES=0: rowids -- A/B)
+    g.values = getenv("QE_PLAN_VALUES") && getenv("QE_PLAN_VALUES")[0] == '0' ? nullptr : e_values;
+    g.length = e_length;
+    g.checksums = e_checksums;
+    g.allreduce = e_allreduce;
+    g.release = e_release;
+    g.fallback = e_fallback;
+    g.mat_limit = &e->c->mat_limit;
+    return g;
+}
+
 }  // namespace
 }  // namespace qe
 
@@ -697,9 +820,102 @@ int qe_comm_init(qe_ctx* c, int nranks, int rank, const uint8_t* id, qe_comm** o
     QE_API_END(c)
 }
 
+int qe_comm_init_local(qe_ctx* const* ctxs, int nranks, qe_comm** out) {
+    qe_ctx* c0 = ctxs && nranks > 0 ? ctxs[0] : nullptr;
+    QE_API_BEGIN(c0)
+    if (!c0 || nranks < 1 || nranks > 64) throw Error(QE_EINVAL, "1..64 ranks, one ctx each");
+    for (int r = 0; r < nranks; r++) {
+        if (!ctxs[r]) throw Error(QE_EINVAL, "null ctx");
+        out[r] = nullptr;
+    }
+    LocalGroup* g = new LocalGroup;
+    g->n = nranks;
+    g->red.resize(nranks);
+    g->cnt.resize(nranks);
+    g->keys.assign(nranks, nullptr);
+    g->cols.resize(nranks);
+    if (const char* t = getenv("QE_LOCAL_TIMEOUT_S")) g->timeout_s = atof(t);
+    try {
+        for (int r = 0; r < nranks; r++) {
+            qe_comm* m = new qe_comm;
+            m->nranks = nranks;
+            m->rank = r;
+            m->local = g;
+            g->refs++;
+            out[r] = m;
+            QE_HIP(hipSetDevice(ctxs[r]->device));
+            QE_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+        }
+    } catch (...) {
+        if (g->refs == 0) delete g;            // else the last qe_comm_fini deletes it
+        for (int r = 0; r < nranks; r++)
+            if (out[r]) qe_comm_fini(out[r]);
+        throw;
+    }
+    return 0;
+    QE_API_END(c0)
+}
+
+int qe_run_queries_local(qe_ctx* c, int nranks, const char* text, char** out, size_t* outlen, uint64_t* refused,
+                         uint64_t* bytes_sent) {
+    QE_API_BEGIN(c)
+    *out = nullptr;
+    *outlen = 0;
+    if (nranks < 1 || nranks > 16) throw Error(QE_EINVAL, "1..16 in-process ranks");
+    qe_ctx* w[16];
+    ck(qe_workers(c, nranks, w), c);
+    qe_comm* m[16];
+    ck(qe_comm_init_local(w, nranks, m), w[0]);
+    std::vector<char*> outs(nranks, nullptr);
+    std::vector<size_t> lens(nranks, 0);
+    std::vector<uint64_t> ref(nranks, 0);
+    std::vector<int> rcs(nranks, 0);
+    std::vector<std::thread> th;
+    for (int r = 0; r < nranks; r++)
+        th.emplace_back([&, r] {
+            qe_bind_thread(w[r]);
+            rcs[r] = qe_run_queries_dist(w[r], m[r], text, &outs[r], &lens[r], &ref[r]);
+            if (rcs[r] != 0 && rcs[r] != QE_EEXIT) m[r]->local->fail();   // never leave a peer waiting
+        });
+    for (auto& t : th) t.join();
+    uint64_t sent = 0;
+    for (int r = 0; r < nranks; r++) {
+        uint64_t x = 0, b = 0;
+        qe_comm_stats(m[r], &x, &b);
+        sent += b;
+        qe_comm_fini(m[r]);
+    }
+    if (bytes_sent) *bytes_sent = sent;
+    if (refused) *refused = ref[0];
+    c->last_result_rows = w[0]->last_result_rows;
+    int rc = rcs[0];
+    for (int r = 0; r < nranks && rc == 0; r++)
+        if (rcs[r] != 0) rc = rcs[r];
+    for (int r = 0; r < nranks; r++)
+        if (rcs[r] != 0 && rcs[r] != QE_EEXIT) {
+            c->err = "rank " + std::to_string(r) + ": " + w[r]->err;
+            rc = rcs[r];
+            break;
+        }
+    for (int r = 1; r < nranks; r++) free(outs[r]);
+    *out = outs[0];
+    *outlen = lens[0];
+    return rc;
+    QE_API_END(c)
+}
+
 void qe_comm_fini(qe_comm* m) {
     if (!m) return;
     if (m->stream) (void)hipStreamSynchronize(m->stream);
+    if (m->local) {
+        LocalGroup* g = m->local;
+        bool last;
+        {
+            std::lock_guard<std::mutex> lk(g->mu);
+            last = --g->refs == 0;
+        }
+        if (last) delete g;
+    }
     if (m->comm) {
         StdoutToStderr quiet;
         ncclCommDestroy(m->comm);
@@ -714,6 +930,22 @@ int qe_allreduce_u64(qe_ctx* c, qe_comm* m, uint64_t* vals, int n) {
     QE_API_BEGIN(c)
     if (n < 0 || n > 64) throw Error(QE_EINVAL, "at most 64 values per all-reduce");
     if (!m || n == 0) return 0;        // (one rank still goes through RCCL: the tested path)
+    if (LocalGroup* g = m->local) {    // in-process ranks: post, sum every rank's values, release
+        try {
+            std::copy(vals, vals + n, g->red[m->rank].begin());
+            g->barrier();
+            for (int i = 0; i < n; i++) {
+                uint64_t s = 0;
+                for (int p = 0; p < g->n; p++) s += g->red[p][i];
+                vals[i] = s;
+            }
+            g->barrier();
+        } catch (...) {
+            g->fail();
+            throw;
+        }
+        return 0;
+    }
     std::memcpy(m->h_red, vals, n * sizeof(uint64_t));
     // every RCCL call of the communicator goes on its one stream (so no two of them can run in a
     // different order on two ranks); the values are host numbers, nothing to wait for on the ctx
@@ -775,35 +1007,20 @@ int qe_comm_stats(qe_comm* m, uint64_t* exchanges, uint64_t* bytes_sent) {
 int qe_run_queries_dist(qe_ctx* c, qe_comm* m, const char* text, char** out, size_t* outlen, uint64_t* refused) {
     if (!c) return QE_EINVAL;
     Eng e{c, m, m ? m->nranks : 1, m ? m->rank : 0, 0};
-    qe_engine g{};
-    g.u = &e;
-    g.rank = (uint32_t)e.rank;
-    g.world = (uint32_t)e.world;
-    g.rel_count = e_rel_count;
-    g.rel_shape = e_rel_shape;
-    g.scan = e_scan;
-    g.iota = e_iota;
-    g.refine = e_refine;
-    g.scan2 = e_scan2;
-    g.keys = e_keys;
-    g.base_side = e_base_side;
-    g.exchange_start = e_exchange_start;
-    g.exchange_finish = e_exchange_finish;
-    g.join = e_join;
-    g.take = e_take;
-    g.join_carry = e_join_carry;
-    // the last join in aggregate form (QE_PLAN_AGG=0: materialised, then summed -- A/B)
-    g.join_sums = getenv("QE_PLAN_AGG") && getenv("QE_PLAN_AGG")[0] == '0' ? nullptr : e_join_sums;
-    // select values carried instead of rowids (QE_PLAN_VALUES=0: rowids -- A/B)
-    g.values = getenv("QE_PLAN_VALUES") && getenv("QE_PLAN_VALUES")[0] == '0' ? nullptr : e_values;
-    g.length = e_length;
-    g.checksums = e_checksums;
-    g.allreduce = e_allreduce;
-    g.release = e_release;
-    g.fallback = e_fallback;
+    qe_engine g = make_engine(&e);
     uint64_t rows = c->last_result_rows, nref = 0;
     int rc = qe_plan_run_text(&g, text, out, outlen, &rows, &nref);
     if (refused) *refused = nref;
+    c->last_result_rows = rows;
+    return rc;
+}
+
+int qe_plan_exec_query(qe_ctx* c, query_t* q, FILE* out) {
+    Eng e{c, nullptr, 1, 0, 0};
+    qe_engine g = make_engine(&e);
+    uint64_t rows = c->last_result_rows;
+    int refused = 0;
+    const int rc = qe_plan_run_query(&g, q, out, &rows, &refused);
     c->last_result_rows = rows;
     return rc;
 }

@@ -557,7 +557,8 @@ int qe_bucket_select(qe_ctx* c, qe_col col, uint32_t nparts, uint32_t part, cons
     unsigned long long* d_cnt = reinterpret_cast<unsigned long long*>(c->d_scratch);
     // grid-stride over sub-tiles with exactly the resident blocks (a second round of blocks would
     // run behind the first on a fraction of the CUs)
-    static int cus = 0, per_cu = 0;
+    static int cus = 0;
+    int per_cu = 0;
     const size_t dyn = (size_t)nheavy * sizeof(uint64_t);
     if (!cus) QE_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
     QE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bucket_select_kernel, BS_B, dyn));

@@ -25,17 +25,22 @@
 /* ------------------------------------------------------------------------------------------ */
 
 typedef struct {                 /* mid_result (src/structs.h:44-49), list in HBM */
-    uint64_t relation, pid;
-    int32_t lcs;
+    qe_mid_t h;                  /* relation, predicate id (binding), last_column_sorted */
     qe_list* list;
 } mid_t;
 
 typedef struct { mid_t* e; size_t n, cap; } entity_t;
 typedef struct { entity_t** v; size_t n, cap; } mra_t;
 
-typedef struct { ptrdiff_t ent, idx; } exists_t;
+typedef qe_where_t exists_t;
 
-enum { CLASSIC_JOIN = 1, JOIN_SORT_LHS = 2, JOIN_SORT_RHS = 3, SCAN_JOIN = 4, DO_NOTHING = 5 };
+enum {
+    CLASSIC_JOIN = QE_CLASSIC_JOIN,
+    JOIN_SORT_LHS = QE_JOIN_SORT_LHS,
+    JOIN_SORT_RHS = QE_JOIN_SORT_RHS,
+    SCAN_JOIN = QE_SCAN_JOIN,
+    DO_NOTHING = QE_DO_NOTHING
+};
 
 typedef struct {
     qe_ctx* q;
@@ -136,25 +141,21 @@ static void mra_free(mra_t* M) {
     memset(M, 0, sizeof(*M));
 }
 
-/* relation_exists: newest entity first, first match (src/utilities.c:164-181) */
-static exists_t relation_exists(const mra_t* M, uint64_t relation, uint64_t pid) {
-    exists_t ex = {-1, -1};
-    for (ptrdiff_t i = (ptrdiff_t)M->n - 1; i >= 0; i--)
-        for (size_t j = 0; j < M->v[i]->n; j++)
-            if (M->v[i]->e[j].relation == relation && M->v[i]->e[j].pid == pid) {
-                ex.ent = i;
-                ex.idx = (ptrdiff_t)j;
-                return ex;
-            }
-    return ex;
+/* mid_results_array as the shared view (host/qe_query.h) */
+static size_t v_count(void* u) { return ((mra_t*)u)->n; }
+static size_t v_size(void* u, size_t ent) { return ((mra_t*)u)->v[ent]->n; }
+static qe_mid_t* v_at(void* u, size_t ent, size_t idx) { return &((mra_t*)u)->v[ent]->e[idx].h; }
+static void v_push_entity(void* u) { (void)new_entity((mra_t*)u); }
+
+static qe_mids view(const mra_t* M) {
+    qe_mids v = {(void*)M, v_count, v_size, v_at, v_push_entity};
+    return v;
 }
 
-/* relation_exists_current: last match in one entity (src/utilities.c:183-194) */
-static ptrdiff_t relation_exists_current(const entity_t* E, uint64_t relation, uint64_t pid) {
-    ptrdiff_t f = -1;
-    for (size_t i = 0; i < E->n; i++)
-        if (E->e[i].relation == relation && E->e[i].pid == pid) f = (ptrdiff_t)i;
-    return f;
+/* relation_exists (src/utilities.c:164-181) */
+static exists_t relation_exists(const mra_t* M, uint64_t relation, uint64_t pid) {
+    const qe_mids v = view(M);
+    return qe_mid_exists(&v, relation, pid);
 }
 
 static qe_col column(exec_t* x, uint64_t relation, uint64_t col) {
@@ -204,17 +205,17 @@ static void fix_all(exec_t* x, const jres_t* jr, exists_t ex, mra_t* M, uint32_t
     size_t nedit = 0, npick = 0;
     ptrdiff_t first_edit = -1;
     for (size_t i = 0; i < E->n; i++)
-        if (E->e[i].relation != relR && E->e[i].relation != relS) {
+        if (E->e[i].h.relation != relR && E->e[i].h.relation != relS) {
             nedit++;
             if (first_edit < 0) first_edit = (ptrdiff_t)i;
-            if (!x->dle || x->live[E->e[i].pid]) {
+            if (!x->dle || x->live[E->e[i].h.pid]) {
                 pick[i] = 1;
                 npick++;
             }
         }
     if (nedit) {
         for (size_t i = 0; i < E->n; i++)   /* join_payloads' guard, on every entry, dead or not */
-            if (E->e[i].relation != relR && E->e[i].relation != relS && E->e[i].list->n < update->n) {
+            if (E->e[i].h.relation != relR && E->e[i].h.relation != relS && E->e[i].list->n < update->n) {
                 free(pick);
                 fail(x, QE_EINVAL, "join_payloads on lists of different lengths (reference-undefined)");
             }
@@ -233,7 +234,7 @@ static void fix_all(exec_t* x, const jres_t* jr, exists_t ex, mra_t* M, uint32_t
         qe_list* outs = NULL;
         if (npick) {
             need_data(x, update);
-            uint64_t rows = rows_of(x, E->e[ex.idx].relation);
+            uint64_t rows = rows_of(x, E->e[ex.idx].h.relation);
             uint32_t* counts = NULL;
             chk(x, qe_driver_counts(x->q, jr->R, jr->S, jr->res[0], jr->res[1], mode, rows, &counts));
             const qe_list** edits = (const qe_list**)malloc(npick * sizeof(qe_list*));
@@ -258,7 +259,7 @@ static void fix_all(exec_t* x, const jres_t* jr, exists_t ex, mra_t* M, uint32_t
         size_t k = 0;
         for (size_t i = 0; i < E->n; i++) {
             mid_t* ed = &E->e[i];
-            if (ed->relation == relR || ed->relation == relS) continue;
+            if (ed->h.relation == relR || ed->h.relation == relS) continue;
             qe_list* nl = new_list(x);
             if (pick[i]) {
                 *nl = outs[k++];
@@ -277,8 +278,8 @@ static void fix_all(exec_t* x, const jres_t* jr, exists_t ex, mra_t* M, uint32_t
 /* update_mid_results (src/join.c:507-628) */
 static void update_mid_results(exec_t* x, const jres_t* jr, mra_t* M, uint64_t relR, uint64_t predR, uint64_t colR,
                                uint64_t relS, uint64_t predS, uint64_t colS, int join_id) {
-    mid_t tR = {relR, predR, (int32_t)colR, jr->res[0]};
-    mid_t tS = {relS, predS, (int32_t)colS, jr->res[1]};
+    mid_t tR = {{relR, predR, (int32_t)colR}, jr->res[0]};
+    mid_t tS = {{relS, predS, (int32_t)colS}, jr->res[1]};
     exists_t ex;
     switch (join_id) {
     case CLASSIC_JOIN:
@@ -316,69 +317,18 @@ static void update_mid_results(exec_t* x, const jres_t* jr, mra_t* M, uint64_t r
     }
 }
 
-/* build_relations (src/join.c:152-292): pick the variant, gather both inputs */
+/* build_relations (src/join.c:152-292): the variant (host/qe_query.c, shared with the plan's
+ * replay), then both inputs gathered from the entries it names (NULL: the whole base relation) */
 static int build_relations(exec_t* x, const query_t* q, const pred_t* p, mra_t* M, qe_pairs rel[2],
                            const qe_list* src[2]) {
-    uint64_t lhs_rel = q->rels[p->frel], lhs_col = p->fcol;
-    uint64_t rhs_rel = q->rels[p->srel], rhs_col = p->scol;
-    if (lhs_rel == rhs_rel && lhs_col == rhs_col) return DO_NOTHING;
-    entity_t* E = M->n == 0 ? new_entity(M) : M->v[M->n - 1];
-    ptrdiff_t li = relation_exists_current(E, lhs_rel, p->frel);
-    ptrdiff_t ri = relation_exists_current(E, rhs_rel, p->srel);
-    if (li != -1 && ri == -1) {
-        src[0] = E->e[li].list;
-        gather(x, &rel[0], lhs_rel, lhs_col, src[0]);
-        exists_t ex = relation_exists(M, rhs_rel, p->srel);
-        mid_t* T = NULL;
-        if (ex.idx != -1) {
-            T = &M->v[ex.ent]->e[ex.idx];
-            src[1] = T->list;
-        }
-        gather(x, &rel[1], rhs_rel, rhs_col, src[1]);
-        mid_t* mid = &E->e[li];
-        if (!T) {
-            if (mid->lcs == (int32_t)lhs_col) return JOIN_SORT_RHS;
-            mid->lcs = (int32_t)lhs_col;
-            return CLASSIC_JOIN;
-        }
-        if (mid->lcs == (int32_t)lhs_col && T->lcs == (int32_t)rhs_col) return SCAN_JOIN;
-        if (mid->lcs == (int32_t)lhs_col) return JOIN_SORT_RHS;
-        if (T->lcs == (int32_t)rhs_col) return JOIN_SORT_LHS;
-        return CLASSIC_JOIN;
-    }
-    if (li != -1 && ri != -1) {
-        src[0] = E->e[li].list;
-        gather(x, &rel[0], lhs_rel, lhs_col, src[0]);
-        src[1] = E->e[ri].list;
-        gather(x, &rel[1], rhs_rel, rhs_col, src[1]);
-        return SCAN_JOIN;
-    }
-    if (li == -1 && ri != -1) {
-        src[1] = E->e[ri].list;
-        gather(x, &rel[1], rhs_rel, rhs_col, src[1]);
-        exists_t ex = relation_exists(M, lhs_rel, p->frel);
-        mid_t* T = NULL;
-        if (ex.idx != -1) {
-            T = &M->v[ex.ent]->e[ex.idx];
-            src[0] = T->list;
-        }
-        gather(x, &rel[0], lhs_rel, lhs_col, src[0]);
-        mid_t* mid = &E->e[ri];
-        if (!T) {
-            if (mid->lcs == (int32_t)rhs_col) return JOIN_SORT_LHS;
-            mid->lcs = (int32_t)rhs_col;
-            return CLASSIC_JOIN;
-        }
-        if (mid->lcs == (int32_t)rhs_col && T->lcs == (int32_t)lhs_col) return SCAN_JOIN;
-        if (mid->lcs == (int32_t)rhs_col) return JOIN_SORT_RHS;   /* reference quirk, src/join.c:258-259 */
-        if (mid->lcs == (int32_t)lhs_col) return JOIN_SORT_LHS;   /* reference quirk, src/join.c:261-262 */
-        return CLASSIC_JOIN;
-    }
-    new_entity(M);                                                /* src/join.c:270-285 */
-    gather(x, &rel[1], rhs_rel, rhs_col, NULL);
-    gather(x, &rel[0], lhs_rel, lhs_col, NULL);
-    if (rhs_rel != lhs_rel || p->frel != p->srel) return CLASSIC_JOIN;
-    return SCAN_JOIN;
+    const qe_mids v = view(M);
+    const qe_join_choice_t j = qe_build_relations(&v, q, p);
+    if (j.variant == DO_NOTHING) return DO_NOTHING;
+    src[0] = j.lhs.ent >= 0 ? M->v[j.lhs.ent]->e[j.lhs.idx].list : NULL;
+    src[1] = j.rhs.ent >= 0 ? M->v[j.rhs.ent]->e[j.rhs.idx].list : NULL;
+    gather(x, &rel[0], q->rels[p->frel], p->fcol, src[0]);
+    gather(x, &rel[1], q->rels[p->srel], p->scol, src[1]);
+    return j.variant;
 }
 
 /* fix_all on this entity would re-materialise nothing: it holds no other relation's entry */
@@ -386,7 +336,7 @@ static int fix_all_trivial(const mra_t* M, exists_t ex, uint64_t relR, uint64_t 
     if (ex.idx == -1) return 1;
     const entity_t* E = M->v[ex.ent];
     for (size_t i = 0; i < E->n; i++)
-        if (E->e[i].relation != relR && E->e[i].relation != relS) return 0;
+        if (E->e[i].h.relation != relR && E->e[i].h.relation != relS) return 0;
     return 1;
 }
 
@@ -565,7 +515,7 @@ static int execute_filter(exec_t* x, const query_t* q, const pred_t* p, mra_t* M
         }
         fprintf(x->out, "%d\n", (int)(uint32_t)l->n);             /* src/filter.c:32 */
     } else {                                                      /* exec_filter_rel_no_exists */
-        mid_t m = {relation, p->frel, -1, new_list(x)};
+        mid_t m = {{relation, p->frel, -1}, new_list(x)};
         entity_push(E, m);
         qe_list* l = m.list;
         if (!op_valid(p->op)) {
@@ -776,6 +726,7 @@ typedef struct {
     size_t* lens;
     int* rcs;
     atomic_int* stop;          /* the first query index known to end the batch (+1), 0 none */
+    int plan;                  /* QE_EXEC_PLAN: the partitioned plan, faithful fallback */
 } lane_t;
 
 static void* lane_main(void* arg) {
@@ -794,7 +745,7 @@ static void* lane_main(void* arg) {
             L->rcs[i] = QE_ENOMEM;
         } else {
             qe_arrange_predicates(&L->qs[i]);
-            L->rcs[i] = qe_exec_query(L->ctx, &L->qs[i], f);
+            L->rcs[i] = L->plan ? qe_plan_exec_query(L->ctx, &L->qs[i], f) : qe_exec_query(L->ctx, &L->qs[i], f);
             fclose(f);
         }
         if (L->rcs[i] != 0) {                   /* remember the earliest failing query */
@@ -807,9 +758,19 @@ static void* lane_main(void* arg) {
 }
 
 int qe_run_queries_parallel(qe_ctx* ctx, int workers, const char* text, char** out, size_t* outlen) {
+    return qe_run_queries_lanes(ctx, workers, QE_EXEC_FAITHFUL, text, out, outlen);
+}
+
+int qe_run_queries_lanes(qe_ctx* ctx, int workers, int executor, const char* text, char** out, size_t* outlen) {
     *out = NULL;
     *outlen = 0;
-    if (workers <= 1) return qe_run_queries(ctx, text, out, outlen);
+    if (executor != QE_EXEC_FAITHFUL && executor != QE_EXEC_PLAN) return QE_EINVAL;
+    const int plan = executor == QE_EXEC_PLAN;
+    if (workers <= 1) {
+        if (!plan) return qe_run_queries(ctx, text, out, outlen);
+        uint64_t refused = 0;
+        return qe_run_queries_dist(ctx, NULL, text, out, outlen, &refused);
+    }
     qe_ctx* w[16];
     int rc = qe_workers(ctx, workers, w);
     if (rc != 0) return rc;
@@ -824,7 +785,7 @@ int qe_run_queries_parallel(qe_ctx* ctx, int workers, const char* text, char** o
     pthread_t th[16];
     int started = 0;
     for (int k = 0; k < workers; k++) {
-        lane_t l = {w[k], qs, nq, &next, outs, lens, rcs, &stop};
+        lane_t l = {w[k], qs, nq, &next, outs, lens, rcs, &stop, plan};
         lanes[k] = l;
         if (pthread_create(&th[k], NULL, lane_main, &lanes[k]) == 0) started++;
         else break;

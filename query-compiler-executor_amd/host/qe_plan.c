@@ -32,7 +32,7 @@ const char* qe_plan_why(void) { return g_why; }
  * (rows of one tuple sequence); len: lists with one len id have equal lengths; distinct: no rowid
  * twice; sorted: the binding column it is ascending on (-1: none). */
 typedef struct { int tag, len, ok, distinct, sorted; } slist;
-typedef struct { uint64_t relation, pid; int32_t lcs; int l; } smid;   /* mid_result, list by index */
+typedef struct { qe_mid_t h; int l; } smid;   /* mid_result, list by index */
 typedef struct { smid* e; size_t n; } sent;
 
 typedef struct {
@@ -79,25 +79,22 @@ static void s_push(replay_t* r, sent* E, smid m) {
     E->e[E->n++] = m;     /* an entry is pushed only for a (relation, pid) with none anywhere */
 }
 
-typedef struct { ptrdiff_t ent, idx; } sexists_t;
+typedef qe_where_t sexists_t;
 
-static sexists_t s_exists(const replay_t* r, uint64_t relation, uint64_t pid) {   /* relation_exists */
-    sexists_t ex = {-1, -1};
-    for (ptrdiff_t i = (ptrdiff_t)r->ne - 1; i >= 0; i--)
-        for (size_t j = 0; j < r->E[i].n; j++)
-            if (r->E[i].e[j].relation == relation && r->E[i].e[j].pid == pid) {
-                ex.ent = i;
-                ex.idx = (ptrdiff_t)j;
-                return ex;
-            }
-    return ex;
+/* the replay's entities as the shared view (host/qe_query.h) */
+static size_t v_count(void* u) { return ((replay_t*)u)->ne; }
+static size_t v_size(void* u, size_t ent) { return ((replay_t*)u)->E[ent].n; }
+static qe_mid_t* v_at(void* u, size_t ent, size_t idx) { return &((replay_t*)u)->E[ent].e[idx].h; }
+static void v_push_entity(void* u) { (void)s_new_entity((replay_t*)u); }
+
+static qe_mids view(replay_t* r) {
+    qe_mids v = {r, v_count, v_size, v_at, v_push_entity};
+    return v;
 }
 
-static ptrdiff_t s_exists_current(const sent* E, uint64_t relation, uint64_t pid) {
-    ptrdiff_t f = -1;
-    for (size_t i = 0; i < E->n; i++)
-        if (E->e[i].relation == relation && E->e[i].pid == pid) f = (ptrdiff_t)i;
-    return f;
+static sexists_t s_exists(replay_t* r, uint64_t relation, uint64_t pid) {   /* relation_exists */
+    const qe_mids v = view(r);
+    return qe_mid_exists(&v, relation, pid);
 }
 
 static int uf_find(int* p, int x) {
@@ -108,64 +105,14 @@ static int uf_find(int* p, int x) {
 /* the join's inputs as build_relations picks them: list index or -1 (the whole base relation) */
 typedef struct { int variant; int lR, lS; } sjoin_t;
 
-/* build_relations (src/join.c:152-292) on symbolic entries: the variant, the inputs and the
- * entries' last_column_sorted side effects, exactly as the reference (quirks included) */
+/* build_relations (src/join.c:152-292) on symbolic entries: the shared variant choice
+ * (host/qe_query.c, the faithful executor's too), its side effects on the entries included */
 static sjoin_t s_build_relations(replay_t* r, const pred_t* p) {
-    const query_t* q = r->q;
-    sjoin_t j = {0, -1, -1};
-    uint64_t lhs_rel = q->rels[p->frel], lhs_col = p->fcol;
-    uint64_t rhs_rel = q->rels[p->srel], rhs_col = p->scol;
-    if (lhs_rel == rhs_rel && lhs_col == rhs_col) {
-        j.variant = 5;                                   /* DO_NOTHING */
-        return j;
-    }
-    sent* E = r->ne == 0 ? s_new_entity(r) : &r->E[r->ne - 1];
-    ptrdiff_t li = s_exists_current(E, lhs_rel, p->frel);
-    ptrdiff_t ri = s_exists_current(E, rhs_rel, p->srel);
-    if (li != -1 && ri == -1) {
-        j.lR = E->e[li].l;
-        sexists_t ex = s_exists(r, rhs_rel, p->srel);
-        smid* T = ex.idx != -1 ? &r->E[ex.ent].e[ex.idx] : NULL;
-        if (T) j.lS = T->l;
-        smid* mid = &E->e[li];
-        if (!T) {
-            if (mid->lcs == (int32_t)lhs_col) { j.variant = 3; return j; }
-            mid->lcs = (int32_t)lhs_col;
-            j.variant = 1;
-            return j;
-        }
-        if (mid->lcs == (int32_t)lhs_col && T->lcs == (int32_t)rhs_col) j.variant = 4;
-        else if (mid->lcs == (int32_t)lhs_col) j.variant = 3;
-        else if (T->lcs == (int32_t)rhs_col) j.variant = 2;
-        else j.variant = 1;
-        return j;
-    }
-    if (li != -1 && ri != -1) {
-        j.lR = E->e[li].l;
-        j.lS = E->e[ri].l;
-        j.variant = 4;
-        return j;
-    }
-    if (li == -1 && ri != -1) {
-        j.lS = E->e[ri].l;
-        sexists_t ex = s_exists(r, lhs_rel, p->frel);
-        smid* T = ex.idx != -1 ? &r->E[ex.ent].e[ex.idx] : NULL;
-        if (T) j.lR = T->l;
-        smid* mid = &E->e[ri];
-        if (!T) {
-            if (mid->lcs == (int32_t)rhs_col) { j.variant = 2; return j; }
-            mid->lcs = (int32_t)rhs_col;
-            j.variant = 1;
-            return j;
-        }
-        if (mid->lcs == (int32_t)rhs_col && T->lcs == (int32_t)lhs_col) j.variant = 4;
-        else if (mid->lcs == (int32_t)rhs_col) j.variant = 3;    /* reference quirk, src/join.c:258-259 */
-        else if (mid->lcs == (int32_t)lhs_col) j.variant = 2;    /* reference quirk, src/join.c:261-262 */
-        else j.variant = 1;
-        return j;
-    }
-    s_new_entity(r);                                     /* src/join.c:270-285 */
-    j.variant = (rhs_rel != lhs_rel || p->frel != p->srel) ? 1 : 4;
+    const qe_mids v = view(r);
+    const qe_join_choice_t c = qe_build_relations(&v, r->q, p);
+    sjoin_t j = {c.variant, -1, -1};
+    if (c.lhs.ent >= 0) j.lR = r->E[c.lhs.ent].e[c.lhs.idx].l;
+    if (c.rhs.ent >= 0) j.lS = r->E[c.rhs.ent].e[c.rhs.idx].l;
     return j;
 }
 
@@ -199,14 +146,14 @@ static int s_fix_all(replay_t* r, sexists_t ex, uint64_t relR, uint64_t relS, sm
     for (size_t i = 0; i < E->n; i++) {
         if ((ptrdiff_t)i == ex.idx) continue;
         smid* ed = &E->e[i];
-        if (ed->relation == relR || ed->relation == relS) continue;   /* left stale (post pass) */
+        if (ed->h.relation == relR || ed->h.relation == relS) continue;   /* left stale (post pass) */
         const slist edl = r->L[ed->l];
         if (edl.len != upd.len)
             return refuse("join_payloads on lists of possibly different lengths (binding %llu)",
-                          (unsigned long long)ed->pid);
+                          (unsigned long long)ed->h.pid);
         const int ok = edl.tag == upd.tag && edl.ok && upd.ok && other_distinct;
-        if (r->live[ed->pid] && !ok)
-            return refuse("binding %llu is read later but join_payloads makes it %s", (unsigned long long)ed->pid,
+        if (r->live[ed->h.pid] && !ok)
+            return refuse("binding %llu is read later but join_payloads makes it %s", (unsigned long long)ed->h.pid,
                           edl.tag != upd.tag ? "a zip of misaligned lists" : "a non-relational multiset");
         ed->l = new_slist(r, tag, len, ok, 0, -1);
         w_add(w, ed->l);
@@ -241,8 +188,8 @@ static int s_join(replay_t* r, const pred_t* p) {
     const int dS = j.lS < 0 ? 1 : r->L[j.lS].distinct;
     const int tag = ++r->fresh, len = ++r->fresh;
     const uint64_t relR = q->rels[p->frel], relS = q->rels[p->srel];
-    smid tR = {relR, p->frel, (int32_t)p->fcol, new_slist(r, tag, len, 1, 0, (int)p->fcol)};
-    smid tS = {relS, p->srel, (int32_t)p->scol, new_slist(r, tag, len, 1, 0, (int)p->scol)};
+    smid tR = {{relR, p->frel, (int32_t)p->fcol}, new_slist(r, tag, len, 1, 0, (int)p->fcol)};
+    smid tS = {{relS, p->srel, (int32_t)p->scol}, new_slist(r, tag, len, 1, 0, (int)p->scol)};
     wset w = {NULL, 0, 0};
     int rc = 0;
     sexists_t ex;
@@ -282,7 +229,7 @@ static int s_join(replay_t* r, const pred_t* p) {
         for (size_t e = 0; e < r->ne; e++)
             for (size_t i = 0; i < r->E[e].n; i++) {
                 smid* m = &r->E[e].e[i];
-                const int c = uf_find(r->parent, (int)m->pid);
+                const int c = uf_find(r->parent, (int)m->h.pid);
                 if ((c == ca || c == cb) && !w_has(&w, m->l)) {
                     r->L[m->l].ok = 0;
                     r->L[m->l].len = ++r->fresh;
@@ -348,7 +295,7 @@ static int plan_check(const qe_engine* e, const query_t* q) {
             } else {
                 sent* E = r.ne == 0 ? s_new_entity(&r) : &r.E[r.ne - 1];
                 const int tag = ++r.fresh, len = ++r.fresh;
-                smid m = {q->rels[p->frel], p->frel, -1, new_slist(&r, tag, len, 1, 1, -1)};
+                smid m = {{q->rels[p->frel], p->frel, -1}, new_slist(&r, tag, len, 1, 1, -1)};
                 s_push(&r, E, m);
             }
         } else {
@@ -414,6 +361,9 @@ static uint64_t rel_rows(const plan_t* P, uint32_t rel) {
     P->e->rel_shape(P->e->u, rel, &rows, &nc);
     return rows;
 }
+
+/* a join's global pair count beyond the materialisation limit (the reference's DArray bound) */
+static int over_limit(const plan_t* P, uint64_t pairs) { return P->e->mat_limit && pairs > *P->e->mat_limit; }
 
 static int allreduce1(plan_t* P, uint64_t* v) {
     if (P->e->world == 1) return 0;
@@ -622,6 +572,7 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* s
             }
             v[1] = jr == QE_ETOOBIG;
             if (P->e->world > 1) ECHK(P->e->allreduce(P->e->u, v, 2));   /* every rank takes one branch */
+            if (over_limit(P, v[0])) v[1] = 1;
             rel(P, sa.keys);
             rel(P, sb.keys);
             rel(P, sa.vals);
@@ -678,6 +629,7 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* s
         uint64_t v[2] = {0, jr == QE_ETOOBIG};
         if (jr == 0) ECHK(e->length(e->u, oa, &v[0]));
         if (P->e->world > 1) ECHK(P->e->allreduce(P->e->u, v, 2));
+        if (over_limit(P, v[0])) v[1] = 1;
         if (v[1]) {
             rel(P, oa);
             rel(P, ob);
@@ -941,6 +893,35 @@ int qe_plan_check_text(const qe_engine* e, const char* text, uint8_t* accepted, 
     return (int)nq;
 }
 
+int qe_plan_run_query(const qe_engine* e, void* query, void* out, uint64_t* rows, int* refused) {
+    query_t* q = (query_t*)query;
+    FILE* f = (FILE*)out;
+    *refused = 0;
+    if (plan_check(e, q) != 0) {
+        *refused = 1;
+        return e->fallback ? e->fallback(e->u, q, f) : QE_ENOTSUP;
+    }
+    /* the query's bytes are buffered: a join too large to materialise (QE_ETOOBIG, the
+     * reference's DArray bound) sends the whole query to the fallback, whose executor takes
+     * the aggregate form where the reference's output allows it */
+    char* qbuf = NULL;
+    size_t qlen = 0;
+    FILE* qf = open_memstream(&qbuf, &qlen);
+    if (!qf) return QE_ENOMEM;
+    uint64_t r = 0;
+    int rc = plan_query(e, q, qf, &r);
+    fclose(qf);
+    if (rc == QE_ETOOBIG && e->fallback) {
+        *refused = 1;
+        rc = e->fallback(e->u, q, f);
+    } else {
+        if (qlen) fwrite(qbuf, 1, qlen, f);
+        if (rc == 0 && rows) *rows = r;
+    }
+    free(qbuf);
+    return rc;
+}
+
 int qe_plan_run_text(const qe_engine* e, const char* text, char** out, size_t* outlen, uint64_t* rows,
                      uint64_t* nrefused) {
     *out = NULL;
@@ -954,33 +935,10 @@ int qe_plan_run_text(const qe_engine* e, const char* text, char** out, size_t* o
     char first[256] = "";
     for (size_t i = 0; rc == 0 && i < nq; i++) {
         qe_arrange_predicates(&qs[i]);
-        if (plan_check(e, &qs[i]) != 0) {
-            if (!first[0]) snprintf(first, sizeof first, "%s", g_why);
-            refused++;
-            rc = e->fallback ? e->fallback(e->u, &qs[i], f) : QE_ENOTSUP;
-            continue;
-        }
-        /* the query's bytes are buffered: a join too large to materialise (QE_ETOOBIG, the
-         * reference's DArray bound) sends the whole query to the fallback, whose executor takes
-         * the aggregate form where the reference's output allows it */
-        char* qbuf = NULL;
-        size_t qlen = 0;
-        FILE* qf = open_memstream(&qbuf, &qlen);
-        if (!qf) {
-            rc = QE_ENOMEM;
-            break;
-        }
-        uint64_t r = 0;
-        rc = plan_query(e, &qs[i], qf, &r);
-        fclose(qf);
-        if (rc == QE_ETOOBIG && e->fallback) {
-            refused++;
-            rc = e->fallback(e->u, &qs[i], f);
-        } else {
-            if (qlen) fwrite(qbuf, 1, qlen, f);
-            if (rc == 0 && rows) *rows = r;
-        }
-        free(qbuf);
+        int ref = 0;
+        rc = qe_plan_run_query(e, &qs[i], f, rows, &ref);
+        if (ref && !first[0]) snprintf(first, sizeof first, "%s", g_why);
+        refused += (uint64_t)ref;
     }
     snprintf(g_why, sizeof g_why, "%s", first);
     qe_free_queries(qs, nq);

@@ -150,6 +150,96 @@ query_t* qe_parse_text(const char* text, size_t* nq_out) {
     return qs;
 }
 
+qe_where_t qe_mid_exists(const qe_mids* M, uint64_t relation, uint64_t pid) {
+    qe_where_t w = {-1, -1};
+    for (ptrdiff_t i = (ptrdiff_t)M->count(M->u) - 1; i >= 0; i--) {
+        const size_t n = M->size(M->u, (size_t)i);
+        for (size_t j = 0; j < n; j++) {
+            const qe_mid_t* m = M->at(M->u, (size_t)i, j);
+            if (m->relation == relation && m->pid == pid) {
+                w.ent = i;
+                w.idx = (ptrdiff_t)j;
+                return w;
+            }
+        }
+    }
+    return w;
+}
+
+ptrdiff_t qe_mid_exists_current(const qe_mids* M, size_t ent, uint64_t relation, uint64_t pid) {
+    ptrdiff_t f = -1;
+    const size_t n = M->size(M->u, ent);
+    for (size_t i = 0; i < n; i++) {
+        const qe_mid_t* m = M->at(M->u, ent, i);
+        if (m->relation == relation && m->pid == pid) f = (ptrdiff_t)i;
+    }
+    return f;
+}
+
+qe_join_choice_t qe_build_relations(const qe_mids* M, const query_t* q, const pred_t* p) {
+    qe_join_choice_t j = {0, {-1, -1}, {-1, -1}};
+    const uint64_t lhs_rel = q->rels[p->frel], lhs_col = p->fcol;
+    const uint64_t rhs_rel = q->rels[p->srel], rhs_col = p->scol;
+    if (lhs_rel == rhs_rel && lhs_col == rhs_col) {                 /* src/join.c:159-160 */
+        j.variant = QE_DO_NOTHING;
+        return j;
+    }
+    if (M->count(M->u) == 0) M->push_entity(M->u);
+    const size_t E = M->count(M->u) - 1;                            /* the current (newest) entity */
+    const ptrdiff_t li = qe_mid_exists_current(M, E, lhs_rel, p->frel);
+    const ptrdiff_t ri = qe_mid_exists_current(M, E, rhs_rel, p->srel);
+    if (li != -1 && ri == -1) {                                     /* src/join.c:171-226 */
+        j.lhs.ent = (ptrdiff_t)E;
+        j.lhs.idx = li;
+        j.rhs = qe_mid_exists(M, rhs_rel, p->srel);
+        qe_mid_t* mid = M->at(M->u, E, (size_t)li);
+        if (j.rhs.ent == -1) {
+            if (mid->lcs == (int32_t)lhs_col) j.variant = QE_JOIN_SORT_RHS;
+            else {
+                mid->lcs = (int32_t)lhs_col;
+                j.variant = QE_CLASSIC_JOIN;
+            }
+            return j;
+        }
+        const qe_mid_t* T = M->at(M->u, (size_t)j.rhs.ent, (size_t)j.rhs.idx);
+        if (mid->lcs == (int32_t)lhs_col && T->lcs == (int32_t)rhs_col) j.variant = QE_SCAN_JOIN;
+        else if (mid->lcs == (int32_t)lhs_col) j.variant = QE_JOIN_SORT_RHS;
+        else if (T->lcs == (int32_t)rhs_col) j.variant = QE_JOIN_SORT_LHS;
+        else j.variant = QE_CLASSIC_JOIN;
+        return j;
+    }
+    if (li != -1 && ri != -1) {                                     /* src/join.c:227-236 */
+        j.lhs.ent = j.rhs.ent = (ptrdiff_t)E;
+        j.lhs.idx = li;
+        j.rhs.idx = ri;
+        j.variant = QE_SCAN_JOIN;
+        return j;
+    }
+    if (li == -1 && ri != -1) {                                     /* src/join.c:237-268 */
+        j.rhs.ent = (ptrdiff_t)E;
+        j.rhs.idx = ri;
+        j.lhs = qe_mid_exists(M, lhs_rel, p->frel);
+        qe_mid_t* mid = M->at(M->u, E, (size_t)ri);
+        if (j.lhs.ent == -1) {
+            if (mid->lcs == (int32_t)rhs_col) j.variant = QE_JOIN_SORT_LHS;
+            else {
+                mid->lcs = (int32_t)rhs_col;
+                j.variant = QE_CLASSIC_JOIN;
+            }
+            return j;
+        }
+        const qe_mid_t* T = M->at(M->u, (size_t)j.lhs.ent, (size_t)j.lhs.idx);
+        if (mid->lcs == (int32_t)rhs_col && T->lcs == (int32_t)lhs_col) j.variant = QE_SCAN_JOIN;
+        else if (mid->lcs == (int32_t)rhs_col) j.variant = QE_JOIN_SORT_RHS;   /* reference quirk, src/join.c:258-259 */
+        else if (mid->lcs == (int32_t)lhs_col) j.variant = QE_JOIN_SORT_LHS;   /* reference quirk, src/join.c:261-262 */
+        else j.variant = QE_CLASSIC_JOIN;
+        return j;
+    }
+    M->push_entity(M->u);                                           /* src/join.c:270-285 */
+    j.variant = (rhs_rel != lhs_rel || p->frel != p->srel) ? QE_CLASSIC_JOIN : QE_SCAN_JOIN;
+    return j;
+}
+
 void qe_free_queries(query_t* qs, size_t nq) {
     for (size_t i = 0; i < nq; i++) {
         free(qs[i].rels);

@@ -134,6 +134,10 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "qe_run_queries_dist": (I, [P, P, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t),
                                     C.POINTER(C.c_uint64)]),
         "qe_run_queries_parallel": (I, [P, I, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+        "qe_run_queries_lanes": (I, [P, I, I, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+        "qe_comm_init_local": (I, [C.POINTER(C.c_void_p), I, C.POINTER(C.c_void_p)]),
+        "qe_run_queries_local": (I, [P, I, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t),
+                                     C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "qe_workers": (I, [P, I, C.POINTER(C.c_void_p)]),
         "qe_bind_thread": (I, [P]),
     }
@@ -238,6 +242,18 @@ class Ctx:
             raise QEError(rc, self.lib.qe_last_error(self.h).decode())
         return s, (1 if rc == QE_EEXIT else 0)
 
+    def run_lanes(self, text: str, workers: int = 4, plan: bool = True) -> tuple[str, int]:
+        """qe_run_queries_lanes: the batch on `workers` lanes, each query through the partitioned
+        plan (faithful fallback) or the faithful executor -- the same bytes either way"""
+        out, n = C.c_void_p(), C.c_size_t()
+        rc = self.lib.qe_run_queries_lanes(self.h, workers, 1 if plan else 0, text.encode(), C.byref(out), C.byref(n))
+        s = C.string_at(out, n.value).decode("latin-1") if out.value else ""
+        if out.value:
+            self.lib.qe_free_host(out)
+        if rc not in (0, QE_EEXIT):
+            raise QEError(rc, self.lib.qe_last_error(self.h).decode())
+        return s, (1 if rc == QE_EEXIT else 0)
+
     def run_dist(self, text: str, comm: "Comm | None" = None) -> tuple[str, int, int]:
         """qe_run_queries_dist: (stdout on rank 0, exit status, queries run the faithful way)"""
         out, n, ref = C.c_void_p(), C.c_size_t(), C.c_uint64()
@@ -249,6 +265,31 @@ class Ctx:
         if rc not in (0, QE_EEXIT):
             raise QEError(rc, self.lib.qe_last_error(self.h).decode())
         return s, (1 if rc == QE_EEXIT else 0), ref.value
+
+    def run_local(self, text: str, nranks: int) -> tuple[str, int, int, int]:
+        """qe_run_queries_local: the partitioned executor on `nranks` in-process ranks of this GPU
+        (worker contexts, one host thread each) -> (stdout, exit status, refused, bytes exchanged)"""
+        out, n, ref, sent = C.c_void_p(), C.c_size_t(), C.c_uint64(), C.c_uint64()
+        rc = self.lib.qe_run_queries_local(self.h, nranks, text.encode(), C.byref(out), C.byref(n), C.byref(ref),
+                                           C.byref(sent))
+        s = C.string_at(out, n.value).decode("latin-1") if out.value else ""
+        if out.value:
+            self.lib.qe_free_host(out)
+        if rc not in (0, QE_EEXIT):
+            raise QEError(rc, self.lib.qe_last_error(self.h).decode())
+        return s, (1 if rc == QE_EEXIT else 0), ref.value, sent.value
+
+    def workers(self, n: int) -> list["Ctx"]:
+        """qe_workers: n contexts on this GPU sharing its relations (owned by this ctx)"""
+        arr = (C.c_void_p * n)()
+        self._chk(self.lib.qe_workers(self.h, n, arr))
+        out = []
+        for i in range(n):
+            w = Ctx.__new__(Ctx)
+            w.lib, w.h, w.device = self.lib, arr[i], self.device
+            w.close = lambda: None              # freed by the owning ctx's qe_fini
+            out.append(w)
+        return out
 
     def buffer_free(self, ptr: int) -> None:
         self.lib.qe_buffer_free(self.h, ptr)
@@ -531,4 +572,45 @@ class Comm:
         if self.h:
             self.lib.qe_comm_fini(self.h)
             self.h = None
+
+
+class LocalComms:
+    """qe_comm_init_local: in-process ranks over `ctxs` (e.g. Ctx.workers on one GPU); run() drives
+    qe_run_queries_dist on every rank from its own host thread (ctypes releases the GIL)"""
+
+    def __init__(self, ctxs: list[Ctx]):
+        self.ctxs, self.lib = ctxs, ctxs[0].lib
+        arr = (C.c_void_p * len(ctxs))(*[c.h for c in ctxs])
+        out = (C.c_void_p * len(ctxs))()
+        ctxs[0]._chk(self.lib.qe_comm_init_local(arr, len(ctxs), out))
+        self.comms = []
+        for i, c in enumerate(ctxs):
+            cm = Comm.__new__(Comm)
+            cm.ctx, cm.lib, cm.h, cm.nranks, cm.rank = c, self.lib, C.c_void_p(out[i]), len(ctxs), i
+            self.comms.append(cm)
+
+    def run(self, text: str) -> list:
+        """per rank: (stdout, status, refused) or the QEError it raised"""
+        import threading
+        res = [None] * len(self.ctxs)
+
+        def go(r):
+            try:
+                self.lib.qe_bind_thread(self.ctxs[r].h)
+                res[r] = self.ctxs[r].run_dist(text, self.comms[r])
+            except QEError as e:
+                res[r] = e
+        th = [threading.Thread(target=go, args=(r,)) for r in range(len(self.ctxs))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        return res
+
+    def bytes_sent(self) -> int:
+        return sum(c.stats()[1] for c in self.comms)
+
+    def close(self):
+        for c in self.comms:
+            c.close()
 

@@ -42,7 +42,7 @@ VALUES, VALUES_SRC = 0xFFFFFFFF, 4   # include/qe_plan.h: QE_PLAN_VALUES, QE_PLA
 
 
 class Engine(C.Structure):
-    _fields_ = [("u", VP), ("rank", U32), ("world", U32)] + FIELDS
+    _fields_ = [("u", VP), ("rank", U32), ("world", U32)] + FIELDS + [("mat_limit", P(U64))]
 
 
 def part_of(k: np.ndarray, nparts: int) -> np.ndarray:
@@ -96,6 +96,12 @@ class NumpyPlanEngine:
             self._cbs.append(cb)
             setattr(e, name, cb)
         self.e = e
+        self._limit = None
+
+    def set_global_limit(self, pairs):
+        """the plan's own check of a join's all-ranks pair count (qe_engine.mat_limit); None: off"""
+        self._limit = None if pairs is None else U64(pairs)
+        self.e.mat_limit = C.pointer(self._limit) if pairs is not None else P(U64)()
 
     # -- plumbing
     def _wrap(self, f, void):
@@ -287,9 +293,10 @@ def free_port():
     return p
 
 
-def worker(rank, world, port, rels, queries, outq, limits=None):
+def worker(rank, world, port, rels, queries, outq, limits=None, global_limit=None):
     """one gloo rank: every query through the C plan, rank 0 reports (stdout, rc, rows, refused);
-    limits[rank] (optional): that rank's materialisation limit"""
+    limits[rank] (optional): that rank's materialisation limit (its local joins); global_limit
+    (optional): the plan's limit on a join's all-ranks pair count"""
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -298,6 +305,8 @@ def worker(rank, world, port, rels, queries, outq, limits=None):
         eng = NumpyPlanEngine(rels, rank, world)
         if limits:
             eng.mat_limit = limits[rank]
+        if global_limit is not None:
+            eng.set_global_limit(global_limit)
         res = [eng.run(q) for q in queries]
         if rank == 0:
             outq.put((res, eng.exchanges, eng.live_handles()))

@@ -59,7 +59,18 @@ def _binary(paths, queries, env=None):
     return r.stdout.decode("latin-1"), r.returncode
 
 
-@pytest.mark.parametrize("mode", ["faithful", "plan", "ranks1", "lanes4", "agg0"])
+MODES = {
+    "default": {},                                        # the plan on 8 lanes, faithful fallback
+    "faithful": {"QE_PLAN": "0", "QE_WORKERS": "1"},      # the reference's state machine, one lane
+    "plan1": {"QE_WORKERS": "1"},                         # the plan, one lane
+    "ranks1": {"QE_GPUS": "1"},                           # rank launcher: fork, RCCL id over a pipe
+    "lanes4": {"QE_PLAN": "0", "QE_WORKERS": "4"},        # the faithful executor on four lanes
+    "agg0": {"QE_PLAN": "0", "QE_AGG_MIN": "0"},          # faithful, aggregate last join at any size
+    "local3": {"QE_LOCAL_RANKS": "3"},                    # three in-process ranks: real exchanges
+}
+
+
+@pytest.mark.parametrize("mode", list(MODES))
 @pytest.mark.parametrize("fixture", [os.path.basename(f)[:-5] for f in goldens.golden_files()])
 def test_dropin_binary_matches_reference_golden(fixture, mode):
     """every golden through build/queries (mmap'd relation files, the reference's stdin protocol).
@@ -67,10 +78,7 @@ def test_dropin_binary_matches_reference_golden(fixture, mode):
     all three of the parser's scan buffers, so no line sees another's leftovers -- and the batch's
     stdout is the concatenation of theirs; every other case (malformed lines, exit(1), multi-line
     inputs) runs on its own."""
-    # the faithful executor; the partitioned executor on one GPU; the same through the rank
-    # launcher (fork, RCCL bootstrap over a pipe, one-rank communicator); four concurrent lanes
-    env = {"faithful": {}, "plan": {"QE_PLAN": "1"}, "ranks1": {"QE_GPUS": "1"}, "lanes4": {"QE_WORKERS": "4"},
-           "agg0": {"QE_AGG_MIN": "0"}}[mode]
+    env = MODES[mode]
     doc = goldens.load(os.path.join(goldens.GOLDEN_DIR, f"{fixture}.json"))
     rels, paths = goldens.dataset(doc["dataset"])
     batch = [c for c in doc["cases"] if c["rc"] == 0 and WELL_FORMED.fullmatch(c["input"])]
@@ -84,3 +92,19 @@ def test_dropin_binary_matches_reference_golden(fixture, mode):
         assert (out, rc) == (want, 0)
     for case in alone:
         assert _binary(paths, case["input"], env) == (case["stdout"], case["rc"]), case["input"]
+
+
+@pytest.mark.parametrize("cut", [0, 8, 16, 40, -8])
+def test_dropin_binary_rejects_a_truncated_relation_file(tmp_path, cut):
+    """a relation file shorter than its header says (cut bytes kept; -8: one value short) ends the
+    run with a message and exit status 1 -- not a SIGBUS (the reference check()s open / fstat /
+    mmap, src/utilities.c:136-146)"""
+    rels = dg.make_relations(dg.chain_spec(2, 1000), 1)
+    paths = dg.write_dataset(str(tmp_path), rels)
+    data = open(paths[1], "rb").read()
+    open(paths[1], "wb").write(data[:cut] if cut >= 0 else data[:cut])
+    r = subprocess.run([QUERIES], input=dg.protocol_input(paths, "0 1|0.1=1.0|0.2 1.2\n").encode(),
+                       capture_output=True, timeout=120)
+    assert r.returncode == 1, (r.returncode, r.stderr)
+    assert r.stdout == b""
+    assert b"[ERROR]" in r.stderr

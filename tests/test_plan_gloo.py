@@ -17,11 +17,12 @@ QE_ENOTSUP = -6
 C3 = "0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>1000000000&3.2<3000000000|1.2 2.2 3.2\n"
 
 
-def _run_world(rels, queries, world, limits=None):
+def _run_world(rels, queries, world, limits=None, global_limit=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = pe.free_port()
-    procs = [ctx.Process(target=pe.worker, args=(r, world, port, rels, queries, q, limits)) for r in range(world)]
+    procs = [ctx.Process(target=pe.worker, args=(r, world, port, rels, queries, q, limits, global_limit))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=600)
@@ -107,3 +108,20 @@ def test_one_rank_too_large_stops_every_rank():
     rels = dg.make_relations(dg.chain_spec(4, rows), 1)
     res, _, _ = _run_world(rels, [C3, "0 1|0.1=1.0|0.2 1.2\n"], 2, limits=[1 << 62, 100])
     assert res[0][1] == -5 and res[1][1] == -5
+
+
+def test_global_pair_count_is_what_the_limit_bounds():
+    """the materialisation limit bounds a join's pair count over ALL ranks (the reference's DArray
+    holds the whole result): a limit every rank's share stays under, but the total exceeds, still
+    ends the query with QE_ETOOBIG on every rank -- as it does on one rank"""
+    rows = 20_000
+    rels = dg.make_relations(dg.chain_spec(4, rows), 1)
+    q2 = "0 1|0.1=1.0|0.2 1.2\n"
+    one = pe.NumpyPlanEngine(rels, 0, 1)
+    out, rc, pairs, _ = one.run(q2)
+    assert rc == 0 and pairs > 1000
+    limit = pairs * 2 // 3                    # above each of two ranks' ~pairs/2, below the total
+    one.set_global_limit(limit)
+    assert one.run(q2)[1] == -5
+    res, _, _ = _run_world(rels, [q2], 2, global_limit=limit)
+    assert res[0][1] == -5
