@@ -76,9 +76,10 @@ typedef struct qe_engine {
     int (*fallback)(void* u, void* query, void* out);
     /* a1 then a2 on the same binding, fused (nullable): rowids r in [start, end) with
      * col1[r] op1 v1 and col2[r] op2 v2, ascending -- one pass over the column(s) instead of a
-     * scan and a refine gathering through its list */
+     * scan and a refine gathering through its list.  values = 1: the plan expects to ask for col1's
+     * values of this list later (`values` below) -- the engine may emit them from the same pass */
     int (*scan2)(void* u, uint32_t rel, uint32_t col1, char op1, uint64_t v1, uint32_t col2, char op2, uint64_t v2,
-                 uint64_t start, uint64_t end, qe_h* out);
+                 uint64_t start, uint64_t end, int values, qe_h* out);
     /* join, with side b's carried rowid columns cb[0..nb) delivered beside the pairs (nullable):
      * outb[k][i] = cb[k][ib] for pair i's b row.  The engine may carry them through its sort
      * and join instead of taking them through the pairs afterwards.  Inputs are borrowed. */

@@ -251,12 +251,14 @@ int e_scan(void* u, uint32_t rel, uint32_t col, uint64_t s, uint64_t t, char op,
 }
 
 int e_scan2(void* u, uint32_t rel, uint32_t col1, char op1, uint64_t v1, uint32_t col2, char op2, uint64_t v2,
-            uint64_t s, uint64_t t, qe_h* out) {
+            uint64_t s, uint64_t t, int values, qe_h* out) {
     Eng* e = E(u);
     return guard(e, [&] {
         qe_ctx* c = e->c;
         uint64_t kor = 0, kand = 0;
-        const bool vals_on = !(getenv("QE_SCAN_VALUES") && getenv("QE_SCAN_VALUES")[0] == '0');
+        // the value-carrying scan (half-size tiles, 4 more bytes written per survivor) only when the
+        // plan expects to ask for col1's values
+        const bool vals_on = values && !(getenv("QE_SCAN_VALUES") && getenv("QE_SCAN_VALUES")[0] == '0');
         if (vals_on && qe_relation_column_bits(c, (int)rel, (int)col1, &kor, &kand) == 0 && !(kor >> 32)) {
             // the survivors' col1 values come out of the same pass (the plan may ask for them)
             const qe_col q1 = column(c, rel, col1), q2 = column(c, rel, col2);

@@ -707,6 +707,20 @@ static uint64_t join_cost(plan_t* P, const pred_t* p) {
     return c;
 }
 
+/* binding b will carry column col's values instead of its rowids (the `values` request of
+ * side_start): it is joined once and every select of it reads col */
+static int values_hint(const query_t* q, int b, uint64_t col) {
+    int joins = 0, sels = 0;
+    for (size_t i = 0; i < q->npreds; i++)
+        if (q->preds[i].type == 0) joins += ((int)q->preds[i].frel == b) + ((int)q->preds[i].srel == b);
+    for (size_t s = 0; s < q->nsel; s++) {
+        if ((int)q->sel[2 * s] != b) continue;
+        if (q->sel[2 * s + 1] != col) return 0;
+        sels++;
+    }
+    return joins == 1 && sels > 0;
+}
+
 static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t* rows_out) {
     plan_t PP;
     plan_t* P = &PP;
@@ -745,7 +759,7 @@ static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t*
                 uint64_t s, t;
                 owned_range(P, rel_rows(P, relid), &s, &t);
                 rc = e->scan2(e->u, relid, (uint32_t)p->fcol, p->op, p->cval, (uint32_t)p2->fcol, p2->op, p2->cval, s,
-                              t, &P->list[b]);
+                              t, values_hint(q, b, p->fcol) && e->values != NULL, &P->list[b]);
                 uint64_t n = 0;
                 if (!rc) rc = e->length(e->u, P->list[b], &n);
                 if (!rc) rc = allreduce1(P, &n);

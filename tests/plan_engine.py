@@ -33,7 +33,7 @@ FIELDS = [
     ("allreduce", C.CFUNCTYPE(I, VP, P(U64), I)),
     ("release", C.CFUNCTYPE(None, VP, H)),
     ("fallback", C.CFUNCTYPE(I, VP, VP, VP)),
-    ("scan2", C.CFUNCTYPE(I, VP, U32, U32, C.c_char, U64, U32, C.c_char, U64, U64, U64, P(H))),
+    ("scan2", C.CFUNCTYPE(I, VP, U32, U32, C.c_char, U64, U32, C.c_char, U64, U64, U64, I, P(H))),
     ("join_carry", C.CFUNCTYPE(I, VP, H, H, H, H, I, P(H), P(H), P(H), P(H))),
     ("join_sums", C.CFUNCTYPE(I, VP, H, H, H, H, I, P(H), I, P(I), P(U32), P(U32), P(U64), P(U64))),
     ("values", C.CFUNCTYPE(I, VP, U32, U32, H, P(H))),
@@ -76,6 +76,7 @@ class NumpyPlanEngine:
         self.exchanges = 0
         self.sums_calls = 0                      # last joins run in aggregate form (join_sums)
         self.values_calls = 0                    # bindings whose select values ride instead of rowids
+        self.scan2_values = 0                    # fused scans asked to emit their col1 values
         self.mat_limit = 1 << 62
         self.lib = C.CDLL(SO)
         self.lib.qe_plan_run_text.argtypes = [P(Engine), C.c_char_p, P(C.c_void_p), P(C.c_size_t), P(U64), P(U64)]
@@ -158,7 +159,8 @@ class NumpyPlanEngine:
         c = self.rels[rel][col][s:t]
         out[0] = self.put((np.nonzero(_OPS[op.decode()](c, np.uint64(v)))[0] + s).astype(np.uint32))
 
-    def cb_scan2(self, u, rel, c1, op1, v1, c2, op2, v2, s, t, out):
+    def cb_scan2(self, u, rel, c1, op1, v1, c2, op2, v2, s, t, values, out):
+        self.scan2_values += bool(values)
         a = self.rels[rel][c1][s:t]
         b = self.rels[rel][c2][s:t]
         m = _OPS[op1.decode()](a, np.uint64(v1)) & _OPS[op2.decode()](b, np.uint64(v2))

@@ -56,6 +56,8 @@ def test_every_golden_is_refused_or_exact(fixture, optional):
         assert accepted["T"] >= 0.75 * t_cases, accepted   # the relational class is the plan's domain
         assert (eng.sums_calls > 0) == on                  # and its last joins take the aggregate form
         assert (eng.values_calls > 0) == on                # and select values ride instead of rowids
+    if fixture == "headline" and on:
+        assert eng.scan2_values > 0                        # C3's fused scan emits 3.2's values
 
 
 def test_check_names_the_reason():
