@@ -4,7 +4,8 @@ Workload: the 14 relations of qe.datagen.c4_spec(1.0) (1e5..1e7 rows, 2..6 colum
 generated in HBM, and the C4 queries that pass the reference's rand-invariance gate at N/100
 (tests/golden/c4.json, made by oracle/gen_golden.py with the real reference binary) and finish
 with exit status 0, run as batches of <= 50 separated by F lines -- the reference's protocol.
-One step = the whole batch through libqe's faithful executor.
+One step = the whole batch through libqe's product default: qe_run_queries_lanes with the
+partitioned plan per query (the faithful executor for the queries it refuses) on concurrent lanes.
 
 Multi-GPU: queries are independent, so the batch is scheduled replicas-style:
 query i runs on rank i mod N, every rank holds every relation (1.8 GB), outputs are gathered to
@@ -70,14 +71,15 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
     t0 = time.time()
     specs = gen_c4(ctx)
     log(f"[c4] {len(specs)} relations in HBM in {time.time() - t0:.2f}s; {len(queries)} gated queries")
-    # the measured line: the batch's queries on concurrent lanes (qe_run_queries_parallel: worker
-    # contexts on this GPU, each its own stream, the relations shared); `--plan faithful` = one lane
+    # the measured line: the batch's queries on concurrent lanes (qe_run_queries_lanes: worker
+    # contexts on this GPU, each its own stream, the relations shared), each query through the
+    # partitioned plan with the faithful executor for what it refuses; `--plan faithful` = the
+    # faithful executor on the lanes
     workers = int(os.environ.get("QE_WORKERS", "8"))
-    if getattr(args, "plan", "auto") == "faithful":
-        workers = 1
+    plan = getattr(args, "plan", "auto") != "faithful"
 
     def run_batch():
-        return ctx.run_parallel(text, workers)
+        return ctx.run_lanes(text, workers, plan=plan)
 
     out = None
     for _ in range(args.warmup):
@@ -103,7 +105,9 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
         d = time.perf_counter() - t1
         return {"ms_per_step": round(d * 1e3, 3), "value": round(len(queries) / d, 2), "stdout_identical": o == out}
     others = {"sequential_faithful (qe_run_queries)": timed(lambda: ctx.run(text)[0]),
-              "partitioned_plan (qe_run_queries_dist)": timed(lambda: ctx.run_dist(text)[0])}
+              "partitioned_plan_one_lane (qe_run_queries_dist)": timed(lambda: ctx.run_dist(text)[0]),
+              "faithful_lanes (qe_run_queries_parallel, %d lanes)" % workers:
+                  timed(lambda: ctx.run_lanes(text, workers, plan=False)[0])}
     res = {
         "metric": METRIC, "value": round(len(queries) * args.steps / dt, 2), "unit": "queries/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
@@ -114,9 +118,10 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
         "config": {"workload": "C4: 14 relations, %d gated SIGMOD-style queries in batches of %d"
                                % (len(queries), dg.C4_BATCH),
                    "rows_total": sum(s.rows for s in specs), "output_lines": out.count("\n"),
-                   "executor": "qe_run_queries_parallel: the faithful executor, %d concurrent lanes (worker "
-                               "contexts = HIP streams on this GPU, relations shared), output in input order"
-                               % workers,
+                   "executor": "qe_run_queries_lanes: %s, %d concurrent lanes (worker contexts = HIP "
+                               "streams on this GPU, relations shared), output in input order"
+                               % ("the partitioned plan per query, faithful fallback" if plan
+                                  else "the faithful executor", workers),
                    "parallelism": "single GPU, inter-query concurrency x%d" % workers},
         "other_executors_same_batch": others,
         "roofline": roofline_fn(stats, traffic_fn() if traffic_fn else None) if roofline_fn else None,
@@ -131,7 +136,8 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
 
 def run_dist(args, log) -> dict | None:
     """replicas-style: rank r runs the r-th contiguous share of the batch on its own GPU (relations
-    replicated), its queries on concurrent lanes (qe_run_queries_parallel); rank 0 joins the shares
+    replicated), its queries on concurrent lanes (qe_run_queries_lanes, the plan per query with the
+    faithful fallback); rank 0 joins the shares
     in rank order -- input order -- cut after the first share where the reference exits.
     torch.distributed (gloo) is the control plane only: barriers, the max time, the gather."""
     import torch
@@ -153,12 +159,12 @@ def run_dist(args, log) -> dict | None:
     gen_c4(ctx)
     res_mine = ("", 0)
     for _ in range(args.warmup):
-        res_mine = ctx.run_parallel(mine, workers)
+        res_mine = ctx.run_lanes(mine, workers)
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        res_mine = ctx.run_parallel(mine, workers)
+        res_mine = ctx.run_lanes(mine, workers)
     ctx.sync()
     torch.cuda.synchronize()
     dist.barrier()
@@ -186,8 +192,8 @@ def run_dist(args, log) -> dict | None:
         "parity": (text == want and rc == 0) if want is not None else None,
         "config": {"workload": "C4: 14 relations, %d gated SIGMOD-style queries" % len(queries),
                    "output_lines": text.count("\n"),
-                   "executor": "qe_run_queries_parallel per rank (%d lanes), a contiguous share of the batch "
-                               "per rank" % workers,
+                   "executor": "qe_run_queries_lanes per rank (the plan per query, faithful fallback; %d "
+                               "lanes), a contiguous share of the batch per rank" % workers,
                    "parallelism": f"query-parallel replicas x{world}"},
         "roofline": None, "cpu_baseline": None,
     }

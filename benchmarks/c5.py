@@ -72,13 +72,13 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
     log(f"[c5] 2 x {rows} rows (Zipf {dg.C5_THETA}) in HBM in {time.time() - t0:.1f}s")
     out = None
     for _ in range(args.warmup):
-        out, rc = ctx.run(dg.C5_QUERY)
+        out, rc, _ = ctx.run_dist(dg.C5_QUERY)
     ctx.set_profiling(True)
     ctx.reset_stats()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out, rc = ctx.run(dg.C5_QUERY)
+        out, rc, refused = ctx.run_dist(dg.C5_QUERY)
     ctx.sync()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -96,9 +96,10 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
         "config": {"workload": "C5: 2-relation join, %d rows/side, Zipf theta=%.1f keys, query %s"
                                % (rows, dg.C5_THETA, dg.C5_QUERY.strip()),
                    "pairs": pairs, "materialised": False,
-                   "path": "libqe faithful executor; its last join of two base columns whose lists only the "
-                           "checksums read runs as qe_join_aggregate (csrc/qe_agg.hip): each side sorted once "
-                           "as (key, select value) words, one merge-path pass counting both sides' partners",
+                   "path": "qe_run_queries_dist on one rank (the product default): the plan's last join of two "
+                           "base relations in aggregate form (engine join_agg -> csrc/qe_agg.hip): each side "
+                           "sorted once as (key, select value) words, one merge-path pass counting both sides' "
+                           "partners", "refused": refused,
                    "pairs_counted_per_s": round(pairs * args.steps / dt, 1),
                    "stdout": out, "parallelism": "single GPU"},
         "roofline": roofline_fn(stats, traffic_fn() if traffic_fn else None) if roofline_fn else None,
@@ -114,40 +115,41 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
 
 
 def run_dist(args, log) -> dict | None:
-    """C5 on N ranks (one per GPU, RCCL): qe.dist.DistAggJoin -- light keys bucketed locally from
-    the replicated columns, heavy keys split across ranks by their row slices and combined with
-    all-reduced counts.  Strong scaling: `--rows` (default 1e9) rows per side in total."""
+    """C5 on N ranks (one per GPU): qe_run_queries_dist over an RCCL communicator (gloo carries only
+    the bootstrap id, the barriers and the max time).  The C plan runs the query's one join -- its
+    last, of two whole base relations -- in the engine's aggregate form: heavy keys (sampled from the
+    replicated key columns) counted per row slice and all-reduced, light keys hash-bucketed locally
+    from the replicated columns and joined in aggregate form, sums all-reduced.  Strong scaling:
+    `--rows` (default 1e9) rows per side in total."""
     import torch
     import torch.distributed as dist
 
-    import numpy as np
-
     from qe import lib
-    from qe.dist import DistAggJoin, GPUEngine
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    backend = os.environ.get("QE_DIST_BACKEND", "nccl")
     dev = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev)
+    torch.cuda.init()
     solo = world == 1
     if not solo and not dist.is_initialized():
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group("gloo")
     rows = args.rows or dg.C5_ROWS
     ctx = lib.Ctx(dev)
+    comm = None
+    if not solo:
+        box = [lib.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        comm = lib.Comm(ctx, world, rank, box[0])   # the data path: RCCL over xGMI
     t0 = time.time()
     gen_c5(ctx, rows)
     ctx.sync()
     if rank == 0:
         log(f"[c5] {world} rank(s): 2 x {rows} rows (Zipf {dg.C5_THETA}) replicated in HBM in {time.time() - t0:.1f}s")
-    ex = DistAggJoin(GPUEngine(ctx, rank, world), [rows, rows])
-    q = dg.C5_QUERY.strip()
+    q = dg.C5_QUERY
     out = None
     for _ in range(args.warmup):
-        out, pairs, nheavy = ex.run(q)
+        out, rc, refused = ctx.run_dist(q, comm)
     ctx.set_profiling(True)
     ctx.reset_stats()
     if not solo:
@@ -155,16 +157,17 @@ def run_dist(args, log) -> dict | None:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out, pairs, nheavy = ex.run(q)
+        out, rc, refused = ctx.run_dist(q, comm)
     ctx.sync()
     torch.cuda.synchronize()
     if not solo:
         dist.barrier()
     dt = time.perf_counter() - t0
     if not solo:
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}" if backend == "nccl" else "cpu")
+        t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    pairs = ctx.last_result_rows()
     stats = ctx.kernel_stats()
     ctx.set_profiling(False)
     res = None
@@ -177,17 +180,21 @@ def run_dist(args, log) -> dict | None:
             "data": "synthetic: qe.datagen.c5_spec(%d) generated in HBM on every rank (seed %d, Zipf %.1f)"
                     % (rows, dg.C5_SEED, dg.C5_THETA),
             "config": {"workload": "C5: 2-relation join, %d rows/side in total, Zipf theta=%.1f keys, query %s"
-                                   % (rows, dg.C5_THETA, q),
-                       "pairs": pairs, "materialised": False, "heavy_keys": nheavy,
-                       "path": "qe.dist.DistAggJoin: heavy keys split by row slice + all-reduced counts; light keys "
-                               "bucketed locally (qe_bucket_select), sorted, qe_merge_join_counts, "
-                               "qe_checksum_weighted; sums all-reduced",
+                                   % (rows, dg.C5_THETA, q.strip()),
+                       "pairs": pairs, "materialised": False, "refused": refused,
+                       "path": "qe_run_queries_dist (host-C plan, include/qe_plan.h): the last join of two base "
+                               "relations in the engine's aggregate form (csrc/qe_comm.hip e_join_agg) -- heavy "
+                               "keys split by row slice with all-reduced counts, light keys bucketed locally "
+                               "(qe_bucket_select) and joined by value-carrying sorts + one counting pass; "
+                               "sums all-reduced over RCCL",
                        "pairs_counted_per_s": round(pairs * args.steps / dt, 1),
-                       "stdout": out + "\n" if not out.endswith("\n") else out,
-                       "parallelism": f"hash buckets + heavy split x{world}"},
+                       "stdout": out,
+                       "parallelism": f"hash buckets + heavy split x{world}" if world > 1 else "single GPU"},
             "stages": {k: {"ms_per_step": round(s["ms"] / args.steps, 3)} for k, s in kern[:10]},
             "cpu_baseline": None,
         }
+    if comm is not None:
+        comm.close()
     if not solo:
         dist.barrier()
     ctx.close()

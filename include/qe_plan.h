@@ -105,6 +105,15 @@ typedef struct qe_engine {
      * takes the same branch at any rank count.  (An engine may also refuse a join whose LOCAL
      * share exceeds it: that share is a lower bound of the global count.) */
     const uint64_t* mat_limit;
+    /* the query's last join when both sides are whole base relations and every select reads one of
+     * its two bindings (nullable): the join in aggregate form -- *pairs = this rank's share of the
+     * pair count, sums[s] = its share of the sum mod 2^64 of column cols[s] of side side[s] (0: a,
+     * 1: b) over the pairs -- the numbers print_sums computes from the lists (src/join.c:325-392,
+     * src/utilities.c:197-224), no pair materialised, any key skew (C5).  Shares add up over the
+     * ranks (the plan all-reduces them).  QE_ENOTSUP: not applicable (the plan then joins as
+     * usual).  No materialisation limit applies: nothing is materialised. */
+    int (*join_agg)(void* u, uint32_t rel_a, uint32_t col_a, uint32_t rel_b, uint32_t col_b, int nsel, const int* side,
+                    const uint32_t* cols, uint64_t* pairs, uint64_t* sums);
 } qe_engine;
 
 /* Replay the reference's variant choice and list bookkeeping for every query of `text` on the

@@ -311,28 +311,14 @@ extern "C" int qe_diag_stamps_ag(uint64_t* out, uint64_t n) {
 }
 #endif
 
-using namespace qe;
+namespace qe {
 
-extern "C" int qe_join_aggregate(qe_ctx* c, qe_col keyR, qe_col valR, qe_col keyS, qe_col valS, uint64_t* out) {
-    QE_API_BEGIN(c)
-    if (!out) throw Error(QE_EINVAL, "null output");
-    if (!keyR.d || !keyS.d) throw Error(QE_EINVAL, "null key column");
-    if ((valR.d && valR.n != keyR.n) || (valS.d && valS.n != keyS.n))
-        throw Error(QE_EINVAL, "value column length differs from its key column");
-    const uint64_t nR = keyR.n, nS = keyS.n;
+void join_aggregate_sides(qe_ctx* c, const AggSide& R, const AggSide& S, uint64_t out[3]) {
+    const uint64_t nR = R.n, nS = S.n;
     out[0] = out[1] = out[2] = 0;
-    if (nR == 0 || nS == 0) return 0;
+    if (nR == 0 || nS == 0) return;
     if (nR >= 0xFFFFFFFFull || nS >= 0xFFFFFFFFull) throw Error(QE_ENOTSUP, "aggregate join side beyond 2^32 rows");
-    uint64_t kr[2], ks[2];
-    col_bits(c, keyR.d, nR, kr);
-    col_bits(c, keyS.d, nS, ks);
-    for (const qe_col* v : {&valR, &valS}) {
-        if (!v->d) continue;
-        uint64_t vb[2];
-        col_bits(c, v->d, v->n, vb);
-        if (vb[0] >> 32) throw Error(QE_ENOTSUP, "aggregate join value column beyond 32 bits");
-    }
-    const uint64_t vary = (kr[0] | ks[0]) & ~(kr[1] & ks[1]);
+    const uint64_t vary = (R.kb[0] | S.kb[0]) & ~(R.kb[1] & S.kb[1]);
     int lo = 0, nb = 0;
     if (vary) {
         lo = __builtin_ctzll(vary);
@@ -340,8 +326,8 @@ extern "C" int qe_join_aggregate(qe_ctx* c, qe_col keyR, qe_col valR, qe_col key
     }
     // (bits outside the field are equal in every key of both sides: comparing fields is exact)
     if (nb > 32) throw Error(QE_ENOTSUP, "aggregate join keys vary in more than 32 bits");
-    uint64_t* wR = sort_words_kv64(c, keyR.d, valR.d, nR, lo, nb);
-    uint64_t* wS = sort_words_kv64(c, keyS.d, valS.d, nS, lo, nb);
+    uint64_t* wR = sort_words_kv64(c, R.keys, R.v64, nR, lo, nb, R.v32);
+    uint64_t* wS = sort_words_kv64(c, S.keys, S.v64, nS, lo, nb, S.v32);
     const uint64_t m = nR + nS;
     const uint32_t nt = (uint32_t)((m + AG_T - 1) / AG_T);
     uint64_t* ra = dalloc_t<uint64_t>(c, (uint64_t)nt + 1);
@@ -373,9 +359,34 @@ extern "C" int qe_join_aggregate(qe_ctx* c, qe_col keyR, qe_col valR, qe_col key
         QE_HIP(hipGetLastError());
     }
     read_words(c, d_out, out, 3);
-    if (!valR.d) out[1] = 0;   // (the words carried row indices)
-    if (!valS.d) out[2] = 0;
+    if (!R.v64 && !R.v32) out[1] = 0;   // (the words carried row indices)
+    if (!S.v64 && !S.v32) out[2] = 0;
     for (void* p : {(void*)wR, (void*)wS, (void*)ra, (void*)bk, (void*)bcR, (void*)bcS, (void*)partial}) dfree(c, p);
+}
+
+}  // namespace qe
+
+using namespace qe;
+
+extern "C" int qe_join_aggregate(qe_ctx* c, qe_col keyR, qe_col valR, qe_col keyS, qe_col valS, uint64_t* out) {
+    QE_API_BEGIN(c)
+    if (!out) throw Error(QE_EINVAL, "null output");
+    if (!keyR.d || !keyS.d) throw Error(QE_EINVAL, "null key column");
+    if ((valR.d && valR.n != keyR.n) || (valS.d && valS.n != keyS.n))
+        throw Error(QE_EINVAL, "value column length differs from its key column");
+    out[0] = out[1] = out[2] = 0;
+    if (keyR.n == 0 || keyS.n == 0) return 0;
+    if (keyR.n >= 0xFFFFFFFFull || keyS.n >= 0xFFFFFFFFull) throw Error(QE_ENOTSUP, "aggregate join side beyond 2^32 rows");
+    AggSide R{keyR.d, valR.d, nullptr, keyR.n, {0, 0}}, S{keyS.d, valS.d, nullptr, keyS.n, {0, 0}};
+    col_bits(c, keyR.d, keyR.n, R.kb);
+    col_bits(c, keyS.d, keyS.n, S.kb);
+    for (const qe_col* v : {&valR, &valS}) {
+        if (!v->d) continue;
+        uint64_t vb[2];
+        col_bits(c, v->d, v->n, vb);
+        if (vb[0] >> 32) throw Error(QE_ENOTSUP, "aggregate join value column beyond 32 bits");
+    }
+    join_aggregate_sides(c, R, S, out);
     return 0;
     QE_API_END(c)
 }

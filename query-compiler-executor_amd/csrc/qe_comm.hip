@@ -707,7 +707,118 @@ int e_values(void* u, uint32_t rel, uint32_t col, qe_h rows, qe_h* out) {
 int e_allreduce(void* u, uint64_t* v, int n) {
     Eng* e = E(u);
     if (!e->comm) return 0;
-    return qe_allreduce_u64(e->c, e->comm, v, n);
+    for (int i = 0; i < n; i += 64) {                 // (the communicator reduces 64 words at a time)
+        const int rc = qe_allreduce_u64(e->c, e->comm, v + i, std::min(64, n - i));
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+// the aggregate join's minimum size (both sides' rows), as the faithful executor's (QE_AGG_MIN)
+uint64_t agg_min_rows() {
+    static const uint64_t v = [] {
+        const char* s = getenv("QE_AGG_MIN");
+        return s ? strtoull(s, nullptr, 10) : (1ull << 24);
+    }();
+    return v;
+}
+
+#ifndef QE_HEAVY_SAMPLE
+#define QE_HEAVY_SAMPLE (1u << 21)
+#endif
+#ifndef QE_HEAVY_DIV
+#define QE_HEAVY_DIV 64
+#endif
+#ifndef QE_HEAVY_MAX
+#define QE_HEAVY_MAX 32
+#endif
+
+// the last join of two whole base relations in aggregate form (C5; SURVEY.md §8(e) "Skew").  One
+// rank: qe_join_aggregate's sorts + counting pass.  N ranks, every rank holding both columns:
+//   heavy keys -- those whose run in the first QE_HEAVY_SAMPLE rows of either key column is longer
+//                 than sample / (N * QE_HEAVY_DIV) (the same list on every rank): each rank counts
+//                 them over its row slice of both sides, the counts are all-reduced, and the rank
+//                 adds sum_{r in its slice, key heavy} val(r) * |other side's key run|; rank 0 adds
+//                 sum_h cA_h * cB_h pairs -- no heavy row moves, no rank takes a whole Zipf head;
+//   light keys -- each rank's hash bucket of both columns without the heavy keys
+//                 (qe_bucket_select, the select column's low words beside each key), joined in
+//                 aggregate form locally.
+// The plan all-reduces the shares.
+int e_join_agg(void* u, uint32_t ra, uint32_t ca, uint32_t rb, uint32_t cb, int nsel, const int* side,
+               const uint32_t* cols, uint64_t* pairs, uint64_t* sums) {
+    Eng* e = E(u);
+    qe_ctx* c = e->c;
+    int vc[2] = {-1, -1};                             // each side's one select column
+    for (int s = 0; s < nsel; s++) {
+        const int sd = side[s] ? 1 : 0;
+        if (vc[sd] >= 0 && vc[sd] != (int)cols[s]) return QE_ENOTSUP;
+        vc[sd] = (int)cols[s];
+    }
+    const uint32_t rel[2] = {ra, rb}, kcol[2] = {ca, cb};
+    uint64_t kb[2][2], rows[2];
+    for (int sd = 0; sd < 2; sd++) {
+        if (qe_relation_rows(c, (int)rel[sd], &rows[sd]) != 0) return QE_ENOTSUP;
+        if (rows[sd] >= 0xFFFFFFFFull) return QE_ENOTSUP;
+        if (qe_relation_column_bits(c, (int)rel[sd], (int)kcol[sd], &kb[sd][0], &kb[sd][1]) != 0) return QE_ENOTSUP;
+        uint64_t vor = 0, vand = 0;
+        if (vc[sd] >= 0 && (qe_relation_column_bits(c, (int)rel[sd], vc[sd], &vor, &vand) != 0 || (vor >> 32)))
+            return QE_ENOTSUP;
+    }
+    const uint64_t vary = (kb[0][0] | kb[1][0]) & ~(kb[0][1] & kb[1][1]);
+    if (vary && 64 - __builtin_clzll(vary) - __builtin_ctzll(vary) > 32) return QE_ENOTSUP;
+    if (rows[0] + rows[1] < agg_min_rows()) return QE_ENOTSUP;
+    return guard(e, [&] {
+        const qe_col key[2] = {column(c, ra, ca), column(c, rb, cb)};
+        qe_col val[2] = {{nullptr, 0}, {nullptr, 0}};
+        for (int sd = 0; sd < 2; sd++)
+            if (vc[sd] >= 0) val[sd] = column(c, rel[sd], (uint32_t)vc[sd]);
+        uint64_t out[3] = {0, 0, 0}, wsum[2] = {0, 0}, heavy_pairs = 0;
+        if (e->world == 1) {
+            AggSide A{key[0].d, val[0].d, nullptr, key[0].n, {kb[0][0], kb[0][1]}};
+            AggSide B{key[1].d, val[1].d, nullptr, key[1].n, {kb[1][0], kb[1][1]}};
+            join_aggregate_sides(c, A, B, out);
+        } else {
+            const std::vector<uint64_t> heavy =
+                heavy_keys_dev(c, key, 2, QE_HEAVY_SAMPLE, (uint64_t)e->world * QE_HEAVY_DIV, QE_HEAVY_MAX);
+            const uint32_t nh = (uint32_t)heavy.size();
+            qe_pairs lp[2] = {};
+            struct Release {
+                qe_ctx* c;
+                qe_pairs* p;
+                ~Release() {
+                    qe_pairs_free(c, &p[0]);
+                    qe_pairs_free(c, &p[1]);
+                }
+            } release{c, lp};
+            for (int sd = 0; sd < 2; sd++)
+                bucket_select_dev(c, key[sd], (uint32_t)e->world, (uint32_t)e->rank, heavy.data(), nh, val[sd].d,
+                                  &lp[sd]);
+            AggSide A{lp[0].key, nullptr, val[0].d ? lp[0].val : nullptr, lp[0].n, {kb[0][0], kb[0][1]}};
+            AggSide B{lp[1].key, nullptr, val[1].d ? lp[1].val : nullptr, lp[1].n, {kb[1][0], kb[1][1]}};
+            join_aggregate_sides(c, A, B, out);
+            if (nh) {
+                uint64_t s0[2], s1[2];
+                std::vector<uint64_t> cnt(2 * (size_t)nh);   // [this rank's slice counts of A | of B]
+                for (int sd = 0; sd < 2; sd++) {
+                    s0[sd] = rows[sd] * (uint64_t)e->rank / (uint64_t)e->world;
+                    s1[sd] = rows[sd] * (uint64_t)(e->rank + 1) / (uint64_t)e->world;
+                    ck(qe_heavy_stats(c, key[sd], s0[sd], s1[sd], heavy.data(), nh, qe_col{nullptr, 0}, nullptr,
+                                      cnt.data() + sd * nh, nullptr),
+                       c);
+                }
+                ck(e_allreduce(u, cnt.data(), 2 * (int)nh), c);   // the heavy keys' global counts
+                for (uint32_t h = 0; h < nh; h++) heavy_pairs += cnt[h] * cnt[nh + h];
+                for (int sd = 0; sd < 2; sd++)
+                    if (val[sd].d)
+                        ck(qe_heavy_stats(c, key[sd], s0[sd], s1[sd], heavy.data(), nh, val[sd],
+                                          cnt.data() + (1 - sd) * nh, nullptr, &wsum[sd]),
+                           c);
+            }
+        }
+        *pairs = out[0] + (e->rank == 0 ? heavy_pairs : 0);
+        const uint64_t sum[2] = {out[1] + wsum[0], out[2] + wsum[1]};
+        for (int s = 0; s < nsel; s++) sums[s] = sum[side[s] ? 1 : 0];
+    });
 }
 
 void e_release(void* u, qe_h h) {
@@ -778,6 +889,8 @@ qe_engine make_engine(Eng* e) {
     g.release = e_release;
     g.fallback = e_fallback;
     g.mat_limit = &e->c->mat_limit;
+    // the last join of two base relations in aggregate form (QE_PLAN_JOIN_AGG=0: as other joins -- A/B)
+    g.join_agg = getenv("QE_PLAN_JOIN_AGG") && getenv("QE_PLAN_JOIN_AGG")[0] == '0' ? nullptr : e_join_agg;
     return g;
 }
 

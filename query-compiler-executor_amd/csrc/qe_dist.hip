@@ -8,6 +8,9 @@
 // sort + merge kernels.  Checksums are added mod 2^64 and all-reduced.
 #include <algorithm>
 
+#include <algorithm>
+#include <vector>
+
 #include "qe_device.h"
 #include "qe_internal.h"
 
@@ -255,7 +258,8 @@ __global__ void __launch_bounds__(BS_B) bucket_select_kernel(const uint64_t* __r
                                                              uint32_t nparts, uint32_t part,
                                                              const uint64_t* __restrict__ heavy, uint32_t nheavy,
                                                              uint64_t* __restrict__ okeys, uint32_t* __restrict__ ovals,
-                                                             uint64_t cap, unsigned long long* __restrict__ counter) {
+                                                             uint64_t cap, unsigned long long* __restrict__ counter,
+                                                             const uint64_t* __restrict__ vals) {
     __shared__ uint64_t s_key[BS_CAP];
     __shared__ uint32_t s_row[BS_CAP];
     extern __shared__ uint64_t s_heavy[];   // nheavy words (dynamic: no LDS when there are none)
@@ -321,7 +325,7 @@ __global__ void __launch_bounds__(BS_B) bucket_select_kernel(const uint64_t* __r
                 if (f[j][v]) {
                     const uint32_t o = fill + s_cnt[(j * 2 + v) * BS_NW + w] + rank[j][v];
                     s_key[o] = k[j][v];
-                    s_row[o] = (uint32_t)(i + v);
+                    s_row[o] = vals ? (uint32_t)vals[i + v] : (uint32_t)(i + v);   // a value column's low word, or the rowid
                 }
         }
         fill += total;
@@ -539,6 +543,81 @@ int qe_join_indices(qe_ctx* c, const uint64_t* keysA, uint64_t nA, const uint64_
 int qe_bucket_select(qe_ctx* c, qe_col col, uint32_t nparts, uint32_t part, const uint64_t* heavy, uint32_t nheavy,
                      qe_pairs* out) {
     QE_API_BEGIN(c)
+    bucket_select_dev(c, col, nparts, part, heavy, nheavy, nullptr, out);
+    return 0;
+    QE_API_END(c)
+}
+
+}  // extern "C"
+
+namespace qe {
+
+// every run longer than thr in a sorted sample: its key and length (first element of the run
+// only; a binary search finds the end), appended through one counter (runs that long are few)
+__global__ void __launch_bounds__(256) heavy_runs_kernel(const uint64_t* __restrict__ s, uint64_t n, uint64_t thr,
+                                                         unsigned long long* __restrict__ cnt, uint64_t* __restrict__ okey,
+                                                         uint64_t* __restrict__ olen, uint32_t cap) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n || i + thr >= n) return;
+    const uint64_t k = s[i];
+    if ((i > 0 && s[i - 1] == k) || s[i + thr] != k) return;
+    uint64_t lo = i + thr, hi = n;   // s[lo] == k; s[hi] != k or hi == n
+    while (lo + 1 < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (s[mid] == k) lo = mid;
+        else hi = mid;
+    }
+    const unsigned long long slot = atomicAdd(cnt, 1ull);
+    if (slot < cap) {
+        okey[slot] = k;
+        olen[slot] = lo + 1 - i;
+    }
+}
+
+std::vector<uint64_t> heavy_keys_dev(qe_ctx* c, const qe_col* cols, int ncols, uint64_t sample, uint64_t div,
+                                     uint32_t maxk) {
+    constexpr uint32_t CAP = 4096;
+    std::vector<std::pair<double, uint64_t>> cand;   // (sample frequency, key)
+    for (int ci = 0; ci < ncols; ci++) {
+        const uint64_t m = std::min<uint64_t>(sample, cols[ci].n);
+        const uint64_t thr = m / std::max<uint64_t>(div, 1);
+        if (m == 0 || thr + 1 >= m) continue;
+        SortOut so = radix_sort_u64(c, cols[ci].d, nullptr, m, false, nullptr, false);
+        const uint64_t* sorted = static_cast<const uint64_t*>(so.keys);
+        uint64_t* d = dalloc_t<uint64_t>(c, 2 * (uint64_t)CAP + 1);
+        unsigned long long* d_cnt = reinterpret_cast<unsigned long long*>(d + 2 * CAP);
+        QE_HIP(hipMemsetAsync(d_cnt, 0, 8, c->stream));
+        hipLaunchKernelGGL(heavy_runs_kernel, dim3(grid_for(m, 256)), dim3(256), 0, c->stream, sorted, m, thr, d_cnt, d,
+                           d + CAP, CAP);
+        QE_HIP(hipGetLastError());
+        const uint64_t got = std::min<uint64_t>(read_u64(c, reinterpret_cast<uint64_t*>(d_cnt)), CAP);
+        std::vector<uint64_t> h(2 * (size_t)CAP);
+        if (got) {
+            QE_HIP(hipMemcpyAsync(h.data(), d, got * 8, hipMemcpyDeviceToHost, c->stream));
+            QE_HIP(hipMemcpyAsync(h.data() + CAP, d + CAP, got * 8, hipMemcpyDeviceToHost, c->stream));
+            QE_HIP(hipStreamSynchronize(c->stream));
+        }
+        for (uint64_t i = 0; i < got; i++) cand.emplace_back((double)h[CAP + i] / (double)m, h[i]);
+        dfree(c, d);
+        if (so.keys_new) dfree(c, so.keys);
+        if (so.vals_new) dfree(c, so.vals);
+    }
+    // the most frequent first (a key heavy on both sides counts with its larger frequency), then
+    // the kept ones sorted ascending -- the same list on every rank (replicated columns)
+    std::sort(cand.begin(), cand.end(), [](const auto& a, const auto& b) {
+        return a.first != b.first ? a.first > b.first : a.second < b.second;
+    });
+    std::vector<uint64_t> keys;
+    for (const auto& x : cand) {
+        if (keys.size() >= maxk) break;
+        if (std::find(keys.begin(), keys.end(), x.second) == keys.end()) keys.push_back(x.second);
+    }
+    std::sort(keys.begin(), keys.end());
+    return keys;
+}
+
+void bucket_select_dev(qe_ctx* c, qe_col col, uint32_t nparts, uint32_t part, const uint64_t* heavy, uint32_t nheavy,
+                       const uint64_t* vals, qe_pairs* out) {
     if (nparts < 1 || part >= nparts) throw Error(QE_EINVAL, "bad bucket");
     if (nheavy > (uint32_t)HEAVY_MAX) throw Error(QE_EINVAL, "at most 1024 heavy keys");
     if (col.n >= 0xFFFFFFFFull) throw Error(QE_EINVAL, "column too large for 32-bit rowids");
@@ -570,7 +649,7 @@ int qe_bucket_select(qe_ctx* c, qe_col col, uint32_t nparts, uint32_t part, cons
         if (n) {
             Timed t(c, "bucket_select", 8.0 * n);
             hipLaunchKernelGGL(bucket_select_kernel, dim3(nb), dim3(BS_B), dyn, c->stream, col.d, n, nparts, part,
-                               d_heavy, nheavy, out->key, out->val, cap, d_cnt);
+                               d_heavy, nheavy, out->key, out->val, cap, d_cnt, vals);
             QE_HIP(hipGetLastError());
         }
         const uint64_t m = read_u64(c, reinterpret_cast<uint64_t*>(d_cnt));
@@ -583,13 +662,15 @@ int qe_bucket_select(qe_ctx* c, qe_col col, uint32_t nparts, uint32_t part, cons
         if (attempt == 1) throw Error(QE_EINVAL, "internal: bucket larger than its column");
         cap = n;
     }
-    add_bytes(c, "bucket_select", 12.0 * out->n);
+    add_bytes(c, "bucket_select", 12.0 * out->n + (vals ? 8.0 * n : 0.0));
     out->owns = 3;
-    out->flags = QE_PAIRS_DISTINCT;
+    out->flags = vals ? 0 : QE_PAIRS_DISTINCT;
     if (d_heavy) dfree(c, d_heavy);
-    return 0;
-    QE_API_END(c)
 }
+
+}  // namespace qe
+
+extern "C" {
 
 int qe_heavy_stats(qe_ctx* c, qe_col keys, uint64_t start, uint64_t end, const uint64_t* heavy, uint32_t nheavy,
                    qe_col vals, const uint64_t* weights, uint64_t* counts, uint64_t* wsum) {

@@ -255,7 +255,30 @@ void partition_dev(qe_ctx* c, const uint64_t* keys, uint64_t n, const uint32_t* 
 void key_bits_u64(qe_ctx* c, const uint64_t* keys, uint64_t n, uint64_t* out);
 // (key field << 32 | (uint32_t) val) words of a base column, stable-sorted by the field
 // (key >> lo) & (2^nb - 1), nb <= 32 (qe_join_aggregate); vals == null packs the row index
-uint64_t* sort_words_kv64(qe_ctx* c, const uint64_t* keys, const uint64_t* vals, uint64_t n, int lo, int nb);
+uint64_t* sort_words_kv64(qe_ctx* c, const uint64_t* keys, const uint64_t* vals, uint64_t n, int lo, int nb,
+                          const uint32_t* vals32 = nullptr);
+// the aggregate join (qe_agg.hip) over two sides given as arrays: keys with bounds kb = {OR, AND}
+// (a superset's are fine), values as a u64 column's low words (v64) or u32 (v32), or none (v64 =
+// v32 = null: that sum is 0).  out = {pairs, sum over pairs of R's value, of S's value} mod 2^64.
+// Sides of 2^32 rows or more, or keys varying in more than 32 bits: QE_ENOTSUP.
+struct AggSide {
+    const uint64_t* keys;
+    const uint64_t* v64;
+    const uint32_t* v32;
+    uint64_t n;
+    uint64_t kb[2];
+};
+void join_aggregate_sides(qe_ctx* c, const AggSide& R, const AggSide& S, uint64_t out[3]);
+// (qe_dist.hip) a replicated base column's bucket `part` of `nparts` without the sorted heavy
+// keys (qe_bucket_select), with a value column's low words beside each key instead of the rowid
+// (vals null: the rowid); out->val holds them
+void bucket_select_dev(qe_ctx* c, qe_col col, uint32_t nparts, uint32_t part, const uint64_t* heavy, uint32_t nheavy,
+                       const uint64_t* vals, qe_pairs* out);
+// (qe_dist.hip) the skew path's heavy keys: over the first `sample` rows of each column, the keys
+// whose run in the sorted sample is longer than sample / div -- at most maxk of them, the most
+// frequent, returned sorted.  Deterministic: every rank of replicated columns gets the same list.
+std::vector<uint64_t> heavy_keys_dev(qe_ctx* c, const qe_col* cols, int ncols, uint64_t sample, uint64_t div,
+                                     uint32_t maxk);
 
 }  // namespace qe
 

@@ -390,6 +390,241 @@ __global__ void __launch_bounds__(CB) compact_pipe_kernel(Op op, uint64_t n, uin
     }
 }
 
+// ---- wave-tile filter scan ----------------------------------------------------------------------
+// The column scans (filter scan, the fused scan + refine, with or without the survivors' values)
+// as WAVE-granular tiles: each wave owns WS_STEPS x 64 consecutive rows, loads them all at once
+// (one 8-byte element per lane per step: a wave instruction reads 512 contiguous bytes), ranks its
+// survivors with one ballot per step (kept in scalar registers), publishes its count, takes its
+// exclusive offset from the wave-parallel lookback and stores every step's survivors straight from
+// registers -- one instruction per step and output writes popcount(ballot) consecutive words.  No
+// LDS, no __syncthreads after the ticket: the four waves of a workgroup are independent, tens of
+// thousands of tiles stay in flight, and no phase of one tile waits for another wave's phase.
+// Deadlock-free by ticket order: a workgroup's ticket names its four consecutive tiles, and a wave
+// waits only for lower tiles, all taken by workgroups already running.
+#ifndef QE_WS_STEPS
+#define QE_WS_STEPS 32
+#endif
+constexpr int WS_STEPS = QE_WS_STEPS;
+constexpr int WS_B = 256;
+
+template <int STEPS, bool TWO, bool VALS>
+__global__ void __launch_bounds__(WS_B) wscan_kernel(FilterScan2Op op, uint64_t n, uint32_t ntiles, uint64_t* status,
+                                                    uint32_t* ticket, uint32_t epoch, uint32_t* __restrict__ out0,
+                                                    uint32_t* __restrict__ out1, uint64_t* total_out) {
+#ifdef QE_DIAG_STAMPS
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#define QE_WSTAMP(k, v)                                                                          \
+    do {                                                                                         \
+        if (l == 0 && tile < STAMP_TILES) g_cp_stamps[(uint64_t)tile * STAMP_SLOTS + (k)] = (v); \
+    } while (0)
+#else
+#define QE_WSTAMP(k, v) ((void)0)
+#endif
+    __shared__ uint32_t s_t;
+    if (threadIdx.x == 0) s_t = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t tile = s_t * (WS_B / WAVE) + (uint32_t)wave_id();
+    if (tile >= ntiles) return;
+    const int l = lane_id();
+    QE_WSTAMP(0, t_start);
+    QE_WSTAMP(1, __builtin_amdgcn_s_memrealtime());
+    const uint64_t lt = lanemask_lt();
+    const uint64_t base = (uint64_t)tile * (STEPS * WAVE) + (uint64_t)l;
+    uint64_t x[STEPS], y[TWO ? STEPS : 1];
+#pragma unroll
+    for (int j = 0; j < STEPS; j++) {
+        const uint64_t i = base + (uint64_t)j * WAVE;
+        x[j] = i < n ? __builtin_nontemporal_load(op.c1 + i) : 0;
+        if (TWO) y[j] = i < n ? __builtin_nontemporal_load(op.c2 + i) : 0;
+    }
+    uint64_t m[STEPS];
+    uint32_t val[VALS ? STEPS : 1];
+    uint32_t total = 0;
+#pragma unroll
+    for (int j = 0; j < STEPS; j++) {
+        const uint64_t i = base + (uint64_t)j * WAVE;
+        const bool f = i < n && cmp_rt(op.o1, x[j], op.v1) && cmp_rt(op.o2, TWO ? y[j] : x[j], op.v2);
+        m[j] = __ballot(f);
+        if (VALS) val[j] = (uint32_t)x[j];
+        total += (uint32_t)__popcll(m[j]);
+    }
+    QE_WSTAMP(2, __builtin_amdgcn_s_memrealtime());
+    lookback_publish(status, epoch, tile, total);
+    uint64_t off = lookback_wait(status, epoch, tile, total);
+    QE_WSTAMP(3, __builtin_amdgcn_s_memrealtime());
+    if (tile == ntiles - 1 && l == 0) *total_out = off + total;
+    const uint32_t row0 = (uint32_t)base;
+#pragma unroll
+    for (int j = 0; j < STEPS; j++) {
+        if ((m[j] >> l) & 1ull) {
+            const uint64_t o = off + (uint64_t)__popcll(m[j] & lt);
+            out0[o] = row0 + (uint32_t)(j * WAVE);
+            if (VALS) out1[o] = val[j];
+        }
+        off += (uint64_t)__popcll(m[j]);
+    }
+    QE_WSTAMP(4, __builtin_amdgcn_s_memrealtime());
+#undef QE_WSTAMP
+}
+
+#ifdef QE_DIAG_STAMPS
+#define QE_STAMP_W(tile, k)                                                                                   \
+    do {                                                                                                      \
+        if (lane_id() == 0 && (tile) < STAMP_TILES)                                                           \
+            g_cp_stamps[(uint64_t)(tile) * STAMP_SLOTS + (k)] = __builtin_amdgcn_s_memrealtime();              \
+    } while (0)
+#else
+#define QE_STAMP_W(tile, k) ((void)0)
+#endif
+
+// The persistent, software-pipelined form: each wave loops over tiles taken by its own ticket.
+// Per iteration: rank tile t (its loads have arrived), publish its count, take the next ticket
+// and issue that tile's loads, THEN wait for t's lookback and store t.  The wait (15.7 us of the
+// one-tile form's 38.5 us per tile, next to 13.7 us of loads -- tools/stamps.py "ws") overlaps
+// the next tile's loads, so a wave's memory pipe stays busy; t's inclusive prefix is published
+// as soon as its predecessors allow, as in the one-tile form.  (Storing t one iteration later
+// instead -- so that its lookback had a whole iteration to resolve -- measured 3.4x slower: the
+// inclusive prefixes then trail a full iteration and every lookback walks thousands of
+// aggregate-only tiles.)  Deadlock-free: a wave holds its current tile (published) and the next
+// (not yet); the smallest unfinished tile is a wave's current one, whose predecessors are all
+// finished.
+template <int STEPS, bool TWO, bool VALS>
+__global__ void __launch_bounds__(WS_B) wscan_pipe_kernel(FilterScan2Op op, uint64_t n, uint32_t ntiles,
+                                                         uint64_t* status, uint32_t* ticket, uint32_t epoch,
+                                                         uint32_t* __restrict__ out0, uint32_t* __restrict__ out1,
+                                                         uint64_t* total_out) {
+    static_assert(STEPS <= 32, "one flag bit per step in a u32");
+    const int l = lane_id();
+    const uint64_t lt = lanemask_lt();
+    auto take = [&]() -> uint32_t {
+        uint32_t t = 0;
+        if (l == 0) t = atomicAdd(ticket, 1u);
+        return (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+    };
+    uint64_t x[STEPS], y[TWO ? STEPS : 1];
+    auto load = [&](uint32_t t) {
+        const uint64_t base = (uint64_t)t * (STEPS * WAVE) + (uint64_t)l;
+#pragma unroll
+        for (int j = 0; j < STEPS; j++) {
+            const uint64_t i = base + (uint64_t)j * WAVE;
+            x[j] = i < n ? __builtin_nontemporal_load(op.c1 + i) : 0;
+            if (TWO) y[j] = i < n ? __builtin_nontemporal_load(op.c2 + i) : 0;
+        }
+    };
+    uint32_t t = take();
+    if (t >= ntiles) return;
+    load(t);
+    for (;;) {
+        const uint64_t base = (uint64_t)t * (STEPS * WAVE) + (uint64_t)l;
+        uint32_t fb = 0, total = 0;   // one flag bit per step (ranks re-derived by ballot at the store)
+        uint32_t val[VALS ? STEPS : 1];
+#pragma unroll
+        for (int j = 0; j < STEPS; j++) {
+            const uint64_t i = base + (uint64_t)j * WAVE;
+            const bool f = i < n && cmp_rt(op.o1, x[j], op.v1) && cmp_rt(op.o2, TWO ? y[j] : x[j], op.v2);
+            fb |= (uint32_t)f << j;
+            total += (uint32_t)__popcll(__ballot(f));
+            if (VALS) val[j] = (uint32_t)x[j];
+        }
+        QE_STAMP_W(t, 0);
+        lookback_publish(status, epoch, t, total);
+        const uint32_t tn = take();
+        if (tn < ntiles) load(tn);                 // in flight during t's lookback and stores
+        uint64_t off = lookback_wait(status, epoch, t, total);
+        QE_STAMP_W(t, 1);
+        if (t == ntiles - 1 && l == 0) *total_out = off + total;
+#pragma unroll
+        for (int j = 0; j < STEPS; j++) {
+            const bool f = (fb >> j) & 1u;
+            const uint64_t m = __ballot(f);
+            if (f) {
+                const uint64_t o = off + (uint64_t)__popcll(m & lt);
+                out0[o] = (uint32_t)base + (uint32_t)(j * WAVE);
+                if (VALS) out1[o] = val[j];
+            }
+            off += (uint64_t)__popcll(m);
+        }
+        QE_STAMP_W(t, 2);
+        if (tn >= ntiles) break;
+        t = tn;
+    }
+}
+
+#ifndef QE_WSP_STEPS
+#define QE_WSP_STEPS 16
+#endif
+#ifndef QE_WSP_VSTEPS
+#define QE_WSP_VSTEPS 16
+#endif
+// steps per wave tile of the pipelined scan: without / with the values output (the values of a
+// late-stored tile live in registers: 16 steps keep it at 2 x 16 VGPRs)
+constexpr int WSP_STEPS = QE_WSP_STEPS, WSP_VSTEPS = QE_WSP_VSTEPS;
+
+static bool wscan_pipe_on() {
+    static bool on = [] {   // tuning knob: QE_WSPIPE=0 keeps one tile per wave (wscan_kernel)
+        const char* s = getenv("QE_WSPIPE");
+        return !(s && s[0] == '0');
+    }();
+    return on;
+}
+
+static bool wscan_on() {
+    static bool on = [] {   // tuning knob: QE_WSCAN=0 keeps the workgroup-tile compaction for scans
+        const char* s = getenv("QE_WSCAN");
+        return !(s && s[0] == '0');
+    }();
+    return on;
+}
+
+// the scans through wscan_kernel: rowids (and c1's low words when outv) of the rows passing both
+// predicates; `bytes` = algorithmic input bytes (4 B per output per survivor added here)
+static uint64_t run_wscan(qe_ctx* c, double bytes, const FilterScan2Op& op, uint64_t n, uint32_t* out,
+                          uint32_t* outv) {
+    if (n == 0) return 0;
+    const bool two = op.c2 != op.c1;
+    const bool pipe = wscan_pipe_on();
+    const uint64_t TILE = (uint64_t)(pipe ? (outv ? WSP_VSTEPS : WSP_STEPS) : WS_STEPS) * WAVE;
+    const uint64_t nt = (n + TILE - 1) / TILE;
+    if (nt >= (1ull << 31)) throw Error(QE_EINVAL, "input too large");
+    LBSlot s = lb_acquire(c, nt);
+    uint64_t* d_total = c->d_scratch;
+    unsigned grid = (unsigned)((nt + WS_B / WAVE - 1) / (WS_B / WAVE));
+    if (pipe) {   // persistent: the workgroups that stay resident (a wave exits when the tickets run out)
+        static int ncu = 0;
+        if (!ncu) QE_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
+        const void* k = two ? (outv ? (const void*)wscan_pipe_kernel<WSP_VSTEPS, true, true>
+                                    : (const void*)wscan_pipe_kernel<WSP_STEPS, true, false>)
+                            : (outv ? (const void*)wscan_pipe_kernel<WSP_VSTEPS, false, true>
+                                    : (const void*)wscan_pipe_kernel<WSP_STEPS, false, false>);
+        int per = 1;
+        QE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, WS_B, 0));
+        grid = std::min<unsigned>(grid, (unsigned)(std::max(ncu, 1) * std::max(per, 1)));
+    }
+    {
+        Timed t(c, "filter_scan", bytes);
+#define QE_WS_LAUNCH(TWO, VALS)                                                                                \
+    if (pipe)                                                                                                  \
+        hipLaunchKernelGGL((wscan_pipe_kernel<VALS ? WSP_VSTEPS : WSP_STEPS, TWO, VALS>), dim3(grid),           \
+                           dim3(WS_B), 0, c->stream, op, n, (uint32_t)nt, s.status, s.ticket, s.epoch, out,     \
+                           outv, d_total);                                                                     \
+    else                                                                                                       \
+        hipLaunchKernelGGL((wscan_kernel<WS_STEPS, TWO, VALS>), dim3(grid), dim3(WS_B), 0, c->stream, op, n,   \
+                           (uint32_t)nt, s.status, s.ticket, s.epoch, out, outv, d_total)
+        if (two) {
+            if (outv) QE_WS_LAUNCH(true, true);
+            else QE_WS_LAUNCH(true, false);
+        } else {
+            if (outv) QE_WS_LAUNCH(false, true);
+            else QE_WS_LAUNCH(false, false);
+        }
+#undef QE_WS_LAUNCH
+        QE_HIP(hipGetLastError());
+    }
+    const uint64_t m = read_u64(c, d_total);
+    add_bytes(c, "filter_scan", (outv ? 8.0 : 4.0) * m);
+    return m;
+}
+
 static bool cp_pipe_on() {
     static bool on = [] {   // tuning knob: QE_CP_PIPE=0 keeps one tile per workgroup
         const char* s = getenv("QE_CP_PIPE");
@@ -403,6 +638,13 @@ extern "C" int qe_diag_stamps_cp(uint64_t* out, uint64_t n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(qe::g_cp_stamps), n * 8) == hipSuccess ? 0 : -2;
 }
 #endif
+
+static uint32_t op_code(char op) {
+    if (op == '=') return OP_EQ;
+    if (op == '>') return OP_GT;
+    if (op == '<') return OP_LT;
+    throw Error(QE_EINVAL, "Wrong operator");
+}
 
 // `bytes` = algorithmic input bytes; 4 B per output list per survivor is added once the count
 // is known (SURVEY.md §8(d) byte model).
@@ -441,6 +683,10 @@ static uint64_t run_compact(qe_ctx* c, const char* name, double bytes, const Op&
 uint64_t filter_scan(qe_ctx* c, const uint64_t* col, uint64_t n, char op, uint64_t v, uint32_t* out) {
     // read 8 B/row; the 4 B/survivor write is added by the caller-visible count below
     double b = 8.0 * n;
+    if (wscan_on()) {   // one predicate: the second is the same comparison of the same word
+        const uint32_t o = op_code(op);
+        return run_wscan(c, b, FilterScan2Op{col, col, v, v, o, o}, n, out, nullptr);
+    }
     uint64_t m;
     switch (op) {
     case '=': m = run_compact<FS_ITEMS, 1>(c, "filter_scan", b, FilterScanOp<OP_EQ>{col, v}, n, out, nullptr); break;
@@ -451,17 +697,11 @@ uint64_t filter_scan(qe_ctx* c, const uint64_t* col, uint64_t n, char op, uint64
     return m;
 }
 
-static uint32_t op_code(char op) {
-    if (op == '=') return OP_EQ;
-    if (op == '>') return OP_GT;
-    if (op == '<') return OP_LT;
-    throw Error(QE_EINVAL, "Wrong operator");
-}
-
 uint64_t filter_scan2(qe_ctx* c, const uint64_t* c1, char op1, uint64_t v1, const uint64_t* c2, char op2, uint64_t v2,
                       uint64_t n, uint32_t* out) {
     // read 8 B/row per distinct column; 4 B/survivor added below
     const FilterScan2Op o{c1, c2, v1, v2, op_code(op1), op_code(op2)};
+    if (wscan_on()) return run_wscan(c, (c1 == c2 ? 8.0 : 16.0) * n, o, n, out, nullptr);
     return run_compact<FS_ITEMS, 1>(c, "filter_scan", (c1 == c2 ? 8.0 : 16.0) * n, o, n, out, nullptr);
 }
 
@@ -473,6 +713,7 @@ uint64_t filter_scan2(qe_ctx* c, const uint64_t* c1, char op1, uint64_t v1, cons
 uint64_t filter_scan2_vals(qe_ctx* c, const uint64_t* c1, char op1, uint64_t v1, const uint64_t* c2, char op2,
                            uint64_t v2, uint64_t n, uint32_t* out, uint32_t* outv) {
     const FilterScan2Op o{c1, c2, v1, v2, op_code(op1), op_code(op2)};
+    if (wscan_on()) return run_wscan(c, (c1 == c2 ? 8.0 : 16.0) * n, o, n, out, outv);
     return run_compact<QE_FSV_ITEMS, 2>(c, "filter_scan", (c1 == c2 ? 8.0 : 16.0) * n, o, n, out, outv);
 }
 

@@ -2014,7 +2014,8 @@ static void complete_lsd(qe_ctx* c, const DeferredSort& d, uint64_t n) {
 // (field << 32 | (uint32_t) val[i]) words of a base column, sorted by the key field
 // (key >> lo) & (2^nb - 1): the aggregate join's sides (qe_join_aggregate), whose select column
 // rides in the word where the other sorts carry the rowid.  vals == null packs the row index.
-uint64_t* sort_words_kv64(qe_ctx* c, const uint64_t* keys, const uint64_t* vals, uint64_t n, int lo, int nb) {
+uint64_t* sort_words_kv64(qe_ctx* c, const uint64_t* keys, const uint64_t* vals, uint64_t n, int lo, int nb,
+                          const uint32_t* vals32) {
     if (n >= 0xFFFFFFFFull) throw Error(QE_EINVAL, "sort input too large");
     PassDesc pd{};
     const uint64_t fmask = nb >= 32 ? 0xFFFFFFFFull : (1ull << nb) - 1;
@@ -2042,13 +2043,17 @@ uint64_t* sort_words_kv64(qe_ctx* c, const uint64_t* keys, const uint64_t* vals,
         uint64_t* wo = buf[p & 1];
         const int dsh = 32 + pd.shift[p] - lo;
         LBSlot s = lb_acquire(c, nt * BINS);
-        Timed t(c, "sort_pass_agg", (p == 0 ? (vals ? 16.0 : 8.0) : 8.0) * n + 8.0 * n);
+        Timed t(c, "sort_pass_agg", (p == 0 ? (vals ? 16.0 : vals32 ? 12.0 : 8.0) : 8.0) * n + 8.0 * n);
         if (p > 0)
             hipLaunchKernelGGL((radix_pass_kernel<uint64_t, IN_WORD, OUT_WORD, true, 8, R_ITEMS, R_NT>), dim3((unsigned)nt),
                                dim3(R_NT), 0, c->stream, keys, win, nullptr, nullptr, wo, nullptr, n, dsh, pd.mask[p], f,
                                hist + p * BINS, s.status, s.ticket, s.epoch);
         // the first pass has no earlier order to keep, and the aggregate join needs none among
         // equal keys: unstable ranks there (the later LSD passes must keep theirs)
+        else if (vals32)   // (values already narrowed to 32 bits: a bucket's, qe_bucket_select_values)
+            hipLaunchKernelGGL((radix_pass_kernel<uint64_t, IN_KV, OUT_WORD, true, 8, R_ITEMS, R_NT, false, false, true>),
+                               dim3((unsigned)nt), dim3(R_NT), 0, c->stream, keys, nullptr, vals32, nullptr, wo, nullptr,
+                               n, dsh, pd.mask[p], f, hist + p * BINS, s.status, s.ticket, s.epoch);
         else if (vals)
             hipLaunchKernelGGL((radix_pass_kernel<uint64_t, IN_KV64, OUT_WORD, true, 8, R_ITEMS, R_NT, false, false, true>),
                                dim3((unsigned)nt), dim3(R_NT), 0, c->stream, keys, nullptr,

@@ -529,6 +529,35 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* s
     const qe_engine* e = P->e;
     const int ba = (int)p->frel, bb = (int)p->srel;
     const int A = component(P, ba), B = component(P, bb);
+    if (last && e->join_agg && is_whole(&P->C[A]) && is_whole(&P->C[B]) && P->q->nsel <= 64) {
+        /* the last join of two whole base relations, every select on one of them: aggregate form */
+        const query_t* q = P->q;
+        int side[64], ok = 1;
+        uint32_t cols[64];
+        for (size_t s = 0; ok && s < q->nsel; s++) {
+            const int b = (int)q->sel[2 * s];
+            side[s] = b == ba ? 0 : 1;
+            cols[s] = (uint32_t)q->sel[2 * s + 1];
+            ok = b == ba || b == bb;
+        }
+        if (ok) {
+            uint64_t pairs = 0;
+            const int jr = e->join_agg(e->u, q->rels[ba], (uint32_t)p->fcol, q->rels[bb], (uint32_t)p->scol,
+                                       (int)q->nsel, side, cols, &pairs, P->agg_sums);
+            if (jr == 0) {
+                ECHK(allreduce1(P, &pairs));
+                free_comp(P, A);
+                free_comp(P, B);
+                P->agg = 1;
+                P->agg_size = pairs;
+                return 0;
+            }
+            if (jr != QE_ENOTSUP) {
+                P->rc = jr;
+                return jr;
+            }
+        }
+    }
     side_t sa, sb;
     /* derived sides first, so their exchanges overlap the base side's local bucket scan */
     if (is_whole(&P->C[A])) {

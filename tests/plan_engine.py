@@ -41,8 +41,11 @@ FIELDS = [
 VALUES, VALUES_SRC = 0xFFFFFFFF, 4   # include/qe_plan.h: QE_PLAN_VALUES, QE_PLAN_VALUES_SRC
 
 
+JOIN_AGG = C.CFUNCTYPE(I, VP, U32, U32, U32, U32, I, P(I), P(U32), P(U64), P(U64))
+
+
 class Engine(C.Structure):
-    _fields_ = [("u", VP), ("rank", U32), ("world", U32)] + FIELDS + [("mat_limit", P(U64))]
+    _fields_ = [("u", VP), ("rank", U32), ("world", U32)] + FIELDS + [("mat_limit", P(U64)), ("join_agg", JOIN_AGG)]
 
 
 def part_of(k: np.ndarray, nparts: int) -> np.ndarray:
@@ -70,7 +73,8 @@ def join_local(ka, kb):
 class NumpyPlanEngine:
     """one rank: relations replicated as numpy columns; handles index a dict of arrays"""
 
-    def __init__(self, rels, rank=0, world=1, group=None, fused_scan=True, join_carry=True, join_sums=True, values=True):
+    def __init__(self, rels, rank=0, world=1, group=None, fused_scan=True, join_carry=True, join_sums=True, values=True,
+                 join_agg=True):
         self.rels, self.rank, self.world, self.group = rels, rank, world, group
         self.h, self.next, self.borrowed = {}, 1, set()
         self.exchanges = 0
@@ -96,6 +100,10 @@ class NumpyPlanEngine:
             cb = ftype(fn)
             self._cbs.append(cb)
             setattr(e, name, cb)
+        if join_agg:
+            self._agg_cb = JOIN_AGG(self._wrap(self.cb_join_agg, False))
+            e.join_agg = self._agg_cb
+        self.agg_calls = 0                       # last joins of two base relations in aggregate form
         self.e = e
         self._limit = None
 
@@ -249,6 +257,26 @@ class NumpyPlanEngine:
             with np.errstate(over="ignore"):
                 sums[s] = int(np.sum(cnt * vals, dtype=np.uint64))
 
+    def cb_join_agg(self, u, ra, ca, rb, cb, nsel, side, cols, pairs, sums):
+        """this rank's share: its row slice of each side, each row weighted by its key's partner
+        count in the other (replicated) side -- the shares add up to the join's numbers"""
+        self.agg_calls += 1
+        ka, kb = self.rels[ra][ca], self.rels[rb][cb]
+        sa, sb = np.sort(ka), np.sort(kb)
+        def slice_of(n):
+            return n * self.rank // self.world, n * (self.rank + 1) // self.world
+        a0, a1 = slice_of(len(ka))
+        b0, b1 = slice_of(len(kb))
+        ca_ = (np.searchsorted(sb, ka[a0:a1], "right") - np.searchsorted(sb, ka[a0:a1], "left")).astype(np.uint64)
+        cb_ = (np.searchsorted(sa, kb[b0:b1], "right") - np.searchsorted(sa, kb[b0:b1], "left")).astype(np.uint64)
+        pairs[0] = int(ca_.sum())
+        with np.errstate(over="ignore"):
+            for s in range(nsel):
+                if side[s] == 0:
+                    sums[s] = int(np.sum(ca_ * self.rels[ra][cols[s]][a0:a1], dtype=np.uint64))
+                else:
+                    sums[s] = int(np.sum(cb_ * self.rels[rb][cols[s]][b0:b1], dtype=np.uint64))
+
     def cb_values(self, u, rel, col, rows, out):
         c = self.rels[rel][col]
         if len(c) and int(c.max()) >> 32:
@@ -295,7 +323,7 @@ def free_port():
     return p
 
 
-def worker(rank, world, port, rels, queries, outq, limits=None, global_limit=None):
+def worker(rank, world, port, rels, queries, outq, limits=None, global_limit=None, opts=None):
     """one gloo rank: every query through the C plan, rank 0 reports (stdout, rc, rows, refused);
     limits[rank] (optional): that rank's materialisation limit (its local joins); global_limit
     (optional): the plan's limit on a join's all-ranks pair count"""
@@ -304,7 +332,7 @@ def worker(rank, world, port, rels, queries, outq, limits=None, global_limit=Non
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        eng = NumpyPlanEngine(rels, rank, world)
+        eng = NumpyPlanEngine(rels, rank, world, **(opts or {}))
         if limits:
             eng.mat_limit = limits[rank]
         if global_limit is not None:

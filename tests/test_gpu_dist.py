@@ -1,15 +1,15 @@
 """GPU tests of the multi-GPU plan's primitives (partition, bucket select, heavy stats, slices)
-and of the C5 aggregate plan (qe.dist.DistAggJoin) on qe.dist.GPUEngine.  The relational plan's
-GPU tests are tests/test_gpu_comm.py."""
+and of the C5 skew path inside the C plan (the engine's aggregate last join: heavy keys split by
+row slice, light keys bucketed) through qe_run_queries_local.  The relational plan's GPU tests
+are tests/test_gpu_comm.py and tests/test_gpu_local_ranks.py."""
 import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-import dist_cpu_engine as dce
+import goldens
 import gpu_dist_worker
 import plan_engine as pe
 from qe import datagen as dg
-from qe.dist import GPUEngine
 
 pytestmark = pytest.mark.gpu
 
@@ -110,34 +110,44 @@ def test_join_indices_and_take(ctx):
     np.testing.assert_array_equal(ctx.list_to_host(t), ha * 3)
 
 
-@pytest.mark.parametrize("world", [1, 2])
-def test_gpu_agg_plan_equals_faithful_executor_on_c5(ctx, world):
-    """DistAggJoin (heavy split + local buckets + aggregate merge) on the GPU equals the faithful
-    executor's aggregate path on the same Zipf data; world 2 = two gloo ranks on the one GPU"""
-    from qe.dist import DistAggJoin
-    rows = 3_000_000
-    queries = ["0 1|0.1=1.0|0.2 1.2", "0 1|0.1=1.0|1.2 0.2 0.0 1.1 0.1", "1 0|0.0=1.1|0.2 1.2"]
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_skew_join_on_ranks_equals_faithful_executor_on_c5(ctx, world):
+    """C5-shaped Zipf data (9 M rows per side: above QE_AGG_MIN = 2^24 rows in total, where the
+    aggregate form takes over): the C plan's aggregate last join at W in-process ranks -- heavy keys sampled, counted per row slice and all-reduced, light keys bucketed
+    locally -- prints the faithful executor's bytes (its qe_join_aggregate path) for every query"""
+    rows = 9_000_000
+    queries = ["0 1|0.1=1.0|0.2 1.2\n", "0 1|0.1=1.0|1.2 0.2 0.2 1.2\n", "1 0|0.0=1.1|0.2 1.2\n",
+               "0 1|0.1=1.0|0.2\n"]
     ctx.drop_relations()
-    dg.gen_c5(ctx, rows)
-    want = [ctx.run(q + "\n")[0] for q in queries]
-    if world == 1:
-        res = [DistAggJoin(GPUEngine(ctx, 0, 1), [rows, rows]).run(q) for q in queries]
+    try:
+        dg.gen_c5(ctx, rows)
+        for q in queries:
+            want, _ = ctx.run(q)
+            pairs = ctx.last_result_rows()
+            if world == 1:
+                out, rc, refused = ctx.run_dist(q)
+            else:
+                out, rc, refused, _ = ctx.run_local(q, world)
+            assert (out, rc, refused) == (want, 0, 0), (q, world)
+            assert ctx.last_result_rows() == pairs
+    finally:
         ctx.drop_relations()
-    else:
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_skew_join_on_ranks_matches_c5_goldens(ctx, world):
+    """every C5 golden of the real reference at W in-process ranks, bytes and status"""
+    doc = goldens.load(f"{goldens.GOLDEN_DIR}/c5.json")
+    rels, _ = goldens.dataset(doc["dataset"])
+    ctx.drop_relations()
+    try:
+        for cols in rels:
+            ctx.load_relation(cols)
+        for c in doc["cases"]:
+            out, rc, _, _ = ctx.run_local(c["input"], world)
+            assert (out, rc) == (c["stdout"], c["rc"]), c["input"]
+    finally:
         ctx.drop_relations()
-        mpc = mp.get_context("spawn")
-        q = mpc.Queue()
-        port = dce.free_port()
-        procs = [mpc.Process(target=gpu_dist_worker.agg_worker, args=(r, 2, port, rows, queries, q))
-                 for r in range(2)]
-        for p in procs:
-            p.start()
-        res = q.get(timeout=600)
-        for p in procs:
-            p.join(timeout=120)
-            assert p.exitcode == 0
-        assert all(nheavy > 0 for _, _, nheavy in res)
-    assert [r[0] for r in res] == want
 
 
 def test_c4_replicas_two_ranks_share_one_gpu():
@@ -145,7 +155,7 @@ def test_c4_replicas_two_ranks_share_one_gpu():
     plane) on the one GPU: the joined output is the full-size fixture's, byte for byte"""
     mpc = mp.get_context("spawn")
     q = mpc.Queue()
-    port = dce.free_port()
+    port = pe.free_port()
     procs = [mpc.Process(target=gpu_dist_worker.c4_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()

@@ -17,11 +17,11 @@ QE_ENOTSUP = -6
 C3 = "0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>1000000000&3.2<3000000000|1.2 2.2 3.2\n"
 
 
-def _run_world(rels, queries, world, limits=None, global_limit=None):
+def _run_world(rels, queries, world, limits=None, global_limit=None, opts=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = pe.free_port()
-    procs = [ctx.Process(target=pe.worker, args=(r, world, port, rels, queries, q, limits, global_limit))
+    procs = [ctx.Process(target=pe.worker, args=(r, world, port, rels, queries, q, limits, global_limit, opts))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -41,7 +41,7 @@ def test_every_golden_is_refused_or_exact(fixture, optional):
     doc = goldens.load(f"{goldens.GOLDEN_DIR}/{fixture}.json")
     rels, _ = goldens.dataset(doc["dataset"])
     on = optional == "all"
-    eng = pe.NumpyPlanEngine(rels, 0, 1, fused_scan=on, join_carry=on, join_sums=on, values=on)
+    eng = pe.NumpyPlanEngine(rels, 0, 1, fused_scan=on, join_carry=on, join_sums=on, values=on, join_agg=on)
     accepted = {"T": 0, "W": 0}
     for c in doc["cases"]:
         out, rc, _, _ = eng.run(c["input"])
@@ -58,6 +58,7 @@ def test_every_golden_is_refused_or_exact(fixture, optional):
         assert (eng.values_calls > 0) == on                # and select values ride instead of rowids
     if fixture == "headline" and on:
         assert eng.scan2_values > 0                        # C3's fused scan emits 3.2's values
+        assert eng.agg_calls > 0                           # G1/G2: two base relations, aggregate form
 
 
 def test_check_names_the_reason():
@@ -108,8 +109,11 @@ def test_one_rank_too_large_stops_every_rank():
     the query with QE_ETOOBIG together (one all-reduce), none waits forever in the next exchange"""
     rows = 20_000
     rels = dg.make_relations(dg.chain_spec(4, rows), 1)
-    res, _, _ = _run_world(rels, [C3, "0 1|0.1=1.0|0.2 1.2\n"], 2, limits=[1 << 62, 100])
+    res, _, _ = _run_world(rels, [C3, "0 1|0.1=1.0|0.2 1.2\n"], 2, limits=[1 << 62, 100], opts={"join_agg": False})
     assert res[0][1] == -5 and res[1][1] == -5
+    # the last join of two base relations in aggregate form materialises nothing: no limit applies
+    res, _, _ = _run_world(rels, ["0 1|0.1=1.0|0.2 1.2\n"], 2, limits=[1 << 62, 100])
+    assert res[0][1] == 0
 
 
 def test_global_pair_count_is_what_the_limit_bounds():
@@ -119,11 +123,11 @@ def test_global_pair_count_is_what_the_limit_bounds():
     rows = 20_000
     rels = dg.make_relations(dg.chain_spec(4, rows), 1)
     q2 = "0 1|0.1=1.0|0.2 1.2\n"
-    one = pe.NumpyPlanEngine(rels, 0, 1)
+    one = pe.NumpyPlanEngine(rels, 0, 1, join_agg=False)
     out, rc, pairs, _ = one.run(q2)
     assert rc == 0 and pairs > 1000
     limit = pairs * 2 // 3                    # above each of two ranks' ~pairs/2, below the total
     one.set_global_limit(limit)
     assert one.run(q2)[1] == -5
-    res, _, _ = _run_world(rels, [q2], 2, global_limit=limit)
+    res, _, _ = _run_world(rels, [q2], 2, global_limit=limit, opts={"join_agg": False})
     assert res[0][1] == -5

@@ -24,6 +24,8 @@ PHASES = {
     "cp": ["ticket", "load+ballots", "scan+lookback", "stage", "write"],
     "ag": ["load+keys", "walks", "sums"],
     "cpp": ["ballots (data wait)", "scan+publish", "stage+prefetch+lookback", "write"],
+    "ws": ["ticket", "loads+ballots", "lookback", "stores"],
+    "wsp": ["lookback (next loads in flight)", "stores"],
     "hj": ["bounds+loads issued", "R loaded+hist", "scan+scatter", "S counts+wave scans", "slice atomic", "emit (t0)"],
 }
 
@@ -32,7 +34,7 @@ def report(ctx, which, ntiles):
     buf = np.zeros(ntiles * SLOTS, dtype=np.uint64)
     fn = ctx.lib.qe_diag_stamps
     fn.argtypes = [C.c_char_p, C.c_void_p, C.c_uint64]
-    rc = fn(("cp" if which == "cpp" else which).encode(), buf.ctypes.data, buf.size)   # "hj": the sort file
+    rc = fn(("cp" if which in ("cpp", "ws", "wsp") else which).encode(), buf.ctypes.data, buf.size)   # "hj": the sort file
     assert rc == 0, rc
     st = buf.reshape(ntiles, SLOTS).astype(np.int64)
     names = PHASES[which]
@@ -43,6 +45,10 @@ def report(ctx, which, ntiles):
     d = np.diff(st, axis=1) * 10.0 / 1000.0   # ticks of 10 ns -> us
     span = (st[:, -1].max() - st[:, 0].min()) * 10.0 / 1000.0
     busy = (st[:, -1] - st[:, 0]).sum() * 10.0 / 1000.0
+    if which in ("ws", "wsp"):   # start/end order: how far behind its dispatch a tile's lookback resolves
+        order = np.argsort(st[:, 0])
+        print(f"   start spread {np.ptp(st[:, 0]) * 0.01:.1f} us; tiles ordered by start finish "
+              f"{np.mean(np.diff(st[order, -1]) < 0) * 100:.1f}% out of order")
     print(f"== {which}: {ok.sum()} tiles, span {span:.1f} us, mean tiles in flight {busy / span:.1f}, "
           f"mean tile {(st[:, -1] - st[:, 0]).mean() * 0.01:.2f} us")
     for i, nm in enumerate(names):
@@ -95,7 +101,12 @@ def main():
     if "cp" in a.what:
         l1 = ctx.filter_scan(ctx.column(r0, 2), ">", 1_000_000_000)
         ctx.sync()
-        report(ctx, "cpp" if os.environ.get("QE_CP_PIPE", "1") != "0" else "cp", (n + a.cp_tile - 1) // a.cp_tile)
+        if os.environ.get("QE_WSCAN", "1") != "0" and os.environ.get("QE_WSPIPE", "1") != "0":
+            report(ctx, "wsp", (n + 1023) // 1024)             # persistent wave tiles of 16 x 64 rows
+        elif os.environ.get("QE_WSCAN", "1") != "0":           # wave tiles of WS_STEPS x 64 rows
+            report(ctx, "ws", (n + 2047) // 2048)
+        else:
+            report(ctx, "cpp" if os.environ.get("QE_CP_PIPE", "1") != "0" else "cp", (n + a.cp_tile - 1) // a.cp_tile)
         ctx.list_free(l1)
     if "sort" not in a.what and "mj" not in a.what:
         ctx.close()
