@@ -43,11 +43,12 @@ typedef struct qe_engine {
     /* relation metadata (replicated on every rank) */
     int (*rel_count)(void* u, uint32_t* n);
     int (*rel_shape)(void* u, uint32_t rel, uint64_t* rows, uint32_t* ncols);
-    /* a1 on rows [start, end): rowids (global numbering) with col[r] op v, ascending */
+    /* a1 on rows [start, end): rowids (global numbering) with col[r] op v, in no particular order
+     * (the plan's lists feed only order-free consumers: its accepted queries are relational) */
     int (*scan)(void* u, uint32_t rel, uint32_t col, uint64_t start, uint64_t end, char op, uint64_t v, qe_h* out);
     /* rowids start .. start + n - 1 */
     int (*iota)(void* u, uint64_t start, uint64_t n, qe_h* out);
-    /* a2: the rowids r of `rows` with col[r] op v, in order (`rows` is consumed) */
+    /* a2: the rowids r of `rows` with col[r] op v, in their order (`rows` is consumed) */
     int (*refine)(void* u, uint32_t rel, uint32_t col, qe_h rows, char op, uint64_t v, qe_h* out);
     /* a4: keys col[rows[i]] (`rows` is borrowed) */
     int (*keys)(void* u, uint32_t rel, uint32_t col, qe_h rows, qe_h* out);
@@ -75,7 +76,7 @@ typedef struct qe_engine {
      * reference's exit code path (QE_EEXIT) -- identical on every rank */
     int (*fallback)(void* u, void* query, void* out);
     /* a1 then a2 on the same binding, fused (nullable): rowids r in [start, end) with
-     * col1[r] op1 v1 and col2[r] op2 v2, ascending -- one pass over the column(s) instead of a
+     * col1[r] op1 v1 and col2[r] op2 v2, in no particular order -- one pass over the column(s) instead of a
      * scan and a refine gathering through its list.  values = 1: the plan expects to ask for col1's
      * values of this list later (`values` below) -- the engine may emit them from the same pass */
     int (*scan2)(void* u, uint32_t rel, uint32_t col1, char op1, uint64_t v1, uint32_t col2, char op2, uint64_t v2,

@@ -102,11 +102,6 @@ __global__ void __launch_bounds__(256) gather_u32_kernel(const uint64_t* __restr
     }
 }
 
-__global__ void __launch_bounds__(256) shift_u32_kernel(uint32_t* __restrict__ a, uint64_t n, uint32_t add) {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < n) a[i] += add;
-}
-
 // sum of a list's own u32 values mod 2^64 (a binding that carries its select's values)
 __global__ void __launch_bounds__(256) sum_u32_kernel(const uint32_t* __restrict__ v, uint64_t n,
                                                       unsigned long long* __restrict__ out) {
@@ -241,12 +236,18 @@ qe_col column(qe_ctx* c, uint32_t rel, uint32_t col) {
     return q;
 }
 
+// the plan's scans: its lists feed only order-free consumers (key gathers before a sort, the
+// bucket join, sums), so they come from the unordered wave-tile scan (qe_scan.hip)
 int e_scan(void* u, uint32_t rel, uint32_t col, uint64_t s, uint64_t t, char op, uint64_t v, qe_h* out) {
     Eng* e = E(u);
     return guard(e, [&] {
-        qe_list l{};
-        ck(qe_filter_scan_range(e->c, column(e->c, rel, col), s, t, op, v, &l), e->c);
-        *out = H(new_arr(e->c, l.d, l.n, false));
+        qe_ctx* c = e->c;
+        const qe_col q = column(c, rel, col);
+        if (t > q.n || s > t) throw Error(QE_EINVAL, "bad row range");
+        const uint64_t n = t - s;
+        uint32_t* d = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
+        const uint64_t m = filter_scan2_unordered(c, q.d + s, op, v, q.d + s, op, v, n, (uint32_t)s, d, nullptr);
+        *out = H(new_arr(c, d, m, false));
     });
 }
 
@@ -256,31 +257,23 @@ int e_scan2(void* u, uint32_t rel, uint32_t col1, char op1, uint64_t v1, uint32_
     return guard(e, [&] {
         qe_ctx* c = e->c;
         uint64_t kor = 0, kand = 0;
-        // the value-carrying scan (half-size tiles, 4 more bytes written per survivor) only when the
-        // plan expects to ask for col1's values
-        const bool vals_on = values && !(getenv("QE_SCAN_VALUES") && getenv("QE_SCAN_VALUES")[0] == '0');
-        if (vals_on && qe_relation_column_bits(c, (int)rel, (int)col1, &kor, &kand) == 0 && !(kor >> 32)) {
-            // the survivors' col1 values come out of the same pass (the plan may ask for them)
-            const qe_col q1 = column(c, rel, col1), q2 = column(c, rel, col2);
-            if (t > q1.n || t > q2.n || s > t) throw Error(QE_EINVAL, "bad row range");
-            const uint64_t n = t - s;
-            uint32_t* d = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
-            uint32_t* dv = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
-            const uint64_t m = filter_scan2_vals(c, q1.d + s, op1, v1, q2.d + s, op2, v2, n, d, dv);
-            if (s && m) {   // rowids in the relation's numbering (this rank's slice starts at s)
-                hipLaunchKernelGGL(shift_u32_kernel, dim3(grid_for(m, 256)), dim3(256), 0, c->stream, d, m, (uint32_t)s);
-                QE_HIP(hipGetLastError());
-            }
-            DArr* a = new_arr(c, d, m, false);
+        // the survivors' col1 values come out of the same pass when the plan expects to ask for them
+        // (4 more bytes written per survivor)
+        const bool vals = values && !(getenv("QE_SCAN_VALUES") && getenv("QE_SCAN_VALUES")[0] == '0') &&
+                          qe_relation_column_bits(c, (int)rel, (int)col1, &kor, &kand) == 0 && !(kor >> 32);
+        const qe_col q1 = column(c, rel, col1), q2 = column(c, rel, col2);
+        if (t > q1.n || t > q2.n || s > t) throw Error(QE_EINVAL, "bad row range");
+        const uint64_t n = t - s;
+        uint32_t* d = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
+        uint32_t* dv = vals ? dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1)) : nullptr;
+        const uint64_t m = filter_scan2_unordered(c, q1.d + s, op1, v1, q2.d + s, op2, v2, n, (uint32_t)s, d, dv);
+        DArr* a = new_arr(c, d, m, false);
+        if (vals) {
             a->vcache = dv;
             a->vrel = rel;
             a->vcol = col1;
-            *out = H(a);
-            return;
         }
-        qe_list l{};
-        ck(qe_filter_scan2_range(c, column(c, rel, col1), op1, v1, column(c, rel, col2), op2, v2, s, t, &l), c);
-        *out = H(new_arr(c, l.d, l.n, false));
+        *out = H(a);
     });
 }
 

@@ -390,6 +390,8 @@ __global__ void __launch_bounds__(CB) compact_pipe_kernel(Op op, uint64_t n, uin
     }
 }
 
+static uint32_t op_code(char op);
+
 // ---- wave-tile filter scan ----------------------------------------------------------------------
 // The column scans (filter scan, the fused scan + refine, with or without the survivors' values)
 // as WAVE-granular tiles: each wave owns WS_STEPS x 64 consecutive rows, loads them all at once
@@ -467,107 +469,6 @@ __global__ void __launch_bounds__(WS_B) wscan_kernel(FilterScan2Op op, uint64_t 
 #undef QE_WSTAMP
 }
 
-#ifdef QE_DIAG_STAMPS
-#define QE_STAMP_W(tile, k)                                                                                   \
-    do {                                                                                                      \
-        if (lane_id() == 0 && (tile) < STAMP_TILES)                                                           \
-            g_cp_stamps[(uint64_t)(tile) * STAMP_SLOTS + (k)] = __builtin_amdgcn_s_memrealtime();              \
-    } while (0)
-#else
-#define QE_STAMP_W(tile, k) ((void)0)
-#endif
-
-// The persistent, software-pipelined form: each wave loops over tiles taken by its own ticket.
-// Per iteration: rank tile t (its loads have arrived), publish its count, take the next ticket
-// and issue that tile's loads, THEN wait for t's lookback and store t.  The wait (15.7 us of the
-// one-tile form's 38.5 us per tile, next to 13.7 us of loads -- tools/stamps.py "ws") overlaps
-// the next tile's loads, so a wave's memory pipe stays busy; t's inclusive prefix is published
-// as soon as its predecessors allow, as in the one-tile form.  (Storing t one iteration later
-// instead -- so that its lookback had a whole iteration to resolve -- measured 3.4x slower: the
-// inclusive prefixes then trail a full iteration and every lookback walks thousands of
-// aggregate-only tiles.)  Deadlock-free: a wave holds its current tile (published) and the next
-// (not yet); the smallest unfinished tile is a wave's current one, whose predecessors are all
-// finished.
-template <int STEPS, bool TWO, bool VALS>
-__global__ void __launch_bounds__(WS_B) wscan_pipe_kernel(FilterScan2Op op, uint64_t n, uint32_t ntiles,
-                                                         uint64_t* status, uint32_t* ticket, uint32_t epoch,
-                                                         uint32_t* __restrict__ out0, uint32_t* __restrict__ out1,
-                                                         uint64_t* total_out) {
-    static_assert(STEPS <= 32, "one flag bit per step in a u32");
-    const int l = lane_id();
-    const uint64_t lt = lanemask_lt();
-    auto take = [&]() -> uint32_t {
-        uint32_t t = 0;
-        if (l == 0) t = atomicAdd(ticket, 1u);
-        return (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-    };
-    uint64_t x[STEPS], y[TWO ? STEPS : 1];
-    auto load = [&](uint32_t t) {
-        const uint64_t base = (uint64_t)t * (STEPS * WAVE) + (uint64_t)l;
-#pragma unroll
-        for (int j = 0; j < STEPS; j++) {
-            const uint64_t i = base + (uint64_t)j * WAVE;
-            x[j] = i < n ? __builtin_nontemporal_load(op.c1 + i) : 0;
-            if (TWO) y[j] = i < n ? __builtin_nontemporal_load(op.c2 + i) : 0;
-        }
-    };
-    uint32_t t = take();
-    if (t >= ntiles) return;
-    load(t);
-    for (;;) {
-        const uint64_t base = (uint64_t)t * (STEPS * WAVE) + (uint64_t)l;
-        uint32_t fb = 0, total = 0;   // one flag bit per step (ranks re-derived by ballot at the store)
-        uint32_t val[VALS ? STEPS : 1];
-#pragma unroll
-        for (int j = 0; j < STEPS; j++) {
-            const uint64_t i = base + (uint64_t)j * WAVE;
-            const bool f = i < n && cmp_rt(op.o1, x[j], op.v1) && cmp_rt(op.o2, TWO ? y[j] : x[j], op.v2);
-            fb |= (uint32_t)f << j;
-            total += (uint32_t)__popcll(__ballot(f));
-            if (VALS) val[j] = (uint32_t)x[j];
-        }
-        QE_STAMP_W(t, 0);
-        lookback_publish(status, epoch, t, total);
-        const uint32_t tn = take();
-        if (tn < ntiles) load(tn);                 // in flight during t's lookback and stores
-        uint64_t off = lookback_wait(status, epoch, t, total);
-        QE_STAMP_W(t, 1);
-        if (t == ntiles - 1 && l == 0) *total_out = off + total;
-#pragma unroll
-        for (int j = 0; j < STEPS; j++) {
-            const bool f = (fb >> j) & 1u;
-            const uint64_t m = __ballot(f);
-            if (f) {
-                const uint64_t o = off + (uint64_t)__popcll(m & lt);
-                out0[o] = (uint32_t)base + (uint32_t)(j * WAVE);
-                if (VALS) out1[o] = val[j];
-            }
-            off += (uint64_t)__popcll(m);
-        }
-        QE_STAMP_W(t, 2);
-        if (tn >= ntiles) break;
-        t = tn;
-    }
-}
-
-#ifndef QE_WSP_STEPS
-#define QE_WSP_STEPS 16
-#endif
-#ifndef QE_WSP_VSTEPS
-#define QE_WSP_VSTEPS 16
-#endif
-// steps per wave tile of the pipelined scan: without / with the values output (the values of a
-// late-stored tile live in registers: 16 steps keep it at 2 x 16 VGPRs)
-constexpr int WSP_STEPS = QE_WSP_STEPS, WSP_VSTEPS = QE_WSP_VSTEPS;
-
-static bool wscan_pipe_on() {
-    static bool on = [] {   // tuning knob: QE_WSPIPE=0 keeps one tile per wave (wscan_kernel)
-        const char* s = getenv("QE_WSPIPE");
-        return !(s && s[0] == '0');
-    }();
-    return on;
-}
-
 static bool wscan_on() {
     static bool on = [] {   // tuning knob: QE_WSCAN=0 keeps the workgroup-tile compaction for scans
         const char* s = getenv("QE_WSCAN");
@@ -582,34 +483,17 @@ static uint64_t run_wscan(qe_ctx* c, double bytes, const FilterScan2Op& op, uint
                           uint32_t* outv) {
     if (n == 0) return 0;
     const bool two = op.c2 != op.c1;
-    const bool pipe = wscan_pipe_on();
-    const uint64_t TILE = (uint64_t)(pipe ? (outv ? WSP_VSTEPS : WSP_STEPS) : WS_STEPS) * WAVE;
+    constexpr uint64_t TILE = (uint64_t)WS_STEPS * WAVE;
     const uint64_t nt = (n + TILE - 1) / TILE;
     if (nt >= (1ull << 31)) throw Error(QE_EINVAL, "input too large");
     LBSlot s = lb_acquire(c, nt);
     uint64_t* d_total = c->d_scratch;
-    unsigned grid = (unsigned)((nt + WS_B / WAVE - 1) / (WS_B / WAVE));
-    if (pipe) {   // persistent: the workgroups that stay resident (a wave exits when the tickets run out)
-        static int ncu = 0;
-        if (!ncu) QE_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
-        const void* k = two ? (outv ? (const void*)wscan_pipe_kernel<WSP_VSTEPS, true, true>
-                                    : (const void*)wscan_pipe_kernel<WSP_STEPS, true, false>)
-                            : (outv ? (const void*)wscan_pipe_kernel<WSP_VSTEPS, false, true>
-                                    : (const void*)wscan_pipe_kernel<WSP_STEPS, false, false>);
-        int per = 1;
-        QE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, WS_B, 0));
-        grid = std::min<unsigned>(grid, (unsigned)(std::max(ncu, 1) * std::max(per, 1)));
-    }
+    const unsigned grid = (unsigned)((nt + WS_B / WAVE - 1) / (WS_B / WAVE));
     {
         Timed t(c, "filter_scan", bytes);
 #define QE_WS_LAUNCH(TWO, VALS)                                                                                \
-    if (pipe)                                                                                                  \
-        hipLaunchKernelGGL((wscan_pipe_kernel<VALS ? WSP_VSTEPS : WSP_STEPS, TWO, VALS>), dim3(grid),           \
-                           dim3(WS_B), 0, c->stream, op, n, (uint32_t)nt, s.status, s.ticket, s.epoch, out,     \
-                           outv, d_total);                                                                     \
-    else                                                                                                       \
-        hipLaunchKernelGGL((wscan_kernel<WS_STEPS, TWO, VALS>), dim3(grid), dim3(WS_B), 0, c->stream, op, n,   \
-                           (uint32_t)nt, s.status, s.ticket, s.epoch, out, outv, d_total)
+    hipLaunchKernelGGL((wscan_kernel<WS_STEPS, TWO, VALS>), dim3(grid), dim3(WS_B), 0, c->stream, op, n,       \
+                       (uint32_t)nt, s.status, s.ticket, s.epoch, out, outv, d_total)
         if (two) {
             if (outv) QE_WS_LAUNCH(true, true);
             else QE_WS_LAUNCH(true, false);
@@ -621,6 +505,113 @@ static uint64_t run_wscan(qe_ctx* c, double bytes, const FilterScan2Op& op, uint
         QE_HIP(hipGetLastError());
     }
     const uint64_t m = read_u64(c, d_total);
+    add_bytes(c, "filter_scan", (outv ? 8.0 : 4.0) * m);
+    return m;
+}
+
+// ---- unordered filter scan (the partitioned plan's) ---------------------------------------------
+// The plan's filter lists feed only order-free consumers (key gathers whose sort follows, the
+// bucket join, sums): so its scans need no lookback.  Each wave loads its US_STEPS x 64 rows and
+// ranks its survivors by ballot as above; the workgroup adds up its waves' counts, reserves its
+// output run with ONE atomic on a global counter and every wave stores its part -- no ticket (a
+// workgroup waits for nobody: tile = block id), no status words.  The ordered form's per-tile
+// time was 38.5 us: 4.2 ticket, 13.7 loads, 15.7 lookback wait, 4.9 stores (tools/stamps.py "ws",
+// profiles/r03_wscan_stamps.log).  One atomic per WAVE measured slower than the ordered form
+// (0.625 vs 0.347 ms per 1e8 rows, profiles/r03_uscan_wave_ab.log): 48.8 k returning atomics on one
+// address serialise at the memory side (~12 ns each), so the reservation is per workgroup of
+// US_B / 64 waves.  A run is ascending, the runs are in no particular order.  row_base is added
+// to every rowid (a rank's slice numbered globally).
+#ifndef QE_US_B
+#define QE_US_B 1024
+#endif
+#ifndef QE_US_STEPS
+#define QE_US_STEPS 16
+#endif
+constexpr int US_B = QE_US_B, US_STEPS = QE_US_STEPS;
+
+template <int STEPS, bool TWO, bool VALS>
+__global__ void __launch_bounds__(US_B) uscan_kernel(FilterScan2Op op, uint64_t n, uint32_t row_base,
+                                                    uint32_t* __restrict__ out0, uint32_t* __restrict__ out1,
+                                                    unsigned long long* __restrict__ counter) {
+    constexpr int NW = US_B / WAVE;
+    __shared__ uint32_t s_wtot[NW];
+    __shared__ uint64_t s_base;
+    const int w = wave_id(), l = lane_id();
+    const uint64_t tile = (uint64_t)blockIdx.x * NW + (uint64_t)w;
+    const uint64_t lt = lanemask_lt();
+    const uint64_t base = tile * (STEPS * WAVE) + (uint64_t)l;
+    uint64_t x[STEPS], y[TWO ? STEPS : 1];
+#pragma unroll
+    for (int j = 0; j < STEPS; j++) {
+        const uint64_t i = base + (uint64_t)j * WAVE;
+        x[j] = i < n ? __builtin_nontemporal_load(op.c1 + i) : 0;
+        if (TWO) y[j] = i < n ? __builtin_nontemporal_load(op.c2 + i) : 0;
+    }
+    uint32_t fb = 0, total = 0;
+    uint32_t val[VALS ? STEPS : 1];
+#pragma unroll
+    for (int j = 0; j < STEPS; j++) {
+        const uint64_t i = base + (uint64_t)j * WAVE;
+        const bool f = i < n && cmp_rt(op.o1, x[j], op.v1) && cmp_rt(op.o2, TWO ? y[j] : x[j], op.v2);
+        fb |= (uint32_t)f << j;
+        total += (uint32_t)__popcll(__ballot(f));
+        if (VALS) val[j] = (uint32_t)x[j];
+    }
+    if (l == 0) s_wtot[w] = total;
+    __syncthreads();
+    if (w == 0) {   // the waves' exclusive offsets inside the workgroup's run; one atomic for the run
+        const uint32_t c = l < NW ? s_wtot[l] : 0u;
+        const uint32_t inc = wave_incl_scan_u32(c);
+        const uint32_t sum = (uint32_t)__shfl((int)inc, 63, 64);
+        if (l < NW) s_wtot[l] = inc - c;
+        if (l == 0) s_base = sum ? atomicAdd(counter, (unsigned long long)sum) : 0ull;
+    }
+    __syncthreads();
+    uint64_t off = s_base + s_wtot[w];
+    if (total == 0) return;
+    const uint32_t row0 = (uint32_t)base + row_base;
+#pragma unroll
+    for (int j = 0; j < STEPS; j++) {
+        const bool f = (fb >> j) & 1u;
+        const uint64_t m = __ballot(f);
+        if (f) {
+            const uint64_t o = off + (uint64_t)__popcll(m & lt);
+            out0[o] = row0 + (uint32_t)(j * WAVE);
+            if (VALS) out1[o] = val[j];
+        }
+        off += (uint64_t)__popcll(m);
+    }
+}
+
+uint64_t filter_scan2_unordered(qe_ctx* c, const uint64_t* c1, char op1, uint64_t v1, const uint64_t* c2, char op2,
+                                uint64_t v2, uint64_t n, uint32_t row_base, uint32_t* out, uint32_t* outv) {
+    if (n == 0) return 0;
+    const FilterScan2Op op{c1, c2, v1, v2, op_code(op1), op_code(op2)};
+    static const bool ordered = getenv("QE_PLAN_USCAN") && getenv("QE_PLAN_USCAN")[0] == '0';   // A/B knob
+    if (ordered && row_base == 0) return run_wscan(c, (c1 == c2 ? 8.0 : 16.0) * n, op, n, out, outv);
+    const bool two = c2 != c1;
+    constexpr uint64_t TILE = (uint64_t)US_STEPS * US_B;   // rows per workgroup
+    const uint64_t nt = (n + TILE - 1) / TILE;
+    if (nt >= (1ull << 31)) throw Error(QE_EINVAL, "input too large");
+    unsigned long long* d_cnt = reinterpret_cast<unsigned long long*>(c->d_scratch);
+    QE_HIP(hipMemsetAsync(d_cnt, 0, sizeof(uint64_t), c->stream));
+    const unsigned grid = (unsigned)nt;
+    {
+        Timed t(c, "filter_scan", (two ? 16.0 : 8.0) * n);
+#define QE_US_LAUNCH(TWO, VALS)                                                                                \
+    hipLaunchKernelGGL((uscan_kernel<US_STEPS, TWO, VALS>), dim3(grid), dim3(US_B), 0, c->stream, op, n,       \
+                       row_base, out, outv, d_cnt)
+        if (two) {
+            if (outv) QE_US_LAUNCH(true, true);
+            else QE_US_LAUNCH(true, false);
+        } else {
+            if (outv) QE_US_LAUNCH(false, true);
+            else QE_US_LAUNCH(false, false);
+        }
+#undef QE_US_LAUNCH
+        QE_HIP(hipGetLastError());
+    }
+    const uint64_t m = read_u64(c, reinterpret_cast<uint64_t*>(d_cnt));
     add_bytes(c, "filter_scan", (outv ? 8.0 : 4.0) * m);
     return m;
 }

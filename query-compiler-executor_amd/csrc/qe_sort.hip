@@ -1281,6 +1281,139 @@ __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
     }
 }
 
+// The same join with R's rows CHAINED by key value instead of counting-sorted: one LDS exchange per
+// R row (head[v] <- i, nxt[i] <- old head) replaces the histogram, the scan of the 2^L counts and
+// the scatter -- two barrier-separated phases of the ~10.4 us per bucket (3.1 us scan + scatter,
+// profiles/r02_hjoin_stamps.log).  An S row counts its partners by walking its value's chain (mean
+// length |R bucket| / 2^L, ~0.75 at C3) and the wave-cooperative emission walks it again to the
+// pair's partner.  Output is the same multiset of pairs (in no particular order, as before).
+constexpr uint32_t HJ_NONE = 0xFFFFu;
+static_assert(TL_CAP < HJ_NONE, "chain links are 16-bit row indices");
+
+template <int DBITS, bool CARRY = false>
+__global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
+tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict__ bsR, const uint64_t* __restrict__ wS,
+                      const uint32_t* __restrict__ bsS, int L, uint32_t* __restrict__ outR, uint32_t* __restrict__ outS,
+                      uint64_t cap, uint64_t* total_out, const uint64_t* __restrict__ xS = nullptr,
+                      uint32_t* __restrict__ outX0 = nullptr, uint32_t* __restrict__ outX1 = nullptr) {
+    __shared__ uint32_t head[1 << DBITS];   // per key value: the last R row inserted (HJ_NONE: none)
+    __shared__ uint16_t nxt[TL_CAP];        // per R row: the previous row of its value
+    __shared__ uint32_t rr[TL_CAP];         // per R row: its rowid
+    __shared__ uint32_t tab[HJ_I * HJ_NW];
+    __shared__ uint64_t s_excl;
+    __shared__ uint32_t s_total;
+    const uint32_t b = blockIdx.x;
+    const uint32_t r0 = bsR[b], mR = bsR[b + 1] - r0, s0 = bsS[b], mS = bsS[b + 1] - s0;
+    if (mR > (uint32_t)TL_CAP || mS > (uint32_t)TL_CAP) {   // beyond LDS (the sorts were not checked): flag it
+        if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(total_out + 1), 1ull);
+        return;
+    }
+    const uint32_t D = 1u << L, dmask = D - 1u;
+    const int w = wave_id(), l = lane_id();
+    uint64_t wr[HJ_I], ws[HJ_I];
+#pragma unroll
+    for (int j = 0; j < HJ_I; j++) {
+        const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
+        wr[j] = i < mR ? wR[r0 + i] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < HJ_I; j++) {
+        const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
+        ws[j] = i < mS ? wS[s0 + i] : 0;
+    }
+    uint64_t xv[CARRY ? HJ_I : 1];
+    if constexpr (CARRY) {
+#pragma unroll
+        for (int j = 0; j < HJ_I; j++) {
+            const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
+            xv[j] = i < mS ? xS[s0 + i] : 0ull;
+        }
+    }
+    for (uint32_t v = threadIdx.x; v < D; v += HJ_NT) head[v] = HJ_NONE;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < HJ_I; j++) {
+        const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
+        if (i < mR) {
+            nxt[i] = (uint16_t)atomicExch(&head[fld(wr[j]) & dmask], i);
+            rr[i] = (uint32_t)wr[j];
+        }
+    }
+    __syncthreads();
+    uint32_t pre[HJ_I], hd[HJ_I], tot[HJ_I];
+#pragma unroll
+    for (int j = 0; j < HJ_I; j++) {
+        uint32_t cnt = 0, h = HJ_NONE;
+        if ((uint32_t)j * HJ_NT + threadIdx.x < mS) {
+            h = head[fld(ws[j]) & dmask];
+            for (uint32_t p = h; p != HJ_NONE; p = nxt[p]) cnt++;
+        }
+        hd[j] = h;
+        const uint32_t inc = wave_incl_scan_u32(cnt);
+        pre[j] = inc - cnt;
+        tot[j] = (uint32_t)__shfl((int)inc, 63, 64);   // the item's pairs in this wave
+        if (l == 63) tab[j * HJ_NW + w] = inc;
+    }
+    __syncthreads();
+    if (w == 0) {   // (row group, wave) totals in row order -> bucket offsets; one atomic per bucket
+        constexpr uint32_t E = HJ_I * HJ_NW;
+        const uint32_t a0 = 2u * l < E ? tab[2 * l] : 0u, a1 = 2u * l + 1 < E ? tab[2 * l + 1] : 0u;
+        const uint32_t inc = wave_incl_scan_u32(a0 + a1);
+        const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
+        if (2u * l < E) tab[2 * l] = inc - a0 - a1;
+        if (2u * l + 1 < E) tab[2 * l + 1] = inc - a1;
+        if (l == 0) {
+            s_excl = total ? atomicAdd(reinterpret_cast<unsigned long long*>(total_out), (unsigned long long)total)
+                           : 0ull;
+            s_total = total;
+        }
+    }
+    __syncthreads();
+    const uint64_t gofs = s_excl;
+    if (gofs + s_total > cap) return;   // outgrew the buffers: the host re-runs with the exact size
+#pragma unroll
+    for (int j = 0; j < HJ_I; j++) {   // wave-cooperative emission, as tl_hjoin_kernel's
+        const uint32_t pj = pre[j], all = tot[j];
+        const uint64_t ob = gofs + tab[j * HJ_NW + w];
+        const uint32_t srow = (uint32_t)ws[j];
+        for (uint32_t q0 = 0; q0 < all; q0 += 64) {   // wave-uniform
+            const uint32_t q = q0 + (uint32_t)l;
+            int owner = 0;
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1) {
+                const int cand = owner + step;
+                const uint32_t pc = (uint32_t)__shfl((int)pj, cand < 64 ? cand : 63, 64);
+                if (cand < 64 && pc <= q) owner = cand;
+            }
+            const uint32_t k = q - (uint32_t)__shfl((int)pj, owner, 64);
+            uint32_t p = (uint32_t)__shfl((int)hd[j], owner, 64);
+            const uint32_t sr = (uint32_t)__shfl((int)srow, owner, 64);
+            uint32_t x0 = 0, x1 = 0;
+            if constexpr (CARRY) {
+                x0 = (uint32_t)__shfl((int)(uint32_t)xv[j], owner, 64);
+                x1 = (uint32_t)__shfl((int)(uint32_t)(xv[j] >> 32), owner, 64);
+            }
+            if (q < all) {
+                for (uint32_t s = 0; s < k; s++) p = nxt[p];   // the k-th partner on the chain
+                outR[ob + q] = rr[p];
+                outS[ob + q] = sr;
+                if constexpr (CARRY) {
+                    outX0[ob + q] = x0;
+                    if (outX1) outX1[ob + q] = x1;
+                }
+            }
+        }
+    }
+}
+
+static bool hj_chain_on() {
+    static bool on = [] {   // tuning knob: QE_HJ_CHAIN=0 keeps the counting-sort bucket join
+        const char* s = getenv("QE_HJ_CHAIN");
+        return !(s && s[0] == '0');
+    }();
+    return on;
+}
+
 // Non-packable pairs (64-bit keys with > 32 varying bits AND a rowid): key and rowid staged
 // separately.  Kept simple: rare in this workload (never in the measured configs).
 template <typename K, bool VIN>
@@ -2192,7 +2325,22 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
         {
             // algorithmic bytes: both sides' words in (+ 8 B per pair below; + S's payloads)
             Timed t(c, "bucket_join", 8.0 * (double)(nR + nS) + (carry ? 8.0 * (double)nS : 0.0));
-            if (carry && dR.L <= 12)
+            if (hj_chain_on()) {
+                if (carry && dR.L <= 12)
+                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream,
+                                       dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17,
+                                       dS.x, x0, x1);
+                else if (carry)
+                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<HJ_DBITS, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
+                                       c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
+                                       c->d_scratch + 17, dS.x, x0, x1);
+                else if (dR.L <= 12)
+                    hipLaunchKernelGGL(tl_hjoin_chain_kernel<12>, dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream, dR.words,
+                                       dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17);
+                else
+                    hipLaunchKernelGGL(tl_hjoin_chain_kernel<HJ_DBITS>, dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream,
+                                       dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17);
+            } else if (carry && dR.L <= 12)
                 hipLaunchKernelGGL((tl_hjoin_kernel<12, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream, dR.words,
                                    dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17, dS.x, x0, x1);
             else if (carry)

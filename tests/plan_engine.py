@@ -163,16 +163,20 @@ class NumpyPlanEngine:
         rows[0] = len(self.rels[rel][0]) if self.rels[rel] else 0
         ncols[0] = len(self.rels[rel])
 
+    def _unordered(self, rows):
+        """like libqe's unordered scans: the plan must not depend on a list's order"""
+        return np.random.default_rng(len(rows) + 31 * self.rank).permutation(rows).astype(np.uint32)
+
     def cb_scan(self, u, rel, col, s, t, op, v, out):
         c = self.rels[rel][col][s:t]
-        out[0] = self.put((np.nonzero(_OPS[op.decode()](c, np.uint64(v)))[0] + s).astype(np.uint32))
+        out[0] = self.put(self._unordered(np.nonzero(_OPS[op.decode()](c, np.uint64(v)))[0] + s))
 
     def cb_scan2(self, u, rel, c1, op1, v1, c2, op2, v2, s, t, values, out):
         self.scan2_values += bool(values)
         a = self.rels[rel][c1][s:t]
         b = self.rels[rel][c2][s:t]
         m = _OPS[op1.decode()](a, np.uint64(v1)) & _OPS[op2.decode()](b, np.uint64(v2))
-        out[0] = self.put((np.nonzero(m)[0] + s).astype(np.uint32))
+        out[0] = self.put(self._unordered(np.nonzero(m)[0] + s))
 
     def cb_iota(self, u, s, n, out):
         out[0] = self.put(np.arange(s, s + n, dtype=np.uint32))
