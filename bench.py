@@ -74,6 +74,21 @@ def roofline(stats: dict, traffic: dict | None):
             "launches": s["launches"]}
 
 
+def stage_roofline(stats: dict, traffic: dict | None) -> dict:
+    out = {}
+    for name, s in sorted(stats.items(), key=lambda kv: -kv[1]["ms"]):
+        if not s["launches"] or s["ms"] <= 0 or not s["alg_bytes"]:
+            continue
+        per_ms = s["ms"] / s["launches"]
+        per_b = s["alg_bytes"] / s["launches"]
+        gbs = per_b / (per_ms * 1e-3) / 1e9
+        t = traffic.get(name) if traffic else None
+        out[name] = {"launches": s["launches"], "avg_launch_ms": round(per_ms, 4), "alg_gb_per_launch": round(per_b / 1e9, 4),
+                     "achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 3),
+                     "traffic_over_alg": round(t / per_b, 3) if t else None}
+    return out
+
+
 def load_traffic(workload: str = "c3"):
     """HBM bytes per launch from the rocprofv3 PMC passes committed under profiles/ for this
     workload (files without a "workload" key are C3), or None -- never another workload's."""
@@ -234,6 +249,9 @@ def run_dist(args):
             "host_round_trips_per_step": stage_stats.get("host_round_trip", {}).get("launches", 0) / args.steps,
             "stage_table_loop_ms_per_step": round(dt_stages / args.steps * 1e3, 3),
             "stages": {k: {"ms_per_step": round(s["ms"] / args.steps, 3)} for k, s in kern[:12]},
+            # every stage against the same roofline (algorithmic bytes per launch / mean launch time
+            # of the stage-table loop), with its PMC traffic ratio where profiles/ has one
+            "stage_roofline": stage_roofline(stage_stats, load_traffic("c3_plan")),
         }
         if not args.no_cpu:
             res["cpu_baseline"] = cpu_baseline(args.cpu_rows, args.seed, ctx)

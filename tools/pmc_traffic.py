@@ -43,7 +43,7 @@ STAGES = [
     (r"tl_hjoin_sums_kernel|hjoin_sums_reduce_kernel", "bucket_join_sums"),
     (r"gather_u32_kernel", "gather_values"),
     (r"sum_u32_kernel", "checksum"),
-    (r"tl_hjoin_kernel", "bucket_join"),
+    (r"tl_hjoin_kernel|tl_hjoin_chain_kernel", "bucket_join"),
     (r"mj_fused", "mj_fused"),
     (r"mj_partition", "mj_partition"),
     (r"mj_tile<1>", "mj_write"),
@@ -52,7 +52,7 @@ STAGES = [
     (r"expand_kernel<0>|tile_scan_kernel", "payload_count"),
     (r"NonzeroPairsOp", "payload_prune"),
     (r"nonzero_bitmap_kernel", "payload_bitmap"),
-    (r"FilterScanOp|FilterScan2Op", "filter_scan"),
+    (r"FilterScanOp|FilterScan2Op|wscan_kernel|uscan_kernel", "filter_scan"),
     (r"zip_take_kernel", "take_u32"),
     (r"ag_tile_kernel|ag_reduce_kernel", "agg_count"),
     (r"ag_split_kernel", "agg_split"),
