@@ -291,6 +291,252 @@ __global__ void __launch_bounds__(1024) ag_reduce_kernel(const uint64_t* __restr
     }
 }
 
+// ---- the bucketed aggregate join ---------------------------------------------------------------
+// Both sides' (key field << 32 | value) words partitioned into the 2^15 buckets of the field's top
+// bits (partition_words_kv: the two-level sort's two global passes, no per-bucket sort); inside a
+// bucket a key is its field's L low bits, a dense domain of 2^L values counted in LDS.  Per bucket
+// (one workgroup):  cnt <- S's key counts;  R rows: pairs += cnt[k], sumR += valR * cnt[k];
+// cnt <- R's key counts;  S rows: sumS += valS * cnt[k].  Two reads of each side's words, no
+// merge, no search.  A bucket side beyond AB_BIG rows (a Zipf head key) goes to the giant path:
+// many workgroups per bucket, counts pre-aggregated in LDS per chunk and added to a per-bucket
+// global count table.  Counting takes ONE LDS atomic per wave for the lanes whose key equals the
+// first valid lane's (a head key fills whole waves), one per lane otherwise.
+constexpr int AB_NT = 1024, AB_U = 8;
+#ifndef QE_AB_BIG
+#define QE_AB_BIG (1u << 18)
+#endif
+constexpr uint32_t AB_BIG = QE_AB_BIG;
+constexpr uint32_t AB_CHUNK = 1u << 16;   // giant path: rows per workgroup
+
+__device__ __forceinline__ uint32_t ab_val(uint64_t w, uint32_t dmask) { return (uint32_t)(w >> 32) & dmask; }
+
+__device__ __forceinline__ void ab_count(const uint64_t* __restrict__ w, uint32_t m, uint32_t dmask,
+                                         uint32_t* __restrict__ cnt) {
+    const int l = lane_id();
+    for (uint32_t i0 = threadIdx.x; i0 < m; i0 += AB_NT * AB_U) {   // (block-uniform trip count: i0 - tid)
+        uint64_t x[AB_U];
+#pragma unroll
+        for (int u = 0; u < AB_U; u++) {
+            const uint32_t i = i0 + (uint32_t)u * AB_NT;
+            x[u] = i < m ? w[i] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < AB_U; u++) {
+            const uint32_t i = i0 + (uint32_t)u * AB_NT;
+            const bool valid = i < m;
+            const uint32_t v = ab_val(x[u], dmask);
+            const uint64_t vb = __ballot(valid);
+            if (!vb) continue;
+            const int leader = __ffsll((unsigned long long)vb) - 1;
+            const uint32_t v0 = (uint32_t)__shfl((int)v, leader, 64);
+            const uint64_t same = __ballot(valid && v == v0);
+            if (valid) {
+                if (v != v0) atomicAdd(&cnt[v], 1u);
+                else if (l == leader) atomicAdd(&cnt[v0], (uint32_t)__popcll(same));
+            }
+        }
+    }
+}
+
+// rows of w[0..m): a0 += cnt[k], a1 += (u32) value * cnt[k]
+__device__ __forceinline__ void ab_lookup(const uint64_t* __restrict__ w, uint32_t m, uint32_t dmask,
+                                          const uint32_t* __restrict__ cnt, uint64_t& a0, uint64_t& a1) {
+    for (uint32_t i0 = threadIdx.x; i0 < m; i0 += AB_NT * AB_U) {
+        uint64_t x[AB_U];
+#pragma unroll
+        for (int u = 0; u < AB_U; u++) {
+            const uint32_t i = i0 + (uint32_t)u * AB_NT;
+            x[u] = i < m ? w[i] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < AB_U; u++) {
+            const uint32_t i = i0 + (uint32_t)u * AB_NT;
+            if (i < m) {
+                const uint64_t c = cnt[ab_val(x[u], dmask)];
+                a0 += c;
+                a1 += (uint64_t)(uint32_t)x[u] * c;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void ab_zero(uint32_t* cnt, uint32_t D) {
+    for (uint32_t v = threadIdx.x * 4; v < D; v += AB_NT * 4) *reinterpret_cast<uint4*>(cnt + v) = make_uint4(0, 0, 0, 0);
+}
+
+// block sum of three u64 -> out[0..2] (plain stores, thread 0)
+__device__ __forceinline__ void ab_reduce3(uint64_t a0, uint64_t a1, uint64_t a2, uint64_t* __restrict__ out,
+                                           bool atomic) {
+    __shared__ uint64_t red[AB_NT / 64][3];
+    a0 = wave_sum_u64(a0);
+    a1 = wave_sum_u64(a1);
+    a2 = wave_sum_u64(a2);
+    if (lane_id() == 0) {
+        red[wave_id()][0] = a0;
+        red[wave_id()][1] = a1;
+        red[wave_id()][2] = a2;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        uint64_t t = 0;
+        for (int w = 0; w < AB_NT / 64; w++) t += red[w][threadIdx.x];
+        if (atomic) atomicAdd(reinterpret_cast<unsigned long long*>(out + threadIdx.x), (unsigned long long)t);
+        else out[threadIdx.x] = t;
+    }
+}
+
+// one workgroup per bucket; a giant bucket is listed (b, mR, mS) for the giant path
+__global__ void __launch_bounds__(AB_NT) ab_bucket_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict__ bsR,
+                                                          const uint64_t* __restrict__ wS, const uint32_t* __restrict__ bsS,
+                                                          int L, uint64_t* __restrict__ part, uint32_t* __restrict__ big,
+                                                          unsigned long long* __restrict__ nbig) {
+    __shared__ uint32_t cnt[1u << 15];
+    const uint32_t b = blockIdx.x;
+    const uint32_t r0 = bsR[b], mR = bsR[b + 1] - r0, s0 = bsS[b], mS = bsS[b + 1] - s0;
+    if (mR == 0 || mS == 0) {
+        if (threadIdx.x < 3) part[(uint64_t)b * 3 + threadIdx.x] = 0;
+        return;
+    }
+    if (mR > AB_BIG || mS > AB_BIG) {
+        if (threadIdx.x < 3) part[(uint64_t)b * 3 + threadIdx.x] = 0;
+        if (threadIdx.x == 0) {
+            const unsigned long long k = atomicAdd(nbig, 1ull);
+            big[3 * k] = b;
+            big[3 * k + 1] = mR;
+            big[3 * k + 2] = mS;
+        }
+        return;
+    }
+    const uint32_t D = 1u << L, dmask = D - 1u;
+    const uint64_t* __restrict__ bR = wR + r0;
+    const uint64_t* __restrict__ bS = wS + s0;
+    uint64_t pairs = 0, sR = 0, sS = 0, dummy = 0;
+    ab_zero(cnt, D);
+    __syncthreads();
+    ab_count(bS, mS, dmask, cnt);
+    __syncthreads();
+    ab_lookup(bR, mR, dmask, cnt, pairs, sR);
+    __syncthreads();
+    ab_zero(cnt, D);
+    __syncthreads();
+    ab_count(bR, mR, dmask, cnt);
+    __syncthreads();
+    ab_lookup(bS, mS, dmask, cnt, dummy, sS);
+    ab_reduce3(pairs, sR, sS, part + (uint64_t)b * 3, false);
+}
+
+// giant path, counting: workgroup (x, g) counts rows [x * AB_CHUNK, ...) of giant g's side in LDS
+// and adds the nonzero counts to g's global table
+__global__ void __launch_bounds__(AB_NT) ab_big_count_kernel(const uint64_t* __restrict__ w, const uint32_t* __restrict__ bs,
+                                                             const uint32_t* __restrict__ big, int side, int L,
+                                                             uint32_t* __restrict__ gcnt) {
+    __shared__ uint32_t cnt[1u << 15];
+    const uint32_t g = blockIdx.y, b = big[3 * g], m = big[3 * g + 1 + side];
+    const uint32_t c0 = blockIdx.x * AB_CHUNK;
+    if (c0 >= m) return;
+    const uint32_t mc = m - c0 < AB_CHUNK ? m - c0 : AB_CHUNK;
+    const uint32_t D = 1u << L, dmask = D - 1u;
+    ab_zero(cnt, D);
+    __syncthreads();
+    ab_count(w + bs[b] + c0, mc, dmask, cnt);
+    __syncthreads();
+    uint32_t* __restrict__ gc = gcnt + (uint64_t)g * D;
+    for (uint32_t v = threadIdx.x; v < D; v += AB_NT)
+        if (cnt[v]) atomicAdd(&gc[v], cnt[v]);
+}
+
+// giant path, lookups against g's global table: acc[0] += counts (with_pairs), acc[1 + side] +=
+// value * count
+__global__ void __launch_bounds__(AB_NT) ab_big_look_kernel(const uint64_t* __restrict__ w, const uint32_t* __restrict__ bs,
+                                                            const uint32_t* __restrict__ big, int side, int L,
+                                                            const uint32_t* __restrict__ gcnt, int with_pairs,
+                                                            uint64_t* __restrict__ acc) {
+    const uint32_t g = blockIdx.y, b = big[3 * g], m = big[3 * g + 1 + side];
+    const uint32_t c0 = blockIdx.x * AB_CHUNK;
+    if (c0 >= m) return;
+    const uint32_t mc = m - c0 < AB_CHUNK ? m - c0 : AB_CHUNK;
+    const uint32_t D = 1u << L, dmask = D - 1u;
+    uint64_t a0 = 0, a1 = 0;
+    ab_lookup(w + bs[b] + c0, mc, dmask, gcnt + (uint64_t)g * D, a0, a1);
+    ab_reduce3(with_pairs ? a0 : 0, side == 0 ? a1 : 0, side == 1 ? a1 : 0, acc, true);
+}
+
+__global__ void __launch_bounds__(256) ab_sum3_kernel(const uint64_t* __restrict__ part, uint32_t nb,
+                                                      uint64_t* __restrict__ out) {
+    const uint32_t k = blockIdx.x;
+    uint64_t t = 0;
+    for (uint32_t b = threadIdx.x; b < nb; b += 256) t += part[(uint64_t)b * 3 + k];
+    t = wave_sum_u64(t);
+    __shared__ uint64_t red[4];
+    if (lane_id() == 0) red[wave_id()] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) out[k] += red[0] + red[1] + red[2] + red[3];
+}
+
+static bool agg_buckets_on() {
+    static bool on = [] {   // tuning knob: QE_AGG_BUCKETS=0 keeps the sort + merge-path counting form
+        const char* s = getenv("QE_AGG_BUCKETS");
+        return !(s && s[0] == '0');
+    }();
+    return on;
+}
+
+// out = {pairs, sumR, sumS} (values as AggSide: none -> the caller zeroes that sum)
+static void join_aggregate_buckets(qe_ctx* c, const AggSide& R, const AggSide& S, int lo, int nb, uint64_t out[3]) {
+    constexpr uint32_t NB = 1u << AGG_BUCKET_BITS;
+    const int L = nb - AGG_BUCKET_BITS;
+    uint64_t *wR = nullptr, *wS = nullptr;
+    uint32_t *bsR = nullptr, *bsS = nullptr;
+    partition_words_kv(c, R.keys, R.v64, R.v32, R.n, lo, nb, &wR, &bsR);
+    partition_words_kv(c, S.keys, S.v64, S.v32, S.n, lo, nb, &wS, &bsS);
+    uint64_t* part = dalloc_t<uint64_t>(c, (size_t)NB * 3);
+    uint32_t* big = dalloc_t<uint32_t>(c, (size_t)NB * 3);
+    uint64_t* d = dalloc_t<uint64_t>(c, 4);   // [pairs, sumR, sumS, giant buckets]
+    QE_HIP(hipMemsetAsync(d, 0, 4 * sizeof(uint64_t), c->stream));
+    {
+        Timed t(c, "agg_count", 8.0 * 2.0 * (double)(R.n + S.n));
+        hipLaunchKernelGGL(ab_bucket_kernel, dim3(NB), dim3(AB_NT), 0, c->stream, wR, bsR, wS, bsS, L, part, big,
+                           reinterpret_cast<unsigned long long*>(d + 3));
+        QE_HIP(hipGetLastError());
+        hipLaunchKernelGGL(ab_sum3_kernel, dim3(3), dim3(256), 0, c->stream, part, NB, d);
+        QE_HIP(hipGetLastError());
+    }
+    uint64_t h[4];
+    read_words(c, d, h, 4);
+    const uint32_t ng = (uint32_t)h[3];
+    if (ng) {   // the giant buckets (Zipf head keys): many workgroups each
+        std::vector<uint32_t> bl(3 * (size_t)ng);
+        QE_HIP(hipMemcpyAsync(bl.data(), big, bl.size() * 4, hipMemcpyDeviceToHost, c->stream));
+        QE_HIP(hipStreamSynchronize(c->stream));
+        uint32_t mx[2] = {1, 1};
+        for (uint32_t g = 0; g < ng; g++)
+            for (int sd = 0; sd < 2; sd++) mx[sd] = std::max(mx[sd], bl[3 * g + 1 + sd]);
+        const size_t D = (size_t)1 << L;
+        uint32_t* gc = dalloc_t<uint32_t>(c, (size_t)ng * D);
+        Timed t(c, "agg_big", 0.0);   // (its bytes are counted in agg_count)
+        for (int phase = 0; phase < 2; phase++) {
+            const int cs = phase == 0 ? 1 : 0, ls = phase == 0 ? 0 : 1;   // count side, lookup side
+            const uint64_t* wc = cs ? wS : wR;
+            const uint32_t* bc = cs ? bsS : bsR;
+            const uint64_t* wl = ls ? wS : wR;
+            const uint32_t* bl_ = ls ? bsS : bsR;
+            QE_HIP(hipMemsetAsync(gc, 0, (size_t)ng * D * 4, c->stream));
+            hipLaunchKernelGGL(ab_big_count_kernel, dim3((mx[cs] + AB_CHUNK - 1) / AB_CHUNK, ng), dim3(AB_NT), 0, c->stream,
+                               wc, bc, big, cs, L, gc);
+            QE_HIP(hipGetLastError());
+            hipLaunchKernelGGL(ab_big_look_kernel, dim3((mx[ls] + AB_CHUNK - 1) / AB_CHUNK, ng), dim3(AB_NT), 0, c->stream,
+                               wl, bl_, big, ls, L, gc, phase == 0 ? 1 : 0, d);
+            QE_HIP(hipGetLastError());
+        }
+        read_words(c, d, h, 3);
+        dfree(c, gc);
+    }
+    out[0] = h[0];
+    out[1] = h[1];
+    out[2] = h[2];
+    for (void* p : {(void*)wR, (void*)wS, (void*)bsR, (void*)bsS, (void*)part, (void*)big, (void*)d}) dfree(c, p);
+}
+
 // OR / AND of a column: the load-time statistics of a relation column, else one pass
 static void col_bits(qe_ctx* c, const uint64_t* d, uint64_t n, uint64_t kb[2]) {
     for (const Relation& r : c->rels)
@@ -326,6 +572,12 @@ void join_aggregate_sides(qe_ctx* c, const AggSide& R, const AggSide& S, uint64_
     }
     // (bits outside the field are equal in every key of both sides: comparing fields is exact)
     if (nb > 32) throw Error(QE_ENOTSUP, "aggregate join keys vary in more than 32 bits");
+    if (agg_buckets_on() && nb > AGG_BUCKET_BITS && nb <= AGG_BUCKET_BITS + 15 && nR + nS >= (1ull << 22)) {
+        join_aggregate_buckets(c, R, S, lo, nb, out);   // two partition passes per side, LDS counting
+        if (!R.v64 && !R.v32) out[1] = 0;
+        if (!S.v64 && !S.v32) out[2] = 0;
+        return;
+    }
     uint64_t* wR = sort_words_kv64(c, R.keys, R.v64, nR, lo, nb, R.v32);
     uint64_t* wS = sort_words_kv64(c, S.keys, S.v64, nS, lo, nb, S.v32);
     const uint64_t m = nR + nS;

@@ -273,6 +273,12 @@ struct AggSide {
     uint64_t kb[2];
 };
 void join_aggregate_sides(qe_ctx* c, const AggSide& R, const AggSide& S, uint64_t out[3]);
+// (qe_sort.hip) the two-level sort's two global passes alone over (key field << 32 | value) words:
+// *words (n) partitioned into 2^15 buckets of the field's top 15 bits, *bstart the 2^15 + 1 bucket
+// starts -- no order inside a bucket.  nb (the field's width, from bit lo) in 16..31.
+void partition_words_kv(qe_ctx* c, const uint64_t* keys, const uint64_t* v64, const uint32_t* v32, uint64_t n, int lo,
+                        int nb, uint64_t** words, uint32_t** bstart);
+constexpr int AGG_BUCKET_BITS = 15;
 // (qe_dist.hip) a replicated base column's bucket `part` of `nparts` without the sorted heavy
 // keys (qe_bucket_select), with a value column's low words beside each key instead of the rowid
 // (vals null: the rowid); out->val holds them

@@ -2205,6 +2205,71 @@ uint64_t* sort_words_kv64(qe_ctx* c, const uint64_t* keys, const uint64_t* vals,
     return buf[last];
 }
 
+// The two global passes of the two-level sort, alone, over (key field << 32 | value) words: the
+// words come out partitioned into the TL_BUCKETS buckets of the field's top TL_H bits (bucket b =
+// words [bstart[b], bstart[b+1]), no order inside a bucket), lookback-free (tl_hist_tiles_kernel
+// counts + column scans).  The aggregate join (qe_agg.hip) needs exactly that: inside a bucket a
+// key is its field's L = nb - TL_H low bits, a dense domain it counts in LDS -- no per-bucket
+// sort.  Values: a u64 column's low words (v64), u32 (v32), or neither (the row index).
+void partition_words_kv(qe_ctx* c, const uint64_t* keys, const uint64_t* v64, const uint32_t* v32, uint64_t n, int lo,
+                        int nb, uint64_t** words, uint32_t** bstart_out) {
+    if (n == 0 || n >= 0xFFFFFFFFull || nb <= TL_H || nb > TL_H + 16) throw Error(QE_ENOTSUP, "partition geometry");
+    const uint64_t fmask = nb >= 32 ? 0xFFFFFFFFull : (1ull << nb) - 1;
+    const Field f{lo, fmask, 0};
+    const int L = nb - TL_H;
+    const uint32_t nt = (uint32_t)((n + RTILE - 1) / RTILE);
+    const uint32_t G = (nt + TL_TPG - 1) / TL_TPG;
+    const uint32_t Q = G >= 256 ? 1u : 256u / G;
+    const uint32_t nseg = 256u * G;
+    uint32_t* tcnt = dalloc_t<uint32_t>(c, (size_t)nt * 256);
+    uint32_t* gcnt = dalloc_t<uint32_t>(c, (size_t)nseg * 128);
+    uint32_t* hist = dalloc_t<uint32_t>(c, TL_BUCKETS);
+    uint32_t* bstart = dalloc_t<uint32_t>(c, TL_BUCKETS + 1);
+    uint32_t* seg = dalloc_t<uint32_t>(c, (size_t)nseg + 1);
+    QE_HIP(hipMemsetAsync(gcnt, 0, (size_t)nseg * 128 * sizeof(uint32_t), c->stream));
+    {
+        Timed t(c, "sort_hist", 8.0 * n);
+        hipLaunchKernelGGL((tl_hist_tiles_kernel<uint64_t>), dim3(G * Q), dim3(1024), 0, c->stream, keys, n, f, L, nt, G, Q,
+                           tcnt, gcnt);
+        QE_HIP(hipGetLastError());
+        hipLaunchKernelGGL(tl_gsum_kernel, dim3(256), dim3(128), 0, c->stream, gcnt, G, hist);
+        QE_HIP(hipGetLastError());
+        hipLaunchKernelGGL(tl_bstart_kernel, dim3(1), dim3(1024), 0, c->stream, hist, bstart, c->d_scratch + 34);
+        QE_HIP(hipGetLastError());
+    }
+    {
+        Timed t(c, "sort_scan", 8.0 * ((double)nt * 256 + (double)nseg * 128));
+        column_scans(c, tcnt, nt, gcnt, nseg, seg, G, (uint32_t)n);
+    }
+    uint64_t* w1 = dalloc_t<uint64_t>(c, n);
+    uint64_t* w2 = dalloc_t<uint64_t>(c, n);
+    {
+        Timed t(c, "sort_pass_agg", (8.0 + (v64 ? 8.0 : v32 ? 4.0 : 0.0) + 8.0) * n);
+#define QE_PW1(IN, V)                                                                                                   \
+    hipLaunchKernelGGL((radix_pass_kernel<uint64_t, IN, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, false, true>), \
+                       dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, V, nullptr, w1, nullptr, n,       \
+                       32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr)
+        if (v64) QE_PW1(IN_KV64, reinterpret_cast<const uint32_t*>(v64));
+        else if (v32) QE_PW1(IN_KV, v32);
+        else QE_PW1(IN_KIOTA, nullptr);
+#undef QE_PW1
+        QE_HIP(hipGetLastError());
+    }
+    {
+        Timed t(c, "sort_pass_agg", 16.0 * n);
+        hipLaunchKernelGGL((tl_pass2_kernel<uint64_t, false, true>), dim3(xcd_grid(nseg)), dim3(TL2_NT), 0, c->stream, w1,
+                           w2, n, 32 + L + 8, seg, gcnt, G, nullptr, nullptr);
+        QE_HIP(hipGetLastError());
+    }
+    dfree(c, w1);
+    dfree(c, tcnt);
+    dfree(c, gcnt);
+    dfree(c, hist);
+    dfree(c, seg);
+    *words = w2;
+    *bstart_out = bstart;
+}
+
 void pairs_need_keys(qe_ctx* c, const qe_pairs* p) {
     if (!p || !p->key) return;
     auto it = c->deferred.find(p->key);

@@ -43,11 +43,25 @@ def _heavy(rng, n, domain, heavy_frac, nheavy=3):
 
 
 @pytest.mark.parametrize("shape", ["uniform", "heavy_both", "heavy_one", "const_bits", "no_val_s", "disjoint",
-                                   "tiny", "one_key"])
+                                   "tiny", "one_key", "small_uniform", "wide_domain", "zipf"])
 def test_join_aggregate_matches_numpy(ctx, shape):
+    """from 2^22 rows in total with 16..30 varying key bits the bucketed form runs (two partition
+    passes per side, LDS counting, giant buckets on many workgroups), below it the sort + merge-path
+    form (small_uniform, tiny, one_key)"""
     rng = np.random.default_rng(len(shape))
     nR, nS, dom = 3_000_017, 2_000_003, 1 << 22
-    if shape == "uniform":
+    if shape == "small_uniform":
+        nR, nS = 1_000_003, 900_001
+        kR = rng.integers(0, dom, nR, dtype=np.uint64)
+        kS = rng.integers(0, dom, nS, dtype=np.uint64)
+    elif shape == "wide_domain":         # 30 varying bits: 2^15 values per bucket, mostly empty
+        kR = rng.integers(0, 1 << 30, nR, dtype=np.uint64)
+        kS = rng.integers(0, 1 << 30, nS, dtype=np.uint64)
+        kS[::3] = kR[: len(kS[::3])]     # a third of S joins
+    elif shape == "zipf":                # a C5-like head: many giant buckets, light keys in between
+        kR = (rng.zipf(1.4, nR).astype(np.uint64) * np.uint64(2654435761)) % np.uint64(1 << 28)
+        kS = (rng.zipf(1.4, nS).astype(np.uint64) * np.uint64(2654435761)) % np.uint64(1 << 28)
+    elif shape == "uniform":
         kR = rng.integers(0, dom, nR, dtype=np.uint64)
         kS = rng.integers(0, dom, nS, dtype=np.uint64)
     elif shape == "heavy_both":          # runs of ~10^5 rows: every heavy key crosses many tiles
