@@ -54,7 +54,8 @@ STAGES = [
     (r"nonzero_bitmap_kernel", "payload_bitmap"),
     (r"FilterScanOp|FilterScan2Op|wscan_kernel|uscan_kernel", "filter_scan"),
     (r"zip_take_kernel", "take_u32"),
-    (r"ag_tile_kernel|ag_reduce_kernel", "agg_count"),
+    (r"ag_tile_kernel|ag_reduce_kernel|ab_bucket_kernel|ab_sum3_kernel", "agg_count"),
+    (r"ab_big_count_kernel|ab_big_look_kernel", "agg_big"),
     (r"ag_split_kernel", "agg_split"),
     (r"FilterRefineOp", "filter_refine"),
     (r"ScanJoinOp", "scan_join"),
@@ -64,8 +65,12 @@ STAGES = [
 ]
 
 
-def stage_of(kname: str):
-    for pat, st in STAGES:
+# C5 (the aggregate join): every radix pass is one of its word sorts / partition passes
+STAGES_C5 = [(r"radix_pass_kernel|tl_pass2_kernel", "sort_pass_agg")]
+
+
+def stage_of(kname: str, workload: str = "c3"):
+    for pat, st in (STAGES_C5 if workload == "c5" else []) + STAGES:
         if re.search(pat, kname):
             return st
     return None
@@ -90,10 +95,10 @@ def read_counter(d: str, counter: str):
     return out
 
 
-def per_stage(disp):
+def per_stage(disp, workload="c3"):
     acc = defaultdict(lambda: [0.0, 0, set()])
     for name, v in disp.values():
-        st = stage_of(name)
+        st = stage_of(name, workload)
         if st is None:
             continue
         a = acc[st]
@@ -111,8 +116,8 @@ def main():
     ap.add_argument("--command", default="")
     ap.add_argument("--workload", default="c3")
     a = ap.parse_args()
-    f = per_stage(read_counter(a.fetch, "FETCH_SIZE"))
-    w = per_stage(read_counter(a.write, "WRITE_SIZE"))
+    f = per_stage(read_counter(a.fetch, "FETCH_SIZE"), a.workload)
+    w = per_stage(read_counter(a.write, "WRITE_SIZE"), a.workload)
     kern = {}
     for st in sorted(set(f) | set(w)):
         fk, fn, names = f.get(st, [0.0, 0, set()])

@@ -20,14 +20,15 @@ def main():
     ap.add_argument("stats_csv")
     ap.add_argument("--out")
     ap.add_argument("--command", default="")
+    ap.add_argument("--workload", default="c3")
     a = ap.parse_args()
     acc = defaultdict(lambda: [0, 0.0])
     with open(a.stats_csv) as f:
         for row in csv.DictReader(f):
-            st = stage_of(row["Name"]) or row["Name"].split("(")[0][:60]
+            st = stage_of(row["Name"], a.workload) or row["Name"].split("(")[0][:60]
             acc[st][0] += int(row["Calls"])
             acc[st][1] += float(row["TotalDurationNs"])
-    doc = {"command": a.command, "source": a.stats_csv,
+    doc = {"command": a.command, "source": a.stats_csv, "workload": a.workload,
            "stages": {k: {"calls": c, "total_ms": round(t / 1e6, 3), "avg_ms": round(t / 1e6 / c, 4)}
                       for k, (c, t) in sorted(acc.items(), key=lambda kv: -kv[1][1])}}
     for k, v in doc["stages"].items():
