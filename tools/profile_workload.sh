@@ -13,3 +13,12 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/${TAG}_fetch -o run -- python3 $R/bench.py $A > $O/${TAG}_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/${TAG}_write -o run -- python3 $R/bench.py $A > $O/${TAG}_write.log 2>&1
 echo profile-done
+# summaries on the box (a batch workload's raw traces can exceed what gpurun brings back)
+cd $R
+python3 tools/stage_stats.py $(find $O/${TAG}_trace -name "*kernel_stats.csv" | head -1) --workload $W \
+    --out $O/${TAG}_stage_stats.json --command "rocprofv3 --kernel-trace --stats -- python3 bench.py $A" > /dev/null
+cp $(find $O/${TAG}_trace -name "*kernel_stats.csv" | head -1) $O/${TAG}_kernel_stats.csv
+python3 tools/pmc_traffic.py --fetch $O/${TAG}_fetch --write $O/${TAG}_write --out $O/${TAG}_traffic.json --workload $W \
+    --command "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE -- python3 bench.py $A" > /dev/null
+rm -rf $O/${TAG}_trace $O/${TAG}_fetch $O/${TAG}_write
+echo summaries-done
