@@ -82,10 +82,13 @@ typedef struct qe_engine {
     int (*scan2)(void* u, uint32_t rel, uint32_t col1, char op1, uint64_t v1, uint32_t col2, char op2, uint64_t v2,
                  uint64_t start, uint64_t end, int values, qe_h* out);
     /* join, with side b's carried rowid columns cb[0..nb) delivered beside the pairs (nullable):
-     * outb[k][i] = cb[k][ib] for pair i's b row.  The engine may carry them through its sort
-     * and join instead of taking them through the pairs afterwards.  Inputs are borrowed. */
-    int (*join_carry)(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h* cb, qe_h* oa, qe_h* ob,
-                      qe_h* outb);
+     * outb[k][i] = cb[k][ib] for pair i's b row.  xa (0: none): a column handle of `column` below,
+     * side a being that column's base relation (ka its key column or bucket, va its rowids or 0):
+     * *outxa[i] = the column's value at pair i's a row -- its next join's key, which then needs no
+     * gather through the rowids.  The engine may carry them through its sorts and join instead of
+     * taking them through the pairs afterwards.  Inputs are borrowed. */
+    int (*join_carry)(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h* cb, qe_h xa, qe_h* oa, qe_h* ob,
+                      qe_h* outb, qe_h* outxa);
     /* the last join of a query when only the checksums read its lists and side a carries no
      * binding (nullable): *pairs = the local pair count, sums[s] = the local sum mod 2^64 of
      * col_s (relation rels[s], column cols[s]) over the pairs' b rows, through b's vals (src[s]
@@ -115,6 +118,12 @@ typedef struct qe_engine {
      * usual).  No materialisation limit applies: nothing is materialised. */
     int (*join_agg)(void* u, uint32_t rel_a, uint32_t col_a, uint32_t rel_b, uint32_t col_b, int nsel, const int* side,
                     const uint32_t* cols, uint64_t* pairs, uint64_t* sums);
+    /* a base column as join_carry's xa (nullable): QE_ENOTSUP when its values do not all fit 32
+     * bits.  Released like any handle (the column itself stays). */
+    int (*column)(void* u, uint32_t rel, uint32_t col, qe_h* out);
+    /* keys from a list of the key column's values (nullable; join_carry's outxa): the keys `keys`
+     * would gather through the rowids, without the gather (`vals` borrowed) */
+    int (*keys_of)(void* u, uint32_t rel, uint32_t col, qe_h vals, qe_h* out);
 } qe_engine;
 
 /* Replay the reference's variant choice and list bookkeeping for every query of `text` on the

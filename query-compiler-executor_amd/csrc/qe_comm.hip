@@ -102,6 +102,13 @@ __global__ void __launch_bounds__(256) gather_u32_kernel(const uint64_t* __restr
     }
 }
 
+// keys = a list of carried key values, widened (the plain form of widen_with_hist)
+__global__ void __launch_bounds__(256) widen_u32_kernel(const uint32_t* __restrict__ v, uint64_t n,
+                                                        uint64_t* __restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) out[i] = v[i];
+}
+
 // sum of a list's own u32 values mod 2^64 (a binding that carries its select's values)
 __global__ void __launch_bounds__(256) sum_u32_kernel(const uint32_t* __restrict__ v, uint64_t n,
                                                       unsigned long long* __restrict__ out) {
@@ -144,6 +151,7 @@ struct DArr : Obj {
     // a fused scan's survivors' values of (vrel, vcol) as u32, kept for a later `values` request
     uint32_t* vcache = nullptr;
     uint32_t vrel = 0, vcol = 0;
+    bool colview = false;   // a base column (e_column): d is the column, n its rows
     ~DArr() override {
         if (vcache) dfree(c, vcache);
         if (owned && d) {
@@ -314,6 +322,46 @@ int e_keys(void* u, uint32_t rel, uint32_t col, qe_h rows, qe_h* out) {
         k->kor = p.kor;
         k->kand = p.kand;
         *out = H(k);
+    });
+}
+
+// a base column as a payload: its values ride with the relation's rows through the join
+// (join_carry's xa) when all of them fit 32 bits
+int e_column(void* u, uint32_t rel, uint32_t col, qe_h* out) {
+    Eng* e = E(u);
+    qe_ctx* c = e->c;
+    uint64_t kor = 0, kand = 0;
+    if (qe_relation_column_bits(c, (int)rel, (int)col, &kor, &kand) != 0 || (kor >> 32)) return QE_ENOTSUP;
+    return guard(e, [&] {
+        const qe_col q = column(c, rel, col);
+        DArr* a = new_arr(c, const_cast<uint64_t*>(q.d), q.n, true, false);
+        a->colview = true;
+        *out = H(a);
+    });
+}
+
+// keys from the carried values of the key column: widened, with the sort's histogram when the
+// sort will take it -- what e_keys computes, without the random gather through the rowids
+int e_keys_of(void* u, uint32_t rel, uint32_t col, qe_h vals, qe_h* out) {
+    Eng* e = E(u);
+    return guard(e, [&] {
+        qe_ctx* c = e->c;
+        uint64_t kor = 0, kand = 0;
+        ck(qe_relation_column_bits(c, (int)rel, (int)col, &kor, &kand), c);
+        const DArr* v = A(vals);
+        const uint64_t n = v->n;
+        uint64_t* k = dalloc_t<uint64_t>(c, std::max<uint64_t>(n, 1));
+        const uint32_t* vd = static_cast<const uint32_t*>(v->d);
+        if (n && !widen_with_hist(c, vd, n, kor, kand, k)) {
+            Timed t(c, "widen_keys", 12.0 * n);
+            hipLaunchKernelGGL(widen_u32_kernel, dim3(grid_for(n, 256 * 8, 8192)), dim3(256), 0, c->stream, vd, n, k);
+            QE_HIP(hipGetLastError());
+        }
+        DArr* a = new_arr(c, k, n, true);
+        a->bits = true;
+        a->kor = kor;
+        a->kand = kand;
+        *out = H(a);
     });
 }
 
@@ -520,25 +568,49 @@ int e_join(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, qe_h* oa, qe_h* ob) {
 }
 
 // the join with b's carried columns: up to two ride through b's sort and the bucket join (S =
-// b); otherwise (or on a bucket beyond LDS) the join runs on b's positions and every column,
-// b's vals included, is taken through them
-int e_join_carry(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h* cb, qe_h* oa, qe_h* ob, qe_h* outb) {
+// b), and a's payload column (xa: a's next join key) through a's sort (R = a); otherwise (or on a
+// bucket beyond LDS) the join runs on b's positions and every column, b's vals included, is taken
+// through them, a's payload gathered through a's rowids
+int e_join_carry(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h* cb, qe_h xa, qe_h* oa, qe_h* ob,
+                 qe_h* outb, qe_h* outxa) {
     Eng* e = E(u);
     return guard(e, [&] {
         qe_ctx* c = e->c;
+        const DArr* X = xa ? A(xa) : nullptr;
+        if (X && !X->colview) throw Error(QE_EINVAL, "join_carry: xa is not a column");
         qe_pairs P = side_pairs(A(ka), va ? A(va) : nullptr);
         qe_pairs Q = side_pairs(A(kb), vb ? A(vb) : nullptr);
-        qe_list la{}, lb{}, lx0{}, lx1{};
-        if (nb >= 1 && nb <= 2 &&
-            join_pairs_carry(c, &P, &Q, static_cast<const uint32_t*>(A(cb[0])->d),
-                             nb == 2 ? static_cast<const uint32_t*>(A(cb[1])->d) : nullptr, &la, &lb, &lx0, &lx1)) {
-            qe_pairs_free(c, &P);
-            qe_pairs_free(c, &Q);
-            *oa = H(new_arr(c, la.d, la.n, false));
-            *ob = H(new_arr(c, lb.d, lb.n, false));
-            outb[0] = H(new_arr(c, lx0.d, lx0.n, false));
-            if (nb == 2) outb[1] = H(new_arr(c, lx1.d, lx1.n, false));
-            return;
+        qe_list la{}, lb{}, lx0{}, lx1{}, lxa{};
+        auto gather_col = [&](const uint32_t* rows, uint64_t n) {   // X's values at rowids
+            uint32_t* d = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
+            if (n) {
+                Timed t(c, "gather_values", 12.0 * n);
+                hipLaunchKernelGGL(gather_u32_kernel, dim3(grid_for(n, 256 * 16, 8192)), dim3(256), 0, c->stream,
+                                   static_cast<const uint64_t*>(X->d), rows, n, d);
+                QE_HIP(hipGetLastError());
+            }
+            return d;
+        };
+        if (nb >= 0 && nb <= 2 && (nb >= 1 || X)) {
+            // a's payload in a's input order: the column itself (a = the whole column, row i), or
+            // its values at a's rowids (a rank's bucket: ascending rows, a near-sequential read)
+            const uint64_t* rc64 = X && !va ? static_cast<const uint64_t*>(X->d) : nullptr;
+            uint32_t* rx32 = X && va ? gather_col(static_cast<const uint32_t*>(A(va)->d), A(va)->n) : nullptr;
+            const bool done =
+                join_pairs_carry(c, &P, &Q, nb >= 1 ? static_cast<const uint32_t*>(A(cb[0])->d) : nullptr,
+                                 nb == 2 ? static_cast<const uint32_t*>(A(cb[1])->d) : nullptr, &la, &lb, &lx0, &lx1,
+                                 rx32, rc64, X ? &lxa : nullptr);
+            dfree(c, rx32);
+            if (done) {
+                qe_pairs_free(c, &P);
+                qe_pairs_free(c, &Q);
+                *oa = H(new_arr(c, la.d, la.n, false));
+                *ob = H(new_arr(c, lb.d, lb.n, false));
+                if (nb >= 1) outb[0] = H(new_arr(c, lx0.d, lx0.n, false));
+                if (nb == 2) outb[1] = H(new_arr(c, lx1.d, lx1.n, false));
+                if (X) *outxa = H(new_arr(c, lxa.d, lxa.n, false));
+                return;
+            }
         }
         qe_pairs Qp = side_pairs(A(kb), nullptr);   // b's positions
         const int rc = qe_join_pairs(c, &P, &Qp, &la, &lb);
@@ -546,6 +618,7 @@ int e_join_carry(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h
         qe_pairs_free(c, &Qp);
         ck(rc, c);
         *oa = H(new_arr(c, la.d, la.n, false));
+        if (X) *outxa = H(new_arr(c, gather_col(la.d, la.n), la.n, false));   // la: a's rowids
         auto take = [&](const DArr* src) {
             qe_list o{};
             ck(qe_take_u32(c, static_cast<const uint32_t*>(src->d), &lb, &o), c);
@@ -597,7 +670,8 @@ int e_join_sums(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h*
         if (rc != 0 || done) return rc;
     }
     qe_h oa = 0, ob = 0, outb[2] = {0, 0};
-    int rc = nb >= 1 ? e_join_carry(u, ka, va, kb, vb, nb, cb, &oa, &ob, outb) : e_join(u, ka, va, kb, vb, &oa, &ob);
+    int rc = nb >= 1 ? e_join_carry(u, ka, va, kb, vb, nb, cb, 0, &oa, &ob, outb, nullptr)
+                     : e_join(u, ka, va, kb, vb, &oa, &ob);
     if (rc == 0) {
         *pairs = A(oa)->n;
         std::vector<qe_h> rows(nsel);
@@ -884,6 +958,11 @@ qe_engine make_engine(Eng* e) {
     g.mat_limit = &e->c->mat_limit;
     // the last join of two base relations in aggregate form (QE_PLAN_JOIN_AGG=0: as other joins -- A/B)
     g.join_agg = getenv("QE_PLAN_JOIN_AGG") && getenv("QE_PLAN_JOIN_AGG")[0] == '0' ? nullptr : e_join_agg;
+    // a base relation's next join key rides with its rows (QE_PLAN_KEY_CARRY=0: gathered -- A/B)
+    if (!(getenv("QE_PLAN_KEY_CARRY") && getenv("QE_PLAN_KEY_CARRY")[0] == '0')) {
+        g.column = e_column;
+        g.keys_of = e_keys_of;
+    }
     return g;
 }
 

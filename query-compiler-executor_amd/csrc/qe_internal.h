@@ -66,6 +66,7 @@ struct DeferredSort {
     uint32_t* bstart = nullptr;   // bucket starts (+ end)
     uint64_t* d_max = nullptr;    // largest bucket (device word: > TL_CAP = skew, not yet checked)
     uint64_t* x = nullptr;        // carried payloads, in the words' order (qe_join_carry), or null
+    uint32_t* x32 = nullptr;      // a 32-bit payload in the words' order (R's next join key), or null
     uint64_t* kout = nullptr;
     uint32_t* vout = nullptr;
     int lo = 0, L = 0;            // field = (key >> lo) & fmask; bucket = field >> L
@@ -138,6 +139,9 @@ struct qe_ctx {
     // a payload for the next deferred lookback-free two-level sort to carry (join_pairs_carry)
     const uint32_t* carry_xa = nullptr;
     const uint32_t* carry_xb = nullptr;
+    // ... or one 32-bit payload: a u32 array, or a u64 column's low words (row i = input element i)
+    const uint32_t* carry_x32 = nullptr;
+    const uint64_t* carry_c64 = nullptr;
     std::vector<qe::PendingEvent> pending;
     std::vector<hipEvent_t> event_pool;
     std::vector<qe::KStat> kstats;
@@ -224,15 +228,22 @@ void pairs_drop_deferred(qe_ctx* c, const qe_pairs* p);   // (also drops a gathe
 bool gather_with_hist(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint64_t n, uint64_t kor, uint64_t kand,
                       uint64_t* keys);
 bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS,
-                 qe_list* outX0 = nullptr, qe_list* outX1 = nullptr);
+                 qe_list* outX0 = nullptr, qe_list* outX1 = nullptr, qe_list* outRX = nullptr);
 // the payload carry of join_pairs_carry applies: both sides' sorts will be deferred two-level
 // ones with one bucket geometry, S's in the lookback-free form
-bool carry_eligible(const qe_pairs* R, const qe_pairs* S);
+// (rpay: R carries a payload too -- its sort must be the lookback-free form as well)
+bool carry_eligible(const qe_pairs* R, const qe_pairs* S, bool rpay = false);
 // qe_join_pairs with S carrying one or two u32 payload columns (xa, xb nullable) through its sort
-// and the bucket join: outX0 / outX1 aligned with the pairs.  False: nothing was produced and the
-// inputs are as they were (ineligible, or a bucket beyond LDS) -- the caller joins without it.
+// and the bucket join: outX0 / outX1 aligned with the pairs; and/or R carrying one 32-bit payload,
+// a u32 array (rx32) or a u64 column's low words (rc64), both in R's input order: outRX.  False:
+// nothing was produced and the inputs are as they were (ineligible, or a bucket beyond LDS) --
+// the caller joins without it.
 bool join_pairs_carry(qe_ctx* c, qe_pairs* R, qe_pairs* S, const uint32_t* xa, const uint32_t* xb, qe_list* outR,
-                      qe_list* outS, qe_list* outX0, qe_list* outX1);
+                      qe_list* outS, qe_list* outX0, qe_list* outX1, const uint32_t* rx32 = nullptr,
+                      const uint64_t* rc64 = nullptr, qe_list* outRX = nullptr);
+// keys = (u64) vals for a list whose sort will be the lookback-free two-level one, with that
+// sort's histogram (gather_with_hist without the gather); false: not that sort
+bool widen_with_hist(qe_ctx* c, const uint32_t* vals, uint64_t n, uint64_t kor, uint64_t kand, uint64_t* keys);
 // the join's checksums without its pairs (the plan's last join): sums[k] = sum over pairs of
 // col_k[S-side rowid], the rowid being S's val (src 0) or the low / high half of its carried
 // payload (src 1 / 2); *pairs = the pair count.  False: not applicable (geometry, a bucket

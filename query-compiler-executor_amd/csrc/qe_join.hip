@@ -1611,16 +1611,23 @@ int qe_join_pairs(qe_ctx* c, qe_pairs* R, qe_pairs* S, qe_list* outR, qe_list* o
 
 namespace qe {
 bool join_pairs_carry(qe_ctx* c, qe_pairs* R, qe_pairs* S, const uint32_t* xa, const uint32_t* xb, qe_list* outR,
-                      qe_list* outS, qe_list* outX0, qe_list* outX1) {
-    if (!xa || !carry_eligible(R, S)) return false;
+                      qe_list* outS, qe_list* outX0, qe_list* outX1, const uint32_t* rx32, const uint64_t* rc64,
+                      qe_list* outRX) {
+    const bool rpay = rx32 || rc64;
+    if ((!xa && !rpay) || !carry_eligible(R, S, rpay)) return false;
     const qe_pairs R0 = *R, S0 = *S;   // views of the caller's arrays (nothing owned)
     if ((R0.owns | S0.owns) & 7) return false;
+    c->carry_x32 = rx32;
+    c->carry_c64 = rc64;
     sort_pairs(c, R, true);
+    c->carry_x32 = nullptr;   // (consumed by R's sort; cleared in any case)
+    c->carry_c64 = nullptr;
     c->carry_xa = xa;
     c->carry_xb = xb;
     sort_pairs(c, S, true);
     c->carry_xa = c->carry_xb = nullptr;   // (consumed by S's sort; cleared in any case)
-    if (bucket_join(c, R, S, outR, outS, outX0, xb ? outX1 : nullptr)) return true;
+    if (bucket_join(c, R, S, outR, outS, xa ? outX0 : nullptr, xa && xb ? outX1 : nullptr, rpay ? outRX : nullptr))
+        return true;
     // a bucket beyond LDS: drop both deferred sorts, give the caller its inputs back
     qe_pairs_free(c, R);
     qe_pairs_free(c, S);

@@ -177,15 +177,18 @@ static inline uint32_t xcd_grid(uint64_t items) {
 // PRE = true: the tile's global digit offsets were computed before the launch (the two-level
 // sort's first pass, whose per-tile counts come out of the histogram read it does anyway,
 // tl_hist_tiles_kernel) -- `offs` is a table of BINS offsets per tile; no ticket, no lookback.
-// CARRY (PRE, OUT_WORD only): a 64-bit payload per element rides along -- xa[i] | xb[i] << 32 in
-// input order (xb nullable), written to xout at the element's output position.  The words are
-// written first; the same LDS stage then takes the payloads in the words' slots, so they leave
-// in the same runs (the partitioned plan's carried bindings, qe_join_carry).
+// CARRY (PRE, OUT_WORD only): a payload per element rides along, written to xout at the element's
+// output position -- X64: 64 bits, xa[i] | xb[i] << 32 in input order (xb nullable; the partitioned
+// plan's carried bindings, qe_join_carry); X32: 32 bits, xa[i] (u32 input); XCOL: 32 bits, the low
+// word of the u64 column xa points to (a base relation's next join key riding with its rows).  The
+// words are written first; the same LDS stage then takes the payloads in the words' slots, so
+// they leave in the same runs.
 // UNSTABLE: ranks from per-wave LDS counters (one ds_add_rtn per element) instead of the 8-ballot
 // match-any -- equal digits keep no order.  For the partitioned plan's deferred sorts (their
 // consumer, bucket_join, needs the buckets, not an order inside them) and the first LSD pass of
 // the aggregate join's sorts (no earlier order to keep, none needed among equal keys).
-template <typename K, int IN, int OUT, bool PACK, int RBITS, int ITEMS, int NT, bool PRE = false, bool CARRY = false,
+enum { X_NONE = 0, X64 = 1, X32 = 2, XCOL = 3 };
+template <typename K, int IN, int OUT, bool PACK, int RBITS, int ITEMS, int NT, bool PRE = false, int CARRY = X_NONE,
           bool UNSTABLE = false>
 __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ kin, const uint64_t* __restrict__ win,
                                                         const uint32_t* __restrict__ vin, K* __restrict__ kout,
@@ -196,7 +199,7 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
                                                         const uint32_t* __restrict__ xa = nullptr,
                                                         const uint32_t* __restrict__ xb = nullptr,
                                                         uint64_t* __restrict__ xout = nullptr) {
-    static_assert(!CARRY || (PRE && OUT == OUT_WORD), "payload carry: the lookback-free first pass only");
+    static_assert(CARRY == X_NONE || (PRE && OUT == OUT_WORD), "payload carry: the lookback-free first pass only");
     constexpr int BINS = 1 << RBITS, DPT = BINS >= NT ? BINS / NT : 1;   // digits per thread
     constexpr int NW = NT / 64;
     constexpr int TILE = NT * ITEMS, WT = 64 * ITEMS;
@@ -314,14 +317,16 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
             uint32_t dd = (uint32_t)(word[j] >> dsh) & mask;
             const uint32_t slot = bexcl[dd] + whist[w][dd] + pos[j];
             stage[slot] = word[j];
-            if constexpr (CARRY) pos[j] = slot;   // the payload takes the same slot later
+            if constexpr (CARRY != X_NONE) pos[j] = slot;   // the payload takes the same slot later
         }
     }
-    if constexpr (CARRY) {   // the payloads load into the words' registers, in flight during the write-out
+    if constexpr (CARRY != X_NONE) {   // the payloads load into the words' registers, in flight during the write-out
 #pragma unroll
         for (int j = 0; j < ITEMS; j++) {
             const uint64_t i = wave_base + (uint64_t)j * 64 + l;
-            word[j] = i < n ? ((uint64_t)xa[i] | (xb ? (uint64_t)xb[i] << 32 : 0ull)) : 0ull;
+            if constexpr (CARRY == X64) word[j] = i < n ? ((uint64_t)xa[i] | (xb ? (uint64_t)xb[i] << 32 : 0ull)) : 0ull;
+            else if constexpr (CARRY == X32) word[j] = i < n ? xa[i] : 0u;
+            else word[j] = i < n ? (uint32_t)reinterpret_cast<const uint64_t*>(xa)[i] : 0u;
         }
     }
 #pragma unroll
@@ -347,11 +352,11 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
     QE_STAMP(g_sort_stamps, tile, 5);
     const uint64_t tbase = (uint64_t)tile * TILE;
     const uint32_t tn = (uint32_t)((n - tbase) < (uint64_t)TILE ? (n - tbase) : (uint64_t)TILE);
-    uint32_t pk[CARRY ? ITEMS : 1];
+    uint32_t pk[CARRY != X_NONE ? ITEMS : 1];
 #pragma unroll
     for (int k = 0; k < ITEMS; k++) {
         uint32_t i = (uint32_t)k * NT + threadIdx.x;
-        if (CARRY) pk[k] = 0xFFFFFFFFu;
+        if (CARRY != X_NONE) pk[k] = 0xFFFFFFFFu;
         if (i < tn) {
             uint64_t wd = stage[i];
 #ifdef QE_DIAG_SORT_LINEAR   // ablation only: contiguous output instead of the digit scatter
@@ -360,7 +365,7 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
             uint32_t p = gofs[(uint32_t)(wd >> dsh) & mask] + i;
 #endif
             if ((uint64_t)p >= n) continue;   // never taken with consistent offsets; keeps stores in bounds
-            if constexpr (CARRY) pk[k] = p;
+            if constexpr (CARRY != X_NONE) pk[k] = p;
             if (OUT == OUT_WORD) {
                 QE_ST(&wout[p], wd);
             } else if (PACK) {
@@ -371,7 +376,7 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
             }
         }
     }
-    if constexpr (CARRY) {
+    if constexpr (CARRY != X_NONE) {
         __syncthreads();   // every word is out of the stage
 #pragma unroll
         for (int j = 0; j < ITEMS; j++)
@@ -380,7 +385,10 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
 #pragma unroll
         for (int k = 0; k < ITEMS; k++) {
             const uint32_t i = (uint32_t)k * NT + threadIdx.x;
-            if (i < tn && pk[k] != 0xFFFFFFFFu) QE_ST(&xout[pk[k]], stage[i]);
+            if (i < tn && pk[k] != 0xFFFFFFFFu) {
+                if constexpr (CARRY == X64) QE_ST(&xout[pk[k]], stage[i]);
+                else QE_ST(&reinterpret_cast<uint32_t*>(xout)[pk[k]], (uint32_t)stage[i]);
+            }
         }
     }
     QE_STAMP(g_sort_stamps, tile, 6);
@@ -746,7 +754,9 @@ __global__ void __launch_bounds__(1024) tl_hist_tiles_kernel(const K* __restrict
 }
 
 // tl_hist_tiles_kernel fused into the gather that produces the keys: keys = col[rows] in list
-// order, and the same per-tile / per-segment counts (one pass instead of a gather + a re-read)
+// order, and the same per-tile / per-segment counts (one pass instead of a gather + a re-read).
+// DIRECT: keys = rows[i] widened -- a list of carried key values (no gather)
+template <bool DIRECT = false>
 __global__ void __launch_bounds__(1024) tl_gather_hist_kernel(const uint64_t* __restrict__ col,
                                                               const uint32_t* __restrict__ rows, uint64_t n,
                                                               uint64_t* __restrict__ keys, Field f, int L, uint32_t nt,
@@ -781,7 +791,7 @@ __global__ void __launch_bounds__(1024) tl_gather_hist_kernel(const uint64_t* __
 #pragma unroll
         for (int j = 0; j < 8; j++) {   // 8 random gathers in flight per thread
             const uint64_t i = base + (uint64_t)j * 1024 + threadIdx.x;
-            k[j] = i < n ? col[r[j]] : 0;
+            k[j] = i < n ? (DIRECT ? (uint64_t)r[j] : col[r[j]]) : 0;
         }
         if (t + Q < t_end) load_rows(t + Q);
         if (t != g * TL_TPG + q && threadIdx.x < 256) {
@@ -931,9 +941,9 @@ __global__ void __launch_bounds__(256) cs_apply_kernel(CSJobs js) {
 #endif
 constexpr int TL2_NT = QE_TL2_NT, TL2_ITEMS = QE_TL2_ITEMS, TL2_TILE = TL2_NT * TL2_ITEMS;   // 9216: mean 8192 + 11 sd
 
-// CARRY: the 64-bit payloads of pass 1 (xin, in pass-1 order) follow the words to xout, staged
-// in the words' LDS slots after the words have left (as in radix_pass_kernel).
-template <typename K, bool CARRY = false, bool UNSTABLE = false>
+// CARRY: the payloads of pass 1 (xin, in pass-1 order; X64: 64-bit, X32: 32-bit) follow the words
+// to xout, staged in the words' LDS slots after the words have left (as in radix_pass_kernel).
+template <typename K, int CARRY = X_NONE, bool UNSTABLE = false>
 __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const uint64_t* __restrict__ win, uint64_t* __restrict__ wout,
                                                          uint64_t n, int dsh, const uint32_t* __restrict__ seg,
                                                          const uint32_t* __restrict__ off2, uint32_t G,
@@ -1024,18 +1034,22 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
                 const uint32_t r = (pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
                 const uint32_t sl = bexcl[dd] + whist[w][dd] + r;
                 stage[sl] = word[j];
-                if constexpr (CARRY)   // pos2 becomes the slot (< TL2_TILE: still 16 bits)
+                if constexpr (CARRY != X_NONE)   // pos2 becomes the slot (< TL2_TILE: still 16 bits)
                     pos2[j >> 1] = (j & 1) ? ((pos2[j >> 1] & 0xFFFFu) | (sl << 16)) : ((pos2[j >> 1] & 0xFFFF0000u) | sl);
             }
         }
-        if constexpr (CARRY) {   // the payloads load into the words' registers, in flight during the write-out
+        if constexpr (CARRY != X_NONE) {   // the payloads load into the words' registers, in flight during the write-out
             const uint64_t* xsrc = xin + base;
             const uint32_t o0 = (uint32_t)w * WT + l;
 #pragma unroll
-            for (int j = 0; j < TL2_ITEMS; j++) word[j] = xsrc[std::min(o0 + (uint32_t)j * 64, m - 1)];
+            for (int j = 0; j < TL2_ITEMS; j++) {
+                const uint32_t o = std::min(o0 + (uint32_t)j * 64, m - 1);
+                if constexpr (CARRY == X64) word[j] = xsrc[o];
+                else word[j] = reinterpret_cast<const uint32_t*>(xin)[base + o];
+            }
         }
         __syncthreads();
-        if constexpr (CARRY) {
+        if constexpr (CARRY != X_NONE) {
             // the payloads: each slot's destination is read back from its word before the slot
             // is reused (one u32 per slot in the LDS word itself: high half = destination)
 #pragma unroll 6
@@ -1049,12 +1063,31 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
                 }
             }
             __syncthreads();
+            if constexpr (CARRY == X64) {
 #pragma unroll
-            for (int j = 0; j < TL2_ITEMS; j++) {   // payload j goes straight to its slot's destination
-                if (j * 64 < lim) {
-                    const uint32_t sl = (pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-                    const uint32_t dst = reinterpret_cast<const uint32_t*>(stage)[2 * sl];
-                    if ((uint64_t)dst < n) QE_ST(&xout[dst], word[j]);
+                for (int j = 0; j < TL2_ITEMS; j++) {   // payload j goes straight to its slot's destination
+                    if (j * 64 < lim) {
+                        const uint32_t sl = (pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                        const uint32_t dst = reinterpret_cast<const uint32_t*>(stage)[2 * sl];
+                        if ((uint64_t)dst < n) QE_ST(&xout[dst], word[j]);
+                    }
+                }
+            } else {
+                // a 32-bit payload joins its destination in the slot's other half, and the slots
+                // then leave in order: the payloads are written as runs, like the words
+                uint32_t* st32 = reinterpret_cast<uint32_t*>(stage);
+#pragma unroll
+                for (int j = 0; j < TL2_ITEMS; j++)
+                    if (j * 64 < lim) st32[2 * ((pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu) + 1] = (uint32_t)word[j];
+                __syncthreads();
+                uint32_t* xo = reinterpret_cast<uint32_t*>(xout);
+#pragma unroll 6
+                for (int k = 0; k < TL2_ITEMS; k++) {
+                    const uint32_t i = (uint32_t)k * TL2_NT + threadIdx.x;
+                    if (i < m) {
+                        const uint2 dv = reinterpret_cast<const uint2*>(stage)[i];
+                        if ((uint64_t)dv.x < n) QE_ST(&xo[dv.x], dv.y);
+                    }
                 }
             }
         } else {
@@ -1287,15 +1320,19 @@ __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
 // profiles/r02_hjoin_stamps.log).  An S row counts its partners by walking its value's chain (mean
 // length |R bucket| / 2^L, ~0.75 at C3) and the wave-cooperative emission walks it again to the
 // pair's partner.  Output is the same multiset of pairs (in no particular order, as before).
+// RX: R's rows carry a 32-bit payload too (xR, in R's word order -- a base relation's next join
+// key, sorted along with it): the partner's payload is read back from xR (the bucket's 20 KB, L2
+// after the first touch) and written to outRX -- LDS stays as without it.
 constexpr uint32_t HJ_NONE = 0xFFFFu;
 static_assert(TL_CAP < HJ_NONE, "chain links are 16-bit row indices");
 
-template <int DBITS, bool CARRY = false>
+template <int DBITS, bool CARRY = false, bool RX = false>
 __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
 tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict__ bsR, const uint64_t* __restrict__ wS,
                       const uint32_t* __restrict__ bsS, int L, uint32_t* __restrict__ outR, uint32_t* __restrict__ outS,
                       uint64_t cap, uint64_t* total_out, const uint64_t* __restrict__ xS = nullptr,
-                      uint32_t* __restrict__ outX0 = nullptr, uint32_t* __restrict__ outX1 = nullptr) {
+                      uint32_t* __restrict__ outX0 = nullptr, uint32_t* __restrict__ outX1 = nullptr,
+                      const uint32_t* __restrict__ xR = nullptr, uint32_t* __restrict__ outRX = nullptr) {
     __shared__ uint32_t head[1 << DBITS];   // per key value: the last R row inserted (HJ_NONE: none)
     __shared__ uint16_t nxt[TL_CAP];        // per R row: the previous row of its value
     __shared__ uint32_t rr[TL_CAP];         // per R row: its rowid
@@ -1397,6 +1434,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
                 for (uint32_t s = 0; s < k; s++) p = nxt[p];   // the k-th partner on the chain
                 outR[ob + q] = rr[p];
                 outS[ob + q] = sr;
+                if constexpr (RX) outRX[ob + q] = xR[r0 + p];
                 if constexpr (CARRY) {
                     outX0[ob + q] = x0;
                     if (outX1) outX1[ob + q] = x1;
@@ -1764,24 +1802,38 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     K* kout = dalloc_t<K>(c, n);
     uint32_t* vout = dalloc_t<uint32_t>(c, n);
     // a payload to carry (join_pairs_carry asked for it on this deferred sort)
+    // (X64: S's carried bindings; X32 / XCOL: one 32-bit payload, R's next join key)
     const uint32_t* cxa = dfr ? c->carry_xa : nullptr;
     const uint32_t* cxb = dfr ? c->carry_xb : nullptr;
-    c->carry_xa = c->carry_xb = nullptr;
-    uint64_t* x1 = cxa ? dalloc_t<uint64_t>(c, n) : nullptr;
-    uint64_t* x2 = cxa ? dalloc_t<uint64_t>(c, n) : nullptr;
+    const int xm = !dfr ? X_NONE : c->carry_xa ? X64 : c->carry_x32 ? X32 : c->carry_c64 ? XCOL : X_NONE;
+    if (xm == X32) cxa = c->carry_x32;
+    if (xm == XCOL) cxa = reinterpret_cast<const uint32_t*>(c->carry_c64);
+    c->carry_xa = c->carry_xb = c->carry_x32 = nullptr;
+    c->carry_c64 = nullptr;
+    const size_t xsz = xm == X64 ? 8 : 4;
+    uint64_t* x1 = xm ? static_cast<uint64_t*>(dalloc(c, n * xsz)) : nullptr;
+    uint64_t* x2 = xm ? static_cast<uint64_t*>(dalloc(c, n * xsz)) : nullptr;
     // a deferred sort's consumer needs its buckets, not an order inside them: unstable ranks
     const bool uns = dfr && sort_unstable_on();
 #define QE_P1(IN, CR, UN, XA, XB, XO)                                                                                   \
     hipLaunchKernelGGL((radix_pass_kernel<K, IN, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, CR, UN>),            \
                        dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, \
                        255u, f, tcnt, nullptr, nullptr, 0u, XA, XB, XO)
-    if (cxa) {
+    if (xm == X64) {
         const double xb = cxb ? 8.0 : 4.0;
         Timed t(c, "sort_pass_carry", ((double)sizeof(K) + (vals ? 4.0 : 0.0) + 8.0 + xb + 8.0) * n);
-        if (vals && uns) QE_P1(IN_KV, true, true, cxa, cxb, x1);
-        else if (vals) QE_P1(IN_KV, true, false, cxa, cxb, x1);
-        else if (uns) QE_P1(IN_KIOTA, true, true, cxa, cxb, x1);
-        else QE_P1(IN_KIOTA, true, false, cxa, cxb, x1);
+        if (vals && uns) QE_P1(IN_KV, X64, true, cxa, cxb, x1);
+        else if (vals) QE_P1(IN_KV, X64, false, cxa, cxb, x1);
+        else if (uns) QE_P1(IN_KIOTA, X64, true, cxa, cxb, x1);
+        else QE_P1(IN_KIOTA, X64, false, cxa, cxb, x1);
+        QE_HIP(hipGetLastError());
+    } else if (xm) {
+        // key (+ rowid) in, + the payload's 4 (X32) or 8 (XCOL: a u64 column) bytes; word + 4 B out
+        Timed t(c, "sort_pass_carry", ((double)sizeof(K) + (vals ? 4.0 : 0.0) + (xm == XCOL ? 8.0 : 4.0) + 12.0) * n);
+        if (xm == X32 && vals) QE_P1(IN_KV, X32, true, cxa, nullptr, x1);
+        else if (xm == X32) QE_P1(IN_KIOTA, X32, true, cxa, nullptr, x1);
+        else if (vals) QE_P1(IN_KV, XCOL, true, cxa, nullptr, x1);
+        else QE_P1(IN_KIOTA, XCOL, true, cxa, nullptr, x1);
         QE_HIP(hipGetLastError());
     } else {
         // algorithmic bytes: key (+ rowid when given; generated otherwise) in, packed word out
@@ -1794,13 +1846,14 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     }
 #undef QE_P1
     {
-        Timed t(c, cxa ? "sort_pass_carry" : prof_split() ? "sort_pass2" : name, (cxa ? 32.0 : 16.0) * n);
-        auto kern = cxa ? (uns ? tl_pass2_kernel<K, true, true> : tl_pass2_kernel<K, true, false>)
-                        : (uns ? tl_pass2_kernel<K, false, true> : tl_pass2_kernel<K, false, false>);
+        Timed t(c, xm ? "sort_pass_carry" : prof_split() ? "sort_pass2" : name, (16.0 + 2.0 * (double)(xm ? xsz : 0)) * n);
+        auto kern = xm == X64 ? (uns ? tl_pass2_kernel<K, X64, true> : tl_pass2_kernel<K, X64, false>)
+                    : xm      ? tl_pass2_kernel<K, X32, true>   // (the X32 / XCOL first pass is unstable too)
+                              : (uns ? tl_pass2_kernel<K, X_NONE, true> : tl_pass2_kernel<K, X_NONE, false>);
         hipLaunchKernelGGL(kern, dim3(xcd_grid(nseg)), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8, seg, gcnt, G,
                            x1, x2);
         QE_HIP(hipGetLastError());
-        if (cxa) dfree(c, x1);
+        if (xm) dfree(c, x1);
     }
     // the two passes are valid whatever the bucket sizes, so they are queued before the host
     // reads the largest bucket: the GPU stays busy through that round trip
@@ -1818,7 +1871,8 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
             d.words = w2;
             d.bstart = bstart;
             d.d_max = d_max;
-            d.x = x2;
+            d.x = xm == X64 ? x2 : nullptr;
+            d.x32 = xm && xm != X64 ? reinterpret_cast<uint32_t*>(x2) : nullptr;
             d.kout = (uint64_t*)kout;
             d.vout = vout;
             d.lo = f.lo;
@@ -2103,6 +2157,7 @@ static void drop(qe_ctx* c, const DeferredSort& d) {
     dfree(c, d.bstart);
     dfree(c, d.d_max);
     dfree(c, d.x);
+    dfree(c, d.x32);
 }
 
 // A deferred sort with a bucket beyond LDS (skew) completes by plain LSD passes over the packed
@@ -2304,8 +2359,8 @@ void pairs_drop_deferred(qe_ctx* c, const qe_pairs* p) {
     c->deferred.erase(it);
 }
 
-bool gather_with_hist(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint64_t n, uint64_t kor, uint64_t kand,
-                      uint64_t* keys) {
+static bool gather_hist_impl(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint64_t n, uint64_t kor,
+                             uint64_t kand, uint64_t* keys) {
     // exactly the plan radix_sort_impl will choose for these keys and bounds: the packed
     // two-level sort in its lookback-free form
     if (n < 2 || n >= 0xFFFFFFFFull) return false;
@@ -2326,10 +2381,15 @@ bool gather_with_hist(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint
     uint32_t* tcnt = dalloc_t<uint32_t>(c, (size_t)nt * 256);
     uint32_t* gcnt = dalloc_t<uint32_t>(c, (size_t)nseg * 128);
     QE_HIP(hipMemsetAsync(gcnt, 0, (size_t)nseg * 128 * sizeof(uint32_t), c->stream));
-    {
+    if (col) {
         Timed t(c, "gather_keys", 12.0 * n + 8.0 * n);
-        hipLaunchKernelGGL(tl_gather_hist_kernel, dim3(G * Q), dim3(1024), 0, c->stream, col, rows, n, keys, f, L, nt, G,
-                           Q, tcnt, gcnt);
+        hipLaunchKernelGGL(tl_gather_hist_kernel<false>, dim3(G * Q), dim3(1024), 0, c->stream, col, rows, n, keys, f, L,
+                           nt, G, Q, tcnt, gcnt);
+        QE_HIP(hipGetLastError());
+    } else {
+        Timed t(c, "widen_keys", 12.0 * n);
+        hipLaunchKernelGGL(tl_gather_hist_kernel<true>, dim3(G * Q), dim3(1024), 0, c->stream, nullptr, rows, n, keys, f,
+                           L, nt, G, Q, tcnt, gcnt);
         QE_HIP(hipGetLastError());
     }
     PreHist ph;
@@ -2340,6 +2400,15 @@ bool gather_with_hist(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint
     ph.fmask = fmask;
     c->prehist[keys] = ph;
     return true;
+}
+
+bool gather_with_hist(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint64_t n, uint64_t kor, uint64_t kand,
+                      uint64_t* keys) {
+    return gather_hist_impl(c, col, rows, n, kor, kand, keys);
+}
+
+bool widen_with_hist(qe_ctx* c, const uint32_t* vals, uint64_t n, uint64_t kor, uint64_t kand, uint64_t* keys) {
+    return gather_hist_impl(c, nullptr, vals, n, kor, kand, keys);
 }
 
 // the bucket geometry radix_sort_impl would give a deferred sort of p (its pass plan, from the
@@ -2362,23 +2431,24 @@ static bool deferred_geometry(const qe_pairs* p, bool need_pre, int* lo, int* nb
     return true;
 }
 
-bool carry_eligible(const qe_pairs* R, const qe_pairs* S) {
+bool carry_eligible(const qe_pairs* R, const qe_pairs* S, bool rpay) {
     int loR, nbR, loS, nbS;
     uint64_t kcR, kcS;
-    if (!deferred_geometry(R, false, &loR, &nbR, &kcR) || !deferred_geometry(S, true, &loS, &nbS, &kcS)) return false;
+    if (!deferred_geometry(R, rpay, &loR, &nbR, &kcR) || !deferred_geometry(S, true, &loS, &nbS, &kcS)) return false;
     return loR == loS && nbR == nbS && kcR == kcS && nbR - TL_H <= HJ_DBITS;
 }
 
 bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS, qe_list* outX0,
-                 qe_list* outX1) {
+                 qe_list* outX1, qe_list* outRX) {
     auto iR = c->deferred.find(R->key), iS = c->deferred.find(S->key);
     if (iR == c->deferred.end() || iS == c->deferred.end() || R->key == S->key) return false;
     const DeferredSort& dR = iR->second;
     const DeferredSort& dS = iS->second;
     if (dR.lo != dS.lo || dR.L != dS.L || dR.fmask != dS.fmask || dR.kconst != dS.kconst || dR.L > HJ_DBITS)
         return false;   // different bucket geometry, or a bucket domain beyond LDS
-    const bool carry = outX0 != nullptr;
+    const bool carry = outX0 != nullptr, rx = outRX != nullptr;
     if (carry && !dS.x) return false;   // S's sort did not carry the payload
+    if (rx && (!dR.x32 || !hj_chain_on())) return false;   // R's neither (or no chain kernel to take it)
     const uint64_t nR = R->n, nS = S->n;
     uint64_t cap = nR + nS;   // optimistic (fan-out ~1); an outgrown launch re-runs with the exact size
     for (int attempt = 0; attempt < 2; attempt++) {
@@ -2386,11 +2456,30 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
         uint32_t* oS = dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1));
         uint32_t* x0 = carry ? dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1)) : nullptr;
         uint32_t* x1 = carry && outX1 ? dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1)) : nullptr;
+        uint32_t* xr = rx ? dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1)) : nullptr;
         QE_HIP(hipMemsetAsync(c->d_scratch + 17, 0, 2 * sizeof(uint64_t), c->stream));   // [pairs, oversize]
         {
-            // algorithmic bytes: both sides' words in (+ 8 B per pair below; + S's payloads)
-            Timed t(c, "bucket_join", 8.0 * (double)(nR + nS) + (carry ? 8.0 * (double)nS : 0.0));
-            if (hj_chain_on()) {
+            // algorithmic bytes: both sides' words in (+ 8 B per pair below; + the payloads)
+            Timed t(c, "bucket_join", 8.0 * (double)(nR + nS) + (carry ? 8.0 * (double)nS : 0.0) + (rx ? 4.0 * (double)nR : 0.0));
+            if (rx) {
+                const uint64_t* xs = carry ? dS.x : nullptr;
+                if (carry && dR.L <= 12)
+                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
+                                       c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
+                                       c->d_scratch + 17, xs, x0, x1, dR.x32, xr);
+                else if (carry)
+                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<HJ_DBITS, true, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
+                                       c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
+                                       c->d_scratch + 17, xs, x0, x1, dR.x32, xr);
+                else if (dR.L <= 12)
+                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, false, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
+                                       c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
+                                       c->d_scratch + 17, nullptr, nullptr, nullptr, dR.x32, xr);
+                else
+                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<HJ_DBITS, false, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
+                                       c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
+                                       c->d_scratch + 17, nullptr, nullptr, nullptr, dR.x32, xr);
+            } else if (hj_chain_on()) {
                 if (carry && dR.L <= 12)
                     hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream,
                                        dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17,
@@ -2428,6 +2517,7 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
             dfree(c, oS);
             dfree(c, x0);
             dfree(c, x1);
+            dfree(c, xr);
             return false;
         }
         if (P <= cap) {
@@ -2437,6 +2527,7 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
                 dfree(c, oS);
                 dfree(c, x0);
                 dfree(c, x1);
+                dfree(c, xr);
                 char msg[160];
                 snprintf(msg, sizeof msg, "join of %llu pairs exceeds the materialisation limit %llu",
                          (unsigned long long)P, (unsigned long long)c->mat_limit);
@@ -2447,7 +2538,7 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
             outR->n = outS->n = P;
             outR->cap = outS->cap = cap;
             outR->flags = outS->flags = 0;
-            for (auto [ol, xd] : {std::pair<qe_list*, uint32_t*>{outX0, x0}, {outX1, x1}})
+            for (auto [ol, xd] : {std::pair<qe_list*, uint32_t*>{outX0, x0}, {outX1, x1}, {outRX, xr}})
                 if (ol) {
                     ol->d = xd;
                     ol->n = P;
@@ -2460,6 +2551,7 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
         dfree(c, oS);
         dfree(c, x0);
         dfree(c, x1);
+        dfree(c, xr);
         cap = P;
     }
     throw Error(QE_EINVAL, "internal: bucket join outgrew its exact size");

@@ -324,8 +324,10 @@ static int plan_check(const qe_engine* e, const query_t* q) {
 
 #define NONE ((qe_h)0)
 
-typedef struct { int b; qe_h rows; int whole; int vcol; } member;  /* whole: every row of the relation;
-                                                                     vcol = c + 1: rows holds column c's values */
+/* whole: every row of the relation; vcol = c + 1: rows holds column c's values; kvals (kcol = c + 1):
+ * column c's values at the binding's rows -- its next join's key, delivered by the join that made
+ * the component (join_carry's outxa), consumed or dropped by the component's next join */
+typedef struct { int b; qe_h rows; int whole; int vcol; qe_h kvals; int kcol; } member;
 typedef struct { member* m; int n; uint64_t size; int alive; } comp_t;
 
 typedef struct {
@@ -421,11 +423,14 @@ typedef struct {
     int keep_b[64];
     int keep_v[64];
     int base;                   /* keys is a whole base column (vals NONE = row i) */
+    qe_h pay;                   /* base side: the column of its binding's next join key (join_carry's xa) */
+    int pay_col;                /* that column + 1 */
 } side_t;
 
 static int is_whole(const comp_t* c) { return c->n == 1 && c->m[0].whole; }
 
-static int side_start(plan_t* P, int cid, int b, uint32_t col, const uint8_t* need, const int* sel1, side_t* s) {
+static int side_start(plan_t* P, int cid, int b, uint32_t col, const uint8_t* need, const int* sel1, const int* kcol1,
+                      side_t* s) {
     const qe_engine* e = P->e;
     comp_t* c = &P->C[cid];
     memset(s, 0, sizeof *s);
@@ -436,12 +441,30 @@ static int side_start(plan_t* P, int cid, int b, uint32_t col, const uint8_t* ne
             s->ncar = 1;
             s->car_b[0] = b;
             s->car_rows[0] = NONE;
+            if (kcol1[b] && e->column && e->keys_of && e->join_carry) {
+                /* its next join's key column rides with its rows: no gather through them later */
+                const int r = e->column(e->u, P->q->rels[b], (uint32_t)(kcol1[b] - 1), &s->pay);
+                if (r == 0) s->pay_col = kcol1[b];
+                else if (r != QE_ENOTSUP) {
+                    P->rc = r;
+                    return r;
+                }
+            }
         }
         return 0;
     }
     member* mb = &c->m[member_idx(c, b)];
     ECHK(rows_of(P, mb));
-    ECHK(e->keys(e->u, P->q->rels[b], col, mb->rows, &s->keys));
+    if (mb->kvals != NONE && mb->kcol == (int)col + 1) {     /* the key's values came with the rows */
+        ECHK(e->keys_of(e->u, P->q->rels[b], col, mb->kvals, &s->keys));
+    } else {
+        ECHK(e->keys(e->u, P->q->rels[b], col, mb->rows, &s->keys));
+    }
+    for (int i = 0; i < c->n; i++) {                         /* kvals live one join: consumed or dropped */
+        rel(P, c->m[i].kvals);
+        c->m[i].kvals = NONE;
+        c->m[i].kcol = 0;
+    }
     if (e->values && sel1[b] && c->n == 1 && mb->vcol == 0) {
         /* a filtered list (ascending rowids) read after this join only by selects of one column:
          * its values ride instead of its rowids (gathered here in order, not at random later) */
@@ -518,14 +541,17 @@ static int side_finish(plan_t* P, side_t* s) {
 
 static void free_comp(plan_t* P, int cid) {
     comp_t* c = &P->C[cid];
-    for (int i = 0; i < c->n; i++) rel(P, c->m[i].rows);
+    for (int i = 0; i < c->n; i++) {
+        rel(P, c->m[i].rows);
+        rel(P, c->m[i].kvals);
+    }
     free(c->m);
     c->m = NULL;
     c->n = 0;
     c->alive = 0;
 }
 
-static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* sel1, int last) {
+static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* sel1, const int* kcol1, int last) {
     const qe_engine* e = P->e;
     const int ba = (int)p->frel, bb = (int)p->srel;
     const int A = component(P, ba), B = component(P, bb);
@@ -561,11 +587,16 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* s
     side_t sa, sb;
     /* derived sides first, so their exchanges overlap the base side's local bucket scan */
     if (is_whole(&P->C[A])) {
-        ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, sel1, &sb));
-        ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, sel1, &sa));
+        ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, sel1, kcol1, &sb));
+        ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, sel1, kcol1, &sa));
     } else {
-        ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, sel1, &sa));
-        ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, sel1, &sb));
+        ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, sel1, kcol1, &sa));
+        ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, sel1, kcol1, &sb));
+    }
+    if (sa.pay && sb.pay) {                                  /* one payload column per join */
+        rel(P, sb.pay);
+        sb.pay = NONE;
+        sb.pay_col = 0;
     }
     ECHK(side_finish(P, &sa));
     ECHK(side_finish(P, &sb));
@@ -606,6 +637,8 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* s
             rel(P, sb.keys);
             rel(P, sa.vals);
             rel(P, sb.vals);
+            rel(P, sa.pay);
+            rel(P, sb.pay);
             for (int k = 0; k < sa.ncar; k++) rel(P, sa.car_rows[k]);
             for (int k = 0; k < sb.ncar; k++) rel(P, sb.car_rows[k]);
             free_comp(P, A);
@@ -621,24 +654,33 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* s
     }
     qe_h oa = NONE, ob = NONE;
     /* a side carrying several bindings: its first rides as the join's vals, the others (up to two)
-     * ride through the engine's join beside the pairs (join_carry) instead of being taken after */
+     * ride through the engine's join beside the pairs (join_carry) instead of being taken after;
+     * a base side's payload column (its binding's next join key) rides on the other side of it */
     qe_h made[2][64];
     for (int k = 0; k < 2; k++)
         for (int i = 0; i < 64; i++) made[k][i] = NONE;
     int cs = -1;
     if (e->join_carry) {
-        if (sb.ncar >= 2 && sb.ncar <= 3 && sb.vals == NONE) cs = 1;
+        if (sa.pay) cs = 1;
+        else if (sb.pay) cs = 0;
+        else if (sb.ncar >= 2 && sb.ncar <= 3 && sb.vals == NONE) cs = 1;
         else if (sa.ncar >= 2 && sa.ncar <= 3 && sa.vals == NONE) cs = 0;
     }
     int jr;
+    qe_h oxa = NONE;                                        /* the payload side's next join key values */
     if (cs >= 0) {
         side_t* C = cs ? &sb : &sa;
         side_t* O = cs ? &sa : &sb;
-        C->vals = C->car_rows[0];
-        C->car_rows[0] = NONE;                              /* now rides as vals */
-        qe_h oo = NONE, oc = NONE, ox[2] = {NONE, NONE};
-        jr = e->join_carry(e->u, O->keys, O->vals, C->keys, C->vals, C->ncar - 1, &C->car_rows[1], &oo, &oc, ox);
-        for (int i = 1; i < C->ncar && jr == 0; i++) made[cs][i] = ox[i - 1];
+        int nb = 0;
+        if (C->ncar >= 2) {
+            C->vals = C->car_rows[0];
+            C->car_rows[0] = NONE;                          /* now rides as vals */
+            nb = C->ncar - 1;
+        }
+        qe_h oo = NONE, oc = NONE, ox[64];
+        for (int i = 0; i < 64; i++) ox[i] = NONE;
+        jr = e->join_carry(e->u, O->keys, O->vals, C->keys, C->vals, nb, &C->car_rows[1], O->pay, &oo, &oc, ox, &oxa);
+        for (int i = 1; i < C->ncar && i <= nb && jr == 0; i++) made[cs][i] = ox[i - 1];
         if (cs) {
             oa = oo;
             ob = oc;
@@ -662,6 +704,9 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* s
         if (v[1]) {
             rel(P, oa);
             rel(P, ob);
+            rel(P, oxa);
+            rel(P, sa.pay);
+            rel(P, sb.pay);
             for (int k = 0; k < 2; k++)
                 for (int i = 0; i < 64; i++) rel(P, made[k][i]);
             rel(P, sa.keys);
@@ -686,6 +731,11 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* s
         for (int i = 0; i < s->ncar; i++) {
             m[n].b = s->car_b[i];
             m[n].vcol = s->car_v[i];
+            if (s->pay && oxa != NONE) {                    /* (a base side carries its one binding) */
+                m[n].kvals = oxa;
+                m[n].kcol = s->pay_col;
+                oxa = NONE;
+            }
             if (made[k][i] != NONE) {                        /* delivered by join_carry */
                 m[n].rows = made[k][i];
                 rel(P, s->car_rows[i]);
@@ -709,6 +759,9 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* s
     rel(P, sb.keys);
     rel(P, sa.vals);
     rel(P, sb.vals);
+    rel(P, sa.pay);
+    rel(P, sb.pay);
+    rel(P, oxa);                         /* (not taken by a member) */
     if (!used[0]) rel(P, oa);
     if (!used[1]) rel(P, ob);
     const uint64_t size = P->C[A].size;
@@ -765,6 +818,7 @@ static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t*
     const int reorder = !(getenv("QE_DIST_REORDER") && getenv("QE_DIST_REORDER")[0] == '0');
     uint8_t* need = (uint8_t*)calloc(nb, 1);
     int* sel1 = (int*)calloc(nb, sizeof(int));
+    int* kcol1 = (int*)calloc(nb, sizeof(int));
     int* pending = (int*)malloc((q->npreds + 1) * sizeof(int));
     size_t k = 0;
     int rc = 0;
@@ -851,7 +905,19 @@ static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t*
             }
             for (size_t x = 0; x < nb; x++)
                 if (sel1[x] < 0) sel1[x] = 0;
-            rc = do_join(P, jp, need, sel1, np == 0 && end == q->npreds);
+            /* kcol1[b] = c + 1: binding b joins again after this join, always on its column c */
+            for (size_t x = 0; x < nb; x++) kcol1[x] = 0;
+            for (size_t i = 0; i < np + (q->npreds - end); i++) {
+                const pred_t* r = i < np ? &q->preds[pending[i]] : &q->preds[end + (i - np)];
+                if (r->type != 0) continue;
+                const size_t xs[2] = {r->frel, r->srel};
+                const int cs2[2] = {(int)r->fcol + 1, (int)r->scol + 1};
+                for (int t = 0; t < 2; t++)
+                    kcol1[xs[t]] = kcol1[xs[t]] == 0 ? cs2[t] : kcol1[xs[t]] == cs2[t] ? cs2[t] : -1;
+            }
+            for (size_t x = 0; x < nb; x++)
+                if (kcol1[x] < 0) kcol1[x] = 0;
+            rc = do_join(P, jp, need, sel1, kcol1, np == 0 && end == q->npreds);
         }
         k = end;
     }
@@ -913,6 +979,7 @@ static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t*
     free(P->list_size);
     free(need);
     free(sel1);
+    free(kcol1);
     free(pending);
     return rc ? rc : P->rc;
 }

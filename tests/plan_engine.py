@@ -34,7 +34,7 @@ FIELDS = [
     ("release", C.CFUNCTYPE(None, VP, H)),
     ("fallback", C.CFUNCTYPE(I, VP, VP, VP)),
     ("scan2", C.CFUNCTYPE(I, VP, U32, U32, C.c_char, U64, U32, C.c_char, U64, U64, U64, I, P(H))),
-    ("join_carry", C.CFUNCTYPE(I, VP, H, H, H, H, I, P(H), P(H), P(H), P(H))),
+    ("join_carry", C.CFUNCTYPE(I, VP, H, H, H, H, I, P(H), H, P(H), P(H), P(H), P(H))),
     ("join_sums", C.CFUNCTYPE(I, VP, H, H, H, H, I, P(H), I, P(I), P(U32), P(U32), P(U64), P(U64))),
     ("values", C.CFUNCTYPE(I, VP, U32, U32, H, P(H))),
 ]
@@ -42,10 +42,13 @@ VALUES, VALUES_SRC = 0xFFFFFFFF, 4   # include/qe_plan.h: QE_PLAN_VALUES, QE_PLA
 
 
 JOIN_AGG = C.CFUNCTYPE(I, VP, U32, U32, U32, U32, I, P(I), P(U32), P(U64), P(U64))
+COLUMN = C.CFUNCTYPE(I, VP, U32, U32, P(H))
+KEYS_OF = C.CFUNCTYPE(I, VP, U32, U32, H, P(H))
 
 
 class Engine(C.Structure):
-    _fields_ = [("u", VP), ("rank", U32), ("world", U32)] + FIELDS + [("mat_limit", P(U64)), ("join_agg", JOIN_AGG)]
+    _fields_ = [("u", VP), ("rank", U32), ("world", U32)] + FIELDS + [("mat_limit", P(U64)), ("join_agg", JOIN_AGG),
+                                                                      ("column", COLUMN), ("keys_of", KEYS_OF)]
 
 
 def part_of(k: np.ndarray, nparts: int) -> np.ndarray:
@@ -74,7 +77,7 @@ class NumpyPlanEngine:
     """one rank: relations replicated as numpy columns; handles index a dict of arrays"""
 
     def __init__(self, rels, rank=0, world=1, group=None, fused_scan=True, join_carry=True, join_sums=True, values=True,
-                 join_agg=True):
+                 join_agg=True, key_carry=True):
         self.rels, self.rank, self.world, self.group = rels, rank, world, group
         self.h, self.next, self.borrowed = {}, 1, set()
         self.exchanges = 0
@@ -104,6 +107,11 @@ class NumpyPlanEngine:
             self._agg_cb = JOIN_AGG(self._wrap(self.cb_join_agg, False))
             e.join_agg = self._agg_cb
         self.agg_calls = 0                       # last joins of two base relations in aggregate form
+        self.keys_of_calls = 0                   # join keys that rode with their rows (no gather)
+        if key_carry:
+            self._col_cb = COLUMN(self._wrap(self.cb_column, False))
+            self._ko_cb = KEYS_OF(self._wrap(self.cb_keys_of, False))
+            e.column, e.keys_of = self._col_cb, self._ko_cb
         self.e = e
         self._limit = None
 
@@ -235,14 +243,29 @@ class NumpyPlanEngine:
         oa[0] = self.put(self.get(va)[ia] if va else ia)
         ob[0] = self.put(self.get(vb)[ib] if vb else ib)
 
-    def cb_join_carry(self, u, ka, va, kb, vb, nb, cb, oa, ob, outb):
+    def cb_join_carry(self, u, ka, va, kb, vb, nb, cb, xa, oa, ob, outb, outxa):
         ia, ib = join_local(self.get(ka), self.get(kb))
         if len(ia) > self.mat_limit:
             return -5
-        oa[0] = self.put(self.get(va)[ia] if va else ia)
+        ra = self.get(va)[ia] if va else ia      # a's rowids (a whole column: positions are rowids)
+        oa[0] = self.put(ra)
         ob[0] = self.put(self.get(vb)[ib] if vb else ib)
         for k in range(nb):
             outb[k] = self.put(self.get(cb[k])[ib])
+        if xa:
+            tag, col = self.get(xa)
+            assert tag == "column"
+            outxa[0] = self.put(col[ra].astype(np.uint32))
+
+    def cb_column(self, u, rel, col, out):
+        c = self.rels[rel][col]
+        if len(c) and int(c.max()) >> 32:
+            return -6                            # QE_ENOTSUP: the key is gathered later
+        out[0] = self.put(("column", c))
+
+    def cb_keys_of(self, u, rel, col, vals, out):
+        self.keys_of_calls += 1
+        out[0] = self.put(self.get(vals).astype(np.uint64))
 
     def cb_join_sums(self, u, ka, va, kb, vb, nb, cb, nsel, src, rels, cols, pairs, sums):
         """aggregate form, computed independently of the join: each b row counts its a partners"""

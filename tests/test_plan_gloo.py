@@ -37,11 +37,13 @@ def _run_world(rels, queries, world, limits=None, global_limit=None, opts=None):
 def test_every_golden_is_refused_or_exact(fixture, optional):
     """with the engine's optional entries (scan2: a fused scan + refine; join_carry: a side's
     extra bindings delivered by the join; join_sums: the last join's checksums without its
-    pairs) and without them (a scan then a refine; takes; a materialised last join)"""
+    pairs; column / keys_of: a base relation's next join key riding with its rows) and without
+    them (a scan then a refine; takes; a materialised last join; gathered keys)"""
     doc = goldens.load(f"{goldens.GOLDEN_DIR}/{fixture}.json")
     rels, _ = goldens.dataset(doc["dataset"])
     on = optional == "all"
-    eng = pe.NumpyPlanEngine(rels, 0, 1, fused_scan=on, join_carry=on, join_sums=on, values=on, join_agg=on)
+    eng = pe.NumpyPlanEngine(rels, 0, 1, fused_scan=on, join_carry=on, join_sums=on, values=on, join_agg=on,
+                             key_carry=on)
     accepted = {"T": 0, "W": 0}
     for c in doc["cases"]:
         out, rc, _, _ = eng.run(c["input"])
@@ -59,6 +61,7 @@ def test_every_golden_is_refused_or_exact(fixture, optional):
     if fixture == "headline" and on:
         assert eng.scan2_values > 0                        # C3's fused scan emits 3.2's values
         assert eng.agg_calls > 0                           # G1/G2: two base relations, aggregate form
+        assert eng.keys_of_calls > 0                       # C3: R2's and R1's next join keys rode with them
 
 
 def test_check_names_the_reason():
