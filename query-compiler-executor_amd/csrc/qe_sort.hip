@@ -1117,7 +1117,10 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
 // pairs need no order, the per-bucket LDS sorts of both sides (12 B/row written and read back)
 // and the merge's searches: words in (8 B/row), pairs out (8 B/pair).  LDS: run bounds (4 B per
 // key value of the bucket) + R rowids (4 B per row) -- four workgroups per CU at L = 12.
-constexpr int HJ_NT = 1024, HJ_NW = HJ_NT / 64;   // 53 VGPRs: two blocks = 32 waves per CU
+#ifndef QE_HJ_NT
+#define QE_HJ_NT 1024
+#endif
+constexpr int HJ_NT = QE_HJ_NT, HJ_NW = HJ_NT / 64;   // 1024: 53 VGPRs, two blocks = 32 waves per CU
 constexpr int HJ_I = (TL_CAP + HJ_NT - 1) / HJ_NT;   // rows per thread per side
 constexpr int HJ_DBITS = 13;                          // largest in-bucket key domain (2^13 values)
 static_assert(HJ_I * HJ_NW <= 128, "the (row-group, wave) table is scanned by one wave, two entries per lane");
@@ -1321,9 +1324,13 @@ __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
 // length |R bucket| / 2^L, ~0.75 at C3) and the wave-cooperative emission walks it again to the
 // pair's partner.  Output is the same multiset of pairs (in no particular order, as before).
 // RX: R's rows carry a 32-bit payload too (xR, in R's word order -- a base relation's next join
-// key, sorted along with it): the partner's payload is read back from xR (the bucket's 20 KB, L2
-// after the first touch) and written to outRX -- LDS stays as without it.
+// key, sorted along with it): staged in LDS beside the rowids (two blocks per CU are the wave
+// limit anyway: 67 KB each fits) and written to outRX with the partner.  (Re-reading R's rowids or
+// payloads from L2 at emission instead measured 0.2-0.5 ms slower per C3 query.)
 constexpr uint32_t HJ_NONE = 0xFFFFu;
+#ifndef QE_HJ_RR_GLOBAL
+#define QE_HJ_RR_GLOBAL 0
+#endif
 static_assert(TL_CAP < HJ_NONE, "chain links are 16-bit row indices");
 
 template <int DBITS, bool CARRY = false, bool RX = false>
@@ -1335,7 +1342,12 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
                       const uint32_t* __restrict__ xR = nullptr, uint32_t* __restrict__ outRX = nullptr) {
     __shared__ uint32_t head[1 << DBITS];   // per key value: the last R row inserted (HJ_NONE: none)
     __shared__ uint16_t nxt[TL_CAP];        // per R row: the previous row of its value
+#if QE_HJ_RR_GLOBAL
+    uint32_t* rr = nullptr;                 // (R's rowids re-read from its words, L2-hot, at emission)
+#else
     __shared__ uint32_t rr[TL_CAP];         // per R row: its rowid
+#endif
+    __shared__ uint32_t rx[RX ? TL_CAP : 1];  // per R row: its payload
     __shared__ uint32_t tab[HJ_I * HJ_NW];
     __shared__ uint64_t s_excl;
     __shared__ uint32_t s_total;
@@ -1366,6 +1378,14 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
             xv[j] = i < mS ? xS[s0 + i] : 0ull;
         }
     }
+    uint32_t xr[RX ? HJ_I : 1];
+    if constexpr (RX) {
+#pragma unroll
+        for (int j = 0; j < HJ_I; j++) {
+            const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
+            xr[j] = i < mR ? xR[r0 + i] : 0u;
+        }
+    }
     for (uint32_t v = threadIdx.x; v < D; v += HJ_NT) head[v] = HJ_NONE;
     __syncthreads();
 #pragma unroll
@@ -1373,7 +1393,8 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
         const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
         if (i < mR) {
             nxt[i] = (uint16_t)atomicExch(&head[fld(wr[j]) & dmask], i);
-            rr[i] = (uint32_t)wr[j];
+            if (!QE_HJ_RR_GLOBAL) rr[i] = (uint32_t)wr[j];
+            if constexpr (RX) rx[i] = xr[j];
         }
     }
     __syncthreads();
@@ -1432,9 +1453,9 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
             }
             if (q < all) {
                 for (uint32_t s = 0; s < k; s++) p = nxt[p];   // the k-th partner on the chain
-                outR[ob + q] = rr[p];
+                outR[ob + q] = QE_HJ_RR_GLOBAL ? (uint32_t)wR[r0 + p] : rr[p];
                 outS[ob + q] = sr;
-                if constexpr (RX) outRX[ob + q] = xR[r0 + p];
+                if constexpr (RX) outRX[ob + q] = rx[p];
                 if constexpr (CARRY) {
                     outX0[ob + q] = x0;
                     if (outX1) outX1[ob + q] = x1;
@@ -2448,7 +2469,8 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
         return false;   // different bucket geometry, or a bucket domain beyond LDS
     const bool carry = outX0 != nullptr, rx = outRX != nullptr;
     if (carry && !dS.x) return false;   // S's sort did not carry the payload
-    if (rx && (!dR.x32 || !hj_chain_on())) return false;   // R's neither (or no chain kernel to take it)
+    // R's neither (or no chain kernel to take it, or a 2^13-value bucket domain: 82 KB of LDS)
+    if (rx && (!dR.x32 || !hj_chain_on() || dR.L > 12)) return false;
     const uint64_t nR = R->n, nS = S->n;
     uint64_t cap = nR + nS;   // optimistic (fan-out ~1); an outgrown launch re-runs with the exact size
     for (int attempt = 0; attempt < 2; attempt++) {
@@ -2463,20 +2485,12 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
             Timed t(c, "bucket_join", 8.0 * (double)(nR + nS) + (carry ? 8.0 * (double)nS : 0.0) + (rx ? 4.0 * (double)nR : 0.0));
             if (rx) {
                 const uint64_t* xs = carry ? dS.x : nullptr;
-                if (carry && dR.L <= 12)
+                if (carry)
                     hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
                                        c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
                                        c->d_scratch + 17, xs, x0, x1, dR.x32, xr);
-                else if (carry)
-                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<HJ_DBITS, true, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
-                                       c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
-                                       c->d_scratch + 17, xs, x0, x1, dR.x32, xr);
-                else if (dR.L <= 12)
-                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, false, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
-                                       c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
-                                       c->d_scratch + 17, nullptr, nullptr, nullptr, dR.x32, xr);
                 else
-                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<HJ_DBITS, false, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
+                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, false, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
                                        c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
                                        c->d_scratch + 17, nullptr, nullptr, nullptr, dR.x32, xr);
             } else if (hj_chain_on()) {
