@@ -1622,10 +1622,11 @@ bool join_pairs_carry(qe_ctx* c, qe_pairs* R, qe_pairs* S, const uint32_t* xa, c
     sort_pairs(c, R, true);
     c->carry_x32 = nullptr;   // (consumed by R's sort; cleared in any case)
     c->carry_c64 = nullptr;
-    c->carry_xa = xa;
+    c->carry_xa = xb ? xa : nullptr;   // two columns: one 64-bit payload; one: 32-bit
     c->carry_xb = xb;
+    c->carry_x32 = xb ? nullptr : xa;
     sort_pairs(c, S, true);
-    c->carry_xa = c->carry_xb = nullptr;   // (consumed by S's sort; cleared in any case)
+    c->carry_xa = c->carry_xb = c->carry_x32 = nullptr;   // (consumed by S's sort; cleared in any case)
     if (bucket_join(c, R, S, outR, outS, xa ? outX0 : nullptr, xa && xb ? outX1 : nullptr, rpay ? outRX : nullptr))
         return true;
     // a bucket beyond LDS: drop both deferred sorts, give the caller its inputs back
@@ -1642,10 +1643,11 @@ bool join_pairs_sums(qe_ctx* c, qe_pairs* R, qe_pairs* S, const uint32_t* xa, co
     const qe_pairs R0 = *R, S0 = *S;
     if ((R0.owns | S0.owns) & 7) return false;
     sort_pairs(c, R, true);
-    c->carry_xa = xa;   // (null: no payload)
+    c->carry_xa = xb ? xa : nullptr;   // (null: no payload; one column: 32-bit)
     c->carry_xb = xb;
+    c->carry_x32 = xb ? nullptr : xa;
     sort_pairs(c, S, true);
-    c->carry_xa = c->carry_xb = nullptr;
+    c->carry_xa = c->carry_xb = c->carry_x32 = nullptr;
     if (bucket_join_sums(c, R, S, sc, pairs, sums)) return true;
     qe_pairs_free(c, R);
     qe_pairs_free(c, S);

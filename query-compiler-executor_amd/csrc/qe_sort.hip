@@ -1333,13 +1333,15 @@ constexpr uint32_t HJ_NONE = 0xFFFFu;
 #endif
 static_assert(TL_CAP < HJ_NONE, "chain links are 16-bit row indices");
 
-template <int DBITS, bool CARRY = false, bool RX = false>
+// S32: S's payload is 32-bit (xS32: one carried binding), outX0 only.
+template <int DBITS, bool CARRY = false, bool RX = false, bool S32 = false>
 __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
 tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict__ bsR, const uint64_t* __restrict__ wS,
                       const uint32_t* __restrict__ bsS, int L, uint32_t* __restrict__ outR, uint32_t* __restrict__ outS,
                       uint64_t cap, uint64_t* total_out, const uint64_t* __restrict__ xS = nullptr,
                       uint32_t* __restrict__ outX0 = nullptr, uint32_t* __restrict__ outX1 = nullptr,
-                      const uint32_t* __restrict__ xR = nullptr, uint32_t* __restrict__ outRX = nullptr) {
+                      const uint32_t* __restrict__ xR = nullptr, uint32_t* __restrict__ outRX = nullptr,
+                      const uint32_t* __restrict__ xS32 = nullptr) {
     __shared__ uint32_t head[1 << DBITS];   // per key value: the last R row inserted (HJ_NONE: none)
     __shared__ uint16_t nxt[TL_CAP];        // per R row: the previous row of its value
 #if QE_HJ_RR_GLOBAL
@@ -1375,7 +1377,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
 #pragma unroll
         for (int j = 0; j < HJ_I; j++) {
             const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
-            xv[j] = i < mS ? xS[s0 + i] : 0ull;
+            xv[j] = i < mS ? (S32 ? (uint64_t)xS32[s0 + i] : xS[s0 + i]) : 0ull;
         }
     }
     uint32_t xr[RX ? HJ_I : 1];
@@ -1449,7 +1451,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
             uint32_t x0 = 0, x1 = 0;
             if constexpr (CARRY) {
                 x0 = (uint32_t)__shfl((int)(uint32_t)xv[j], owner, 64);
-                x1 = (uint32_t)__shfl((int)(uint32_t)(xv[j] >> 32), owner, 64);
+                if constexpr (!S32) x1 = (uint32_t)__shfl((int)(uint32_t)(xv[j] >> 32), owner, 64);
             }
             if (q < all) {
                 for (uint32_t s = 0; s < k; s++) p = nxt[p];   // the k-th partner on the chain
@@ -1458,7 +1460,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
                 if constexpr (RX) outRX[ob + q] = rx[p];
                 if constexpr (CARRY) {
                     outX0[ob + q] = x0;
-                    if (outX1) outX1[ob + q] = x1;
+                    if (!S32 && outX1) outX1[ob + q] = x1;
                 }
             }
         }
@@ -2468,7 +2470,9 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
     if (dR.lo != dS.lo || dR.L != dS.L || dR.fmask != dS.fmask || dR.kconst != dS.kconst || dR.L > HJ_DBITS)
         return false;   // different bucket geometry, or a bucket domain beyond LDS
     const bool carry = outX0 != nullptr, rx = outRX != nullptr;
-    if (carry && !dS.x) return false;   // S's sort did not carry the payload
+    if (carry && !dS.x && !dS.x32) return false;   // S's sort did not carry the payload
+    const bool s32 = carry && !dS.x;                // ... or carried one 32-bit column (chain kernel only)
+    if (s32 && (outX1 || !hj_chain_on() || dR.L > 12)) return false;
     // R's neither (or no chain kernel to take it, or a 2^13-value bucket domain: 82 KB of LDS)
     if (rx && (!dR.x32 || !hj_chain_on() || dR.L > 12)) return false;
     const uint64_t nR = R->n, nS = S->n;
@@ -2483,7 +2487,15 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
         {
             // algorithmic bytes: both sides' words in (+ 8 B per pair below; + the payloads)
             Timed t(c, "bucket_join", 8.0 * (double)(nR + nS) + (carry ? 8.0 * (double)nS : 0.0) + (rx ? 4.0 * (double)nR : 0.0));
-            if (rx) {
+            if (s32 && rx) {
+                hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, true, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
+                                   c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
+                                   c->d_scratch + 17, nullptr, x0, nullptr, dR.x32, xr, dS.x32);
+            } else if (s32) {
+                hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, false, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
+                                   c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
+                                   c->d_scratch + 17, nullptr, x0, nullptr, nullptr, nullptr, dS.x32);
+            } else if (rx) {
                 const uint64_t* xs = carry ? dS.x : nullptr;
                 if (carry)
                     hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
@@ -2583,7 +2595,7 @@ __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
 tl_hjoin_sums_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict__ bsR,
                      const uint64_t* __restrict__ wS, const uint32_t* __restrict__ bsS, int L,
                      const uint64_t* __restrict__ xS, HjSums sc, uint64_t* __restrict__ part,
-                     unsigned long long* __restrict__ flag) {
+                     unsigned long long* __restrict__ flag, const uint32_t* __restrict__ xS32) {
     __shared__ uint32_t cnt[1 << HJ_DBITS];
     __shared__ uint64_t red[HJ_NW][HJ_SUMS + 1];
     const uint32_t b = blockIdx.x;
@@ -2600,7 +2612,7 @@ tl_hjoin_sums_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict
         const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
         wr[j] = i < mR ? wR[r0 + i] : 0;
         ws[j] = i < mS ? wS[s0 + i] : 0;
-        xv[j] = xS && i < mS ? xS[s0 + i] : 0ull;
+        xv[j] = xS32 && i < mS ? (uint64_t)xS32[s0 + i] : xS && i < mS ? xS[s0 + i] : 0ull;
     }
     for (uint32_t v = threadIdx.x; v < D; v += HJ_NT) cnt[v] = 0;
     __syncthreads();
@@ -2670,7 +2682,9 @@ bool bucket_join_sums(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const HjS
     if (sc.n < 0 || sc.n > HJ_SUMS) return false;
     bool carry = false;
     for (int s = 0; s < sc.n; s++) carry |= (sc.src[s] & 3) != 0;
-    if (carry && !dS.x) return false;   // S's sort did not carry the payload
+    if (carry && !dS.x && !dS.x32) return false;   // S's sort did not carry the payload
+    for (int s = 0; s < sc.n; s++)
+        if (!dS.x && (sc.src[s] & 3) == 2) return false;   // (a 32-bit payload has no high half)
     uint64_t* part = dalloc_t<uint64_t>(c, (size_t)TL_BUCKETS * (HJ_SUMS + 1));
     uint64_t* out = dalloc_t<uint64_t>(c, 8);   // [pairs-free sums..., pairs, oversize]
     QE_HIP(hipMemsetAsync(out, 0, 8 * sizeof(uint64_t), c->stream));
@@ -2678,7 +2692,7 @@ bool bucket_join_sums(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const HjS
         Timed t(c, "bucket_join_sums", 8.0 * (double)(R->n + S->n) + (carry ? 8.0 * (double)S->n : 0.0));
         hipLaunchKernelGGL(tl_hjoin_sums_kernel, dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream, dR.words, dR.bstart,
                            dS.words, dS.bstart, dR.L, carry ? dS.x : nullptr, sc, part,
-                           reinterpret_cast<unsigned long long*>(out + HJ_SUMS + 1));
+                           reinterpret_cast<unsigned long long*>(out + HJ_SUMS + 1), carry ? dS.x32 : nullptr);
         QE_HIP(hipGetLastError());
         hipLaunchKernelGGL(hjoin_sums_reduce_kernel, dim3(HJ_SUMS + 1), dim3(256), 0, c->stream, part,
                            (uint32_t)TL_BUCKETS, out);
