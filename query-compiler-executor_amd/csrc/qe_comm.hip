@@ -530,6 +530,7 @@ int e_exchange_finish(void* u, qe_h ticket, qe_h* keys, qe_h* cols) {
 }
 
 qe_pairs side_pairs(const DArr* k, const DArr* v) {
+    if (v && v->colview) throw Error(QE_EINVAL, "a column's values as a join side's vals: join_carry only");
     qe_pairs p{};
     p.key = static_cast<uint64_t*>(k->d);
     p.val = v ? static_cast<uint32_t*>(v->d) : nullptr;
@@ -578,15 +579,19 @@ int e_join_carry(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h
         qe_ctx* c = e->c;
         const DArr* X = xa ? A(xa) : nullptr;
         if (X && !X->colview) throw Error(QE_EINVAL, "join_carry: xa is not a column");
-        qe_pairs P = side_pairs(A(ka), va ? A(va) : nullptr);
+        // va a column (a whole base relation whose binding rides as that column's values): a's
+        // rows are its positions, and its sort packs the column's low words in place of them
+        const DArr* VC = va && A(va)->colview ? A(va) : nullptr;
+        if (VC && A(ka)->n != VC->n) throw Error(QE_EINVAL, "join_carry: vals column of another length");
+        qe_pairs P = side_pairs(A(ka), va && !VC ? A(va) : nullptr);
         qe_pairs Q = side_pairs(A(kb), vb ? A(vb) : nullptr);
         qe_list la{}, lb{}, lx0{}, lx1{}, lxa{};
-        auto gather_col = [&](const uint32_t* rows, uint64_t n) {   // X's values at rowids
+        auto gather_col = [&](const uint32_t* rows, uint64_t n, const DArr* col) {   // a column's values at rowids
             uint32_t* d = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
             if (n) {
                 Timed t(c, "gather_values", 12.0 * n);
                 hipLaunchKernelGGL(gather_u32_kernel, dim3(grid_for(n, 256 * 16, 8192)), dim3(256), 0, c->stream,
-                                   static_cast<const uint64_t*>(X->d), rows, n, d);
+                                   static_cast<const uint64_t*>(col->d), rows, n, d);
                 QE_HIP(hipGetLastError());
             }
             return d;
@@ -594,12 +599,12 @@ int e_join_carry(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h
         if (nb >= 0 && nb <= 2 && (nb >= 1 || X)) {
             // a's payload in a's input order: the column itself (a = the whole column, row i), or
             // its values at a's rowids (a rank's bucket: ascending rows, a near-sequential read)
-            const uint64_t* rc64 = X && !va ? static_cast<const uint64_t*>(X->d) : nullptr;
-            uint32_t* rx32 = X && va ? gather_col(static_cast<const uint32_t*>(A(va)->d), A(va)->n) : nullptr;
+            const uint64_t* rc64 = X && (!va || VC) ? static_cast<const uint64_t*>(X->d) : nullptr;
+            uint32_t* rx32 = X && va && !VC ? gather_col(static_cast<const uint32_t*>(A(va)->d), A(va)->n, X) : nullptr;
             const bool done =
                 join_pairs_carry(c, &P, &Q, nb >= 1 ? static_cast<const uint32_t*>(A(cb[0])->d) : nullptr,
                                  nb == 2 ? static_cast<const uint32_t*>(A(cb[1])->d) : nullptr, &la, &lb, &lx0, &lx1,
-                                 rx32, rc64, X ? &lxa : nullptr);
+                                 rx32, rc64, X ? &lxa : nullptr, VC ? static_cast<const uint64_t*>(VC->d) : nullptr);
             dfree(c, rx32);
             if (done) {
                 qe_pairs_free(c, &P);
@@ -617,8 +622,13 @@ int e_join_carry(void* u, qe_h ka, qe_h va, qe_h kb, qe_h vb, int nb, const qe_h
         qe_pairs_free(c, &P);
         qe_pairs_free(c, &Qp);
         ck(rc, c);
-        *oa = H(new_arr(c, la.d, la.n, false));
-        if (X) *outxa = H(new_arr(c, gather_col(la.d, la.n), la.n, false));   // la: a's rowids
+        if (X) *outxa = H(new_arr(c, gather_col(la.d, la.n, X), la.n, false));   // la: a's rowids
+        if (VC) {   // a's binding as the column's values
+            *oa = H(new_arr(c, gather_col(la.d, la.n, VC), la.n, false));
+            dfree(c, la.d);
+        } else {
+            *oa = H(new_arr(c, la.d, la.n, false));
+        }
         auto take = [&](const DArr* src) {
             qe_list o{};
             ck(qe_take_u32(c, static_cast<const uint32_t*>(src->d), &lb, &o), c);

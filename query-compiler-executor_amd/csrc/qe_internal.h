@@ -67,6 +67,7 @@ struct DeferredSort {
     uint64_t* d_max = nullptr;    // largest bucket (device word: > TL_CAP = skew, not yet checked)
     uint64_t* x = nullptr;        // carried payloads, in the words' order (qe_join_carry), or null
     uint32_t* x32 = nullptr;      // a 32-bit payload in the words' order (R's next join key), or null
+    const uint64_t* v64 = nullptr;   // the words hold this column's low words, not row indices
     uint64_t* kout = nullptr;
     uint32_t* vout = nullptr;
     int lo = 0, L = 0;            // field = (key >> lo) & fmask; bucket = field >> L
@@ -142,6 +143,8 @@ struct qe_ctx {
     // ... or one 32-bit payload: a u32 array, or a u64 column's low words (row i = input element i)
     const uint32_t* carry_x32 = nullptr;
     const uint64_t* carry_c64 = nullptr;
+    // ... and for a sort without vals: pack this u64 column's low words instead of the row index
+    const uint64_t* sort_v64 = nullptr;
     std::vector<qe::PendingEvent> pending;
     std::vector<hipEvent_t> event_pool;
     std::vector<qe::KStat> kstats;
@@ -238,9 +241,11 @@ bool carry_eligible(const qe_pairs* R, const qe_pairs* S, bool rpay = false);
 // a u32 array (rx32) or a u64 column's low words (rc64), both in R's input order: outRX.  False:
 // nothing was produced and the inputs are as they were (ineligible, or a bucket beyond LDS) --
 // the caller joins without it.
+// rv64 (R without vals only): outR holds this u64 column's low words at R's rows instead of the
+// row indices (R's binding read later only through that column).
 bool join_pairs_carry(qe_ctx* c, qe_pairs* R, qe_pairs* S, const uint32_t* xa, const uint32_t* xb, qe_list* outR,
                       qe_list* outS, qe_list* outX0, qe_list* outX1, const uint32_t* rx32 = nullptr,
-                      const uint64_t* rc64 = nullptr, qe_list* outRX = nullptr);
+                      const uint64_t* rc64 = nullptr, qe_list* outRX = nullptr, const uint64_t* rv64 = nullptr);
 // keys = (u64) vals for a list whose sort will be the lookback-free two-level one, with that
 // sort's histogram (gather_with_hist without the gather); false: not that sort
 bool widen_with_hist(qe_ctx* c, const uint32_t* vals, uint64_t n, uint64_t kor, uint64_t kand, uint64_t* keys);

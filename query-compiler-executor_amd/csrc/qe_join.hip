@@ -1612,16 +1612,27 @@ int qe_join_pairs(qe_ctx* c, qe_pairs* R, qe_pairs* S, qe_list* outR, qe_list* o
 namespace qe {
 bool join_pairs_carry(qe_ctx* c, qe_pairs* R, qe_pairs* S, const uint32_t* xa, const uint32_t* xb, qe_list* outR,
                       qe_list* outS, qe_list* outX0, qe_list* outX1, const uint32_t* rx32, const uint64_t* rc64,
-                      qe_list* outRX) {
+                      qe_list* outRX, const uint64_t* rv64) {
     const bool rpay = rx32 || rc64;
-    if ((!xa && !rpay) || !carry_eligible(R, S, rpay)) return false;
+    if ((!xa && !rpay) || !carry_eligible(R, S, rpay || rv64)) return false;
+    if (rv64 && R->val) return false;
     const qe_pairs R0 = *R, S0 = *S;   // views of the caller's arrays (nothing owned)
     if ((R0.owns | S0.owns) & 7) return false;
     c->carry_x32 = rx32;
     c->carry_c64 = rc64;
+    c->sort_v64 = rv64;
     sort_pairs(c, R, true);
     c->carry_x32 = nullptr;   // (consumed by R's sort; cleared in any case)
     c->carry_c64 = nullptr;
+    c->sort_v64 = nullptr;
+    if (rv64) {   // the values must have gone into R's words (its sort's deferred lookback-free form)
+        auto it = c->deferred.find(R->key);
+        if (it == c->deferred.end() || it->second.v64 != rv64) {
+            qe_pairs_free(c, R);
+            *R = R0;
+            return false;
+        }
+    }
     c->carry_xa = xb ? xa : nullptr;   // two columns: one 64-bit payload; one: 32-bit
     c->carry_xb = xb;
     c->carry_x32 = xb ? nullptr : xa;

@@ -1833,6 +1833,11 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     if (xm == XCOL) cxa = reinterpret_cast<const uint32_t*>(c->carry_c64);
     c->carry_xa = c->carry_xb = c->carry_x32 = nullptr;
     c->carry_c64 = nullptr;
+    // the packed value: a u64 column's low words instead of the row index (a base relation whose
+    // binding is read later only through that column: its values ride in place of the rowids)
+    const uint64_t* cv64 = dfr && !vals && (xm == XCOL || xm == X_NONE) ? c->sort_v64 : nullptr;
+    c->sort_v64 = nullptr;
+    const uint32_t* v64w = reinterpret_cast<const uint32_t*>(cv64);
     const size_t xsz = xm == X64 ? 8 : 4;
     uint64_t* x1 = xm ? static_cast<uint64_t*>(dalloc(c, n * xsz)) : nullptr;
     uint64_t* x2 = xm ? static_cast<uint64_t*>(dalloc(c, n * xsz)) : nullptr;
@@ -1842,7 +1847,18 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     hipLaunchKernelGGL((radix_pass_kernel<K, IN, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, CR, UN>),            \
                        dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, \
                        255u, f, tcnt, nullptr, nullptr, 0u, XA, XB, XO)
-    if (xm == X64) {
+    if (cv64) {
+        Timed t(c, xm ? "sort_pass_carry" : name, ((double)sizeof(K) + 8.0 + (xm ? 8.0 : 0.0) + 8.0 + (xm ? 4.0 : 0.0)) * n);
+        if (xm)
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV64, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, XCOL, true>),
+                               dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, v64w, kout, w1, vout, n,
+                               32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, cxa, nullptr, x1);
+        else
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV64, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, X_NONE, true>),
+                               dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, v64w, kout, w1, vout, n,
+                               32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr);
+        QE_HIP(hipGetLastError());
+    } else if (xm == X64) {
         const double xb = cxb ? 8.0 : 4.0;
         Timed t(c, "sort_pass_carry", ((double)sizeof(K) + (vals ? 4.0 : 0.0) + 8.0 + xb + 8.0) * n);
         if (vals && uns) QE_P1(IN_KV, X64, true, cxa, cxb, x1);
@@ -1895,6 +1911,7 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
             d.bstart = bstart;
             d.d_max = d_max;
             d.x = xm == X64 ? x2 : nullptr;
+            d.v64 = cv64;
             d.x32 = xm && xm != X64 ? reinterpret_cast<uint32_t*>(x2) : nullptr;
             d.kout = (uint64_t*)kout;
             d.vout = vout;

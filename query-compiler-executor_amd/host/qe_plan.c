@@ -430,7 +430,7 @@ typedef struct {
 static int is_whole(const comp_t* c) { return c->n == 1 && c->m[0].whole; }
 
 static int side_start(plan_t* P, int cid, int b, uint32_t col, const uint8_t* need, const int* sel1, const int* kcol1,
-                      side_t* s) {
+                      const int* vok, side_t* s) {
     const qe_engine* e = P->e;
     comp_t* c = &P->C[cid];
     memset(s, 0, sizeof *s);
@@ -446,6 +446,20 @@ static int side_start(plan_t* P, int cid, int b, uint32_t col, const uint8_t* ne
                 const int r = e->column(e->u, P->q->rels[b], (uint32_t)(kcol1[b] - 1), &s->pay);
                 if (r == 0) s->pay_col = kcol1[b];
                 else if (r != QE_ENOTSUP) {
+                    P->rc = r;
+                    return r;
+                }
+            }
+            if (s->pay && vok[b] && s->vals == NONE) {
+                /* read later only by selects of one column (after the next join, which takes its
+                 * key from the payload): the rows ride as that column's values (join_carry packs
+                 * them in place of the row index) -- no gather through them at the end */
+                qe_h v = NONE;
+                const int r = e->column(e->u, P->q->rels[b], (uint32_t)(vok[b] - 1), &v);
+                if (r == 0) {
+                    s->vals = v;
+                    s->car_v[0] = vok[b];
+                } else if (r != QE_ENOTSUP) {
                     P->rc = r;
                     return r;
                 }
@@ -551,7 +565,8 @@ static void free_comp(plan_t* P, int cid) {
     c->alive = 0;
 }
 
-static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* sel1, const int* kcol1, int last) {
+static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* sel1, const int* kcol1, const int* vok,
+                   int last) {
     const qe_engine* e = P->e;
     const int ba = (int)p->frel, bb = (int)p->srel;
     const int A = component(P, ba), B = component(P, bb);
@@ -587,16 +602,21 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* s
     side_t sa, sb;
     /* derived sides first, so their exchanges overlap the base side's local bucket scan */
     if (is_whole(&P->C[A])) {
-        ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, sel1, kcol1, &sb));
-        ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, sel1, kcol1, &sa));
+        ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, sel1, kcol1, vok, &sb));
+        ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, sel1, kcol1, vok, &sa));
     } else {
-        ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, sel1, kcol1, &sa));
-        ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, sel1, kcol1, &sb));
+        ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, sel1, kcol1, vok, &sa));
+        ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, sel1, kcol1, vok, &sb));
     }
     if (sa.pay && sb.pay) {                                  /* one payload column per join */
         rel(P, sb.pay);
         sb.pay = NONE;
         sb.pay_col = 0;
+        if (sb.car_v[0]) {                                   /* (its values mode goes with it) */
+            rel(P, sb.vals);
+            sb.vals = NONE;
+            sb.car_v[0] = 0;
+        }
     }
     ECHK(side_finish(P, &sa));
     ECHK(side_finish(P, &sb));
@@ -819,6 +839,7 @@ static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t*
     uint8_t* need = (uint8_t*)calloc(nb, 1);
     int* sel1 = (int*)calloc(nb, sizeof(int));
     int* kcol1 = (int*)calloc(nb, sizeof(int));
+    int* vok = (int*)calloc(nb, sizeof(int));
     int* pending = (int*)malloc((q->npreds + 1) * sizeof(int));
     size_t k = 0;
     int rc = 0;
@@ -917,7 +938,42 @@ static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t*
             }
             for (size_t x = 0; x < nb; x++)
                 if (kcol1[x] < 0) kcol1[x] = 0;
-            rc = do_join(P, jp, need, sel1, kcol1, np == 0 && end == q->npreds);
+            /* vok[b] = c + 1 (b one of this join's bindings): every select of b reads column c, no
+             * later filter reads b, and the one remaining join touching the merged component is
+             * b's, on kcol1[b] -- so b's next join takes its key from the payload and nothing
+             * after it needs b's rowids: b may ride as column c's values */
+            for (size_t x = 0; x < nb; x++) vok[x] = 0;
+            {
+                const int ca = P->comp_of[jp->frel], cb2 = P->comp_of[jp->srel];
+                uint8_t* inm = (uint8_t*)calloc(nb, 1);
+                for (size_t x = 0; x < nb; x++)
+                    inm[x] = x == jp->frel || x == jp->srel || (P->comp_of[x] >= 0 && (P->comp_of[x] == ca || P->comp_of[x] == cb2));
+                int touching = 0;
+                const pred_t* only = NULL;
+                for (size_t i = 0; i < np + (q->npreds - end); i++) {
+                    const pred_t* r = i < np ? &q->preds[pending[i]] : &q->preds[end + (i - np)];
+                    if (r->type != 0) continue;
+                    if (inm[r->frel] || inm[r->srel]) {
+                        touching++;
+                        only = r;
+                    }
+                }
+                const size_t ends[2] = {jp->frel, jp->srel};
+                for (int t = 0; t < 2 && touching == 1; t++) {
+                    const size_t x = ends[t];
+                    const int on_x = (only->frel == x && (int)only->fcol + 1 == kcol1[x] && !inm[only->srel]) ||
+                                     (only->srel == x && (int)only->scol + 1 == kcol1[x] && !inm[only->frel]);
+                    if (!on_x || !kcol1[x]) continue;
+                    int c1 = 0;
+                    for (size_t s = 0; s < q->nsel; s++)
+                        if (q->sel[2 * s] == x) c1 = c1 == 0 || c1 == (int)q->sel[2 * s + 1] + 1 ? (int)q->sel[2 * s + 1] + 1 : -1;
+                    for (size_t i = end; i < q->npreds; i++)
+                        if (q->preds[i].type == 1 && q->preds[i].frel == x) c1 = -1;
+                    vok[x] = c1 > 0 ? c1 : 0;
+                }
+                free(inm);
+            }
+            rc = do_join(P, jp, need, sel1, kcol1, vok, np == 0 && end == q->npreds);
         }
         k = end;
     }
@@ -980,6 +1036,7 @@ static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t*
     free(need);
     free(sel1);
     free(kcol1);
+    free(vok);
     free(pending);
     return rc ? rc : P->rc;
 }

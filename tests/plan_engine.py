@@ -108,6 +108,7 @@ class NumpyPlanEngine:
             e.join_agg = self._agg_cb
         self.agg_calls = 0                       # last joins of two base relations in aggregate form
         self.keys_of_calls = 0                   # join keys that rode with their rows (no gather)
+        self.values_rows = 0                     # base sides whose rows rode as a column's values
         if key_carry:
             self._col_cb = COLUMN(self._wrap(self.cb_column, False))
             self._ko_cb = KEYS_OF(self._wrap(self.cb_keys_of, False))
@@ -247,8 +248,15 @@ class NumpyPlanEngine:
         ia, ib = join_local(self.get(ka), self.get(kb))
         if len(ia) > self.mat_limit:
             return -5
-        ra = self.get(va)[ia] if va else ia      # a's rowids (a whole column: positions are rowids)
-        oa[0] = self.put(ra)
+        vals = self.get(va) if va else None
+        if isinstance(vals, tuple):              # a whole column whose binding rides as another column's values
+            assert vals[0] == "column" and len(vals[1]) == len(self.get(ka))
+            ra = ia
+            oa[0] = self.put(vals[1][ia].astype(np.uint32))
+            self.values_rows += 1
+        else:
+            ra = vals[ia] if va else ia          # a's rowids (a whole column: positions are rowids)
+            oa[0] = self.put(ra)
         ob[0] = self.put(self.get(vb)[ib] if vb else ib)
         for k in range(nb):
             outb[k] = self.put(self.get(cb[k])[ib])

@@ -62,6 +62,7 @@ def test_every_golden_is_refused_or_exact(fixture, optional):
         assert eng.scan2_values > 0                        # C3's fused scan emits 3.2's values
         assert eng.agg_calls > 0                           # G1/G2: two base relations, aggregate form
         assert eng.keys_of_calls > 0                       # C3: R2's and R1's next join keys rode with them
+        assert eng.values_rows > 0                         # ... and their rows as their select column's values
 
 
 def test_check_names_the_reason():

@@ -22,15 +22,15 @@ from collections import defaultdict
 
 # demangled kernel name -> bench stage (first match wins)
 STAGES = [
-    (r"radix_pass_kernel<unsigned long, \d, \d, true, \d+, \d+, \d+, true, true\b", "sort_pass_carry"),
-    (r"tl_pass2_kernel<unsigned long, true\b", "sort_pass_carry"),
+    (r"radix_pass_kernel<unsigned long, \d, \d, true, \d+, \d+, \d+, true, [123]\b", "sort_pass_carry"),
+    (r"tl_pass2_kernel<unsigned long, [12]\b", "sort_pass_carry"),
     (r"radix_pass_kernel<unsigned long, \d, \d, true", "sort_pass_k64v32"),
     (r"radix_pass_kernel<unsigned int, \d, \d, true", "sort_pass_k32v32"),
     (r"radix_pass_kernel<unsigned long, \d, \d, false", "sort_pass_k64"),
     (r"radix_pass_kv_kernel<unsigned long", "sort_pass_k64v32"),
     (r"radix_pass_kv_kernel<unsigned int", "sort_pass_k32v32"),
-    (r"tl_pass2_kernel<unsigned long(, false\b[^>]*)?>", "sort_pass_k64v32"),
-    (r"tl_pass2_kernel<unsigned int(, false\b[^>]*)?>", "sort_pass_k32v32"),
+    (r"tl_pass2_kernel<unsigned long(, 0\b[^>]*)?>", "sort_pass_k64v32"),
+    (r"tl_pass2_kernel<unsigned int(, 0\b[^>]*)?>", "sort_pass_k32v32"),
     (r"digit_hist_kernel|digit_scan_kernel|tl_hist_kernel|tl_hist8_kernel|tl_hist_tiles_kernel|tl_gsum_kernel|tl_scan_kernel|tl_scan8_kernel", "sort_hist"),
     (r"cs_reduce_kernel|cs_top_kernel|cs_apply_kernel", "sort_scan"),
     (r"tl_local_kernel", "sort_local"),
@@ -47,6 +47,7 @@ STAGES = [
     (r"mj_fused", "mj_fused"),
     (r"mj_partition", "mj_partition"),
     (r"mj_tile<1>", "mj_write"),
+    (r"tl_gather_hist_kernel<true>|widen_u32_kernel", "widen_keys"),
     (r"gather_keys_kernel|tl_gather_hist_kernel", "gather_keys"),
     (r"expand_kernel<1>", "payload_expand"),
     (r"expand_kernel<0>|tile_scan_kernel", "payload_count"),
