@@ -68,6 +68,7 @@ struct DeferredSort {
     uint64_t* x = nullptr;        // carried payloads, in the words' order (qe_join_carry), or null
     uint32_t* x32 = nullptr;      // a 32-bit payload in the words' order (R's next join key), or null
     const uint64_t* v64 = nullptr;   // the words hold this column's low words, not row indices
+    bool w32 = false;             // the words are u32 key fields only (no rows: bucket_join_sums' R)
     uint64_t* kout = nullptr;
     uint32_t* vout = nullptr;
     int lo = 0, L = 0;            // field = (key >> lo) & fmask; bucket = field >> L
@@ -145,6 +146,8 @@ struct qe_ctx {
     const uint64_t* carry_c64 = nullptr;
     // ... and for a sort without vals: pack this u64 column's low words instead of the row index
     const uint64_t* sort_v64 = nullptr;
+    // ... or keep the key fields only (u32 words): the next deferred sort's rows are never read
+    bool sort_keys_only = false;
     std::vector<qe::PendingEvent> pending;
     std::vector<hipEvent_t> event_pool;
     std::vector<qe::KStat> kstats;

@@ -1653,7 +1653,9 @@ bool join_pairs_sums(qe_ctx* c, qe_pairs* R, qe_pairs* S, const uint32_t* xa, co
     if (!carry_eligible(R, S)) return false;
     const qe_pairs R0 = *R, S0 = *S;
     if ((R0.owns | S0.owns) & 7) return false;
+    c->sort_keys_only = !R->val;   // R's keys are only counted: its rows never travel
     sort_pairs(c, R, true);
+    c->sort_keys_only = false;
     c->carry_xa = xb ? xa : nullptr;   // (null: no payload; one column: 32-bit)
     c->carry_xb = xb;
     c->carry_x32 = xb ? nullptr : xa;

@@ -135,7 +135,7 @@ __global__ void __launch_bounds__(256) digit_scan_kernel(uint32_t* hist) {
 
 // input / output formats of a pass
 enum { IN_WORD = 0, IN_KV = 1, IN_KIOTA = 2, IN_KV64 = 3 };   // IN_KV64: `vin` is a u64 column, low 32 bits packed
-enum { OUT_WORD = 0, OUT_KV = 1 };
+enum { OUT_WORD = 0, OUT_KV = 1, OUT_W32 = 2 };   // OUT_W32: the word's field only, as u32 (no rowid)
 
 // word <-> (key, rowid).  PACK: word = ((key >> lo) & fmask) << 32 | rowid, key restored as
 // kconst | (field << lo).  !PACK: word = key (no rowid; key-only sorts of 64-bit words).
@@ -368,6 +368,8 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
             if constexpr (CARRY != X_NONE) pk[k] = p;
             if (OUT == OUT_WORD) {
                 QE_ST(&wout[p], wd);
+            } else if (OUT == OUT_W32) {
+                QE_ST(&reinterpret_cast<uint32_t*>(wout)[p], (uint32_t)(wd >> 32));
             } else if (PACK) {
                 kout[p] = (K)(f.kconst | ((wd >> 32) << f.lo));
                 vout[p] = (uint32_t)wd;
@@ -726,10 +728,15 @@ __global__ void __launch_bounds__(1024) tl_hist_tiles_kernel(const K* __restrict
             k[j] = i < n ? (uint64_t)keys[i] : 0;
         }
     };
-    uint64_t k[8];
+    // the next tile's keys are loaded while this tile is counted: one block per CU (the 128 KiB
+    // histogram) has nothing else to hide a load round trip behind
+    uint64_t k[8], kn[8];
     uint32_t t = g * TL_TPG + q, prev = 0, par = 0;
+    if (t < t_end) load(t, kn);
     for (; t < t_end; t += Q, par ^= 1u) {
-        load(t, k);
+#pragma unroll
+        for (int j = 0; j < 8; j++) k[j] = kn[j];
+        if (t + Q < t_end) load(t + Q, kn);
         if (t != g * TL_TPG + q && threadIdx.x < 256) {   // the previous tile's counts (its barrier passed)
             tcnt[(uint64_t)prev * 256 + threadIdx.x] = th[par ^ 1u][threadIdx.x];
             th[par ^ 1u][threadIdx.x] = 0;
@@ -943,7 +950,8 @@ constexpr int TL2_NT = QE_TL2_NT, TL2_ITEMS = QE_TL2_ITEMS, TL2_TILE = TL2_NT * 
 
 // CARRY: the payloads of pass 1 (xin, in pass-1 order; X64: 64-bit, X32: 32-bit) follow the words
 // to xout, staged in the words' LDS slots after the words have left (as in radix_pass_kernel).
-template <typename K, int CARRY = X_NONE, bool UNSTABLE = false>
+// W32: the words are u32 fields (a key-only first pass, OUT_W32): loaded into the high half, stored back as u32
+template <typename K, int CARRY = X_NONE, bool UNSTABLE = false, bool W32 = false>
 __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const uint64_t* __restrict__ win, uint64_t* __restrict__ wout,
                                                          uint64_t n, int dsh, const uint32_t* __restrict__ seg,
                                                          const uint32_t* __restrict__ off2, uint32_t G,
@@ -976,7 +984,10 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
         const uint64_t* src = win + base;
         const uint32_t o0 = (uint32_t)w * WT + l;
 #pragma unroll
-        for (int j = 0; j < TL2_ITEMS; j++) word[j] = src[std::min(o0 + (uint32_t)j * 64, m - 1)];
+        for (int j = 0; j < TL2_ITEMS; j++) {
+            if constexpr (W32) word[j] = (uint64_t)reinterpret_cast<const uint32_t*>(win)[base + std::min(o0 + (uint32_t)j * 64, m - 1)] << 32;
+            else word[j] = src[std::min(o0 + (uint32_t)j * 64, m - 1)];
+        }
         if (base == start) run = *runp;   // the digit offsets, behind the words (clamped: no branch)
         __syncthreads();   // whist zeroed
 #pragma unroll
@@ -1097,7 +1108,10 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
                 if (i < m) {
                     const uint64_t wd = stage[i];
                     const uint32_t p = gofs[(uint32_t)(wd >> dsh) & (BINS - 1)] + i;
-                    if ((uint64_t)p < n) QE_ST(&wout[p], wd);   // never false with consistent offsets
+                    if ((uint64_t)p < n) {   // never false with consistent offsets
+                        if constexpr (W32) QE_ST(&reinterpret_cast<uint32_t*>(wout)[p], (uint32_t)(wd >> 32));
+                        else QE_ST(&wout[p], wd);
+                    }
                 }
             }
         }
@@ -1838,6 +1852,10 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     const uint64_t* cv64 = dfr && !vals && (xm == XCOL || xm == X_NONE) ? c->sort_v64 : nullptr;
     c->sort_v64 = nullptr;
     const uint32_t* v64w = reinterpret_cast<const uint32_t*>(cv64);
+    // key-only words (the consumer counts this side's keys and never reads its rows: the last
+    // join's aggregate form): u32 fields through both passes, half the bytes
+    const bool w32 = dfr && !vals && xm == X_NONE && !cv64 && sort_unstable_on() && c->sort_keys_only;
+    c->sort_keys_only = false;
     const size_t xsz = xm == X64 ? 8 : 4;
     uint64_t* x1 = xm ? static_cast<uint64_t*>(dalloc(c, n * xsz)) : nullptr;
     uint64_t* x2 = xm ? static_cast<uint64_t*>(dalloc(c, n * xsz)) : nullptr;
@@ -1847,7 +1865,13 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     hipLaunchKernelGGL((radix_pass_kernel<K, IN, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, CR, UN>),            \
                        dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, \
                        255u, f, tcnt, nullptr, nullptr, 0u, XA, XB, XO)
-    if (cv64) {
+    if (w32) {
+        Timed t(c, name, ((double)sizeof(K) + 4.0) * n);
+        hipLaunchKernelGGL((radix_pass_kernel<K, IN_KIOTA, OUT_W32, true, 8, RTILE / PRE_NT, PRE_NT, true, X_NONE, true>),
+                           dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, nullptr, kout, w1, vout, n,
+                           32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr);
+        QE_HIP(hipGetLastError());
+    } else if (cv64) {
         Timed t(c, xm ? "sort_pass_carry" : name, ((double)sizeof(K) + 8.0 + (xm ? 8.0 : 0.0) + 8.0 + (xm ? 4.0 : 0.0)) * n);
         if (xm)
             hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV64, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, XCOL, true>),
@@ -1885,8 +1909,10 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     }
 #undef QE_P1
     {
-        Timed t(c, xm ? "sort_pass_carry" : prof_split() ? "sort_pass2" : name, (16.0 + 2.0 * (double)(xm ? xsz : 0)) * n);
-        auto kern = xm == X64 ? (uns ? tl_pass2_kernel<K, X64, true> : tl_pass2_kernel<K, X64, false>)
+        Timed t(c, xm ? "sort_pass_carry" : prof_split() ? "sort_pass2" : name,
+                (w32 ? 8.0 : 16.0 + 2.0 * (double)(xm ? xsz : 0)) * n);
+        auto kern = w32       ? tl_pass2_kernel<K, X_NONE, true, true>
+                    : xm == X64 ? (uns ? tl_pass2_kernel<K, X64, true> : tl_pass2_kernel<K, X64, false>)
                     : xm      ? tl_pass2_kernel<K, X32, true>   // (the X32 / XCOL first pass is unstable too)
                               : (uns ? tl_pass2_kernel<K, X_NONE, true> : tl_pass2_kernel<K, X_NONE, false>);
         hipLaunchKernelGGL(kern, dim3(xcd_grid(nseg)), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8, seg, gcnt, G,
@@ -1912,6 +1938,7 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
             d.d_max = d_max;
             d.x = xm == X64 ? x2 : nullptr;
             d.v64 = cv64;
+            d.w32 = w32;
             d.x32 = xm && xm != X64 ? reinterpret_cast<uint32_t*>(x2) : nullptr;
             d.kout = (uint64_t*)kout;
             d.vout = vout;
@@ -2370,6 +2397,7 @@ void pairs_need_keys(qe_ctx* c, const qe_pairs* p) {
     auto it = c->deferred.find(p->key);
     if (it == c->deferred.end()) return;
     const DeferredSort d = it->second;
+    if (d.w32) throw Error(QE_EINVAL, "internal: a key-only deferred sort has no rows to complete");
     c->deferred.erase(it);
     const Field f{d.lo, d.fmask, d.kconst};
     if (read_u64(c, d.d_max) > (uint64_t)TL_CAP) {
@@ -2486,6 +2514,7 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
     const DeferredSort& dS = iS->second;
     if (dR.lo != dS.lo || dR.L != dS.L || dR.fmask != dS.fmask || dR.kconst != dS.kconst || dR.L > HJ_DBITS)
         return false;   // different bucket geometry, or a bucket domain beyond LDS
+    if (dR.w32 || dS.w32) return false;   // key-only words: the aggregate form only
     const bool carry = outX0 != nullptr, rx = outRX != nullptr;
     if (carry && !dS.x && !dS.x32) return false;   // S's sort did not carry the payload
     const bool s32 = carry && !dS.x;                // ... or carried one 32-bit column (chain kernel only)
@@ -2612,7 +2641,7 @@ __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
 tl_hjoin_sums_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict__ bsR,
                      const uint64_t* __restrict__ wS, const uint32_t* __restrict__ bsS, int L,
                      const uint64_t* __restrict__ xS, HjSums sc, uint64_t* __restrict__ part,
-                     unsigned long long* __restrict__ flag, const uint32_t* __restrict__ xS32) {
+                     unsigned long long* __restrict__ flag, const uint32_t* __restrict__ xS32, int r32) {
     __shared__ uint32_t cnt[1 << HJ_DBITS];
     __shared__ uint64_t red[HJ_NW][HJ_SUMS + 1];
     const uint32_t b = blockIdx.x;
@@ -2627,7 +2656,7 @@ tl_hjoin_sums_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict
 #pragma unroll
     for (int j = 0; j < HJ_I; j++) {
         const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
-        wr[j] = i < mR ? wR[r0 + i] : 0;
+        wr[j] = i < mR ? (r32 ? (uint64_t)reinterpret_cast<const uint32_t*>(wR)[r0 + i] << 32 : wR[r0 + i]) : 0;
         ws[j] = i < mS ? wS[s0 + i] : 0;
         xv[j] = xS32 && i < mS ? (uint64_t)xS32[s0 + i] : xS && i < mS ? xS[s0 + i] : 0ull;
     }
@@ -2700,6 +2729,7 @@ bool bucket_join_sums(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const HjS
     bool carry = false;
     for (int s = 0; s < sc.n; s++) carry |= (sc.src[s] & 3) != 0;
     if (carry && !dS.x && !dS.x32) return false;   // S's sort did not carry the payload
+    if (dS.w32) return false;
     for (int s = 0; s < sc.n; s++)
         if (!dS.x && (sc.src[s] & 3) == 2) return false;   // (a 32-bit payload has no high half)
     uint64_t* part = dalloc_t<uint64_t>(c, (size_t)TL_BUCKETS * (HJ_SUMS + 1));
@@ -2709,7 +2739,8 @@ bool bucket_join_sums(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const HjS
         Timed t(c, "bucket_join_sums", 8.0 * (double)(R->n + S->n) + (carry ? 8.0 * (double)S->n : 0.0));
         hipLaunchKernelGGL(tl_hjoin_sums_kernel, dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream, dR.words, dR.bstart,
                            dS.words, dS.bstart, dR.L, carry ? dS.x : nullptr, sc, part,
-                           reinterpret_cast<unsigned long long*>(out + HJ_SUMS + 1), carry ? dS.x32 : nullptr);
+                           reinterpret_cast<unsigned long long*>(out + HJ_SUMS + 1), carry ? dS.x32 : nullptr,
+                           dR.w32 ? 1 : 0);
         QE_HIP(hipGetLastError());
         hipLaunchKernelGGL(hjoin_sums_reduce_kernel, dim3(HJ_SUMS + 1), dim3(256), 0, c->stream, part,
                            (uint32_t)TL_BUCKETS, out);
