@@ -728,15 +728,10 @@ __global__ void __launch_bounds__(1024) tl_hist_tiles_kernel(const K* __restrict
             k[j] = i < n ? (uint64_t)keys[i] : 0;
         }
     };
-    // the next tile's keys are loaded while this tile is counted: one block per CU (the 128 KiB
-    // histogram) has nothing else to hide a load round trip behind
-    uint64_t k[8], kn[8];
+    uint64_t k[8];
     uint32_t t = g * TL_TPG + q, prev = 0, par = 0;
-    if (t < t_end) load(t, kn);
     for (; t < t_end; t += Q, par ^= 1u) {
-#pragma unroll
-        for (int j = 0; j < 8; j++) k[j] = kn[j];
-        if (t + Q < t_end) load(t + Q, kn);
+        load(t, k);
         if (t != g * TL_TPG + q && threadIdx.x < 256) {   // the previous tile's counts (its barrier passed)
             tcnt[(uint64_t)prev * 256 + threadIdx.x] = th[par ^ 1u][threadIdx.x];
             th[par ^ 1u][threadIdx.x] = 0;
