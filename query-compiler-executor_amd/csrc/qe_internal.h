@@ -32,6 +32,9 @@ struct Relation {
     bool owned = true;                 // false: another ctx's columns, shared (qe_workers)
     std::vector<uint64_t*> cols;
     std::vector<uint64_t> kor, kand;   // column statistics: OR / AND of all values (at load)
+    // the same columns as u32 where every value fits (the OR below 2^32), else null: what the
+    // sorts' first passes and histograms read -- half the bytes of the u64 column
+    std::vector<uint32_t*> cols32;
 };
 
 struct PendingEvent {
@@ -156,6 +159,16 @@ struct qe_ctx {
 
 namespace qe {
 
+// the u32 copy of a loaded relation's column (by its u64 pointer and length), or null
+inline const uint32_t* narrow_of(const qe_ctx* c, const void* col, uint64_t n) {
+    if (!col) return nullptr;
+    for (const auto& r : c->rels)
+        if (r.rows == n)
+            for (size_t j = 0; j < r.cols.size() && j < r.cols32.size(); j++)
+                if (r.cols[j] == col) return r.cols32[j];
+    return nullptr;
+}
+
 void* dalloc(qe_ctx* c, size_t bytes);
 void dfree(qe_ctx* c, void* p);
 template <class T>
@@ -232,7 +245,7 @@ void pairs_drop_deferred(qe_ctx* c, const qe_pairs* p);   // (also drops a gathe
 // keys = col[rows] for a list whose sort will be the lookback-free two-level one: the sort's
 // histogram is built in the same pass (false: not that sort -- the caller gathers plainly)
 bool gather_with_hist(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint64_t n, uint64_t kor, uint64_t kand,
-                      uint64_t* keys);
+                      uint64_t* keys, uint64_t col_rows = 0);   // col_rows: the column's length (its u32 copy)
 bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS,
                  qe_list* outX0 = nullptr, qe_list* outX1 = nullptr, qe_list* outRX = nullptr);
 // the payload carry of join_pairs_carry applies: both sides' sorts will be deferred two-level

@@ -1541,7 +1541,7 @@ int qe_gather_pairs(qe_ctx* c, qe_col col, const qe_list* rows, qe_pairs* out) {
         for (size_t j = 0; j < r.cols.size(); j++)
             if (r.cols[j] == col.d && r.rows == col.n && j < r.kor.size() && !getenv("QE_GATHER_EXACT_BITS")) {
                 if (n && !(getenv("QE_GATHER_HIST") && getenv("QE_GATHER_HIST")[0] == '0') &&
-                    gather_with_hist(c, col.d, rows->d, n, r.kor[j], r.kand[j], out->key)) {
+                    gather_with_hist(c, col.d, rows->d, n, r.kor[j], r.kand[j], out->key, col.n)) {
                     // gathered together with the histogram its sort will read
                 } else if (n) {
                     Timed t(c, "gather_keys", 12.0 * n + 8.0 * n);

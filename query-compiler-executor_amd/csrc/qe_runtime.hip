@@ -363,8 +363,25 @@ __global__ void __launch_bounds__(256) gen_zipf_kernel(uint64_t* __restrict__ ou
 
 using namespace qe;
 
+namespace qe {
+__global__ void __launch_bounds__(256) narrow_kernel(const uint64_t* __restrict__ in, uint64_t n,
+                                                     uint32_t* __restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) out[i] = (uint32_t)in[i];
+}
+}  // namespace qe
+
+static void free_relation(Relation& r) {
+    if (!r.owned) return;
+    for (auto* p : r.cols) (void)hipFree(p);
+    for (auto* p : r.cols32)
+        if (p) (void)hipFree(p);
+}
+
 // column statistics: OR / AND of every column, one read at load time (zone-map style metadata
-// that lets the radix sort plan its passes without a reduction pass per query)
+// that lets the radix sort plan its passes without a reduction pass per query); and a u32 copy of
+// every column whose values fit 32 bits -- the relation's second layout in HBM, the one the
+// sorts' first passes read (QE_NARROW=0: none)
 static void column_stats(qe_ctx* c, Relation& r) {
     r.kor.resize(r.cols.size());
     r.kand.resize(r.cols.size());
@@ -373,6 +390,25 @@ static void column_stats(qe_ctx* c, Relation& r) {
         key_bits_u64(c, r.cols[j], r.rows, b);
         r.kor[j] = b[0];
         r.kand[j] = b[1];
+    }
+    const char* e = getenv("QE_NARROW");
+    r.cols32.assign(r.cols.size(), nullptr);
+    if (e && e[0] == '0') return;
+    try {
+        for (size_t j = 0; j < r.cols.size(); j++) {
+            if ((r.kor[j] >> 32) || !r.rows) continue;
+            uint32_t* d = nullptr;
+            QE_HIP(hipMalloc(&d, r.rows * sizeof(uint32_t)));
+            r.cols32[j] = d;
+            hipLaunchKernelGGL(narrow_kernel, dim3(grid_for(r.rows, 256 * 8, 16384)), dim3(256), 0, c->stream,
+                               r.cols[j], r.rows, d);
+            QE_HIP(hipGetLastError());
+        }
+        QE_HIP(hipStreamSynchronize(c->stream));
+    } catch (...) {   // (the caller's guard frees the u64 columns)
+        for (auto*& p : r.cols32)
+            if (p) (void)hipFree(p), p = nullptr;
+        throw;
     }
 }
 
@@ -450,9 +486,7 @@ void qe_fini(qe_ctx* c) {
     c->workers.clear();
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    for (auto& r : c->rels)
-        if (r.owned)
-            for (auto* p : r.cols) (void)hipFree(p);
+    for (auto& r : c->rels) free_relation(r);
     for (auto& kv : c->free_blocks) (void)hipFree(kv.second);
     for (auto& kv : c->live) (void)hipFree(kv.first);
     for (auto& p : c->pending) {
@@ -665,9 +699,7 @@ int qe_drop_relations(qe_ctx* c) {
         w->rels.clear();
     }
     sync(c);
-    for (auto& r : c->rels)
-        if (r.owned)
-            for (auto* p : r.cols) QE_HIP(hipFree(p));
+    for (auto& r : c->rels) free_relation(r);
     c->rels.clear();
     return 0;
     QE_API_END(c)

@@ -720,12 +720,30 @@ __global__ void __launch_bounds__(1024) tl_hist_tiles_kernel(const K* __restrict
     __syncthreads();
     const uint32_t g = blockIdx.x / Q, q = blockIdx.x % Q;   // Q blocks share group g's tiles
     const uint32_t t_end = (g + 1) * TL_TPG < nt ? (g + 1) * TL_TPG : nt;
+    // (a tile's counts do not depend on which thread counts which key: u32 keys are loaded two per
+    // 8-B load, so a wave instruction still moves 512 contiguous bytes)
+    uint32_t vm = 0;   // valid keys of this thread
     auto load = [&](uint32_t t, uint64_t (&k)[8]) {
         const uint64_t base = (uint64_t)t * RTILE;
+        vm = 0;
+        if (sizeof(K) == 4 && !(reinterpret_cast<uintptr_t>(keys) & 7)) {
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const uint64_t i = base + (uint64_t)j * 1024 + threadIdx.x;
-            k[j] = i < n ? (uint64_t)keys[i] : 0;
+            for (int j = 0; j < 4; j++) {
+                const uint64_t e = base + 2 * ((uint64_t)j * 1024 + threadIdx.x);
+                uint2 v = make_uint2(0u, 0u);
+                if (e + 1 < n) v = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint32_t*>(keys) + e);
+                else if (e < n) v.x = (uint32_t)keys[e];
+                k[2 * j] = v.x;
+                k[2 * j + 1] = v.y;
+                vm |= (e < n ? 1u : 0u) << (2 * j) | (e + 1 < n ? 1u : 0u) << (2 * j + 1);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint64_t i = base + (uint64_t)j * 1024 + threadIdx.x;
+                k[j] = i < n ? (uint64_t)keys[i] : 0;
+                vm |= (i < n ? 1u : 0u) << j;
+            }
         }
     };
     uint64_t k[8];
@@ -736,11 +754,9 @@ __global__ void __launch_bounds__(1024) tl_hist_tiles_kernel(const K* __restrict
             tcnt[(uint64_t)prev * 256 + threadIdx.x] = th[par ^ 1u][threadIdx.x];
             th[par ^ 1u][threadIdx.x] = 0;
         }
-        const uint64_t base = (uint64_t)t * RTILE;
 #pragma unroll
         for (int j = 0; j < 8; j++) {
-            const uint64_t i = base + (uint64_t)j * 1024 + threadIdx.x;
-            if (i < n) {
+            if ((vm >> j) & 1u) {
                 const uint32_t b = (uint32_t)((((k[j] >> f.lo) & f.fmask) >> L) & (TL_BUCKETS - 1));
                 atomicAdd(&h[((b & 255u) << 7) | (b >> 8)], 1u);
                 atomicAdd(&th[par][b & 255u], 1u);
@@ -757,13 +773,15 @@ __global__ void __launch_bounds__(1024) tl_hist_tiles_kernel(const K* __restrict
 
 // tl_hist_tiles_kernel fused into the gather that produces the keys: keys = col[rows] in list
 // order, and the same per-tile / per-segment counts (one pass instead of a gather + a re-read).
-// DIRECT: keys = rows[i] widened -- a list of carried key values (no gather)
+// DIRECT: keys = rows[i] widened -- a list of carried key values (no gather).  col32: the column's
+// u32 copy (Relation::cols32), read instead when given
 template <bool DIRECT = false>
 __global__ void __launch_bounds__(1024) tl_gather_hist_kernel(const uint64_t* __restrict__ col,
                                                               const uint32_t* __restrict__ rows, uint64_t n,
                                                               uint64_t* __restrict__ keys, Field f, int L, uint32_t nt,
                                                               uint32_t G, uint32_t Q, uint32_t* __restrict__ tcnt,
-                                                              uint32_t* __restrict__ gcnt) {
+                                                              uint32_t* __restrict__ gcnt,
+                                                              const uint32_t* __restrict__ col32 = nullptr) {
     __shared__ uint32_t h[TL_BUCKETS];
     __shared__ uint32_t th[2][256];
     for (int i = threadIdx.x; i < TL_BUCKETS; i += 1024) h[i] = 0;
@@ -793,7 +811,7 @@ __global__ void __launch_bounds__(1024) tl_gather_hist_kernel(const uint64_t* __
 #pragma unroll
         for (int j = 0; j < 8; j++) {   // 8 random gathers in flight per thread
             const uint64_t i = base + (uint64_t)j * 1024 + threadIdx.x;
-            k[j] = i < n ? (DIRECT ? (uint64_t)r[j] : col[r[j]]) : 0;
+            k[j] = i < n ? (DIRECT ? (uint64_t)r[j] : col32 ? (uint64_t)col32[r[j]] : col[r[j]]) : 0;
         }
         if (t + Q < t_end) load_rows(t + Q);
         if (t != g * TL_TPG + q && threadIdx.x < 256) {
@@ -1802,6 +1820,13 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
         dfree(c, bstart);
         dfree(c, seg);
     };
+    // a base column with a u32 copy (Relation::cols32): the histogram and the first pass read that
+    // -- along with the u32 copies of its payload / value columns -- when every one of them has one
+    const uint32_t* kn = dfr && !vals && sizeof(K) == 8 ? narrow_of(c, keys, n) : nullptr;
+    if (kn) {
+        if (c->carry_xa || (c->carry_c64 && !narrow_of(c, c->carry_c64, n)) || (c->sort_v64 && !narrow_of(c, c->sort_v64, n)))
+            kn = nullptr;
+    }
     auto ph = c->prehist.find(keys);   // counted while the keys were gathered?
     const bool have = ph != c->prehist.end() && ph->second.lo == f.lo && ph->second.L == L &&
                       ph->second.fmask == f.fmask;
@@ -1815,8 +1840,11 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
         QE_HIP(hipMemsetAsync(gcnt, 0, (size_t)nseg * 128 * sizeof(uint32_t), c->stream));
     }
     {
-        Timed t(c, "sort_hist", have ? 0.0 : (double)sizeof(K) * n);
-        if (!have)
+        Timed t(c, "sort_hist", have ? 0.0 : (kn ? 4.0 : (double)sizeof(K)) * n);
+        if (!have && kn)
+            hipLaunchKernelGGL((tl_hist_tiles_kernel<uint32_t>), dim3(G * Q), dim3(1024), 0, c->stream, kn, n, f, L, nt,
+                               G, Q, tcnt, gcnt);
+        else if (!have)
             hipLaunchKernelGGL((tl_hist_tiles_kernel<K>), dim3(G * Q), dim3(1024), 0, c->stream, keys, n, f, L, nt, G,
                                Q, tcnt, gcnt);
         QE_HIP(hipGetLastError());
@@ -1860,7 +1888,26 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     hipLaunchKernelGGL((radix_pass_kernel<K, IN, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, CR, UN>),            \
                        dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, \
                        255u, f, tcnt, nullptr, nullptr, 0u, XA, XB, XO)
-    if (w32) {
+#define QE_P1N(IN, CR, VIN, XA)                                                                                         \
+    hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, CR, true>),      \
+                       dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, kn, nullptr, VIN, nullptr, w1, vout, n, 32 + L,     \
+                       255u, f, tcnt, nullptr, nullptr, 0u, XA, nullptr, x1)
+    if (kn && uns) {
+        // u32 key (+ u32 value) (+ u32 payload) in, word (+ payload) out
+        const uint32_t* vt = cv64 ? narrow_of(c, cv64, n) : nullptr;
+        const uint32_t* xt = xm == XCOL ? narrow_of(c, reinterpret_cast<const uint64_t*>(cxa), n) : xm == X32 ? cxa : nullptr;
+        Timed t(c, xm ? "sort_pass_carry" : name, (4.0 + (vt ? 4.0 : 0.0) + (xt ? 4.0 : 0.0) + (w32 ? 4.0 : 8.0) +
+                                                   (xt ? 4.0 : 0.0)) * n);
+        if (w32)
+            hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN_KIOTA, OUT_W32, true, 8, RTILE / PRE_NT, PRE_NT, true, X_NONE, true>),
+                               dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, kn, nullptr, nullptr, nullptr, w1, vout, n,
+                               32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr);
+        else if (vt && xt) QE_P1N(IN_KV, X32, vt, xt);
+        else if (vt) QE_P1N(IN_KV, X_NONE, vt, nullptr);
+        else if (xt) QE_P1N(IN_KIOTA, X32, nullptr, xt);
+        else QE_P1N(IN_KIOTA, X_NONE, nullptr, nullptr);
+        QE_HIP(hipGetLastError());
+    } else if (w32) {
         Timed t(c, name, ((double)sizeof(K) + 4.0) * n);
         hipLaunchKernelGGL((radix_pass_kernel<K, IN_KIOTA, OUT_W32, true, 8, RTILE / PRE_NT, PRE_NT, true, X_NONE, true>),
                            dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, nullptr, kout, w1, vout, n,
@@ -1903,6 +1950,7 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
         QE_HIP(hipGetLastError());
     }
 #undef QE_P1
+#undef QE_P1N
     {
         Timed t(c, xm ? "sort_pass_carry" : prof_split() ? "sort_pass2" : name,
                 (w32 ? 8.0 : 16.0 + 2.0 * (double)(xm ? xsz : 0)) * n);
@@ -2423,7 +2471,7 @@ void pairs_drop_deferred(qe_ctx* c, const qe_pairs* p) {
 }
 
 static bool gather_hist_impl(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint64_t n, uint64_t kor,
-                             uint64_t kand, uint64_t* keys) {
+                             uint64_t kand, uint64_t* keys, const uint32_t* col32 = nullptr) {
     // exactly the plan radix_sort_impl will choose for these keys and bounds: the packed
     // two-level sort in its lookback-free form
     if (n < 2 || n >= 0xFFFFFFFFull) return false;
@@ -2445,9 +2493,9 @@ static bool gather_hist_impl(qe_ctx* c, const uint64_t* col, const uint32_t* row
     uint32_t* gcnt = dalloc_t<uint32_t>(c, (size_t)nseg * 128);
     QE_HIP(hipMemsetAsync(gcnt, 0, (size_t)nseg * 128 * sizeof(uint32_t), c->stream));
     if (col) {
-        Timed t(c, "gather_keys", 12.0 * n + 8.0 * n);
+        Timed t(c, "gather_keys", (col32 ? 8.0 : 12.0) * n + 8.0 * n);
         hipLaunchKernelGGL(tl_gather_hist_kernel<false>, dim3(G * Q), dim3(1024), 0, c->stream, col, rows, n, keys, f, L,
-                           nt, G, Q, tcnt, gcnt);
+                           nt, G, Q, tcnt, gcnt, col32);
         QE_HIP(hipGetLastError());
     } else {
         Timed t(c, "widen_keys", 12.0 * n);
@@ -2466,8 +2514,8 @@ static bool gather_hist_impl(qe_ctx* c, const uint64_t* col, const uint32_t* row
 }
 
 bool gather_with_hist(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint64_t n, uint64_t kor, uint64_t kand,
-                      uint64_t* keys) {
-    return gather_hist_impl(c, col, rows, n, kor, kand, keys);
+                      uint64_t* keys, uint64_t col_rows) {
+    return gather_hist_impl(c, col, rows, n, kor, kand, keys, narrow_of(c, col, col_rows));
 }
 
 bool widen_with_hist(qe_ctx* c, const uint32_t* vals, uint64_t n, uint64_t kor, uint64_t kand, uint64_t* keys) {
