@@ -2392,10 +2392,17 @@ void partition_words_kv(qe_ctx* c, const uint64_t* keys, const uint64_t* v64, co
     uint32_t* bstart = dalloc_t<uint32_t>(c, TL_BUCKETS + 1);
     uint32_t* seg = dalloc_t<uint32_t>(c, (size_t)nseg + 1);
     QE_HIP(hipMemsetAsync(gcnt, 0, (size_t)nseg * 128 * sizeof(uint32_t), c->stream));
+    // base columns with u32 copies (Relation::cols32): the histogram and the first pass read those
+    const uint32_t* kn = narrow_of(c, keys, n);
+    const uint32_t* vn = v64 ? narrow_of(c, v64, n) : nullptr;
     {
-        Timed t(c, "sort_hist", 8.0 * n);
-        hipLaunchKernelGGL((tl_hist_tiles_kernel<uint64_t>), dim3(G * Q), dim3(1024), 0, c->stream, keys, n, f, L, nt, G, Q,
-                           tcnt, gcnt);
+        Timed t(c, "sort_hist", (kn ? 4.0 : 8.0) * n);
+        if (kn)
+            hipLaunchKernelGGL((tl_hist_tiles_kernel<uint32_t>), dim3(G * Q), dim3(1024), 0, c->stream, kn, n, f, L, nt,
+                               G, Q, tcnt, gcnt);
+        else
+            hipLaunchKernelGGL((tl_hist_tiles_kernel<uint64_t>), dim3(G * Q), dim3(1024), 0, c->stream, keys, n, f, L, nt,
+                               G, Q, tcnt, gcnt);
         QE_HIP(hipGetLastError());
         hipLaunchKernelGGL(tl_gsum_kernel, dim3(256), dim3(128), 0, c->stream, gcnt, G, hist);
         QE_HIP(hipGetLastError());
@@ -2409,14 +2416,16 @@ void partition_words_kv(qe_ctx* c, const uint64_t* keys, const uint64_t* v64, co
     uint64_t* w1 = dalloc_t<uint64_t>(c, n);
     uint64_t* w2 = dalloc_t<uint64_t>(c, n);
     {
-        Timed t(c, "sort_pass_agg", (8.0 + (v64 ? 8.0 : v32 ? 4.0 : 0.0) + 8.0) * n);
-#define QE_PW1(IN, V)                                                                                                   \
-    hipLaunchKernelGGL((radix_pass_kernel<uint64_t, IN, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, false, true>), \
-                       dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, V, nullptr, w1, nullptr, n,       \
+        Timed t(c, "sort_pass_agg", ((kn ? 4.0 : 8.0) + (vn ? 4.0 : v64 ? 8.0 : v32 ? 4.0 : 0.0) + 8.0) * n);
+#define QE_PW1(KT, KP, IN, V)                                                                                            \
+    hipLaunchKernelGGL((radix_pass_kernel<KT, IN, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, X_NONE, true>),        \
+                       dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, KP, nullptr, V, nullptr, w1, nullptr, n,         \
                        32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr)
-        if (v64) QE_PW1(IN_KV64, reinterpret_cast<const uint32_t*>(v64));
-        else if (v32) QE_PW1(IN_KV, v32);
-        else QE_PW1(IN_KIOTA, nullptr);
+        if (kn && (vn || v32)) QE_PW1(uint32_t, kn, IN_KV, vn ? vn : v32);
+        else if (kn && !v64) QE_PW1(uint32_t, kn, IN_KIOTA, nullptr);
+        else if (v64) QE_PW1(uint64_t, keys, IN_KV64, reinterpret_cast<const uint32_t*>(v64));
+        else if (v32) QE_PW1(uint64_t, keys, IN_KV, v32);
+        else QE_PW1(uint64_t, keys, IN_KIOTA, nullptr);
 #undef QE_PW1
         QE_HIP(hipGetLastError());
     }
