@@ -24,6 +24,9 @@ from collections import defaultdict
 STAGES = [
     (r"radix_pass_kernel<unsigned long, \d, \d, true, \d+, \d+, \d+, true, [123]\b", "sort_pass_carry"),
     (r"tl_pass2_kernel<unsigned long, [12]\b", "sort_pass_carry"),
+    # a 64-bit key sort's first pass reading the base column's u32 copy (unstable: deferred sorts only)
+    (r"radix_pass_kernel<unsigned int, \d, \d, true, \d+, \d+, \d+, true, [123], true>", "sort_pass_carry"),
+    (r"radix_pass_kernel<unsigned int, \d, \d, true, \d+, \d+, \d+, true, 0, true>", "sort_pass_k64v32"),
     (r"radix_pass_kernel<unsigned long, \d, \d, true", "sort_pass_k64v32"),
     (r"radix_pass_kernel<unsigned int, \d, \d, true", "sort_pass_k32v32"),
     (r"radix_pass_kernel<unsigned long, \d, \d, false", "sort_pass_k64"),
