@@ -89,6 +89,7 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
     ctx.set_profiling(os.environ.get("QE_BENCH_EVENTS", "1") != "0")
     ctx.reset_stats()
     torch.cuda.synchronize()
+    hits0, builds0 = ctx.sort_cache_stats()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out, rc = run_batch()
@@ -97,6 +98,7 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
     dt = time.perf_counter() - t0
     stats = ctx.kernel_stats()
     ctx.set_profiling(False)
+    hits1, builds1 = ctx.sort_cache_stats()
     kern = sorted(stats.items(), key=lambda kv: -kv[1]["ms"])
 
     def timed(fn):
@@ -106,7 +108,15 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
         ctx.sync()
         d = time.perf_counter() - t1
         return {"ms_per_step": round(d * 1e3, 3), "value": round(len(queries) / d, 2), "stdout_identical": o == out}
-    others = {"sequential_faithful (qe_run_queries)": timed(lambda: ctx.run(text)[0]),
+    def no_cache(fn):   # the same lanes without the batch's shared base-column sorts
+        os.environ["QE_SORT_CACHE"] = "0"
+        try:
+            return fn()
+        finally:
+            del os.environ["QE_SORT_CACHE"]
+    others = {"plan_lanes_without_sort_cache (QE_SORT_CACHE=0)":
+                  no_cache(lambda: timed(lambda: ctx.run_lanes(text, workers, plan=plan)[0])),
+              "sequential_faithful (qe_run_queries)": timed(lambda: ctx.run(text)[0]),
               "partitioned_plan_one_lane (qe_run_queries_dist)": timed(lambda: ctx.run_dist(text)[0]),
               "faithful_lanes (qe_run_queries_parallel, %d lanes)" % workers:
                   timed(lambda: ctx.run_lanes(text, workers, plan=False)[0])}
@@ -125,6 +135,10 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
                                % ("the partitioned plan per query, faithful fallback" if plan
                                   else "the faithful executor", workers),
                    "parallelism": "single GPU, inter-query concurrency x%d" % workers},
+        "sort_cache": {"base_column_sorts_reused_per_step": (hits1 - hits0) / args.steps,
+                       "built_per_step": (builds1 - builds0) / args.steps,
+                       "scope": "one batch (qe_sort_cache brackets each qe_run_queries_lanes call): every step "
+                                "sorts each base column it joins at least once"},
         "other_executors_same_batch": others,
         "roofline": roofline_fn(stats, traffic_fn() if traffic_fn else None) if roofline_fn else None,
         "stages_lane0": {k: {"ms_per_step": round(s["ms"] / args.steps, 3), "launches_per_step": s["launches"] / args.steps}

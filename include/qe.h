@@ -137,6 +137,14 @@ int  qe_run_queries_parallel(qe_ctx*, int workers, const char* text, char** out,
 #define QE_EXEC_FAITHFUL 0
 #define QE_EXEC_PLAN 1
 int  qe_run_queries_lanes(qe_ctx*, int workers, int executor, const char* text, char** out, size_t* outlen);
+/* A batch's shared sorts of whole base columns (no reference counterpart: the reference sorts a
+ * base relation again for every join, src/join.c:122-142 + :5-94).  on = 1: from now on the first
+ * join of a column sorts it once, on whichever lane or ctx of this ctx's family needs it first, and
+ * every later join on that column reads that sort (payload-carrying sorts excepted); on = 0: waits
+ * for every stream of the family and frees them.  qe_run_queries_lanes brackets its batch with
+ * it; QE_SORT_CACHE=0 turns it off.  Stats: cached sorts reused / built over finished batches. */
+int  qe_sort_cache(qe_ctx*, int on);
+int  qe_sort_cache_stats(qe_ctx*, uint64_t* hits, uint64_t* builds);
 /* The worker contexts behind qe_run_queries_parallel (made on first use, freed by qe_fini; the
  * relations re-shared at every call); qe_bind_thread makes the ctx's GPU the calling thread's. */
 int  qe_workers(qe_ctx*, int n, qe_ctx** out);

@@ -77,10 +77,15 @@ struct DeferredSort {
     int lo = 0, L = 0;            // field = (key >> lo) & fmask; bucket = field >> L
     uint64_t fmask = 0, kconst = 0;
     int lr_n = 0, lr_bits[4] = {0, 0, 0, 0};
+    bool shared = false;          // words / bstart / d_max belong to a batch's SortCache (not freed by drop)
 };
 
 // The two-level sort's histogram, computed while the keys were gathered (gather_with_hist): the
 // sort of those keys skips its histogram read.  Kept by the pairs' key buffer.
+// A batch's shared sorts of whole base columns (qe_sort_cache, qe_join.hip): one per (column,
+// form), built by the first lane that needs it, read by every later join of the batch.
+struct SortCache;
+
 struct PreHist {
     uint32_t* tcnt = nullptr;   // per first-pass tile digit counts
     uint32_t* gcnt = nullptr;   // per (digit, group) segment digit counts
@@ -137,6 +142,9 @@ struct qe_ctx {
     // worker contexts on the same device (qe_workers): their own stream and allocator, this ctx's
     // relations shared -- the concurrent batch executor's lanes
     std::vector<qe_ctx*> workers;
+    // the batch's shared base-column sorts (qe_sort_cache; null: off), this ctx's and its workers'
+    qe::SortCache* scache = nullptr;
+    uint64_t scache_hits = 0, scache_builds = 0;   // over this ctx's finished batches
 
     // profiling
     bool prof = false;

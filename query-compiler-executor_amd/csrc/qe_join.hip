@@ -18,7 +18,11 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 #include "qe_device.h"
 #include "qe_internal.h"
@@ -1574,7 +1578,7 @@ int qe_gather_pairs(qe_ctx* c, qe_col col, const qe_list* rows, qe_pairs* out) {
 
 // qe_sort_pairs' body; defer: a large two-level sort may stop before its per-bucket step
 // (qe_join_pairs hands such sides to bucket_join)
-static void sort_pairs(qe_ctx* c, qe_pairs* p, bool defer) {
+static void sort_pairs_raw(qe_ctx* c, qe_pairs* p, bool defer) {
     if (p->flags & PF_SORTED) return;
     p->flags &= ~QE_PAIRS_MATCHED;
     uint64_t bits[2] = {p->kor, p->kand};
@@ -1591,6 +1595,167 @@ static void sort_pairs(qe_ctx* c, qe_pairs* p, bool defer) {
         p->owns |= 2;
     }
     p->flags |= PF_SORTED;
+}
+
+// ---- a batch's shared sorts of whole base columns (qe_sort_cache) -----------------------------
+// Within one batch many queries join the same base relation on the same column (the C4 batch:
+// 1292 base join sides over 46 distinct columns).  The sort of a whole column -- (key, row) pairs,
+// rows implicit -- depends on the column alone, so the first lane that needs it sorts it on its
+// own stream and publishes the result with an event; every later join of the batch on that column
+// waits on the event and reads the same buffers.  A deferred two-level sort is shared as its
+// bucket-partitioned words (each reader gets its own, unfilled, key / row buffers for a possible
+// completion: the words are only read); a complete sort as its key and row arrays, lent to the
+// pairs (not owned).  Sorts that carry payloads or pack values are query-specific and never cached.
+// Scope: one qe_sort_cache(ctx, 1) .. qe_sort_cache(ctx, 0) bracket (a batch): nothing outlives it.
+namespace qe {
+struct SortCacheEntry {
+    bool ready = false, deferred = false;
+    DeferredSort d{};                       // deferred: the shared words / bstart / d_max
+    uint64_t* keys = nullptr;               // complete: the sorted keys and rows
+    uint32_t* vals = nullptr;
+    bool own_keys = false, own_vals = false;
+    hipEvent_t ev = nullptr;                // recorded on the builder's stream after the sort
+    qe_ctx* owner = nullptr;                // the builder (its allocator frees the buffers)
+};
+struct SortCache {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::map<std::tuple<const void*, uint64_t, int>, SortCacheEntry> m;
+    uint64_t hits = 0, builds = 0;
+};
+}  // namespace qe
+
+static bool is_base_column(const qe_ctx* c, const void* key, uint64_t n) {
+    for (const auto& r : c->rels)
+        if (r.rows == n)
+            for (const uint64_t* col : r.cols)
+                if (col == key) return true;
+    return false;
+}
+
+// true: p is sorted from (or into) the batch's cache
+static bool sort_cached(qe_ctx* c, qe_pairs* p, bool defer) {
+    SortCache* sc = c->scache;
+    if (!sc || p->val || (p->owns & 3) || !p->key || p->n < 2) return false;
+    if (c->carry_xa || c->carry_xb || c->carry_x32 || c->carry_c64 || c->sort_v64) return false;
+    if (!is_base_column(c, p->key, p->n)) return false;
+    const int mode = defer ? (c->sort_keys_only ? 2 : 1) : 0;
+    const auto key = std::make_tuple((const void*)p->key, p->n, mode);
+    std::unique_lock<std::mutex> lk(sc->mu);
+    auto it = sc->m.find(key);
+    if (it == sc->m.end()) {   // this lane builds it
+        SortCacheEntry& slot = sc->m[key];
+        slot.owner = c;
+        lk.unlock();
+        try {
+            sort_pairs_raw(c, p, defer);
+        } catch (...) {
+            lk.lock();
+            sc->m.erase(key);
+            sc->cv.notify_all();
+            throw;
+        }
+        SortCacheEntry e;
+        e.owner = c;
+        auto dit = c->deferred.find(p->key);
+        if (dit != c->deferred.end()) {
+            dit->second.shared = true;   // this pairs' own key / row buffers stay its own
+            e.deferred = true;
+            e.d = dit->second;
+        } else {
+            e.keys = p->key;
+            e.vals = p->val;
+            e.own_keys = (p->owns & 1) != 0;
+            e.own_vals = (p->owns & 2) != 0;
+            p->owns &= ~3u;                  // lent by the cache from now on
+        }
+        QE_HIP(hipEventCreateWithFlags(&e.ev, hipEventDisableTiming));
+        QE_HIP(hipEventRecord(e.ev, c->stream));
+        e.ready = true;
+        lk.lock();
+        sc->m[key] = e;
+        sc->builds++;
+        sc->cv.notify_all();
+        return true;
+    }
+    sc->cv.wait(lk, [&] {
+        auto j = sc->m.find(key);
+        return j == sc->m.end() || j->second.ready;
+    });
+    it = sc->m.find(key);
+    if (it == sc->m.end()) return false;   // its build failed: sort privately
+    const SortCacheEntry e = it->second;
+    sc->hits++;
+    lk.unlock();
+    if (e.owner != c) QE_HIP(hipStreamWaitEvent(c->stream, e.ev, 0));
+    c->sort_keys_only = false;   // (what the sort would have consumed)
+    p->flags &= ~QE_PAIRS_MATCHED;
+    if (e.deferred) {
+        DeferredSort d = e.d;
+        d.kout = dalloc_t<uint64_t>(c, p->n);   // filled only if a reader completes the sort
+        d.vout = dalloc_t<uint32_t>(c, p->n);
+        d.shared = true;
+        c->deferred[d.kout] = d;
+        p->key = d.kout;
+        p->val = d.vout;
+        p->owns |= 3u;
+    } else {
+        p->key = e.keys;
+        p->val = e.vals;
+        p->owns &= ~3u;
+    }
+    p->flags |= PF_SORTED;
+    return true;
+}
+
+static void sort_pairs(qe_ctx* c, qe_pairs* p, bool defer) {
+    if (p->flags & PF_SORTED) return;
+    if (sort_cached(c, p, defer)) return;
+    sort_pairs_raw(c, p, defer);
+}
+
+int qe_sort_cache(qe_ctx* c, int on) {
+    if (!c) return QE_EINVAL;
+    QE_API_BEGIN(c)
+    if (on) {
+        const char* env = getenv("QE_SORT_CACHE");   // (read per batch: the bench A/Bs it)
+        if (c->scache || (env && env[0] == '0')) return 0;
+        c->scache = new SortCache;
+        for (qe_ctx* w : c->workers) w->scache = c->scache;
+        return 0;
+    }
+    SortCache* sc = c->scache;
+    if (!sc) return 0;
+    c->scache = nullptr;
+    for (qe_ctx* w : c->workers)
+        if (w->scache == sc) w->scache = nullptr;
+    sync(c);   // every reader of the shared buffers has finished
+    for (qe_ctx* w : c->workers) sync(w);
+    for (auto& kv : sc->m) {
+        SortCacheEntry& e = kv.second;
+        qe_ctx* o = e.owner;
+        if (e.deferred) {
+            dfree(o, e.d.words);
+            dfree(o, e.d.bstart);
+            dfree(o, e.d.d_max);
+        } else {
+            if (e.own_keys) dfree(o, e.keys);
+            if (e.own_vals) dfree(o, e.vals);
+        }
+        if (e.ev) QE_HIP(hipEventDestroy(e.ev));
+    }
+    c->scache_hits += sc->hits;
+    c->scache_builds += sc->builds;
+    delete sc;
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_sort_cache_stats(qe_ctx* c, uint64_t* hits, uint64_t* builds) {
+    if (!c) return QE_EINVAL;
+    if (hits) *hits = c->scache_hits;
+    if (builds) *builds = c->scache_builds;
+    return 0;
 }
 
 int qe_join_pairs(qe_ctx* c, qe_pairs* R, qe_pairs* S, qe_list* outR, qe_list* outS) {

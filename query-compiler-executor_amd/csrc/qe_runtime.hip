@@ -724,6 +724,7 @@ int qe_workers(qe_ctx* c, int n, qe_ctx** out) {
         }
         w->mat_limit = c->mat_limit;
         w->prof = c->prof;
+        w->scache = c->scache;
         out[i] = w;
     }
     return 0;

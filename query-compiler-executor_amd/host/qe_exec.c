@@ -769,11 +769,15 @@ int qe_run_queries_lanes(qe_ctx* ctx, int workers, int executor, const char* tex
     if (workers <= 1) {
         if (!plan) return qe_run_queries(ctx, text, out, outlen);
         uint64_t refused = 0;
-        return qe_run_queries_dist(ctx, NULL, text, out, outlen, &refused);
+        int rc = qe_sort_cache(ctx, 1);          /* the batch's base-column sorts, shared */
+        if (rc == 0) rc = qe_run_queries_dist(ctx, NULL, text, out, outlen, &refused);
+        const int rc2 = qe_sort_cache(ctx, 0);
+        return rc != 0 ? rc : rc2;
     }
     qe_ctx* w[16];
     int rc = qe_workers(ctx, workers, w);
     if (rc != 0) return rc;
+    if (plan && (rc = qe_sort_cache(ctx, 1)) != 0) return rc;   /* shared by the lanes */
     size_t nq = 0;
     query_t* qs = qe_parse_text(text, &nq);     /* parsed before anything runs (main/queries_main.c:31-37) */
     char** outs = (char**)calloc(nq ? nq : 1, sizeof(char*));
@@ -793,6 +797,7 @@ int qe_run_queries_lanes(qe_ctx* ctx, int workers, int executor, const char* tex
     if (started == 0) lane_main(&lanes[0]);      /* no threads: run the batch on one lane */
     for (int k = 0; k < started; k++) pthread_join(th[k], NULL);
     for (int k = 0; k < workers; k++) qe_sync(w[k]);
+    const int rc_cache = qe_sort_cache(ctx, 0);
     /* the reference's bytes: every query in input order, up to and including the first that ends
      * the batch (its partial output, then its status) */
     FILE* f = open_memstream(out, outlen);
@@ -806,6 +811,7 @@ int qe_run_queries_lanes(qe_ctx* ctx, int workers, int executor, const char* tex
     }
     if (f) fclose(f);
     else rc = QE_ENOMEM;
+    if (rc == 0) rc = rc_cache;
     for (size_t i = 0; i < nq; i++) free(outs[i]);
     free(outs);
     free(lens);

@@ -135,6 +135,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
                                     C.POINTER(C.c_uint64)]),
         "qe_run_queries_parallel": (I, [P, I, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
         "qe_run_queries_lanes": (I, [P, I, I, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+        "qe_sort_cache": (I, [P, I]),
+        "qe_sort_cache_stats": (I, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "qe_comm_init_local": (I, [C.POINTER(C.c_void_p), I, C.POINTER(C.c_void_p)]),
         "qe_run_queries_local": (I, [P, I, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t),
                                      C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
@@ -142,6 +144,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "qe_bind_thread": (I, [P]),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("QE_LIB_PATH") and not hasattr(lib, name):
+            continue   # an older ablation build (QE_LIB_PATH, tools/) may predate an entry point
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
@@ -253,6 +257,14 @@ class Ctx:
         if rc not in (0, QE_EEXIT):
             raise QEError(rc, self.lib.qe_last_error(self.h).decode())
         return s, (1 if rc == QE_EEXIT else 0)
+
+    def sort_cache_stats(self) -> tuple[int, int]:
+        """(cached base-column sorts reused, built) over this ctx's finished batches"""
+        if not hasattr(self.lib, "qe_sort_cache_stats"):   # (an older ablation build)
+            return 0, 0
+        h, b = C.c_uint64(), C.c_uint64()
+        self.lib.qe_sort_cache_stats(self.h, C.byref(h), C.byref(b))
+        return h.value, b.value
 
     def run_dist(self, text: str, comm: "Comm | None" = None) -> tuple[str, int, int]:
         """qe_run_queries_dist: (stdout on rank 0, exit status, queries run the faithful way)"""

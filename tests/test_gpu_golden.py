@@ -61,6 +61,7 @@ def _binary(paths, queries, env=None):
 
 MODES = {
     "default": {},                                        # the plan on 8 lanes, faithful fallback
+    "nocache": {"QE_SORT_CACHE": "0"},                    # ... without the batch's shared base-column sorts
     "faithful": {"QE_PLAN": "0", "QE_WORKERS": "1"},      # the reference's state machine, one lane
     "plan1": {"QE_WORKERS": "1"},                         # the plan, one lane
     "ranks1": {"QE_GPUS": "1"},                           # rank launcher: fork, RCCL id over a pipe
