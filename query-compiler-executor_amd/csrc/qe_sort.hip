@@ -2263,9 +2263,11 @@ static LocalRounds rounds_of(const DeferredSort& d) {
 }
 
 static void drop(qe_ctx* c, const DeferredSort& d) {
-    dfree(c, d.words);
-    dfree(c, d.bstart);
-    dfree(c, d.d_max);
+    if (!d.shared) {   // a batch's shared sort (qe_sort_cache): other lanes read it until the batch ends
+        dfree(c, d.words);
+        dfree(c, d.bstart);
+        dfree(c, d.d_max);
+    }
     dfree(c, d.x);
     dfree(c, d.x32);
 }
@@ -2549,6 +2551,26 @@ static bool deferred_geometry(const qe_pairs* p, bool need_pre, int* lo, int* nb
     const uint64_t fmask = (1ull << *nb) - 1;
     *kconst = p->kand & ~(fmask << *lo);
     return true;
+}
+
+// Two join sides whose key bounds differ (two columns' load-time OR / AND: the C4 batch's key
+// columns share one domain but not one maximum) get different bucket geometries, and the join falls
+// back to complete sorts + the merge.  Any superset of a side's bounds is valid for its sort, so
+// both take the union bounds when each would then still be a deferred two-level sort with an
+// in-bucket domain the bucket join holds in LDS.
+void unify_geometry(qe_pairs* R, qe_pairs* S) {
+    if (!(R->flags & QE_PAIRS_BITS) || !(S->flags & QE_PAIRS_BITS)) return;
+    if (R->kor == S->kor && R->kand == S->kand) return;
+    if ((R->flags | S->flags) & QE_PAIRS_SORTED) return;
+    qe_pairs r = *R, s = *S;
+    r.kor = s.kor = R->kor | S->kor;
+    r.kand = s.kand = R->kand & S->kand;
+    int lo, nb, lo2, nb2;
+    uint64_t kc, kc2;
+    if (!deferred_geometry(&r, false, &lo, &nb, &kc) || !deferred_geometry(&s, false, &lo2, &nb2, &kc2)) return;
+    if (nb - TL_H > HJ_DBITS) return;
+    R->kor = S->kor = r.kor;
+    R->kand = S->kand = r.kand;
 }
 
 bool carry_eligible(const qe_pairs* R, const qe_pairs* S, bool rpay) {
