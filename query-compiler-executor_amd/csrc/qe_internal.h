@@ -260,6 +260,9 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
 // ones with one bucket geometry, S's in the lookback-free form
 // (rpay: R carries a payload too -- its sort must be the lookback-free form as well)
 bool carry_eligible(const qe_pairs* R, const qe_pairs* S, bool rpay = false);
+// both sides' key bounds widened to their union when that gives both the deferred two-level sort
+// with one bucket geometry (the bucket join instead of complete sorts + the merge)
+void unify_geometry(qe_pairs* R, qe_pairs* S);
 // qe_join_pairs with S carrying one or two u32 payload columns (xa, xb nullable) through its sort
 // and the bucket join: outX0 / outX1 aligned with the pairs; and/or R carrying one 32-bit payload,
 // a u32 array (rx32) or a u64 column's low words (rc64), both in R's input order: outRX.  False:

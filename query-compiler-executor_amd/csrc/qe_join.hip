@@ -109,6 +109,67 @@ __global__ void __launch_bounds__(1024) tile_scan_kernel(uint64_t* __restrict__ 
     if (threadIdx.x == 0) *total = carry;
 }
 
+// the same scan for long arrays: chunk sums, one block over them (tile_scan_kernel), then every
+// chunk rescanned from its base -- the single block walked 1024 values per step and took ~0.8 ms
+// per C4 seq_merge candidate count (profiles/r03_c4_timeline.txt)
+constexpr uint32_t SCAN_PER = 8, SCAN_CH = 1024 * SCAN_PER;
+__global__ void __launch_bounds__(1024) chunk_sum_u64_kernel(const uint64_t* __restrict__ v, uint64_t n,
+                                                             uint64_t* __restrict__ part) {
+    __shared__ uint64_t wsum[16];
+    const uint64_t i0 = (uint64_t)blockIdx.x * SCAN_CH + (uint64_t)threadIdx.x * SCAN_PER;
+    uint64_t s = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER; k++) s += i0 + k < n ? v[i0 + k] : 0ull;
+    const uint64_t inc = wave_incl_scan_u64(s);
+    if (lane_id() == 63) wsum[wave_id()] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (int w = 0; w < 16; w++) t += wsum[w];
+        part[blockIdx.x] = t;
+    }
+}
+
+__global__ void __launch_bounds__(1024) chunk_scan_u64_kernel(uint64_t* __restrict__ v, uint64_t n,
+                                                              const uint64_t* __restrict__ part) {
+    __shared__ uint64_t wsum[16];
+    const uint64_t i0 = (uint64_t)blockIdx.x * SCAN_CH + (uint64_t)threadIdx.x * SCAN_PER;
+    uint64_t x[SCAN_PER], s = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER; k++) {
+        x[k] = i0 + k < n ? v[i0 + k] : 0ull;
+        s += x[k];
+    }
+    const uint64_t inc = wave_incl_scan_u64(s);
+    if (lane_id() == 63) wsum[wave_id()] = inc;
+    __syncthreads();
+    uint64_t run = part[blockIdx.x] + inc - s;
+    for (int w = 0; w < wave_id(); w++) run += wsum[w];
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER; k++) {
+        if (i0 + k < n) v[i0 + k] = run;
+        run += x[k];
+    }
+}
+
+// exclusive scan of n u64 in place on the ctx stream; the total lands in *total (device)
+static void scan_u64(qe_ctx* c, uint64_t* v, uint64_t n, uint64_t* total) {
+    if (n <= 4 * SCAN_CH) {
+        hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, c->stream, v, n, total);
+        QE_HIP(hipGetLastError());
+        return;
+    }
+    const uint64_t nb = (n + SCAN_CH - 1) / SCAN_CH;
+    uint64_t* part = dalloc_t<uint64_t>(c, nb);
+    hipLaunchKernelGGL(chunk_sum_u64_kernel, dim3((unsigned)nb), dim3(1024), 0, c->stream, v, n, part);
+    QE_HIP(hipGetLastError());
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, c->stream, part, nb, total);
+    QE_HIP(hipGetLastError());
+    hipLaunchKernelGGL(chunk_scan_u64_kernel, dim3((unsigned)nb), dim3(1024), 0, c->stream, v, n, part);
+    QE_HIP(hipGetLastError());
+    dfree(c, part);
+}
+
 // S window and output staging are XOR-swizzled: thread t's walk reads S near 8t and its emitted
 // run starts near 8t, so unswizzled the lanes of a wave would hit 4 (u64) / 8 (u32) banks.
 // Both swizzles permute within aligned groups of 8, so linear sweeps stay conflict-free.
@@ -1387,8 +1448,7 @@ void merge_sequential(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* 
         hipLaunchKernelGGL(seqm_count_kernel, dim3(grid_for(nc, 256)), dim3(256), 0, c->stream, R->key, cand, nc,
                            S->key, rec, nrec, cnt, e0s);
         QE_HIP(hipGetLastError());
-        hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, c->stream, cnt, nc, c->d_scratch + 20);
-        QE_HIP(hipGetLastError());
+        scan_u64(c, cnt, nc, c->d_scratch + 20);
         P = read_u64(c, c->d_scratch + 20);
     }
     if (getenv("QE_SEQ_DEBUG"))
@@ -1620,7 +1680,7 @@ struct SortCacheEntry {
 struct SortCache {
     std::mutex mu;
     std::condition_variable cv;
-    std::map<std::tuple<const void*, uint64_t, int>, SortCacheEntry> m;
+    std::map<std::tuple<const void*, uint64_t, int, uint64_t, uint64_t>, SortCacheEntry> m;   // + the bounds
     uint64_t hits = 0, builds = 0;
 };
 }  // namespace qe
@@ -1640,7 +1700,7 @@ static bool sort_cached(qe_ctx* c, qe_pairs* p, bool defer) {
     if (c->carry_xa || c->carry_xb || c->carry_x32 || c->carry_c64 || c->sort_v64) return false;
     if (!is_base_column(c, p->key, p->n)) return false;
     const int mode = defer ? (c->sort_keys_only ? 2 : 1) : 0;
-    const auto key = std::make_tuple((const void*)p->key, p->n, mode);
+    const auto key = std::make_tuple((const void*)p->key, p->n, mode, p->kor, p->kand);
     std::unique_lock<std::mutex> lk(sc->mu);
     auto it = sc->m.find(key);
     if (it == sc->m.end()) {   // this lane builds it
@@ -1760,6 +1820,10 @@ int qe_sort_cache_stats(qe_ctx* c, uint64_t* hits, uint64_t* builds) {
 
 int qe_join_pairs(qe_ctx* c, qe_pairs* R, qe_pairs* S, qe_list* outR, qe_list* outS) {
     QE_API_BEGIN(c)
+    // one bucket geometry for both sides (QE_JOIN_UNIFY=0 keeps each side's own bounds): C4 2504 ->
+    // 2529-2533 queries/s same box, 155 bucket joins per batch instead of 104 (profiles/r03_c4_knobs_ab.log)
+    static const bool unify = !(getenv("QE_JOIN_UNIFY") && getenv("QE_JOIN_UNIFY")[0] == '0');
+    if (unify) unify_geometry(R, S);
     sort_pairs(c, R, true);
     sort_pairs(c, S, true);
     if (bucket_join(c, R, S, outR, outS)) return 0;

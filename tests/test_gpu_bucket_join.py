@@ -4,8 +4,9 @@ multiset of (R val, S val) pairs must be exactly the equi-join's (join_relations
 src/join.c:325-392, emits every matching pair once; the plan needs no order).  Covers both forms of
 the deferred two-level sort (lookback and lookback-free, around 2^25 rows), base columns (rowids
 generated) and gathered lists, fan-out above 1 (the optimistic buffers outgrown: exact re-run),
-and every fallback to the ordinary sort + merge (different key bounds, an in-bucket domain beyond
-LDS, skewed buckets, small inputs)."""
+two sides of different key bounds (both sorted over the union bounds: one bucket geometry), and
+every fallback to the ordinary sort + merge (an in-bucket domain beyond LDS, skewed buckets, small
+inputs)."""
 import numpy as np
 import pytest
 
@@ -84,7 +85,7 @@ def test_bucket_join_base_columns_and_fanout(ctx):
 def test_bucket_join_fallbacks(ctx, shape):
     rng = np.random.default_rng(7)
     n = 3_000_000
-    if shape == "different_bounds":       # R varies in 22 bits, S in 23: different bucket geometry
+    if shape == "different_bounds":       # R varies in 22 bits, S in 23: both sorted over the union bounds
         rk = rng.integers(0, 1 << 22, n, dtype=np.uint64)
         sk = rng.integers(0, 1 << 23, n, dtype=np.uint64)
     elif shape == "wide_domain":          # 30 varying bits: 15 left inside a bucket, beyond LDS
@@ -100,6 +101,8 @@ def test_bucket_join_fallbacks(ctx, shape):
         sk = rng.integers(0, 5000, 3000, dtype=np.uint64)
     if shape == "skewed":   # the join launches, flags the bucket, and the sides complete by LSD passes
         _check(ctx, rk, sk, gathered=True, expect=True, stage="sort_pass_skew")
+    elif shape == "different_bounds":   # one geometry for both (unify_geometry): the bucket join runs
+        _check(ctx, rk, sk, gathered=True, expect=True)
     else:
         _check(ctx, rk, sk, gathered=True, expect=False)
 

@@ -410,18 +410,19 @@ def test_column_bits_at_load(ctx):
 
 
 @pytest.mark.parametrize("shape", ["random_small_domain", "random_large", "r_ascending", "s_descending",
-                                   "all_equal", "r_descending", "s_records_tied", "multi_chunk"])
+                                   "all_equal", "r_descending", "s_records_tied", "multi_chunk",
+                                   "many_candidates"])
 def test_merge_join_unsorted_shapes(ctx, shape):
     """the parallel form of the literal loop on unsorted inputs (prefix maxima + records of S),
     across chunk boundaries of its scans and the degenerate orders"""
     rng = np.random.default_rng(len(shape))
-    n = 70_000 if shape in ("random_large", "multi_chunk") else 3000
+    n = {"random_large": 70_000, "multi_chunk": 70_000, "many_candidates": 200_003}.get(shape, 3000)
     if shape == "random_small_domain":
         rk, sk = rng.integers(0, 50, n, dtype=np.uint64), rng.integers(0, 50, n + 17, dtype=np.uint64)
     elif shape == "random_large":
         rk, sk = rng.integers(0, 1 << 40, n, dtype=np.uint64), rng.integers(0, 1 << 40, n, dtype=np.uint64)
         sk[::97] = rk[::97][: len(sk[::97])]
-    elif shape == "r_ascending":
+    elif shape in ("r_ascending", "many_candidates"):   # every R row a candidate: the long count scan
         rk, sk = np.arange(n, dtype=np.uint64), rng.integers(0, n, n, dtype=np.uint64)
     elif shape == "s_descending":
         rk, sk = rng.integers(0, n, n, dtype=np.uint64), np.arange(n, 0, -1).astype(np.uint64)
