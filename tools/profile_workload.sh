@@ -18,7 +18,8 @@ cd $R
 python3 tools/stage_stats.py $(find $O/${TAG}_trace -name "*kernel_stats.csv" | head -1) --workload $W \
     --out $O/${TAG}_stage_stats.json --command "rocprofv3 --kernel-trace --stats -- python3 bench.py $A" > /dev/null
 cp $(find $O/${TAG}_trace -name "*kernel_stats.csv" | head -1) $O/${TAG}_kernel_stats.csv
-python3 tools/pmc_traffic.py --fetch $O/${TAG}_fetch --write $O/${TAG}_write --out $O/${TAG}_traffic.json --workload $W \
+TW=$W; [ "$W" = c3 ] && case "$PROFILE_EXTRA" in *--no-faithful*) TW=c3_plan;; esac   # (bench.py's C3 tag)
+python3 tools/pmc_traffic.py --fetch $O/${TAG}_fetch --write $O/${TAG}_write --out $O/${TAG}_traffic.json --workload $TW \
     --command "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE -- python3 bench.py $A" > /dev/null
 rm -rf $O/${TAG}_trace $O/${TAG}_fetch $O/${TAG}_write
 echo summaries-done
