@@ -581,14 +581,17 @@ struct LocalRounds {
 
 // IN == IN_WORD: packed words of a bucket-partitioned array (bstart); IN_KV / IN_KIOTA: ONE
 // bucket of single_n (key, rowid) pairs packed on load (a small sort: a single launch)
-template <typename K, int IN>
-__global__ void __launch_bounds__(TL_NT) tl_local_kernel(const uint64_t* __restrict__ win, const K* __restrict__ kin,
+// NT: threads per bucket -- TL_NT, or 64 (one wave, TL_ITEMS x 64 words) for the many small buckets
+// of a two-level sort over a few million keys (32 K buckets of tens to hundreds of words: 512 threads
+// and their barriers per bucket were most of the C4 batch's local-sort time)
+template <typename K, int IN, int NT = TL_NT>
+__global__ void __launch_bounds__(NT) tl_local_kernel(const uint64_t* __restrict__ win, const K* __restrict__ kin,
                                                          const uint32_t* __restrict__ vin, K* __restrict__ kout,
                                                          uint32_t* __restrict__ vout,
                                                          const uint32_t* __restrict__ bstart, uint32_t single_n,
                                                          Field f, LocalRounds lr) {
-    constexpr int NW = TL_NT / 64, BINS = 256;
-    __shared__ uint64_t stage[TL_CAP];
+    constexpr int NW = NT / 64, BINS = 256;
+    __shared__ uint64_t stage[NT * TL_ITEMS];
     __shared__ uint32_t whist[NW][BINS];
     __shared__ uint32_t bexcl[BINS];
     __shared__ uint32_t wsum[NW];
@@ -597,7 +600,7 @@ __global__ void __launch_bounds__(TL_NT) tl_local_kernel(const uint64_t* __restr
     if (m == 0) return;   // block-uniform
     const int w = wave_id(), l = lane_id();
     const uint64_t lt = lanemask_lt();
-    const uint32_t jm = (m + NW * 64 - 1) / (NW * 64);   // <= TL_ITEMS since m <= TL_CAP
+    const uint32_t jm = (m + NW * 64 - 1) / (NW * 64);   // <= TL_ITEMS since m <= NT * TL_ITEMS
     const uint32_t wbase = (uint32_t)w * jm * 64;
     uint64_t word[TL_ITEMS];
 #pragma unroll
@@ -617,7 +620,7 @@ __global__ void __launch_bounds__(TL_NT) tl_local_kernel(const uint64_t* __restr
         const int bits = lr.bits[r];
         if (r > 0) dsh += lr.bits[r - 1];
         const uint32_t mask = (1u << bits) - 1u;
-        for (int i = threadIdx.x; i < NW * BINS; i += TL_NT) (&whist[0][0])[i] = 0;
+        for (int i = threadIdx.x; i < NW * BINS; i += NT) (&whist[0][0])[i] = 0;
         __syncthreads();
         uint32_t pos[TL_ITEMS];
 #pragma unroll
@@ -645,23 +648,36 @@ __global__ void __launch_bounds__(TL_NT) tl_local_kernel(const uint64_t* __restr
             pos[j] = old + (uint32_t)__popcll(peers & lt);
         }
         __syncthreads();
-        uint32_t tot = 0;
-        if (threadIdx.x < BINS) {
-            const uint32_t d = threadIdx.x;
+        // thread t owns digits t * DPT .. + DPT - 1: totals over the waves, then one exclusive scan
+        constexpr int DPT = BINS >= NT ? BINS / NT : 1;
+        const bool owner = DPT > 1 || (int)threadIdx.x < BINS;
+        uint32_t tq[DPT], tot = 0;
 #pragma unroll
-            for (int ww = 0; ww < NW; ww++) {
-                const uint32_t c = whist[ww][d];
-                whist[ww][d] = tot;
-                tot += c;
+        for (int q = 0; q < DPT; q++) {
+            const uint32_t d = threadIdx.x * DPT + q;
+            uint32_t t = 0;
+            if (owner) {
+#pragma unroll
+                for (int ww = 0; ww < NW; ww++) {
+                    const uint32_t c = whist[ww][d];
+                    whist[ww][d] = t;
+                    t += c;
+                }
             }
+            tq[q] = t;
+            tot += t;
         }
         const uint32_t inc = wave_incl_scan_u32(tot);
         if (l == 63) wsum[w] = inc;
         __syncthreads();
-        if (threadIdx.x < BINS) {
+        if (owner) {
             uint32_t ex = inc - tot;
             for (int ww = 0; ww < w; ww++) ex += wsum[ww];
-            bexcl[threadIdx.x] = ex;
+#pragma unroll
+            for (int q = 0; q < DPT; q++) {
+                bexcl[threadIdx.x * DPT + q] = ex;
+                ex += tq[q];
+            }
         }
         __syncthreads();
 #pragma unroll
@@ -1794,6 +1810,23 @@ static bool sort_pre_on() {
     return on;
 }
 
+// the per-bucket LDS step of a two-level sort over packed words: one wave per bucket when the
+// largest bucket fits one wave's TL_ITEMS x 64 words (the 15-bit geometry over up to ~20 M keys:
+// buckets of tens to hundreds of words), else TL_NT threads per bucket.  QE_LOCAL_WAVE=0 (A/B knob)
+// keeps TL_NT threads everywhere.
+template <typename K>
+static void local_sort_buckets(qe_ctx* c, const uint64_t* words, K* kout, uint32_t* vout, const uint32_t* bstart,
+                               unsigned nbuckets, Field f, LocalRounds lr, uint64_t maxb) {
+    static const bool wave_on = !(getenv("QE_LOCAL_WAVE") && getenv("QE_LOCAL_WAVE")[0] == '0');
+    if (wave_on && maxb <= 64u * TL_ITEMS)
+        hipLaunchKernelGGL((tl_local_kernel<K, IN_WORD, 64>), dim3(nbuckets), dim3(64), 0, c->stream, words, nullptr,
+                           nullptr, kout, vout, bstart, 0u, f, lr);
+    else
+        hipLaunchKernelGGL((tl_local_kernel<K, IN_WORD>), dim3(nbuckets), dim3(TL_NT), 0, c->stream, words, nullptr,
+                           nullptr, kout, vout, bstart, 0u, f, lr);
+    QE_HIP(hipGetLastError());
+}
+
 // the two-level sort (H = TL_H) with both global passes lookback-free (see tl_hist_tiles_kernel)
 template <typename K>
 static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, uint64_t n, int bits, Field f,
@@ -1965,7 +1998,8 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     }
     // the two passes are valid whatever the bucket sizes, so they are queued before the host
     // reads the largest bucket: the GPU stays busy through that round trip
-    if (!dfr && read_u64(c, d_max) > (uint64_t)TL_CAP) {   // a bucket beyond LDS (skew): plain LSD passes
+    const uint64_t maxb = dfr ? 0 : read_u64(c, d_max);
+    if (!dfr && maxb > (uint64_t)TL_CAP) {   // a bucket beyond LDS (skew): plain LSD passes
         dfree(c, w1);
         dfree(c, w2);
         dfree(c, kout);
@@ -2003,9 +2037,7 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     }
     {
         Timed t(c, "sort_local", 8.0 * n + ((double)sizeof(K) + 4) * n);
-        hipLaunchKernelGGL((tl_local_kernel<K, IN_WORD>), dim3(TL_BUCKETS), dim3(TL_NT), 0, c->stream, w2, nullptr,
-                           nullptr, kout, vout, bstart, 0u, f, lr);
-        QE_HIP(hipGetLastError());
+        local_sort_buckets<K>(c, w2, kout, vout, bstart, TL_BUCKETS, f, lr, maxb);
     }
     dfree(c, w1);
     dfree(c, w2);
@@ -2051,7 +2083,8 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
         hipLaunchKernelGGL(tl_scan_kernel, dim3(1), dim3(1024), 0, c->stream, hist, bstart, base1, base2, d_max);
         QE_HIP(hipGetLastError());
     }
-    if (!dfr && read_u64(c, d_max) > (uint64_t)TL_CAP) {
+    const uint64_t maxb = dfr ? 0 : read_u64(c, d_max);
+    if (!dfr && maxb > (uint64_t)TL_CAP) {
         dfree(c, hist);
         dfree(c, bstart);
         return false;
@@ -2103,9 +2136,7 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
     }
     {
         Timed t(c, "sort_local", 8.0 * n + ((double)sizeof(K) + 4) * n);
-        hipLaunchKernelGGL((tl_local_kernel<K, IN_WORD>), dim3(1u << H), dim3(TL_NT), 0, c->stream,
-                           H == TL_H ? w2 : w1, nullptr, nullptr, kout, vout, bstart, 0u, f, lr);
-        QE_HIP(hipGetLastError());
+        local_sort_buckets<K>(c, H == TL_H ? w2 : w1, kout, vout, bstart, 1u << H, f, lr, maxb);
     }
     dfree(c, w1);
     if (w2) dfree(c, w2);
@@ -2454,13 +2485,12 @@ void pairs_need_keys(qe_ctx* c, const qe_pairs* p) {
     if (d.w32) throw Error(QE_EINVAL, "internal: a key-only deferred sort has no rows to complete");
     c->deferred.erase(it);
     const Field f{d.lo, d.fmask, d.kconst};
-    if (read_u64(c, d.d_max) > (uint64_t)TL_CAP) {
+    const uint64_t maxb = read_u64(c, d.d_max);
+    if (maxb > (uint64_t)TL_CAP) {
         complete_lsd(c, d, p->n);
     } else {
         Timed t(c, "sort_local", 8.0 * p->n + 12.0 * p->n);
-        hipLaunchKernelGGL((tl_local_kernel<uint64_t, IN_WORD>), dim3(TL_BUCKETS), dim3(TL_NT), 0, c->stream, d.words,
-                           nullptr, nullptr, d.kout, d.vout, d.bstart, 0u, f, rounds_of(d));
-        QE_HIP(hipGetLastError());
+        local_sort_buckets<uint64_t>(c, d.words, d.kout, d.vout, d.bstart, TL_BUCKETS, f, rounds_of(d), maxb);
     }
     drop(c, d);
 }
@@ -2606,7 +2636,8 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
         QE_HIP(hipMemsetAsync(c->d_scratch + 17, 0, 2 * sizeof(uint64_t), c->stream));   // [pairs, oversize]
         {
             // algorithmic bytes: both sides' words in (+ 8 B per pair below; + the payloads)
-            Timed t(c, "bucket_join", 8.0 * (double)(nR + nS) + (carry ? 8.0 * (double)nS : 0.0) + (rx ? 4.0 * (double)nR : 0.0));
+            Timed t(c, "bucket_join", 8.0 * (double)(nR + nS) + (carry ? (s32 ? 4.0 : 8.0) * (double)nS : 0.0) +
+                                          (rx ? 4.0 * (double)nR : 0.0));
             if (s32 && rx) {
                 hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, true, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
                                    c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
@@ -2667,7 +2698,8 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
             return false;
         }
         if (P <= cap) {
-            add_bytes(c, "bucket_join", 8.0 * (double)P);
+            // the pairs (4 + 4 B) and every carried output column (4 B each) written per pair
+            add_bytes(c, "bucket_join", (8.0 + (carry ? 4.0 : 0.0) + (outX1 ? 4.0 : 0.0) + (rx ? 4.0 : 0.0)) * (double)P);
             if (P > c->mat_limit) {   // the reference's DArray cannot hold it either (src/DArray.h:14-15)
                 dfree(c, oR);
                 dfree(c, oS);
@@ -2810,7 +2842,10 @@ bool bucket_join_sums(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const HjS
     uint64_t* out = dalloc_t<uint64_t>(c, 8);   // [pairs-free sums..., pairs, oversize]
     QE_HIP(hipMemsetAsync(out, 0, 8 * sizeof(uint64_t), c->stream));
     {
-        Timed t(c, "bucket_join_sums", 8.0 * (double)(R->n + S->n) + (carry ? 8.0 * (double)S->n : 0.0));
+        // algorithmic bytes: R's words (u32 fields when key-only), S's words and carried payload;
+        // the gathered select values are added below
+        Timed t(c, "bucket_join_sums", (dR.w32 ? 4.0 : 8.0) * (double)R->n + 8.0 * (double)S->n +
+                                           (carry ? (dS.x ? 8.0 : 4.0) * (double)S->n : 0.0));
         hipLaunchKernelGGL(tl_hjoin_sums_kernel, dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream, dR.words, dR.bstart,
                            dS.words, dS.bstart, dR.L, carry ? dS.x : nullptr, sc, part,
                            reinterpret_cast<unsigned long long*>(out + HJ_SUMS + 1), carry ? dS.x32 : nullptr,
@@ -2827,7 +2862,11 @@ bool bucket_join_sums(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const HjS
     if (h[HJ_SUMS + 1]) return false;     // a bucket beyond LDS (skew)
     *pairs = h[HJ_SUMS];
     for (int s = 0; s < sc.n; s++) sums[s] = h[s];
-    add_bytes(c, "bucket_join_sums", 8.0 * (double)sc.n * (double)h[HJ_SUMS]);   // ~ the gathered values
+    // a select whose values ride in the carried list is summed in place; the others gather one 8-B
+    // value per S row with a partner (at most min(pairs, |S|) of them)
+    int gathered = 0;
+    for (int s = 0; s < sc.n; s++) gathered += sc.col[s] && !(sc.src[s] & 4) ? 1 : 0;   // (4: QE_PLAN_VALUES_SRC)
+    add_bytes(c, "bucket_join_sums", 8.0 * gathered * (double)std::min<uint64_t>(h[HJ_SUMS], S->n));
     return true;
 }
 
