@@ -1377,8 +1377,11 @@ constexpr uint32_t HJ_NONE = 0xFFFFu;
 static_assert(TL_CAP < HJ_NONE, "chain links are 16-bit row indices");
 
 // S32: S's payload is 32-bit (xS32: one carried binding), outX0 only.
-template <int DBITS, bool CARRY = false, bool RX = false, bool S32 = false>
-__global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
+// NT: threads per bucket (HJ_NT; 256 for C4-sized joins measured 2 % slower on the batch's wall
+// time -- its bucket joins 99 -> 62 ms of kernel time, but 41 re-runs of overflowing buckets and
+// more interference with the other lanes, profiles/r03_c4_hjsmall_ab.log)
+template <int DBITS, bool CARRY = false, bool RX = false, bool S32 = false, int NT = HJ_NT>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8)))
 tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict__ bsR, const uint64_t* __restrict__ wS,
                       const uint32_t* __restrict__ bsS, int L, uint32_t* __restrict__ outR, uint32_t* __restrict__ outS,
                       uint64_t cap, uint64_t* total_out, const uint64_t* __restrict__ xS = nullptr,
@@ -1386,19 +1389,20 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
                       const uint32_t* __restrict__ xR = nullptr, uint32_t* __restrict__ outRX = nullptr,
                       const uint32_t* __restrict__ xS32 = nullptr) {
     __shared__ uint32_t head[1 << DBITS];   // per key value: the last R row inserted (HJ_NONE: none)
-    __shared__ uint16_t nxt[TL_CAP];        // per R row: the previous row of its value
+    __shared__ uint16_t nxt[NT * HJ_I];        // per R row: the previous row of its value
 #if QE_HJ_RR_GLOBAL
     uint32_t* rr = nullptr;                 // (R's rowids re-read from its words, L2-hot, at emission)
 #else
-    __shared__ uint32_t rr[TL_CAP];         // per R row: its rowid
+    __shared__ uint32_t rr[NT * HJ_I];         // per R row: its rowid
 #endif
-    __shared__ uint32_t rx[RX ? TL_CAP : 1];  // per R row: its payload
-    __shared__ uint32_t tab[HJ_I * HJ_NW];
+    __shared__ uint32_t rx[RX ? NT * HJ_I : 1];  // per R row: its payload
+    constexpr int NW = NT / 64;
+    __shared__ uint32_t tab[HJ_I * NW];
     __shared__ uint64_t s_excl;
     __shared__ uint32_t s_total;
     const uint32_t b = blockIdx.x;
     const uint32_t r0 = bsR[b], mR = bsR[b + 1] - r0, s0 = bsS[b], mS = bsS[b + 1] - s0;
-    if (mR > (uint32_t)TL_CAP || mS > (uint32_t)TL_CAP) {   // beyond LDS (the sorts were not checked): flag it
+    if (mR > (uint32_t)(NT * HJ_I) || mS > (uint32_t)(NT * HJ_I)) {   // beyond LDS (the sorts were not checked): flag it
         if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(total_out + 1), 1ull);
         return;
     }
@@ -1407,19 +1411,19 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
     uint64_t wr[HJ_I], ws[HJ_I];
 #pragma unroll
     for (int j = 0; j < HJ_I; j++) {
-        const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
+        const uint32_t i = (uint32_t)j * NT + threadIdx.x;
         wr[j] = i < mR ? wR[r0 + i] : 0;
     }
 #pragma unroll
     for (int j = 0; j < HJ_I; j++) {
-        const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
+        const uint32_t i = (uint32_t)j * NT + threadIdx.x;
         ws[j] = i < mS ? wS[s0 + i] : 0;
     }
     uint64_t xv[CARRY ? HJ_I : 1];
     if constexpr (CARRY) {
 #pragma unroll
         for (int j = 0; j < HJ_I; j++) {
-            const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
+            const uint32_t i = (uint32_t)j * NT + threadIdx.x;
             xv[j] = i < mS ? (S32 ? (uint64_t)xS32[s0 + i] : xS[s0 + i]) : 0ull;
         }
     }
@@ -1427,15 +1431,15 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
     if constexpr (RX) {
 #pragma unroll
         for (int j = 0; j < HJ_I; j++) {
-            const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
+            const uint32_t i = (uint32_t)j * NT + threadIdx.x;
             xr[j] = i < mR ? xR[r0 + i] : 0u;
         }
     }
-    for (uint32_t v = threadIdx.x; v < D; v += HJ_NT) head[v] = HJ_NONE;
+    for (uint32_t v = threadIdx.x; v < D; v += NT) head[v] = HJ_NONE;
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < HJ_I; j++) {
-        const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
+        const uint32_t i = (uint32_t)j * NT + threadIdx.x;
         if (i < mR) {
             nxt[i] = (uint16_t)atomicExch(&head[fld(wr[j]) & dmask], i);
             if (!QE_HJ_RR_GLOBAL) rr[i] = (uint32_t)wr[j];
@@ -1447,7 +1451,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
 #pragma unroll
     for (int j = 0; j < HJ_I; j++) {
         uint32_t cnt = 0, h = HJ_NONE;
-        if ((uint32_t)j * HJ_NT + threadIdx.x < mS) {
+        if ((uint32_t)j * NT + threadIdx.x < mS) {
             h = head[fld(ws[j]) & dmask];
             for (uint32_t p = h; p != HJ_NONE; p = nxt[p]) cnt++;
         }
@@ -1455,11 +1459,11 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
         const uint32_t inc = wave_incl_scan_u32(cnt);
         pre[j] = inc - cnt;
         tot[j] = (uint32_t)__shfl((int)inc, 63, 64);   // the item's pairs in this wave
-        if (l == 63) tab[j * HJ_NW + w] = inc;
+        if (l == 63) tab[j * NW + w] = inc;
     }
     __syncthreads();
     if (w == 0) {   // (row group, wave) totals in row order -> bucket offsets; one atomic per bucket
-        constexpr uint32_t E = HJ_I * HJ_NW;
+        constexpr uint32_t E = HJ_I * NW;
         const uint32_t a0 = 2u * l < E ? tab[2 * l] : 0u, a1 = 2u * l + 1 < E ? tab[2 * l + 1] : 0u;
         const uint32_t inc = wave_incl_scan_u32(a0 + a1);
         const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
@@ -1477,7 +1481,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
 #pragma unroll
     for (int j = 0; j < HJ_I; j++) {   // wave-cooperative emission, as tl_hjoin_kernel's
         const uint32_t pj = pre[j], all = tot[j];
-        const uint64_t ob = gofs + tab[j * HJ_NW + w];
+        const uint64_t ob = gofs + tab[j * NW + w];
         const uint32_t srow = (uint32_t)ws[j];
         for (uint32_t q0 = 0; q0 < all; q0 += 64) {   // wave-uniform
             const uint32_t q = q0 + (uint32_t)l;

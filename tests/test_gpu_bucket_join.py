@@ -81,6 +81,19 @@ def test_bucket_join_base_columns_and_fanout(ctx):
     assert P > 2 * n
 
 
+@pytest.mark.parametrize("n_small", [40_000, 700_001])
+def test_join_small_side_against_a_big_one(ctx, n_small):
+    """a side too small for the deferred two-level sort joined with a big one (the big side's
+    deferred sort completes, the merge joins them; forcing the small side into the bucket geometry
+    measured slower on C4, profiles/r03_c4_hjsmall_ab.log)"""
+    rng = np.random.default_rng(n_small)
+    n = 3_000_000
+    rk = rng.integers(0, n, n, dtype=np.uint64)
+    sk = rng.integers(0, n, n_small, dtype=np.uint64)
+    _check(ctx, rk, sk, gathered=True, expect=False)
+    _check(ctx, sk, rk, gathered=True, expect=False)   # the small side as R
+
+
 @pytest.mark.parametrize("shape", ["different_bounds", "wide_domain", "skewed", "small"])
 def test_bucket_join_fallbacks(ctx, shape):
     rng = np.random.default_rng(7)
