@@ -2747,6 +2747,10 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
 // looks up its count and gathers its selected values once -- no pairs, no payloads written, no
 // checksum pass reading them back.  Each block writes its partial sums (plain stores); a second
 // launch adds them up (one atomic per block on one word would serialise at the memory side).
+// PERSIST: a resident grid, each workgroup walking buckets blockIdx.x, + gridDim.x, ... with its
+// sums kept in registers across them and reduced once (the per-bucket form reduces and stores
+// five u64 sums per bucket); part is indexed by workgroup in both forms.
+template <bool PERSIST = false>
 __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
 tl_hjoin_sums_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict__ bsR,
                      const uint64_t* __restrict__ wS, const uint32_t* __restrict__ bsS, int L,
@@ -2754,51 +2758,55 @@ tl_hjoin_sums_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict
                      unsigned long long* __restrict__ flag, const uint32_t* __restrict__ xS32, int r32) {
     __shared__ uint32_t cnt[1 << HJ_DBITS];
     __shared__ uint64_t red[HJ_NW][HJ_SUMS + 1];
-    const uint32_t b = blockIdx.x;
-    const uint32_t r0 = bsR[b], mR = bsR[b + 1] - r0, s0 = bsS[b], mS = bsS[b + 1] - s0;
-    if (mR > (uint32_t)TL_CAP || mS > (uint32_t)TL_CAP) {   // beyond LDS: the host takes the other path
-        if (threadIdx.x == 0) atomicOr(flag, 1ull);
-        return;
-    }
     const uint32_t D = 1u << L, dmask = D - 1u;
     const int w = wave_id(), l = lane_id();
-    uint64_t wr[HJ_I], ws[HJ_I], xv[HJ_I];
-#pragma unroll
-    for (int j = 0; j < HJ_I; j++) {
-        const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
-        wr[j] = i < mR ? (r32 ? (uint64_t)reinterpret_cast<const uint32_t*>(wR)[r0 + i] << 32 : wR[r0 + i]) : 0;
-        ws[j] = i < mS ? wS[s0 + i] : 0;
-        xv[j] = xS32 && i < mS ? (uint64_t)xS32[s0 + i] : xS && i < mS ? xS[s0 + i] : 0ull;
-    }
-    for (uint32_t v = threadIdx.x; v < D; v += HJ_NT) cnt[v] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < HJ_I; j++)
-        if ((uint32_t)j * HJ_NT + threadIdx.x < mR) atomicAdd(&cnt[fld(wr[j]) & dmask], 1u);
-    __syncthreads();
-    uint32_t c[HJ_I];
     uint64_t acc[HJ_SUMS + 1];
-    acc[HJ_SUMS] = 0;
 #pragma unroll
-    for (int j = 0; j < HJ_I; j++) {
-        c[j] = (uint32_t)j * HJ_NT + threadIdx.x < mS ? cnt[fld(ws[j]) & dmask] : 0u;
-        acc[HJ_SUMS] += c[j];
-    }
+    for (int s = 0; s <= HJ_SUMS; s++) acc[s] = 0;
+    const uint32_t step = PERSIST ? gridDim.x : (uint32_t)TL_BUCKETS;
+    for (uint32_t b = blockIdx.x; b < (uint32_t)TL_BUCKETS; b += step) {   // block-uniform
+        const uint32_t r0 = bsR[b], mR = bsR[b + 1] - r0, s0 = bsS[b], mS = bsS[b + 1] - s0;
+        if (mR > (uint32_t)TL_CAP || mS > (uint32_t)TL_CAP) {   // beyond LDS: the host takes the other path
+            if (threadIdx.x == 0) atomicOr(flag, 1ull);
+            continue;
+        }
+        uint32_t fr[HJ_I];   // R's key fields only (its rows are never read)
+        uint64_t ws[HJ_I], xv[HJ_I];
 #pragma unroll
-    for (int s = 0; s < HJ_SUMS; s++) {
-        acc[s] = 0;
-        if (s < sc.n) {   // block-uniform
-            const uint64_t* __restrict__ col = sc.col[s];
-            const int src = sc.src[s] & 3;
-            const bool own = (sc.src[s] & 4) != 0;   // the carried list holds the values (QE_PLAN_VALUES_SRC)
-            uint64_t v[HJ_I];
+        for (int j = 0; j < HJ_I; j++) {
+            const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
+            fr[j] = i < mR ? (r32 ? reinterpret_cast<const uint32_t*>(wR)[r0 + i] : fld(wR[r0 + i])) : 0u;
+            ws[j] = i < mS ? wS[s0 + i] : 0;
+            xv[j] = xS32 && i < mS ? (uint64_t)xS32[s0 + i] : xS && i < mS ? xS[s0 + i] : 0ull;
+        }
+        if (PERSIST) __syncthreads();   // the previous bucket's lookups are done with cnt
+        for (uint32_t v = threadIdx.x; v < D; v += HJ_NT) cnt[v] = 0;
+        __syncthreads();
 #pragma unroll
-            for (int j = 0; j < HJ_I; j++) {   // every gather of the select in flight together
-                const uint32_t id = src == 0 ? (uint32_t)ws[j] : src == 1 ? (uint32_t)xv[j] : (uint32_t)(xv[j] >> 32);
-                v[j] = own ? (uint64_t)id : c[j] ? col[id] : 0ull;
+        for (int j = 0; j < HJ_I; j++)
+            if ((uint32_t)j * HJ_NT + threadIdx.x < mR) atomicAdd(&cnt[fr[j] & dmask], 1u);
+        __syncthreads();
+        uint32_t c[HJ_I];
+#pragma unroll
+        for (int j = 0; j < HJ_I; j++) {
+            c[j] = (uint32_t)j * HJ_NT + threadIdx.x < mS ? cnt[fld(ws[j]) & dmask] : 0u;
+            acc[HJ_SUMS] += c[j];
+        }
+#pragma unroll
+        for (int s = 0; s < HJ_SUMS; s++) {
+            if (s < sc.n) {   // block-uniform
+                const uint64_t* __restrict__ col = sc.col[s];
+                const int src = sc.src[s] & 3;
+                const bool own = (sc.src[s] & 4) != 0;   // the carried list holds the values (QE_PLAN_VALUES_SRC)
+                uint64_t v[HJ_I];
+#pragma unroll
+                for (int j = 0; j < HJ_I; j++) {   // every gather of the select in flight together
+                    const uint32_t id = src == 0 ? (uint32_t)ws[j] : src == 1 ? (uint32_t)xv[j] : (uint32_t)(xv[j] >> 32);
+                    v[j] = own ? (uint64_t)id : c[j] ? col[id] : 0ull;
+                }
+#pragma unroll
+                for (int j = 0; j < HJ_I; j++) acc[s] += (uint64_t)c[j] * v[j];
             }
-#pragma unroll
-            for (int j = 0; j < HJ_I; j++) acc[s] += (uint64_t)c[j] * v[j];
         }
     }
 #pragma unroll
@@ -2810,7 +2818,7 @@ tl_hjoin_sums_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict
     if (threadIdx.x <= HJ_SUMS) {
         uint64_t t = 0;
         for (int ww = 0; ww < HJ_NW; ww++) t += red[ww][threadIdx.x];
-        part[(uint64_t)b * (HJ_SUMS + 1) + threadIdx.x] = t;
+        part[(uint64_t)blockIdx.x * (HJ_SUMS + 1) + threadIdx.x] = t;
     }
 }
 
@@ -2850,13 +2858,27 @@ bool bucket_join_sums(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const HjS
         // the gathered select values are added below
         Timed t(c, "bucket_join_sums", (dR.w32 ? 4.0 : 8.0) * (double)R->n + 8.0 * (double)S->n +
                                            (carry ? (dS.x ? 8.0 : 4.0) * (double)S->n : 0.0));
-        hipLaunchKernelGGL(tl_hjoin_sums_kernel, dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream, dR.words, dR.bstart,
-                           dS.words, dS.bstart, dR.L, carry ? dS.x : nullptr, sc, part,
-                           reinterpret_cast<unsigned long long*>(out + HJ_SUMS + 1), carry ? dS.x32 : nullptr,
-                           dR.w32 ? 1 : 0);
+        // a resident grid (two 1024-thread workgroups per CU) walking the buckets, its sums reduced
+        // once per workgroup (QE_HJ_SUMS_PERSIST=0: one workgroup per bucket)
+        static const uint32_t resident = [&] {
+            int ncu = 0;
+            QE_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
+            return (uint32_t)std::max(1, 2 * ncu);
+        }();
+        static const bool persist = !(getenv("QE_HJ_SUMS_PERSIST") && getenv("QE_HJ_SUMS_PERSIST")[0] == '0');
+        const uint32_t grid = persist ? std::min<uint32_t>(resident, TL_BUCKETS) : (uint32_t)TL_BUCKETS;
+        if (persist)
+            hipLaunchKernelGGL(tl_hjoin_sums_kernel<true>, dim3(grid), dim3(HJ_NT), 0, c->stream, dR.words, dR.bstart,
+                               dS.words, dS.bstart, dR.L, carry ? dS.x : nullptr, sc, part,
+                               reinterpret_cast<unsigned long long*>(out + HJ_SUMS + 1), carry ? dS.x32 : nullptr,
+                               dR.w32 ? 1 : 0);
+        else
+            hipLaunchKernelGGL(tl_hjoin_sums_kernel<false>, dim3(grid), dim3(HJ_NT), 0, c->stream, dR.words, dR.bstart,
+                               dS.words, dS.bstart, dR.L, carry ? dS.x : nullptr, sc, part,
+                               reinterpret_cast<unsigned long long*>(out + HJ_SUMS + 1), carry ? dS.x32 : nullptr,
+                               dR.w32 ? 1 : 0);
         QE_HIP(hipGetLastError());
-        hipLaunchKernelGGL(hjoin_sums_reduce_kernel, dim3(HJ_SUMS + 1), dim3(256), 0, c->stream, part,
-                           (uint32_t)TL_BUCKETS, out);
+        hipLaunchKernelGGL(hjoin_sums_reduce_kernel, dim3(HJ_SUMS + 1), dim3(256), 0, c->stream, part, grid, out);
         QE_HIP(hipGetLastError());
     }
     uint64_t h[HJ_SUMS + 2];
