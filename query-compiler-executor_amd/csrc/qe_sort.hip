@@ -980,7 +980,10 @@ constexpr int TL2_NT = QE_TL2_NT, TL2_ITEMS = QE_TL2_ITEMS, TL2_TILE = TL2_NT * 
 // CARRY: the payloads of pass 1 (xin, in pass-1 order; X64: 64-bit, X32: 32-bit) follow the words
 // to xout, staged in the words' LDS slots after the words have left (as in radix_pass_kernel).
 // W32: the words are u32 fields (a key-only first pass, OUT_W32): loaded into the high half, stored back as u32
-template <typename K, int CARRY = X_NONE, bool UNSTABLE = false, bool W32 = false>
+// XS (X64 only): the 64-bit payloads are staged too -- each slot's second-pass digit is kept in a
+// byte of a register while its word leaves, the payloads then take the words' slots and leave as
+// the same runs (coalesced), instead of every lane storing its payload at its slot's destination.
+template <typename K, int CARRY = X_NONE, bool UNSTABLE = false, bool W32 = false, bool XS = false>
 __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const uint64_t* __restrict__ win, uint64_t* __restrict__ wout,
                                                          uint64_t n, int dsh, const uint32_t* __restrict__ seg,
                                                          const uint32_t* __restrict__ off2, uint32_t G,
@@ -1089,7 +1092,37 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
             }
         }
         __syncthreads();
-        if constexpr (CARRY != X_NONE) {
+        if constexpr (CARRY == X64 && XS) {
+            uint32_t dg[(TL2_ITEMS + 3) / 4];   // slot k's digit in byte k % 4 of dg[k / 4]
+#pragma unroll
+            for (int k = 0; k < TL2_ITEMS; k++) {
+                const uint32_t i = (uint32_t)k * TL2_NT + threadIdx.x;
+                uint32_t dd = 0;
+                if (i < m) {
+                    const uint64_t wd = stage[i];
+                    dd = (uint32_t)(wd >> dsh) & (BINS - 1);
+                    const uint32_t p = gofs[dd] + i;
+                    if ((uint64_t)p < n) QE_ST(&wout[p], wd);
+                }
+                if (k & 3) dg[k >> 2] |= dd << (8 * (k & 3));
+                else dg[k >> 2] = dd;
+                if (k % 6 == 5) __builtin_amdgcn_sched_barrier(0);   // six slots' LDS reads in flight, not 18
+            }
+            __syncthreads();   // every word is out of the stage
+#pragma unroll
+            for (int j = 0; j < TL2_ITEMS; j++)
+                if (j * 64 < lim) stage[(pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu] = word[j];
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < TL2_ITEMS; k++) {
+                const uint32_t i = (uint32_t)k * TL2_NT + threadIdx.x;
+                if (i < m) {
+                    const uint32_t p = gofs[(dg[k >> 2] >> (8 * (k & 3))) & 0xFFu] + i;
+                    if ((uint64_t)p < n) QE_ST(&xout[p], stage[i]);
+                }
+                if (k % 6 == 5) __builtin_amdgcn_sched_barrier(0);
+            }
+        } else if constexpr (CARRY != X_NONE) {
             // the payloads: each slot's destination is read back from its word before the slot
             // is reused (one u32 per slot in the LDS word itself: high half = destination)
 #pragma unroll 6
@@ -1146,6 +1179,12 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
         }
         __syncthreads();   // stage / whist / gofs are rewritten by the next sub-tile
     }
+}
+
+// the staged 64-bit payload form of pass 2 (XS); QE_X64_STAGE=0 (A/B knob) keeps the per-lane stores
+static bool x64_staged() {
+    static const bool on = !(getenv("QE_X64_STAGE") && getenv("QE_X64_STAGE")[0] == '0');
+    return on;
 }
 
 // ---- bucket join (the partitioned plan's join: pairs in no particular order) ----------------
@@ -1992,7 +2031,8 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
         Timed t(c, xm ? "sort_pass_carry" : prof_split() ? "sort_pass2" : name,
                 (w32 ? 8.0 : 16.0 + 2.0 * (double)(xm ? xsz : 0)) * n);
         auto kern = w32       ? tl_pass2_kernel<K, X_NONE, true, true>
-                    : xm == X64 ? (uns ? tl_pass2_kernel<K, X64, true> : tl_pass2_kernel<K, X64, false>)
+                    : xm == X64 ? (uns ? (x64_staged() ? tl_pass2_kernel<K, X64, true, false, true> : tl_pass2_kernel<K, X64, true>)
+                                       : (x64_staged() ? tl_pass2_kernel<K, X64, false, false, true> : tl_pass2_kernel<K, X64, false>))
                     : xm      ? tl_pass2_kernel<K, X32, true>   // (the X32 / XCOL first pass is unstable too)
                               : (uns ? tl_pass2_kernel<K, X_NONE, true> : tl_pass2_kernel<K, X_NONE, false>);
         hipLaunchKernelGGL(kern, dim3(xcd_grid(nseg)), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8, seg, gcnt, G,
