@@ -58,7 +58,10 @@ def gen_chain(ctx, rows: int, seed: int, key_domain: int, row_start: int = 0):
     return [ctx.gen_relation(rows, kinds, seed=seed, gen_rel=r, row_start=row_start) for r in range(4)]
 
 
-def roofline(stats: dict, traffic: dict | None):
+def roofline(stats: dict, traffic: dict | None, steps: int | None = None):
+    """the dominant stage: algorithmic bytes per launch / mean launch time (HIP events), and its
+    PMC traffic per launch = the stage's PMC bytes per query / its launches per step (`steps` =
+    queries behind `stats`) -- both sides over the same launch set"""
     if not stats:
         return None
     name, s = max(stats.items(), key=lambda kv: kv[1]["ms"])
@@ -67,14 +70,21 @@ def roofline(stats: dict, traffic: dict | None):
     achieved = per_launch_bytes / (per_launch_ms * 1e-3) / 1e9 if per_launch_ms > 0 else 0.0
     t = None
     if traffic and name in traffic:
-        t = traffic[name]
+        tq = traffic[name].get("per_query")
+        if tq and steps and s["launches"]:
+            t = round(tq / (s["launches"] / steps))
+        elif tq is None:
+            t = traffic[name].get("per_dispatch")      # workloads profiled without a query count
     return {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": t,
             "alg_bytes_per_launch": per_launch_bytes, "avg_launch_ms": round(per_launch_ms, 4),
             "launches": s["launches"]}
 
 
-def stage_roofline(stats: dict, traffic: dict | None) -> dict:
+def stage_roofline(stats: dict, traffic: dict | None, steps: int) -> dict:
+    """every stage against the same roofline; `traffic_over_alg` = the stage's PMC bytes per query
+    (all of its dispatches) / its algorithmic bytes per step (all of its `Timed` launches) -- a
+    per-query ratio, so a stage whose timer spans several dispatches is not misreported"""
     out = {}
     for name, s in sorted(stats.items(), key=lambda kv: -kv[1]["ms"]):
         if not s["launches"] or s["ms"] <= 0 or not s["alg_bytes"]:
@@ -82,11 +92,25 @@ def stage_roofline(stats: dict, traffic: dict | None) -> dict:
         per_ms = s["ms"] / s["launches"]
         per_b = s["alg_bytes"] / s["launches"]
         gbs = per_b / (per_ms * 1e-3) / 1e9
-        t = traffic.get(name) if traffic else None
+        tq = (traffic.get(name) or {}).get("per_query") if traffic else None
+        alg_q = s["alg_bytes"] / steps
         out[name] = {"launches": s["launches"], "avg_launch_ms": round(per_ms, 4), "alg_gb_per_launch": round(per_b / 1e9, 4),
                      "achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 3),
-                     "traffic_over_alg": round(t / per_b, 3) if t else None}
+                     "alg_gb_per_query": round(alg_q / 1e9, 4),
+                     "pmc_gb_per_query": round(tq / 1e9, 4) if tq else None,
+                     "traffic_over_alg": round(tq / alg_q, 3) if tq else None}
     return out
+
+
+def infer_queries(command: str):
+    """queries a profiled `bench.py` c3 plan command ran: warmup + 2 x steps (the stage-table loop
+    and the timed loop; tools/pmc_traffic.py records it as "queries" from round 4 on)"""
+    import re
+    m_s = re.search(r"--steps (\d+)", command or "")
+    m_w = re.search(r"--warmup (\d+)", command or "")
+    if not m_s or "bench.py" not in command or "--workload c4" in command or "--workload c5" in command:
+        return None
+    return (int(m_w.group(1)) if m_w else 2) + 2 * int(m_s.group(1))
 
 
 def load_traffic(workload: str = "c3"):
@@ -100,7 +124,15 @@ def load_traffic(workload: str = "c3"):
             continue
         if d.get("workload", "c3") != workload:
             continue
-        return {k: v.get("hbm_bytes_per_launch") for k, v in d.get("kernels", {}).items()}
+        q = d.get("queries") or infer_queries(d.get("command", ""))
+        out = {}
+        for k, v in d.get("kernels", {}).items():
+            pq = v.get("hbm_bytes_per_query")
+            if pq is None and q and v.get("launches_fetch_pass"):
+                pq = v["hbm_bytes_per_launch"] * v["launches_fetch_pass"] / q
+            out[k] = {"per_dispatch": v.get("hbm_bytes_per_launch"), "per_query": pq}
+        out["_file"] = os.path.relpath(path, ROOT)
+        return out
     return None
 
 
@@ -225,6 +257,7 @@ def run_dist(args):
                              "value": round(ctx.last_result_rows() * args.steps / dtf, 1),
                              "stdout_identical": faithful == out}
         kern = sorted(stage_stats.items(), key=lambda kv: -kv[1]["ms"])
+        traffic = load_traffic("c3_plan")
         res = {
             "metric": METRIC, "value": round(rows * args.steps / dt, 1), "unit": "joined tuples/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -243,7 +276,7 @@ def run_dist(args):
                        "parallelism": f"hash-partitioned dp{world}" if multi else "partitioned plan, one rank"},
             "faithful_executor": faithful_line,
             "roofline": roofline({dominant: stats[dominant]} if dominant in stats else stats,
-                                 load_traffic("c3_plan")),
+                                 traffic, args.steps),
             # the stage table's loop (every launch timed): kernel time and host round trips per step
             "kernel_ms_per_step": round(sum(s["ms"] for _, s in kern) / args.steps, 3),
             "host_round_trips_per_step": stage_stats.get("host_round_trip", {}).get("launches", 0) / args.steps,
@@ -251,7 +284,8 @@ def run_dist(args):
             "stages": {k: {"ms_per_step": round(s["ms"] / args.steps, 3)} for k, s in kern[:12]},
             # every stage against the same roofline (algorithmic bytes per launch / mean launch time
             # of the stage-table loop), with its PMC traffic ratio where profiles/ has one
-            "stage_roofline": stage_roofline(stage_stats, load_traffic("c3_plan")),
+            "stage_roofline": stage_roofline(stage_stats, traffic, args.steps),
+            "pmc_source": traffic.get("_file") if traffic else None,
         }
         if not args.no_cpu:
             res["cpu_baseline"] = cpu_baseline(args.cpu_rows, args.seed, ctx)
@@ -326,7 +360,7 @@ def run_single(args):
         "all_lists_materialised": {"ms_per_step": round(dt_all / args.steps * 1e3, 3),
                                    "value": round(rows * args.steps / dt_all, 1),
                                    "stdout_identical": out_all == out},
-        "roofline": roofline(stats, load_traffic()),
+        "roofline": roofline(stats, load_traffic(), args.steps),
         "kernel_ms_per_step": round(total_kernel_ms, 3),
         "stages": {k: {"ms_per_step": round(s["ms"] / args.steps, 3), "launches_per_step": s["launches"] / args.steps,
                        "GBps": round(s["alg_bytes"] / (s["ms"] * 1e-3) / 1e9, 1) if s["ms"] > 0 else None}
@@ -341,9 +375,114 @@ def run_single(args):
     return res
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """`--gpus N` with no launcher around us: start N rank processes of this script (RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* set, one per GPU) and relay rank 0's JSON line.  This
+    process never imports torch nor touches a GPU (a GPU-initialised process must not spawn the
+    ranks' runtimes under it); a rank that exits non-zero ends the others and the launch."""
+    import subprocess
+    import tempfile
+    port = free_port()
+    out0 = tempfile.TemporaryFile(mode="w+")
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), QE_BENCH_LAUNCHER="bench.py")
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=out0 if r == 0 else sys.stderr))
+    rc = 0
+    try:
+        while True:
+            live = [p for p in procs if p.poll() is None]
+            bad = [p for p in procs if p.returncode not in (None, 0)]
+            if bad:
+                rc = bad[0].returncode
+                log(f"[bench] rank {procs.index(bad[0])} exited with status {rc}; stopping the other ranks")
+                break
+            if not live:
+                break
+            time.sleep(0.2)
+    finally:
+        for p in procs:                       # only the processes started here, by their Popen handles
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    if rc:
+        return rc if rc > 0 else 1
+    out0.seek(0)
+    lines = [ln for ln in out0.read().splitlines() if ln.strip()]
+    ours = [ln for ln in lines if ln.startswith("{")]
+    for ln in lines:                          # gloo's own chatter on rank 0's stdout goes to stderr
+        if not ln.startswith("{"):
+            log(ln)
+    for ln in ours:
+        print(ln, flush=True)
+    return 0 if ours else 1
+
+
+def check_world(args) -> tuple[int, int, int]:
+    """(rank, world, local_rank) of this process; exits non-zero when the launch does not match
+    `--gpus` or when this node has fewer GPUs than ranks (never a silent one-rank line)."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE={world}: the launcher and the flag disagree")
+        sys.exit(2)
+    if not args.dry_launch:
+        import torch
+        ngpu = torch.cuda.device_count()           # counting devices does not initialise them
+        if ngpu < world:
+            log(f"[bench] error: --gpus {world} but this node shows {ngpu} GPU(s); one rank per GPU is required")
+            sys.exit(3)
+    return rank, world, local
+
+
+def dry_launch(args):
+    """--dry-launch: every rank joins the gloo control plane and stops before any GPU work; rank 0
+    prints what the launch produced (the CPU test of the launcher)."""
+    import torch.distributed as dist
+    rank, world, local = check_world(args)
+    if world > 1:
+        dist.init_process_group("gloo")
+        got = [None] * world
+        dist.all_gather_object(got, {"rank": rank, "local_rank": local, "pid": os.getpid()})
+        dist.barrier()
+        dist.destroy_process_group()
+    else:
+        got = [{"rank": 0, "local_rank": 0, "pid": os.getpid()}]
+    if rank == 0:
+        return {"dry_launch": True, "world_size": world, "gpus": args.gpus, "workload": args.workload,
+                "launcher": os.environ.get("QE_BENCH_LAUNCHER", "external" if "WORLD_SIZE" in os.environ else "none"),
+                "ranks": got}
+    return None
+
+
+SCALE_NOTE = ("N > 1 runs one rank process per GPU (bench.py starts them itself, or runs under "
+              "torch.distributed.run); no 1/2/4/8-GPU curve has been measured by this build's author "
+              "(1-GPU pool) -- the N > 1 path was exercised with in-process ranks on one GPU")
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks = GPUs of this node (default: $WORLD_SIZE or 1); without a launcher, N > 1 "
+                         "starts N rank processes of this script")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="start the ranks, join the gloo control plane, stop before any GPU work (launcher test)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--rows", type=int, default=None,
@@ -367,7 +506,19 @@ def main():
                          "executor is timed beside it); faithful = qe_run_queries alone (N = 1); c5: dist = "
                          "the aggregate plan at N = 1 too")
     args = ap.parse_args()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus is None:
+        args.gpus = int(env_world or "1")
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.dry_launch:
+        res = dry_launch(args)
+        if res is not None:
+            print(json.dumps(res), flush=True)
+        return
+    _, world, _ = check_world(args)
     if args.rows is None and args.workload != "c5":
         args.rows = 100_000_000
     if args.workload == "c5":
@@ -387,6 +538,8 @@ def main():
     else:
         res = run_dist(args)
     if res is not None:
+        res["launcher"] = os.environ.get("QE_BENCH_LAUNCHER", "external (WORLD_SIZE set)" if env_world else "none")
+        res["scale_note"] = SCALE_NOTE
         print(json.dumps(res), flush=True)
 
 

@@ -30,6 +30,25 @@ METRIC = "input rows/sec, C5 2-relation Zipf(0.9) join, 1e9 rows/side (pairs cou
 
 gen_c5 = dg.gen_c5
 
+PATH_ONE_RANK = ("qe_run_queries_dist on one rank (the product default): the plan's last join of two base "
+                 "relations in aggregate form (engine join_agg, csrc/qe_comm.hip e_join_agg -> qe_join_aggregate, "
+                 "csrc/qe_agg.hip): per side a histogram read and the two-level sort's two lookback-free "
+                 "partition passes of (key field << 32 | select value) words into 2^15 buckets "
+                 "(partition_words_kv), then one counting workgroup per bucket (ab_bucket_kernel: S's key "
+                 "counts in LDS, R rows add pairs and valR*cnt, then R's counts, S rows add valS*cnt; head keys "
+                 "beyond 2^18 rows per bucket side on the chunked giant path)")
+PATH_N_RANKS = ("qe_run_queries_dist (host-C plan, include/qe_plan.h) over RCCL: e_join_agg at N ranks -- heavy "
+                "keys (sampled from the replicated key columns) counted over each rank's row slice and "
+                "all-reduced, light keys hash-bucketed locally from the replicated columns (bucket_select_dev) "
+                "and joined by the bucketed aggregate join above; sums all-reduced")
+
+
+def pinned_parity(rows: int, out: str, pairs: int):
+    """the line against the pinned 1e9 output (qe.datagen.C5_1E9_*); None at other sizes"""
+    if rows != dg.C5_ROWS:
+        return None
+    return out == dg.C5_1E9_STDOUT and pairs == dg.C5_1E9_PAIRS
+
 
 def cpu_sample(ctx, sample_rows: int, budget_note: str = "") -> dict:
     """oracle/cpu_ref, one core, on the first `sample_rows` rows of both relations (same Zipf
@@ -93,13 +112,13 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
         "data": "synthetic: qe.datagen.c5_spec(%d) generated in HBM (seed %d, Zipf %.1f, shared permutation)"
                 % (rows, dg.C5_SEED, dg.C5_THETA),
+        "parity": pinned_parity(rows, out, pairs),
+        "parity_detail": {"equals_pinned_c5_1e9": pinned_parity(rows, out, pairs),
+                          "pinned_by": "tests/test_gpu_fullsize_batch.py (sharded aggregate truth on the device columns)"},
         "config": {"workload": "C5: 2-relation join, %d rows/side, Zipf theta=%.1f keys, query %s"
                                % (rows, dg.C5_THETA, dg.C5_QUERY.strip()),
                    "pairs": pairs, "materialised": False,
-                   "path": "qe_run_queries_dist on one rank (the product default): the plan's last join of two "
-                           "base relations in aggregate form (engine join_agg -> csrc/qe_agg.hip): each side "
-                           "sorted once as (key, select value) words, one merge-path pass counting both sides' "
-                           "partners", "refused": refused,
+                   "path": PATH_ONE_RANK, "refused": refused,
                    "pairs_counted_per_s": round(pairs * args.steps / dt, 1),
                    "stdout": out, "parallelism": "single GPU"},
         "roofline": roofline_fn(stats, traffic_fn() if traffic_fn else None) if roofline_fn else None,
@@ -179,14 +198,11 @@ def run_dist(args, log) -> dict | None:
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u64",
             "data": "synthetic: qe.datagen.c5_spec(%d) generated in HBM on every rank (seed %d, Zipf %.1f)"
                     % (rows, dg.C5_SEED, dg.C5_THETA),
+            "parity": pinned_parity(rows, out, pairs),
             "config": {"workload": "C5: 2-relation join, %d rows/side in total, Zipf theta=%.1f keys, query %s"
                                    % (rows, dg.C5_THETA, q.strip()),
                        "pairs": pairs, "materialised": False, "refused": refused,
-                       "path": "qe_run_queries_dist (host-C plan, include/qe_plan.h): the last join of two base "
-                               "relations in the engine's aggregate form (csrc/qe_comm.hip e_join_agg) -- heavy "
-                               "keys split by row slice with all-reduced counts, light keys bucketed locally "
-                               "(qe_bucket_select) and joined by value-carrying sorts + one counting pass; "
-                               "sums all-reduced over RCCL",
+                       "path": PATH_N_RANKS if world > 1 else PATH_ONE_RANK,
                        "pairs_counted_per_s": round(pairs * args.steps / dt, 1),
                        "stdout": out,
                        "parallelism": f"hash buckets + heavy split x{world}" if world > 1 else "single GPU"},

@@ -229,6 +229,12 @@ C5_ROWS = 1_000_000_000
 C5_THETA = 0.9
 C5_PERM_SEED = 55
 C5_QUERY = "0 1|0.1=1.0|0.2 1.2\n"
+# C5 at its own size (C5_ROWS per side): the printed bytes and the pair count, pinned against the
+# key-range-sharded aggregate truth by tests/test_gpu_fullsize_batch.py (print_sums,
+# src/utilities.c:216-219, over the join of src/join.c:325-392); benchmarks/c5.py checks its
+# line against them in-run
+C5_1E9_STDOUT = "896635233956162571 9653025849244459604 \n"
+C5_1E9_PAIRS = 384016487678819
 
 
 def c5_spec(rows: int = C5_ROWS, theta: float = C5_THETA, domain: int | None = None) -> list[RelSpec]:

@@ -72,5 +72,21 @@ def test_c5_1e9_against_sharded_aggregate_truth(ctx):
         assert pairs > (1 << 46)                 # past the merge lookback's 46-bit pair field
         assert pairs_gpu == pairs
         assert out == f"{s0} {s1} \n"
+        # the constants bench.py --workload c5 checks its line against
+        assert (pairs, out) == (dg.C5_1E9_PAIRS, dg.C5_1E9_STDOUT)
+    finally:
+        ctx.drop_relations()
+
+
+def test_c5_1e9_plan_matches_pinned(ctx):
+    """the partitioned plan's own path at 1e9 rows (qe_run_queries_dist: the plan's e_join_agg
+    bookkeeping, not the faithful executor) against the pinned output"""
+    ctx.drop_relations()
+    try:
+        dg.gen_c5(ctx, dg.C5_ROWS)
+        out, rc, refused = ctx.run_dist(dg.C5_QUERY)
+        assert rc == 0 and refused == 0
+        assert ctx.last_result_rows() == dg.C5_1E9_PAIRS
+        assert out == dg.C5_1E9_STDOUT
     finally:
         ctx.drop_relations()

@@ -9,8 +9,12 @@ L2's memory-side requests; on gfx950 FETCH_SIZE reports 1/2 of the bytes of a wi
 streaming read, so it is doubled here (`fetch_corrected`); WRITE_SIZE is taken as is.  The two
 counters cannot share a pass, hence two runs of the same command.
 
-Kernels are mapped to the stage names libqe's own timers use (bench.py "stages"), so the
-roofline's `traffic` lines up with its `achieved` (same launches, per launch).
+Kernels are mapped to the stage names libqe's own timers use (bench.py "stages").  One libqe
+stage timer (`Timed`) may cover several dispatches (bucket_join_sums = the sums kernel + its
+reduce; sort_hist = the histogram + its column sums), so per-dispatch averages are NOT comparable
+with the bench's per-`Timed` launches: the comparable figure is bytes PER QUERY
+(`hbm_bytes_per_query` = all of the stage's dispatches in the profiled run / the queries it ran,
+`--queries`; bench.py's c3 loop with `--steps S --warmup W` runs W + 2 S of them).
 """
 import argparse
 import csv
@@ -112,6 +116,15 @@ def per_stage(disp, workload="c3"):
     return acc
 
 
+def infer_queries(command: str):
+    """bench.py's c3 plan loop runs warmup + 2 x steps queries (the stage table + the timed loop)"""
+    m_s = re.search(r"--steps (\d+)", command or "")
+    m_w = re.search(r"--warmup (\d+)", command or "")
+    if not m_s or "bench.py" not in command or "--workload c4" in command or "--workload c5" in command:
+        return None
+    return (int(m_w.group(1)) if m_w else 2) + 2 * int(m_s.group(1))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fetch", required=True)
@@ -119,7 +132,10 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--command", default="")
     ap.add_argument("--workload", default="c3")
+    ap.add_argument("--queries", type=int, default=None,
+                    help="queries the profiled command ran (bench.py c3 plan: warmup + 2 x steps)")
     a = ap.parse_args()
+    q = a.queries or infer_queries(a.command)
     f = per_stage(read_counter(a.fetch, "FETCH_SIZE"), a.workload)
     w = per_stage(read_counter(a.write, "WRITE_SIZE"), a.workload)
     kern = {}
@@ -132,8 +148,10 @@ def main():
         kern[st] = {"hbm_bytes_per_launch": round(hbm), "fetch_raw_bytes_per_launch": round(fpl) if fpl else None,
                     "fetch_corrected_bytes_per_launch": round(2 * fpl) if fpl else None,
                     "write_bytes_per_launch": round(wpl) if wpl else None, "launches_fetch_pass": fn,
-                    "launches_write_pass": wn, "kernels": sorted(names | names2)}
-    doc = {"command": a.command, "workload": a.workload,
+                    "launches_write_pass": wn, "kernels": sorted(names | names2),
+                    "hbm_bytes_per_query": round((2.0 * fk + wk) * 1024.0 / q) if q else None,
+                    "dispatches_per_query": round(fn / q, 3) if q else None}
+    doc = {"command": a.command, "workload": a.workload, "queries": q,
            "units": "bytes per launch; FETCH_SIZE/WRITE_SIZE KiB x 1024",
            "correction": "gfx950: FETCH_SIZE x2 (MI355X_MICROARCH.md HBM section); WRITE_SIZE as is",
            "kernels": kern}
