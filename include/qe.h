@@ -317,7 +317,8 @@ int  qe_counts_to_host(qe_ctx*, const uint32_t* d, uint64_t n, uint32_t* h);
 /* device memory in use / cached by the ctx allocator (bytes) */
 int  qe_mem_stats(qe_ctx*, uint64_t* in_use, uint64_t* cached);
 /* host -> HBM loads so far (qe_load_relation): wall seconds and bytes, PCIe and the pinned
- * staging included -- the loader of the reference, read_relations (src/utilities.c:124-162) */
+ * staging included, and the load-time layout work too (the column OR/AND read and the u32 copies
+ * of narrow columns) -- the loader of the reference, read_relations (src/utilities.c:124-162) */
 int  qe_load_stats(qe_ctx*, double* seconds, double* bytes);
 int  qe_mem_trim(qe_ctx*);
 

@@ -34,6 +34,26 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// A buffer descriptor over [p, p + bytes) built from wave-uniform inputs (readfirstlane'd so the
+// compiler can prove it: no waterfall loop around the loads).  Loads through it take a 32-bit
+// per-lane byte offset + a scalar one (one VGPR of addressing per stream instead of a 64-bit
+// address per load) and return 0 past `bytes` (the range check replaces the `i < n` guards).
+typedef unsigned int qe_v2u __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, uint32_t bytes) {
+    const uint64_t a = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const uint32_t n = __builtin_amdgcn_readfirstlane(bytes);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, (int)n, 0x00020000);
+}
+__device__ __forceinline__ uint2 buf_load_u2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    const qe_v2u x = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0);
+    return make_uint2(x.x, x.y);
+}
+__device__ __forceinline__ uint32_t buf_load_u32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
+}
+
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) v += shfl_xor_u64(v, m);

@@ -8,6 +8,7 @@
 #include <map>
 #include <stdexcept>
 #include <string>
+#include <unordered_set>
 #include <unordered_map>
 #include <vector>
 
@@ -126,7 +127,14 @@ struct qe_ctx {
     // small device scratch + pinned host mirror for scalar results
     uint64_t* d_scratch = nullptr;   // 64 words
     uint64_t* h_scratch = nullptr;   // pinned, 64 words
-    hipEvent_t wait_ev = nullptr;    // polled for scalar results (read_u64 / read_words)
+    hipEvent_t wait_ev = nullptr;    // polled for scalar results (read_u64 / read_words, QE_WAIT=event)
+    // device blocks a batch's shared sort holds (qe_sort_cache): dfree of one of them is a bug
+    // (a lane returning shared words to its allocator while other lanes read them -- the round-3
+    // fault) and throws instead of recycling the block
+    std::unordered_set<const void*> pinned;
+    uint64_t* h_ret = nullptr;       // pinned coherent host words: [0] = sequence flag, [1..] = the result
+    uint64_t* d_ret = nullptr;       // (h_ret as the device addresses it)
+    uint64_t ret_seq = 0;            // the last sequence number published
 
     // loader (qe_load_relation): pinned staging ring for pageable host columns
     static constexpr int STAGE_SLOTS = 3;

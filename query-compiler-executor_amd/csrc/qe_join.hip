@@ -1707,9 +1707,15 @@ static bool sort_cached(qe_ctx* c, qe_pairs* p, bool defer) {
         SortCacheEntry& slot = sc->m[key];
         slot.owner = c;
         lk.unlock();
+        // everything that can throw before the entry is published sits in this try: a slot left
+        // unready would block every other lane that needs the column forever
+        hipEvent_t ev = nullptr;
         try {
+            QE_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
             sort_pairs_raw(c, p, defer);
+            QE_HIP(hipEventRecord(ev, c->stream));
         } catch (...) {
+            if (ev) (void)hipEventDestroy(ev);
             lk.lock();
             sc->m.erase(key);
             sc->cv.notify_all();
@@ -1717,20 +1723,21 @@ static bool sort_cached(qe_ctx* c, qe_pairs* p, bool defer) {
         }
         SortCacheEntry e;
         e.owner = c;
+        e.ev = ev;
         auto dit = c->deferred.find(p->key);
         if (dit != c->deferred.end()) {
             dit->second.shared = true;   // this pairs' own key / row buffers stay its own
             e.deferred = true;
             e.d = dit->second;
+            c->pinned.insert({e.d.words, e.d.bstart, e.d.d_max});   // freed only when the batch ends
         } else {
             e.keys = p->key;
             e.vals = p->val;
             e.own_keys = (p->owns & 1) != 0;
             e.own_vals = (p->owns & 2) != 0;
             p->owns &= ~3u;                  // lent by the cache from now on
+            c->pinned.insert({(const void*)e.keys, (const void*)e.vals});
         }
-        QE_HIP(hipEventCreateWithFlags(&e.ev, hipEventDisableTiming));
-        QE_HIP(hipEventRecord(e.ev, c->stream));
         e.ready = true;
         lk.lock();
         sc->m[key] = e;
@@ -1794,6 +1801,7 @@ int qe_sort_cache(qe_ctx* c, int on) {
     for (auto& kv : sc->m) {
         SortCacheEntry& e = kv.second;
         qe_ctx* o = e.owner;
+        o->pinned.clear();
         if (e.deferred) {
             dfree(o, e.d.words);
             dfree(o, e.d.bstart);

@@ -63,6 +63,7 @@ void* dalloc(qe_ctx* c, size_t bytes) {
 
 void dfree(qe_ctx* c, void* p) {
     if (!p) return;
+    if (!c->pinned.empty() && c->pinned.count(p)) throw Error(QE_EINVAL, "internal: dfree of a shared sort's buffer");
     auto it = c->live.find(p);
     if (it == c->live.end()) return;   // not ours (e.g. a relation column)
     size_t sz = it->second;
@@ -183,20 +184,39 @@ void sync(qe_ctx* c) {
     QE_HIP(hipStreamSynchronize(c->stream));
 }
 
-// Wait for a scalar result the host needs to go on (a list length, a pair count, a sum): the
-// host polls an event instead of sleeping in hipStreamSynchronize, so the next launches follow
-// the result by a few microseconds (the trace showed ~22 us between such a read and the next
-// kernel, ~16 of them per C3 query).  QE_SPIN_WAIT=0 restores the blocking wait.
-static void wait_result(qe_ctx* c) {
-    count_round_trip(c);
-    static const bool spin = [] {
-        const char* s = getenv("QE_SPIN_WAIT");
-        return !(s && s[0] == '0');
-    }();
-    if (!spin) {
-        QE_HIP(hipStreamSynchronize(c->stream));
-        return;
+// Scalar results the host needs to go on (a list length, a pair count, a sum): one kernel copies
+// them from HBM into pinned coherent host memory and then raises a sequence number there (a
+// system-scope release: one wave, so its lanes' stores are all ordered before the flag); the host
+// spins on that word in its own memory -- no HIP runtime call in the wait loop.  The round-3 wait
+// (hipEventQuery spun by up to 8 lane threads at once) took ~22 us less per result than
+// hipStreamSynchronize but crashed inside the runtime under rocprofv3's kernel trace with the
+// bench's timing events on.  A wait longer than ~2 ms blocks in
+// hipStreamSynchronize once (which also surfaces a faulted stream) before the flag is re-read.
+// QE_WAIT=event: the round-3 event spin; QE_WAIT=sync: copy + hipStreamSynchronize.
+constexpr int RET_WORDS = 512;
+__global__ void __launch_bounds__(256) publish_kernel(const uint64_t* __restrict__ d, int n, uint64_t* out,
+                                                      uint64_t seq) {
+    for (int i = threadIdx.x; i < n; i += 256)
+        __hip_atomic_store(&out[1 + i], d[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(&out[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+enum { WAIT_FLAG = 0, WAIT_EVENT = 1, WAIT_SYNC = 2 };
+static int wait_mode() {
+    static const int m = [] {
+        const char* s = getenv("QE_WAIT");
+        if (const char* o = getenv("QE_SPIN_WAIT"); o && o[0] == '0') return (int)WAIT_SYNC;   // (round-3 knob)
+        if (!s) return (int)WAIT_FLAG;
+        return !strcmp(s, "event") ? (int)WAIT_EVENT : !strcmp(s, "sync") ? (int)WAIT_SYNC : (int)WAIT_FLAG;
+    }();
+    return m;
+}
+
+static void wait_event(qe_ctx* c) {
     if (!c->wait_ev) QE_HIP(hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming));
     QE_HIP(hipEventRecord(c->wait_ev, c->stream));
     hipError_t e;
@@ -205,16 +225,44 @@ static void wait_result(qe_ctx* c) {
     QE_HIP(e);
 }
 
-uint64_t read_u64(qe_ctx* c, const uint64_t* d) {
-    QE_HIP(hipMemcpyAsync(c->h_scratch, d, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
-    wait_result(c);
-    return c->h_scratch[0];
+// h[0..n) = d[0..n) (device words), the one host round trip of a result
+void read_words(qe_ctx* c, const uint64_t* d, uint64_t* h, int n) {
+    count_round_trip(c);
+    const int mode = wait_mode();
+    if (mode != WAIT_FLAG || n > RET_WORDS) {
+        QE_HIP(hipMemcpyAsync(c->h_scratch, d, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+        if (mode == WAIT_EVENT) wait_event(c);
+        else QE_HIP(hipStreamSynchronize(c->stream));
+        memcpy(h, c->h_scratch, n * sizeof(uint64_t));
+        return;
+    }
+    if (!c->h_ret) {
+        QE_HIP(hipHostMalloc((void**)&c->h_ret, (1 + RET_WORDS) * sizeof(uint64_t),
+                             hipHostMallocCoherent | hipHostMallocMapped));
+        QE_HIP(hipHostGetDevicePointer((void**)&c->d_ret, c->h_ret, 0));
+        __atomic_store_n(&c->h_ret[0], 0ull, __ATOMIC_RELEASE);
+        c->ret_seq = 0;
+    }
+    const uint64_t seq = ++c->ret_seq;
+    hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(256), 0, c->stream, d, n, c->d_ret, seq);
+    QE_HIP(hipGetLastError());
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spins = 1; __atomic_load_n(&c->h_ret[0], __ATOMIC_ACQUIRE) != seq; spins++) {
+        if ((spins & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(2000)) {
+            QE_HIP(hipStreamSynchronize(c->stream));   // a long wait: block once (errors surface here)
+            if (__atomic_load_n(&c->h_ret[0], __ATOMIC_ACQUIRE) != seq)
+                throw Error(QE_EINVAL, "internal: a result's sequence flag never arrived");
+            break;
+        }
+        __builtin_ia32_pause();
+    }
+    for (int i = 0; i < n; i++) h[i] = __atomic_load_n(&c->h_ret[1 + i], __ATOMIC_RELAXED);
 }
 
-void read_words(qe_ctx* c, const uint64_t* d, uint64_t* h, int n) {
-    QE_HIP(hipMemcpyAsync(c->h_scratch, d, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
-    wait_result(c);
-    memcpy(h, c->h_scratch, n * sizeof(uint64_t));
+uint64_t read_u64(qe_ctx* c, const uint64_t* d) {
+    uint64_t v;
+    read_words(c, d, &v, 1);
+    return v;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -381,7 +429,7 @@ static void free_relation(Relation& r) {
 // column statistics: OR / AND of every column, one read at load time (zone-map style metadata
 // that lets the radix sort plan its passes without a reduction pass per query); and a u32 copy of
 // every column whose values fit 32 bits -- the relation's second layout in HBM, the one the
-// sorts' first passes read (QE_NARROW=0: none)
+// sorts' first passes read (QE_NARROW=0: none; a copy that does not fit in memory is skipped)
 static void column_stats(qe_ctx* c, Relation& r) {
     r.kor.resize(r.cols.size());
     r.kand.resize(r.cols.size());
@@ -398,7 +446,12 @@ static void column_stats(qe_ctx* c, Relation& r) {
         for (size_t j = 0; j < r.cols.size(); j++) {
             if ((r.kor[j] >> 32) || !r.rows) continue;
             uint32_t* d = nullptr;
-            QE_HIP(hipMalloc(&d, r.rows * sizeof(uint32_t)));
+            if (hipMalloc(&d, r.rows * sizeof(uint32_t)) != hipSuccess) {
+                // best effort: a relation near the memory limit loads without its u32 copies
+                // (every reader of cols32 takes the u64 column when the copy is null)
+                (void)hipGetLastError();
+                continue;
+            }
             r.cols32[j] = d;
             hipLaunchKernelGGL(narrow_kernel, dim3(grid_for(r.rows, 256 * 8, 16384)), dim3(256), 0, c->stream,
                                r.cols[j], r.rows, d);
@@ -498,6 +551,7 @@ void qe_fini(qe_ctx* c) {
     if (c->lb_tickets) (void)hipFree(c->lb_tickets);
     if (c->d_scratch) (void)hipFree(c->d_scratch);
     if (c->h_scratch) (void)hipHostFree(c->h_scratch);
+    if (c->h_ret) (void)hipHostFree(c->h_ret);
     if (c->wait_ev) (void)hipEventDestroy(c->wait_ev);
     for (int k = 0; k < qe_ctx::STAGE_SLOTS; k++) {
         if (c->h_stage[k]) (void)hipHostFree(c->h_stage[k]);
@@ -556,9 +610,9 @@ int qe_load_relation(qe_ctx* c, uint64_t rows, uint64_t ncols, const uint64_t* c
             h2d_staged(c, d, host_cols[j], rows * sizeof(uint64_t));
     }
     QE_HIP(hipStreamSynchronize(c->stream));
+    column_stats(c, r);   // (its OR/AND read and u32 copies are part of the load: timed with it)
     c->load_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     c->load_bytes += (double)rows * ncols * sizeof(uint64_t);
-    column_stats(c, r);
     guard.keep = true;
     c->rels.push_back(std::move(r));
     return (int)c->rels.size() - 1;

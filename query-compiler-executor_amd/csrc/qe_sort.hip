@@ -1410,6 +1410,11 @@ __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
 // limit anyway: 67 KB each fits) and written to outRX with the partner.  (Re-reading R's rowids or
 // payloads from L2 at emission instead measured 0.2-0.5 ms slower per C3 query.)
 constexpr uint32_t HJ_NONE = 0xFFFFu;
+// A lane's k-th partner is k links down its key's chain, so emission costs sum(k) per S row:
+// quadratic in a long chain (thousands of equal keys on both sides of one bucket).  A bucket with
+// a chain longer than HJ_CHAIN_MAX is flagged like one beyond LDS, and the join takes the sorts +
+// merge path (linear in the pairs) instead.
+constexpr uint32_t HJ_CHAIN_MAX = 64;
 #ifndef QE_HJ_RR_GLOBAL
 #define QE_HJ_RR_GLOBAL 0
 #endif
@@ -1438,7 +1443,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
     constexpr int NW = NT / 64;
     __shared__ uint32_t tab[HJ_I * NW];
     __shared__ uint64_t s_excl;
-    __shared__ uint32_t s_total;
+    __shared__ uint32_t s_total, s_long;
     const uint32_t b = blockIdx.x;
     const uint32_t r0 = bsR[b], mR = bsR[b + 1] - r0, s0 = bsS[b], mS = bsS[b + 1] - s0;
     if (mR > (uint32_t)(NT * HJ_I) || mS > (uint32_t)(NT * HJ_I)) {   // beyond LDS (the sorts were not checked): flag it
@@ -1475,6 +1480,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
         }
     }
     for (uint32_t v = threadIdx.x; v < D; v += NT) head[v] = HJ_NONE;
+    if (threadIdx.x == 0) s_long = 0;
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < HJ_I; j++) {
@@ -1492,7 +1498,8 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
         uint32_t cnt = 0, h = HJ_NONE;
         if ((uint32_t)j * NT + threadIdx.x < mS) {
             h = head[fld(ws[j]) & dmask];
-            for (uint32_t p = h; p != HJ_NONE; p = nxt[p]) cnt++;
+            for (uint32_t p = h; p != HJ_NONE && cnt <= HJ_CHAIN_MAX; p = nxt[p]) cnt++;
+            if (cnt > HJ_CHAIN_MAX) s_long = 1;
         }
         hd[j] = h;
         const uint32_t inc = wave_incl_scan_u32(cnt);
@@ -1501,6 +1508,10 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
         if (l == 63) tab[j * NW + w] = inc;
     }
     __syncthreads();
+    if (s_long) {   // block-uniform: a chain too long to emit by walking (the sorts + merge take the join)
+        if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(total_out + 1), 1ull);
+        return;
+    }
     if (w == 0) {   // (row group, wave) totals in row order -> bucket offsets; one atomic per bucket
         constexpr uint32_t E = HJ_I * NW;
         const uint32_t a0 = 2u * l < E ? tab[2 * l] : 0u, a1 = 2u * l + 1 < E ? tab[2 * l + 1] : 0u;
@@ -2790,7 +2801,12 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
 // PERSIST: a resident grid, each workgroup walking buckets blockIdx.x, + gridDim.x, ... with its
 // sums kept in registers across them and reduced once (the per-bucket form reduces and stores
 // five u64 sums per bucket); part is indexed by workgroup in both forms.
-template <bool PERSIST = false>
+// XK: S's carried payload -- 0 none, 1 u32 (xS32), 2 u64 (xS).  Every S word and payload is held as
+// 32-bit halves, so a row's key field dies at its count lookup and no payload register exists when
+// no select reads one: with five u64 sums across the walk, the form that held (word, payload) as
+// u64 pairs spilled 17 VGPRs at the 64-register occupancy target (0.31 GB of scratch writes per
+// C3 launch).
+template <bool PERSIST = false, int XK = 2>
 __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
 tl_hjoin_sums_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict__ bsR,
                      const uint64_t* __restrict__ wS, const uint32_t* __restrict__ bsS, int L,
@@ -2800,24 +2816,47 @@ tl_hjoin_sums_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict
     __shared__ uint64_t red[HJ_NW][HJ_SUMS + 1];
     const uint32_t D = 1u << L, dmask = D - 1u;
     const int w = wave_id(), l = lane_id();
-    uint64_t acc[HJ_SUMS + 1];
-#pragma unroll
-    for (int s = 0; s <= HJ_SUMS; s++) acc[s] = 0;
+    // the sums as five named registers: an array of them became one padded 16-VGPR vector
+    // register tuple (copied whole on every update) in the persistent loop
+    uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, ap = 0;
+    static_assert(HJ_SUMS == 4, "one named accumulator per select");
+#define QE_ACC(s) (*((s) == 0 ? &a0 : (s) == 1 ? &a1 : (s) == 2 ? &a2 : &a3))
     const uint32_t step = PERSIST ? gridDim.x : (uint32_t)TL_BUCKETS;
+    const uint32_t o8 = threadIdx.x * 8u, o4 = threadIdx.x * 4u;   // the loads' only per-lane addressing
+    // R's key fields: a u32 array, or the high halves of its u64 words
+    const uint32_t rstride = r32 ? 4u : 8u, oR = r32 ? o4 : o8 + 4u;
     for (uint32_t b = blockIdx.x; b < (uint32_t)TL_BUCKETS; b += step) {   // block-uniform
         const uint32_t r0 = bsR[b], mR = bsR[b + 1] - r0, s0 = bsS[b], mS = bsS[b + 1] - s0;
         if (mR > (uint32_t)TL_CAP || mS > (uint32_t)TL_CAP) {   // beyond LDS: the host takes the other path
             if (threadIdx.x == 0) atomicOr(flag, 1ull);
             continue;
         }
+        // this bucket's slices as buffer descriptors: rows past the bucket read as 0
+        const auto rR = buf_rsrc(reinterpret_cast<const uint32_t*>(wR) + (r32 ? r0 : 2u * r0), mR * rstride);
+        const auto rS = buf_rsrc(wS + s0, mS * 8u);
         uint32_t fr[HJ_I];   // R's key fields only (its rows are never read)
-        uint64_t ws[HJ_I], xv[HJ_I];
+        uint32_t fs[HJ_I], sl[HJ_I];   // S's key field, S's word's low half (rowid or value)
+        uint32_t xl[XK ? HJ_I : 1], xh[XK == 2 ? HJ_I : 1];   // S's payload halves
 #pragma unroll
         for (int j = 0; j < HJ_I; j++) {
-            const uint32_t i = (uint32_t)j * HJ_NT + threadIdx.x;
-            fr[j] = i < mR ? (r32 ? reinterpret_cast<const uint32_t*>(wR)[r0 + i] : fld(wR[r0 + i])) : 0u;
-            ws[j] = i < mS ? wS[s0 + i] : 0;
-            xv[j] = xS32 && i < mS ? (uint64_t)xS32[s0 + i] : xS && i < mS ? xS[s0 + i] : 0ull;
+            fr[j] = buf_load_u32(rR, oR, (uint32_t)j * HJ_NT * rstride);
+            const uint2 ws = buf_load_u2(rS, o8, (uint32_t)j * HJ_NT * 8u);
+            fs[j] = ws.y;
+            sl[j] = ws.x;
+        }
+        if constexpr (XK == 1) {
+            const auto rX = buf_rsrc(xS32 + s0, mS * 4u);
+#pragma unroll
+            for (int j = 0; j < HJ_I; j++) xl[j] = buf_load_u32(rX, o4, (uint32_t)j * HJ_NT * 4u);
+        }
+        if constexpr (XK == 2) {
+            const auto rX = buf_rsrc(xS + s0, mS * 8u);
+#pragma unroll
+            for (int j = 0; j < HJ_I; j++) {
+                const uint2 x = buf_load_u2(rX, o8, (uint32_t)j * HJ_NT * 8u);
+                xl[j] = x.x;
+                xh[j] = x.y;
+            }
         }
         if (PERSIST) __syncthreads();   // the previous bucket's lookups are done with cnt
         for (uint32_t v = threadIdx.x; v < D; v += HJ_NT) cnt[v] = 0;
@@ -2829,8 +2868,8 @@ tl_hjoin_sums_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict
         uint32_t c[HJ_I];
 #pragma unroll
         for (int j = 0; j < HJ_I; j++) {
-            c[j] = (uint32_t)j * HJ_NT + threadIdx.x < mS ? cnt[fld(ws[j]) & dmask] : 0u;
-            acc[HJ_SUMS] += c[j];
+            c[j] = (uint32_t)j * HJ_NT + threadIdx.x < mS ? cnt[fs[j] & dmask] : 0u;
+            ap += c[j];
         }
 #pragma unroll
         for (int s = 0; s < HJ_SUMS; s++) {
@@ -2838,22 +2877,32 @@ tl_hjoin_sums_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict
                 const uint64_t* __restrict__ col = sc.col[s];
                 const int src = sc.src[s] & 3;
                 const bool own = (sc.src[s] & 4) != 0;   // the carried list holds the values (QE_PLAN_VALUES_SRC)
-                uint64_t v[HJ_I];
+                uint32_t id[HJ_I];
 #pragma unroll
-                for (int j = 0; j < HJ_I; j++) {   // every gather of the select in flight together
-                    const uint32_t id = src == 0 ? (uint32_t)ws[j] : src == 1 ? (uint32_t)xv[j] : (uint32_t)(xv[j] >> 32);
-                    v[j] = own ? (uint64_t)id : c[j] ? col[id] : 0ull;
+                for (int j = 0; j < HJ_I; j++) {
+                    if constexpr (XK == 0) id[j] = sl[j];
+                    else if constexpr (XK == 1) id[j] = src == 0 ? sl[j] : xl[j];
+                    else id[j] = src == 0 ? sl[j] : src == 1 ? xl[j] : xh[j];
                 }
+                if (own) {   // c * value: one 32 x 32 -> 64 multiply-add per row
 #pragma unroll
-                for (int j = 0; j < HJ_I; j++) acc[s] += (uint64_t)c[j] * v[j];
+                    for (int j = 0; j < HJ_I; j++) QE_ACC(s) += (uint64_t)c[j] * id[j];
+                } else {
+                    uint64_t v[HJ_I];
+#pragma unroll
+                    for (int j = 0; j < HJ_I; j++) v[j] = c[j] ? col[id[j]] : 0ull;   // every gather in flight together
+#pragma unroll
+                    for (int j = 0; j < HJ_I; j++) QE_ACC(s) += (uint64_t)c[j] * v[j];
+                }
             }
         }
     }
 #pragma unroll
     for (int s = 0; s <= HJ_SUMS; s++) {
-        const uint64_t t = wave_sum_u64(acc[s]);
+        const uint64_t t = wave_sum_u64(s == HJ_SUMS ? ap : QE_ACC(s));
         if (l == 0) red[w][s] = t;
     }
+#undef QE_ACC
     __syncthreads();
     if (threadIdx.x <= HJ_SUMS) {
         uint64_t t = 0;
@@ -2907,16 +2956,20 @@ bool bucket_join_sums(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const HjS
         }();
         static const bool persist = !(getenv("QE_HJ_SUMS_PERSIST") && getenv("QE_HJ_SUMS_PERSIST")[0] == '0');
         const uint32_t grid = persist ? std::min<uint32_t>(resident, TL_BUCKETS) : (uint32_t)TL_BUCKETS;
+        // S's payload as the kernel holds it: none when no select reads one, else u32 or u64
+        const int xk = !carry ? 0 : dS.x32 ? 1 : 2;
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(HJ_NT), 0, c->stream, dR.words, dR.bstart, dS.words, dS.bstart,
+                               dR.L, carry ? dS.x : nullptr, sc, part,
+                               reinterpret_cast<unsigned long long*>(out + HJ_SUMS + 1), carry ? dS.x32 : nullptr,
+                               dR.w32 ? 1 : 0);
+        };
         if (persist)
-            hipLaunchKernelGGL(tl_hjoin_sums_kernel<true>, dim3(grid), dim3(HJ_NT), 0, c->stream, dR.words, dR.bstart,
-                               dS.words, dS.bstart, dR.L, carry ? dS.x : nullptr, sc, part,
-                               reinterpret_cast<unsigned long long*>(out + HJ_SUMS + 1), carry ? dS.x32 : nullptr,
-                               dR.w32 ? 1 : 0);
+            xk == 0 ? go(tl_hjoin_sums_kernel<true, 0>) : xk == 1 ? go(tl_hjoin_sums_kernel<true, 1>)
+                                                        : go(tl_hjoin_sums_kernel<true, 2>);
         else
-            hipLaunchKernelGGL(tl_hjoin_sums_kernel<false>, dim3(grid), dim3(HJ_NT), 0, c->stream, dR.words, dR.bstart,
-                               dS.words, dS.bstart, dR.L, carry ? dS.x : nullptr, sc, part,
-                               reinterpret_cast<unsigned long long*>(out + HJ_SUMS + 1), carry ? dS.x32 : nullptr,
-                               dR.w32 ? 1 : 0);
+            xk == 0 ? go(tl_hjoin_sums_kernel<false, 0>) : xk == 1 ? go(tl_hjoin_sums_kernel<false, 1>)
+                                                         : go(tl_hjoin_sums_kernel<false, 2>);
         QE_HIP(hipGetLastError());
         hipLaunchKernelGGL(hjoin_sums_reduce_kernel, dim3(HJ_SUMS + 1), dim3(256), 0, c->stream, part, grid, out);
         QE_HIP(hipGetLastError());

@@ -120,6 +120,23 @@ def test_bucket_join_fallbacks(ctx, shape):
         _check(ctx, rk, sk, gathered=True, expect=False)
 
 
+def test_bucket_join_long_chain_in_one_bucket_is_linear(ctx):
+    """~3000 equal keys on BOTH sides of one bucket that still fits LDS (9 M pairs from one key):
+    the chain join would emit each pair k links down the chain (quadratic: minutes in one
+    workgroup); a chain past HJ_CHAIN_MAX flags the bucket and the sorts + merge join take it"""
+    import time
+    rng = np.random.default_rng(11)
+    n = 3_000_000
+    rk = rng.integers(0, 1 << 24, n, dtype=np.uint64)
+    sk = rng.integers(0, 1 << 24, n, dtype=np.uint64)
+    rk[:3000] = 12345
+    sk[:3000] = 12345
+    t0 = time.time()
+    P = _check(ctx, rk, sk, gathered=True, expect=True)
+    assert P >= 9_000_000
+    assert time.time() - t0 < 30
+
+
 def test_bucket_join_materialisation_limit(ctx):
     n = 3_000_000
     rng = np.random.default_rng(9)
