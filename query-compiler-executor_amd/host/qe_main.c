@@ -19,6 +19,10 @@
  *                 qe_run_queries_lanes)
  *   QE_LOCAL_RANKS=N  (one GPU, N >= 2) the partitioned executor on N in-process ranks of this GPU
  *                 (qe_run_queries_local: the multi-GPU data path with its exchanges, rehearsed)
+ *
+ * Exit status: 0; 1 where the reference calls exit(EXIT_FAILURE); EXIT_LIBQE (70, sysexits'
+ * EX_SOFTWARE) when libqe reports an error (a message on stderr); a rank of QE_GPUS=N killed by
+ * signal s: 128 + s, as the shell reports it.
  */
 #define _GNU_SOURCE
 #include <fcntl.h>
@@ -32,6 +36,8 @@
 #include <unistd.h>
 
 #include "qe.h"
+
+#define EXIT_LIBQE 70   /* libqe returned an error: distinct from a crash (128 + signal) */
 
 typedef struct { char** paths; size_t n; char* text; } input_t;
 
@@ -125,7 +131,7 @@ static int finish(int rc, char* out, size_t outlen, int print) {
     if (rc == QE_EEXIT) return EXIT_FAILURE;
     if (rc != 0) {
         fprintf(stderr, "[ERROR] query execution failed (%d)\n", rc);
-        return 139;
+        return EXIT_LIBQE;
     }
     return EXIT_SUCCESS;
 }
@@ -164,8 +170,10 @@ static int run_rank(const input_t* in, int rank, int world, int* to_peers, int f
 /* the QE_GPUS launcher's wait: rank 0's status is the process's.  A rank that ends badly while
  * others still run can leave them blocked in RCCL -- whichever rank it is, the rest get 10 s to
  * finish on their own (a reference exit(1) ends every rank alike), then are killed. */
+static int exit_code(int st) { return WIFEXITED(st) ? WEXITSTATUS(st) : WIFSIGNALED(st) ? 128 + WTERMSIG(st) : EXIT_LIBQE; }
+
 static int wait_ranks(const pid_t* pid, int world) {
-    int status0 = 139, left = world, done0 = 0, killed = 0;
+    int status0 = EXIT_LIBQE, left = world, done0 = 0, killed = 0;
     int* done = (int*)calloc((size_t)world, sizeof(int));
     while (left > 0) {
         int st = 0;
@@ -176,7 +184,7 @@ static int wait_ranks(const pid_t* pid, int world) {
         if (r == world) continue;
         done[r] = 1;
         left--;
-        const int code = WIFEXITED(st) ? WEXITSTATUS(st) : 139;
+        const int code = exit_code(st);
         if (r == 0) {
             status0 = code;
             done0 = 1;
@@ -190,7 +198,7 @@ static int wait_ranks(const pid_t* pid, int world) {
                     left--;
                     reaped = 1;
                     if (q == 0) {
-                        status0 = WIFEXITED(st) ? WEXITSTATUS(st) : 139;
+                        status0 = exit_code(st);
                         done0 = 1;
                     }
                 }

@@ -68,6 +68,12 @@ MODES = {
     "lanes4": {"QE_PLAN": "0", "QE_WORKERS": "4"},        # the faithful executor on four lanes
     "agg0": {"QE_PLAN": "0", "QE_AGG_MIN": "0"},          # faithful, aggregate last join at any size
     "local3": {"QE_LOCAL_RANKS": "3"},                    # three in-process ranks: real exchanges
+    # the plan's multi-rank aggregate join (e_join_agg: heavy keys by row slice, light hash
+    # buckets) at golden sizes, which stay below its default minimum (QE_AGG_MIN, read once per
+    # process: set before the binary starts)
+    "local2agg0": {"QE_LOCAL_RANKS": "2", "QE_AGG_MIN": "0"},
+    "local3agg0": {"QE_LOCAL_RANKS": "3", "QE_AGG_MIN": "0"},
+    "local8agg0": {"QE_LOCAL_RANKS": "8", "QE_AGG_MIN": "0"},
 }
 
 
