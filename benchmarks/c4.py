@@ -84,9 +84,10 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
     out = None
     for _ in range(args.warmup):
         out, rc = run_batch()
-    # (QE_BENCH_EVENTS=0: no HIP-event stage table -- under rocprofv3's kernel trace the lanes'
-    # concurrent event records crashed inside the runtime; rocprof times the kernels itself)
-    ctx.set_profiling(os.environ.get("QE_BENCH_EVENTS", "1") != "0")
+    # the HIP-event stage table on every lane (round 3 switched it off under rocprofv3, where the
+    # lanes' event-query spins crashed inside the runtime; results now come back through a pinned
+    # flag -- qe_runtime.hip read_words -- with no runtime call in the wait)
+    ctx.set_profiling(True)
     ctx.reset_stats()
     torch.cuda.synchronize()
     hits0, builds0 = ctx.sort_cache_stats()

@@ -353,30 +353,46 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
     const uint64_t tbase = (uint64_t)tile * TILE;
     const uint32_t tn = (uint32_t)((n - tbase) < (uint64_t)TILE ? (n - tbase) : (uint64_t)TILE);
     uint32_t pk[CARRY != X_NONE ? ITEMS : 1];
+    // written in chunks of RW_CH slots: a chunk's stage and offset reads are all issued before its
+    // first store (no branch between them: a slot past the tile reads a stale word and is not
+    // stored), the next chunk held back (sched_barrier) so the registers stay within budget
+    constexpr int RW_CH = ITEMS % 8 == 0 ? 8 : 1;
 #pragma unroll
-    for (int k = 0; k < ITEMS; k++) {
-        uint32_t i = (uint32_t)k * NT + threadIdx.x;
-        if (CARRY != X_NONE) pk[k] = 0xFFFFFFFFu;
-        if (i < tn) {
-            uint64_t wd = stage[i];
+    for (int k0 = 0; k0 < ITEMS; k0 += RW_CH) {
+        uint64_t wd[RW_CH];
+        uint32_t pp[RW_CH];
+#pragma unroll
+        for (int q = 0; q < RW_CH; q++) wd[q] = stage[(uint32_t)(k0 + q) * NT + threadIdx.x];
+#pragma unroll
+        for (int q = 0; q < RW_CH; q++) {
+            const uint32_t i = (uint32_t)(k0 + q) * NT + threadIdx.x;
 #ifdef QE_DIAG_SORT_LINEAR   // ablation only: contiguous output instead of the digit scatter
-            uint32_t p = (uint32_t)(tbase + i);
+            pp[q] = (uint32_t)(tbase + i);
 #else
-            uint32_t p = gofs[(uint32_t)(wd >> dsh) & mask] + i;
+            pp[q] = gofs[(uint32_t)(wd[q] >> dsh) & mask] + i;
 #endif
-            if ((uint64_t)p >= n) continue;   // never taken with consistent offsets; keeps stores in bounds
-            if constexpr (CARRY != X_NONE) pk[k] = p;
+        }
+#pragma unroll
+        for (int q = 0; q < RW_CH; q++) {
+            const int k = k0 + q;
+            const uint32_t i = (uint32_t)k * NT + threadIdx.x, p = pp[q];
+            // (p >= n: never with consistent offsets; keeps stores in bounds)
+            const bool ok = i < tn && (uint64_t)p < n;
+            if constexpr (CARRY != X_NONE) pk[k] = ok ? p : 0xFFFFFFFFu;
+            if (!ok) continue;
+            const uint64_t x = wd[q];
             if (OUT == OUT_WORD) {
-                QE_ST(&wout[p], wd);
+                QE_ST(&wout[p], x);
             } else if (OUT == OUT_W32) {
-                QE_ST(&reinterpret_cast<uint32_t*>(wout)[p], (uint32_t)(wd >> 32));
+                QE_ST(&reinterpret_cast<uint32_t*>(wout)[p], (uint32_t)(x >> 32));
             } else if (PACK) {
-                kout[p] = (K)(f.kconst | ((wd >> 32) << f.lo));
-                vout[p] = (uint32_t)wd;
+                kout[p] = (K)(f.kconst | ((x >> 32) << f.lo));
+                vout[p] = (uint32_t)x;
             } else {
-                kout[p] = (K)wd;
+                kout[p] = (K)x;
             }
         }
+        __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (CARRY != X_NONE) {
         __syncthreads();   // every word is out of the stage
@@ -738,28 +754,35 @@ __global__ void __launch_bounds__(1024) tl_hist_tiles_kernel(const K* __restrict
     const uint32_t t_end = (g + 1) * TL_TPG < nt ? (g + 1) * TL_TPG : nt;
     // (a tile's counts do not depend on which thread counts which key: u32 keys are loaded two per
     // 8-B load, so a wave instruction still moves 512 contiguous bytes)
+    // Every load unconditional, all of a tile's in flight at once: guarded loads (`i < n ? ...`)
+    // compiled to a branch and a vmcnt(0) wait per load -- 12 of the 16 loads of a tile served one
+    // after another (round 3: 0.20 ms per 1e8 u32 keys).  A full tile takes 8-B loads of two u32
+    // keys; the last, partial tile clamps its indices and masks the surplus.
     uint32_t vm = 0;   // valid keys of this thread
     auto load = [&](uint32_t t, uint64_t (&k)[8]) {
         const uint64_t base = (uint64_t)t * RTILE;
+        if (base + RTILE <= n) {   // block-uniform
+            vm = 0xFFu;
+            if (sizeof(K) == 4 && !(reinterpret_cast<uintptr_t>(keys) & 7)) {
+                const uint2* k2 = reinterpret_cast<const uint2*>(reinterpret_cast<const uint32_t*>(keys) + base);
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint2 v = k2[j * 1024 + threadIdx.x];
+                    k[2 * j] = v.x;
+                    k[2 * j + 1] = v.y;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; j++) k[j] = (uint64_t)keys[base + (uint64_t)j * 1024 + threadIdx.x];
+            }
+            return;
+        }
         vm = 0;
-        if (sizeof(K) == 4 && !(reinterpret_cast<uintptr_t>(keys) & 7)) {
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint64_t e = base + 2 * ((uint64_t)j * 1024 + threadIdx.x);
-                uint2 v = make_uint2(0u, 0u);
-                if (e + 1 < n) v = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint32_t*>(keys) + e);
-                else if (e < n) v.x = (uint32_t)keys[e];
-                k[2 * j] = v.x;
-                k[2 * j + 1] = v.y;
-                vm |= (e < n ? 1u : 0u) << (2 * j) | (e + 1 < n ? 1u : 0u) << (2 * j + 1);
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const uint64_t i = base + (uint64_t)j * 1024 + threadIdx.x;
-                k[j] = i < n ? (uint64_t)keys[i] : 0;
-                vm |= (i < n ? 1u : 0u) << j;
-            }
+        for (int j = 0; j < 8; j++) {
+            const uint64_t i = base + (uint64_t)j * 1024 + threadIdx.x;
+            k[j] = (uint64_t)keys[i < n ? i : n - 1];
+            vm |= (i < n ? 1u : 0u) << j;
         }
     };
     uint64_t k[8];
@@ -976,6 +999,11 @@ __global__ void __launch_bounds__(256) cs_apply_kernel(CSJobs js) {
 #define QE_TL2_NT 512
 #endif
 constexpr int TL2_NT = QE_TL2_NT, TL2_ITEMS = QE_TL2_ITEMS, TL2_TILE = TL2_NT * TL2_ITEMS;   // 9216: mean 8192 + 11 sd
+#ifndef QE_TL2_WCH
+#define QE_TL2_WCH 6
+#endif
+constexpr int TL2_WCH = QE_TL2_WCH;   // write-out chunk (slots whose LDS reads are in flight together)
+static_assert(TL2_ITEMS % TL2_WCH == 0, "whole chunks");
 
 // CARRY: the payloads of pass 1 (xin, in pass-1 order; X64: 64-bit, X32: 32-bit) follow the words
 // to xout, staged in the words' LDS slots after the words have left (as in radix_pass_kernel).
@@ -1011,14 +1039,20 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
         uint64_t word[TL2_ITEMS];
         uint32_t pos2[(TL2_ITEMS + 1) / 2];   // ranks < TL2_TILE: two u16 per register
         const int lim = (int)m - (int)((uint32_t)w * WT + l);   // element j valid iff j * 64 < lim
-        // every load unconditional (an element past the segment re-reads its last word): no branch
-        // and no wait per element, all 18 in flight at once
-        const uint64_t* src = win + base;
+        // every load unconditional, all 18 in flight at once, through a buffer descriptor over the
+        // sub-tile: one 32-bit lane offset + a constant per element (18 64-bit clamped addresses
+        // held 36 VGPRs and made the kernel spill), elements past the segment read as 0
         const uint32_t o0 = (uint32_t)w * WT + l;
+        {
+            const auto rw = W32 ? buf_rsrc(reinterpret_cast<const uint32_t*>(win) + base, m * 4u) : buf_rsrc(win + base, m * 8u);
 #pragma unroll
-        for (int j = 0; j < TL2_ITEMS; j++) {
-            if constexpr (W32) word[j] = (uint64_t)reinterpret_cast<const uint32_t*>(win)[base + std::min(o0 + (uint32_t)j * 64, m - 1)] << 32;
-            else word[j] = src[std::min(o0 + (uint32_t)j * 64, m - 1)];
+            for (int j = 0; j < TL2_ITEMS; j++) {
+                if constexpr (W32) word[j] = (uint64_t)buf_load_u32(rw, o0 * 4u, (uint32_t)j * 256u) << 32;
+                else {
+                    const uint2 v = buf_load_u2(rw, o0 * 8u, (uint32_t)j * 512u);
+                    word[j] = (uint64_t)v.y << 32 | v.x;
+                }
+            }
         }
         if (base == start) run = *runp;   // the digit offsets, behind the words (clamped: no branch)
         __syncthreads();   // whist zeroed
@@ -1048,6 +1082,7 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
             }
             if (j & 1) pos2[j >> 1] |= r << 16;
             else pos2[j >> 1] = r;
+            if (j % TL2_WCH == TL2_WCH - 1) __builtin_amdgcn_sched_barrier(0);   // a chunk's atomics in flight, not 18
         }
         __syncthreads();
         uint32_t tot = 0;
@@ -1070,25 +1105,42 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
             run += tot;
         }
         __syncthreads();
+        // staged in chunks: a chunk's offset reads all issued before its stores (branch-free up to
+        // the store), the next chunk's held back (sched_barrier) so registers stay within budget
 #pragma unroll
-        for (int j = 0; j < TL2_ITEMS; j++) {
-            if (j * 64 < lim) {
+        for (int j0 = 0; j0 < TL2_ITEMS; j0 += TL2_WCH) {
+            uint32_t sl[TL2_WCH];
+#pragma unroll
+            for (int q = 0; q < TL2_WCH; q++) {
+                const int j = j0 + q;
                 const uint32_t dd = (uint32_t)(word[j] >> dsh) & (BINS - 1);
-                const uint32_t r = (pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-                const uint32_t sl = bexcl[dd] + whist[w][dd] + r;
-                stage[sl] = word[j];
-                if constexpr (CARRY != X_NONE)   // pos2 becomes the slot (< TL2_TILE: still 16 bits)
-                    pos2[j >> 1] = (j & 1) ? ((pos2[j >> 1] & 0xFFFFu) | (sl << 16)) : ((pos2[j >> 1] & 0xFFFF0000u) | sl);
+                sl[q] = bexcl[dd] + whist[w][dd] + ((pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
             }
+#pragma unroll
+            for (int q = 0; q < TL2_WCH; q++) {
+                const int j = j0 + q;
+                if (j * 64 < lim) {
+                    stage[sl[q]] = word[j];
+                    if constexpr (CARRY != X_NONE)   // pos2 becomes the slot (< TL2_TILE: still 16 bits)
+                        pos2[j >> 1] = (j & 1) ? ((pos2[j >> 1] & 0xFFFFu) | (sl[q] << 16)) : ((pos2[j >> 1] & 0xFFFF0000u) | sl[q]);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
         }
-        if constexpr (CARRY != X_NONE) {   // the payloads load into the words' registers, in flight during the write-out
-            const uint64_t* xsrc = xin + base;
-            const uint32_t o0 = (uint32_t)w * WT + l;
+        // the payloads load into the words' registers (a 32-bit one into registers of its own),
+        // in flight during the write-out
+        uint32_t xw[CARRY == X32 ? TL2_ITEMS : 1];
+        if constexpr (CARRY != X_NONE) {
+            const auto rx = CARRY == X64 ? buf_rsrc(xin + base, m * 8u)
+                                         : buf_rsrc(reinterpret_cast<const uint32_t*>(xin) + base, m * 4u);
 #pragma unroll
             for (int j = 0; j < TL2_ITEMS; j++) {
-                const uint32_t o = std::min(o0 + (uint32_t)j * 64, m - 1);
-                if constexpr (CARRY == X64) word[j] = xsrc[o];
-                else word[j] = reinterpret_cast<const uint32_t*>(xin)[base + o];
+                if constexpr (CARRY == X64) {
+                    const uint2 v = buf_load_u2(rx, o0 * 8u, (uint32_t)j * 512u);
+                    word[j] = (uint64_t)v.y << 32 | v.x;
+                } else {
+                    xw[j] = buf_load_u32(rx, o0 * 4u, (uint32_t)j * 256u);
+                }
             }
         }
         __syncthreads();
@@ -1124,16 +1176,27 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
             }
         } else if constexpr (CARRY != X_NONE) {
             // the payloads: each slot's destination is read back from its word before the slot
-            // is reused (one u32 per slot in the LDS word itself: high half = destination)
-#pragma unroll 6
-            for (int k = 0; k < TL2_ITEMS; k++) {
-                const uint32_t i = (uint32_t)k * TL2_NT + threadIdx.x;
-                if (i < m) {
-                    const uint64_t wd = stage[i];
-                    const uint32_t p = gofs[(uint32_t)(wd >> dsh) & (BINS - 1)] + i;
-                    if ((uint64_t)p < n) QE_ST(&wout[p], wd);
-                    reinterpret_cast<uint32_t*>(stage)[2 * i] = p;   // slot i now holds its destination
+            // is reused (one u32 per slot in the LDS word itself: high half = destination).
+            // Write-outs go in chunks of TL2_WCH slots whose LDS reads are all issued before the
+            // first store (branch-free up to the store: one LDS round trip per chunk, not per slot)
+#pragma unroll
+            for (int k0 = 0; k0 < TL2_ITEMS; k0 += TL2_WCH) {
+                uint64_t wd[TL2_WCH];
+                uint32_t p[TL2_WCH];
+#pragma unroll
+                for (int q = 0; q < TL2_WCH; q++) wd[q] = stage[(uint32_t)(k0 + q) * TL2_NT + threadIdx.x];
+#pragma unroll
+                for (int q = 0; q < TL2_WCH; q++)
+                    p[q] = gofs[(uint32_t)(wd[q] >> dsh) & (BINS - 1)] + (uint32_t)(k0 + q) * TL2_NT + threadIdx.x;
+#pragma unroll
+                for (int q = 0; q < TL2_WCH; q++) {
+                    const uint32_t i = (uint32_t)(k0 + q) * TL2_NT + threadIdx.x;
+                    if (i < m) {
+                        if ((uint64_t)p[q] < n) QE_ST(&wout[p[q]], wd[q]);
+                        reinterpret_cast<uint32_t*>(stage)[2 * i] = p[q];   // slot i now holds its destination
+                    }
                 }
+                __builtin_amdgcn_sched_barrier(0);
             }
             __syncthreads();
             if constexpr (CARRY == X64) {
@@ -1151,30 +1214,41 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
                 uint32_t* st32 = reinterpret_cast<uint32_t*>(stage);
 #pragma unroll
                 for (int j = 0; j < TL2_ITEMS; j++)
-                    if (j * 64 < lim) st32[2 * ((pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu) + 1] = (uint32_t)word[j];
+                    if (j * 64 < lim) st32[2 * ((pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu) + 1] = xw[j];
                 __syncthreads();
                 uint32_t* xo = reinterpret_cast<uint32_t*>(xout);
-#pragma unroll 6
-                for (int k = 0; k < TL2_ITEMS; k++) {
-                    const uint32_t i = (uint32_t)k * TL2_NT + threadIdx.x;
-                    if (i < m) {
-                        const uint2 dv = reinterpret_cast<const uint2*>(stage)[i];
-                        if ((uint64_t)dv.x < n) QE_ST(&xo[dv.x], dv.y);
-                    }
+#pragma unroll
+                for (int k0 = 0; k0 < TL2_ITEMS; k0 += TL2_WCH) {
+                    uint2 dv[TL2_WCH];
+#pragma unroll
+                    for (int q = 0; q < TL2_WCH; q++)
+                        dv[q] = reinterpret_cast<const uint2*>(stage)[(uint32_t)(k0 + q) * TL2_NT + threadIdx.x];
+#pragma unroll
+                    for (int q = 0; q < TL2_WCH; q++)
+                        if ((uint32_t)(k0 + q) * TL2_NT + threadIdx.x < m && (uint64_t)dv[q].x < n)
+                            QE_ST(&xo[dv[q].x], dv[q].y);
+                    __builtin_amdgcn_sched_barrier(0);
                 }
             }
         } else {
-#pragma unroll 6   // (fully unrolled, every LDS read is hoisted and the kernel spills)
-            for (int k = 0; k < TL2_ITEMS; k++) {
-                const uint32_t i = (uint32_t)k * TL2_NT + threadIdx.x;
-                if (i < m) {
-                    const uint64_t wd = stage[i];
-                    const uint32_t p = gofs[(uint32_t)(wd >> dsh) & (BINS - 1)] + i;
-                    if ((uint64_t)p < n) {   // never false with consistent offsets
-                        if constexpr (W32) QE_ST(&reinterpret_cast<uint32_t*>(wout)[p], (uint32_t)(wd >> 32));
-                        else QE_ST(&wout[p], wd);
+#pragma unroll
+            for (int k0 = 0; k0 < TL2_ITEMS; k0 += TL2_WCH) {
+                uint64_t wd[TL2_WCH];
+                uint32_t p[TL2_WCH];
+#pragma unroll
+                for (int q = 0; q < TL2_WCH; q++) wd[q] = stage[(uint32_t)(k0 + q) * TL2_NT + threadIdx.x];
+#pragma unroll
+                for (int q = 0; q < TL2_WCH; q++)
+                    p[q] = gofs[(uint32_t)(wd[q] >> dsh) & (BINS - 1)] + (uint32_t)(k0 + q) * TL2_NT + threadIdx.x;
+#pragma unroll
+                for (int q = 0; q < TL2_WCH; q++) {
+                    const uint32_t i = (uint32_t)(k0 + q) * TL2_NT + threadIdx.x;
+                    if (i < m && (uint64_t)p[q] < n) {   // (p < n: never false with consistent offsets)
+                        if constexpr (W32) QE_ST(&reinterpret_cast<uint32_t*>(wout)[p[q]], (uint32_t)(wd[q] >> 32));
+                        else QE_ST(&wout[p[q]], wd[q]);
                     }
                 }
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
         __syncthreads();   // stage / whist / gofs are rewritten by the next sub-tile
@@ -1498,7 +1572,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
         uint32_t cnt = 0, h = HJ_NONE;
         if ((uint32_t)j * NT + threadIdx.x < mS) {
             h = head[fld(ws[j]) & dmask];
-            for (uint32_t p = h; p != HJ_NONE && cnt <= HJ_CHAIN_MAX; p = nxt[p]) cnt++;
+            for (uint32_t p = h; p != HJ_NONE; p = nxt[p]) cnt++;   // (linear in the pairs: cnt of them)
             if (cnt > HJ_CHAIN_MAX) s_long = 1;
         }
         hd[j] = h;
