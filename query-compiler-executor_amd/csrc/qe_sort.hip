@@ -148,6 +148,26 @@ struct Field {
 #ifdef QE_DIAG_STAMPS
 __device__ uint64_t g_sort_stamps[STAMP_TILES * STAMP_SLOTS];
 __device__ uint64_t g_hj_stamps[STAMP_TILES * STAMP_SLOTS];
+__device__ uint32_t g_sort_stamp_on = 1;   // the sort kernels stamp only while this is set
+// QE_STAMP_SEL=p1:K or p2:K (tuning builds only): stamp only the K-th lookback-free first pass /
+// the K-th second pass of the process (1-based; their order is logged to stderr), so one
+// launch of a whole query's sorts can be looked at (tools/stamps.py --what c3p1 / c3p2)
+static void stamp_select(qe_ctx* c, const char* kind, uint64_t n) {
+    static uint32_t cnt[2] = {0, 0};
+    const int k = kind[1] == '1' ? 0 : 1;
+    const uint32_t idx = ++cnt[k];
+    const char* sel = getenv("QE_STAMP_SEL");
+    uint32_t on = 1;
+    if (sel && sel[0] == 'p') on = (sel[1] == kind[1] && (uint32_t)atoi(sel + 3) == idx) ? 1u : 0u;
+    if (sel) fprintf(stderr, "[stamps] %s launch %u: n = %llu%s\n", kind, idx, (unsigned long long)n, on ? " (stamped)" : "");
+    QE_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_sort_stamp_on), &on, sizeof on, 0, hipMemcpyHostToDevice, c->stream));
+}
+#define QE_SORT_STAMP(tile, k) \
+    do {                       \
+        if (g_sort_stamp_on) QE_STAMP(g_sort_stamps, tile, k); \
+    } while (0)
+#else
+#define QE_SORT_STAMP(tile, k) ((void)0)
 #endif
 
 // XCD-contiguous work items for the lookback-free passes: a grid of 8 * per blocks, block b takes
@@ -217,13 +237,13 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
     const uint32_t tile = PRE ? xcd_item(blockIdx.x) : take_ticket(ticket, &s_ticket);
     if (PRE && (uint64_t)tile * TILE >= n) return;   // the XCD grid's padding blocks (block-uniform)
 #ifdef QE_DIAG_STAMPS
-    if (threadIdx.x == 0 && tile < STAMP_TILES) g_sort_stamps[(uint64_t)tile * STAMP_SLOTS] = t_start;
+    if (g_sort_stamp_on && threadIdx.x == 0 && tile < STAMP_TILES) g_sort_stamps[(uint64_t)tile * STAMP_SLOTS] = t_start;
 #endif
     const int w = wave_id(), l = lane_id();
     const uint64_t lt = lanemask_lt();
     for (int i = threadIdx.x; i < NW * BINS; i += NT) (&whist[0][0])[i] = 0;
     __syncthreads();
-    QE_STAMP(g_sort_stamps, tile, 1);
+    QE_SORT_STAMP(tile, 1);
 
     const uint64_t wave_base = (uint64_t)tile * TILE + (uint64_t)w * WT;
     uint64_t word[ITEMS];
@@ -278,7 +298,7 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
 #endif
     }
     __syncthreads();
-    QE_STAMP(g_sort_stamps, tile, 2);
+    QE_SORT_STAMP(tile, 2);
     // thread t owns digits t*DPT .. t*DPT+DPT-1: totals, exclusive over waves, publish aggregate
     uint32_t tot[DPT], tsum = 0;
 #pragma unroll
@@ -308,7 +328,7 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
         run += tot[q];
     }
     __syncthreads();
-    QE_STAMP(g_sort_stamps, tile, 3);
+    QE_SORT_STAMP(tile, 3);
     // stage the tile in digit order (tile-local offsets only)
 #pragma unroll
     for (int j = 0; j < ITEMS; j++) {
@@ -347,9 +367,9 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
 #endif
         gofs[d] = offs[d] + (uint32_t)ex - bexcl[d];
     }
-    QE_STAMP(g_sort_stamps, tile, 4);
+    QE_SORT_STAMP(tile, 4);
     __syncthreads();
-    QE_STAMP(g_sort_stamps, tile, 5);
+    QE_SORT_STAMP(tile, 5);
     const uint64_t tbase = (uint64_t)tile * TILE;
     const uint32_t tn = (uint32_t)((n - tbase) < (uint64_t)TILE ? (n - tbase) : (uint64_t)TILE);
     uint32_t pk[CARRY != X_NONE ? ITEMS : 1];
@@ -409,7 +429,7 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
             }
         }
     }
-    QE_STAMP(g_sort_stamps, tile, 6);
+    QE_SORT_STAMP(tile, 6);
 }
 
 // ---- two-level sort: 14 high bits by two global passes, the rest inside LDS per bucket ---------
@@ -1027,6 +1047,10 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
     if (s >= 256u * G) return;   // the XCD grid's padding blocks (block-uniform)
     // the segment's bounds from the compact table column_scans wrote (48 KB at 1e8 keys, L2-hot):
     // reading them from the 12.5 MB tile-count matrix put a far dependent load before every word load
+#ifdef QE_DIAG_STAMPS
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    if (g_sort_stamp_on && threadIdx.x == 0 && s < STAMP_TILES) g_sort_stamps[(uint64_t)s * STAMP_SLOTS] = t_start;
+#endif
     const uint32_t start = seg[s], end = seg[s + 1];
     const int w = wave_id(), l = lane_id();
     const uint64_t lt = lanemask_lt();
@@ -1056,6 +1080,7 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
         }
         if (base == start) run = *runp;   // the digit offsets, behind the words (clamped: no branch)
         __syncthreads();   // whist zeroed
+        if (base == start) QE_SORT_STAMP(s, 1);
 #pragma unroll
         for (int j = 0; j < TL2_ITEMS; j++) {   // stable rank inside the wave: (j, lane) order
             const bool ok = j * 64 < lim;
@@ -1085,6 +1110,7 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
             if (j % TL2_WCH == TL2_WCH - 1) __builtin_amdgcn_sched_barrier(0);   // a chunk's atomics in flight, not 18
         }
         __syncthreads();
+        if (base == start) QE_SORT_STAMP(s, 2);
         uint32_t tot = 0;
         if (d < BINS) {
 #pragma unroll
@@ -1105,6 +1131,7 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
             run += tot;
         }
         __syncthreads();
+        if (base == start) QE_SORT_STAMP(s, 3);
         // staged in chunks: a chunk's offset reads all issued before its stores (branch-free up to
         // the store), the next chunk's held back (sched_barrier) so registers stay within budget
 #pragma unroll
@@ -1144,6 +1171,7 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
             }
         }
         __syncthreads();
+        if (base == start) QE_SORT_STAMP(s, 4);
         if constexpr (CARRY == X64 && XS) {
             uint32_t dg[(TL2_ITEMS + 3) / 4];   // slot k's digit in byte k % 4 of dg[k / 4]
 #pragma unroll
@@ -1199,6 +1227,7 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
                 __builtin_amdgcn_sched_barrier(0);
             }
             __syncthreads();
+            if (base == start) QE_SORT_STAMP(s, 5);
             if constexpr (CARRY == X64) {
 #pragma unroll
                 for (int j = 0; j < TL2_ITEMS; j++) {   // payload j goes straight to its slot's destination
@@ -1252,6 +1281,7 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
             }
         }
         __syncthreads();   // stage / whist / gofs are rewritten by the next sub-tile
+        if (base == start) QE_SORT_STAMP(s, 6);
     }
 }
 
@@ -2053,6 +2083,9 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, CR, true>),      \
                        dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, kn, nullptr, VIN, nullptr, w1, vout, n, 32 + L,     \
                        255u, f, tcnt, nullptr, nullptr, 0u, XA, nullptr, x1)
+#ifdef QE_DIAG_STAMPS
+    stamp_select(c, "p1", n);
+#endif
     if (kn && uns) {
         // u32 key (+ u32 value) (+ u32 payload) in, word (+ payload) out
         const uint32_t* vt = cv64 ? narrow_of(c, cv64, n) : nullptr;
@@ -2120,6 +2153,9 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
                                        : (x64_staged() ? tl_pass2_kernel<K, X64, false, false, true> : tl_pass2_kernel<K, X64, false>))
                     : xm      ? tl_pass2_kernel<K, X32, true>   // (the X32 / XCOL first pass is unstable too)
                               : (uns ? tl_pass2_kernel<K, X_NONE, true> : tl_pass2_kernel<K, X_NONE, false>);
+#ifdef QE_DIAG_STAMPS
+        stamp_select(c, "p2", n);
+#endif
         hipLaunchKernelGGL(kern, dim3(xcd_grid(nseg)), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8, seg, gcnt, G,
                            x1, x2);
         QE_HIP(hipGetLastError());

@@ -27,6 +27,7 @@ PHASES = {
     "ws": ["ticket", "loads+ballots", "lookback", "stores"],
     "wsp": ["lookback (next loads in flight)", "stores"],
     "hj": ["bounds+loads issued", "R loaded+hist", "scan+scatter", "S counts+wave scans", "slice atomic", "emit (t0)"],
+    "p2": ["zero+loads issued", "rank (loads landed)", "digit scan", "stage+payload loads", "words out", "payloads out"],
 }
 
 
@@ -34,7 +35,8 @@ def report(ctx, which, ntiles):
     buf = np.zeros(ntiles * SLOTS, dtype=np.uint64)
     fn = ctx.lib.qe_diag_stamps
     fn.argtypes = [C.c_char_p, C.c_void_p, C.c_uint64]
-    rc = fn(("cp" if which in ("cpp", "ws", "wsp") else which).encode(), buf.ctypes.data, buf.size)   # "hj": the sort file
+    src = "cp" if which in ("cpp", "ws", "wsp") else "sort" if which == "p2" else which
+    rc = fn(src.encode(), buf.ctypes.data, buf.size)   # "hj", "p2": the sort file
     assert rc == 0, rc
     st = buf.reshape(ntiles, SLOTS).astype(np.int64)
     names = PHASES[which]
@@ -81,6 +83,19 @@ def main():
         dg.gen_c5(ctx, n)
         ctx.run(dg.C5_QUERY)
         report(ctx, "ag", min(65536, (2 * n + 4095) // 4096))
+        ctx.close()
+        return
+    if a.what in ("c3p1", "c3p2"):
+        # one selected first / second pass of the C3 plan's two-level sorts: QE_STAMP_SEL=p1:K / p2:K
+        # must be set in the environment (the launches are numbered on stderr); the query runs once
+        kinds = [("mod", n), ("mod", n), ("hi32",)]
+        for r in range(4):
+            ctx.gen_relation(n, kinds, seed=1, gen_rel=r)
+        ctx.sync()
+        q = "0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>1000000000&3.2<3000000000|1.2 2.2 3.2\n"
+        ctx.run_dist(q, None)
+        ctx.sync()
+        report(ctx, "sort" if a.what == "c3p1" else "p2", 65536)
         ctx.close()
         return
     if "hj" in a.what:   # the bucket join of the last C3 join (the partitioned plan at N = 1)
