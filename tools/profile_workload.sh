@@ -3,6 +3,8 @@
 #   tools/profile_workload.sh TAG c4|c5   -> kernel trace + stats, FETCH_SIZE pass, WRITE_SIZE pass
 set -e
 TAG=$1; W=$2
+# raw traces are large: whatever happens, keep only the summaries (gpurun brings back <= 64 MiB)
+trap 'rm -rf "$O/${TAG}_trace" "$O/${TAG}_fetch" "$O/${TAG}_write"' EXIT
 R=$(pwd)
 O=$R/gpurun_out
 mkdir -p $O

@@ -12,4 +12,6 @@ export QE_LIB_PATH=$PWD/query-compiler-executor_amd/build/diag/libqe_STAMPS.so
   for k in 1 2 3 4 5 6; do
     echo "=== p2:$k"; QE_STAMP_SEL=p2:$k timeout -k 10 120 python tools/stamps.py --what c3p2 2>&1 | grep -v "^\[stamps\] p1" || exit 1
   done ) > gpurun_out/${T}_stamps.log 2>&1
-echo rc=$?
+rc=$?
+echo stamps rc=$rc
+exit $rc
