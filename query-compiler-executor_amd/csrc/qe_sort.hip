@@ -39,6 +39,34 @@ namespace qe {
 #define QE_ST(ptr, v) (*(ptr) = (v))
 #endif
 
+// Where a write-out lane with nothing to write may send its store (QE_STORE_SINK=1 builds): every
+// store of a write-out loop is then issued unconditionally, so the compiler waits for the payload
+// loads with a counted vmcnt(N) instead of vmcnt(0) (a guarded store is a branch; gfx9 counts loads
+// and stores together).  Measured: the sink form 3.08 vs 3.02-3.05 ms of sort_pass_carry per C3
+// query for guarded stores, same box (profiles/r04h_store_sink_ab.log) -- pass 2's sub-tiles leave
+// ~10 % of the lanes without a word, and their sink stores cost more than the waits saved.  The
+// default keeps guarded stores.
+__device__ uint64_t g_store_sink[64];
+#ifndef QE_STORE_SINK
+#define QE_STORE_SINK 0
+#endif
+// QE_STS(ok, ptr, sinkptr, v): the store of a write-out lane -- to ptr when ok, else (sink form)
+// to the sink, or (QE_STORE_SINK=0, A/B build) not at all
+#if QE_STORE_SINK
+#define QE_STS(ok, ptr, sinkp, v) QE_ST((ok) ? (ptr) : (sinkp), (v))
+#define QE_STP(ok, ptr, sinkp, v) (*((ok) ? (ptr) : (sinkp)) = (v))
+#else
+#define QE_STP(ok, ptr, sinkp, v) \
+    do {                          \
+        if (ok) *(ptr) = (v);     \
+    } while (0)
+#define QE_STS(ok, ptr, sinkp, v) \
+    do {                          \
+        if (ok) QE_ST((ptr), (v)); \
+    } while (0)
+#endif
+
+
 constexpr int RB = 256;          // block
 constexpr int RNW = RB / 64;     // waves per block
 #ifndef QE_R_ITEMS
@@ -89,6 +117,33 @@ struct PassDesc {
     uint32_t mask[MAX_PASS];
 };
 
+// Visits keys[0, n): a block takes chunks of blockDim * U consecutive keys (grid-stride), thread t
+// keys t, t + blockDim, ... of its chunk, all U loads of a chunk in flight together -- unconditional
+// in a full chunk, index-clamped and masked in the last one.  (A guarded load per element, `i < n ?
+// keys[i] : 0`, left one load in flight per thread: the histogram kernels below were latency-bound.)
+template <int U, typename K, typename F>
+__device__ __forceinline__ void for_each_key(const K* __restrict__ keys, uint64_t n, F&& f) {
+    const uint64_t per = (uint64_t)blockDim.x * U;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * per; c0 < n; c0 += (uint64_t)gridDim.x * per) {
+        K k[U];
+        if (c0 + per <= n) {   // block-uniform
+#pragma unroll
+            for (int q = 0; q < U; q++) k[q] = keys[c0 + (uint64_t)q * blockDim.x + threadIdx.x];
+#pragma unroll
+            for (int q = 0; q < U; q++) f(k[q]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < U; q++) {
+                const uint64_t i = c0 + (uint64_t)q * blockDim.x + threadIdx.x;
+                k[q] = keys[i < n ? i : n - 1];
+            }
+#pragma unroll
+            for (int q = 0; q < U; q++)
+                if (c0 + (uint64_t)q * blockDim.x + threadIdx.x < n) f(k[q]);
+        }
+    }
+}
+
 template <typename K, int RBITS>
 __global__ void __launch_bounds__(256) digit_hist_kernel(const K* __restrict__ keys, uint64_t n, PassDesc pd,
                                                          uint32_t* __restrict__ hist) {
@@ -97,11 +152,10 @@ __global__ void __launch_bounds__(256) digit_hist_kernel(const K* __restrict__ k
     __shared__ uint32_t h[HP * BINS];
     for (int i = threadIdx.x; i < HP * BINS; i += blockDim.x) h[i] = 0;
     __syncthreads();
-    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        uint64_t k = (uint64_t)keys[i];
+    for_each_key<8>(keys, n, [&](K kk) {
+        const uint64_t k = (uint64_t)kk;
         for (int p = 0; p < pd.npass; p++) atomicAdd(&h[p * BINS + ((uint32_t)(k >> pd.shift[p]) & pd.mask[p])], 1u);
-    }
+    });
     __syncthreads();
     for (int i = threadIdx.x; i < pd.npass * BINS; i += blockDim.x) {
         uint32_t v = h[i];
@@ -241,6 +295,13 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
 #endif
     const int w = wave_id(), l = lane_id();
     const uint64_t lt = lanemask_lt();
+    // PRE: this tile's digit offsets, loaded first -- issued after the payload loads, their wait
+    // also waited for those
+    uint32_t pre_off[PRE ? DPT : 1];
+    if constexpr (PRE) {
+#pragma unroll
+        for (int q = 0; q < DPT; q++) pre_off[q] = owner ? offs[(uint64_t)tile * BINS + threadIdx.x * DPT + q] : 0u;
+    }
     for (int i = threadIdx.x; i < NW * BINS; i += NT) (&whist[0][0])[i] = 0;
     __syncthreads();
     QE_SORT_STAMP(tile, 1);
@@ -248,18 +309,36 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
     const uint64_t wave_base = (uint64_t)tile * TILE + (uint64_t)w * WT;
     uint64_t word[ITEMS];
     uint32_t pos[ITEMS];
+    // every load unconditional, through buffer descriptors over this tile's elements (those past
+    // n read as 0): a guarded load became a branch whose value the compiler waited for inside it
+    const uint64_t tb = (uint64_t)tile * TILE;
+    const uint32_t tcount = (uint32_t)((n - tb) < (uint64_t)TILE ? (n - tb) : (uint64_t)TILE);
+    const uint32_t loc0 = (uint32_t)w * WT + (uint32_t)l;   // this lane's first tile-local element
+    if constexpr (IN == IN_WORD) {
+        const auto rw = buf_rsrc(win + tb, tcount * 8u);
 #pragma unroll
-    for (int j = 0; j < ITEMS; j++) {
-        uint64_t i = wave_base + (uint64_t)j * 64 + l;
-        bool ok = i < n;
-        if (IN == IN_WORD) {
-            word[j] = ok ? win[i] : 0;
-        } else {
-            uint64_t k = ok ? (uint64_t)kin[i] : 0;
+        for (int j = 0; j < ITEMS; j++) {
+            const uint2 v = buf_load_u2(rw, loc0 * 8u, (uint32_t)j * 512u);
+            word[j] = (uint64_t)v.y << 32 | v.x;
+        }
+    } else {
+        const auto rk = buf_rsrc(kin + tb, tcount * (uint32_t)sizeof(K));
+        const auto rv = IN == IN_KV64 ? buf_rsrc(reinterpret_cast<const uint64_t*>(vin) + tb, tcount * 8u)
+                                      : buf_rsrc(IN == IN_KV ? vin + tb : vin, IN == IN_KV ? tcount * 4u : 0u);
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            uint64_t k;
+            if constexpr (sizeof(K) == 8) {
+                const uint2 v = buf_load_u2(rk, loc0 * 8u, (uint32_t)j * 512u);
+                k = (uint64_t)v.y << 32 | v.x;
+            } else {
+                k = buf_load_u32(rk, loc0 * 4u, (uint32_t)j * 256u);
+            }
             if (PACK) {
-                uint32_t v = IN == IN_KV     ? (ok ? vin[i] : 0u)
-                             : IN == IN_KV64 ? (ok ? (uint32_t)reinterpret_cast<const uint64_t*>(vin)[i] : 0u)
-                                             : (uint32_t)i;
+                uint32_t v;
+                if constexpr (IN == IN_KV) v = buf_load_u32(rv, loc0 * 4u, (uint32_t)j * 256u);
+                else if constexpr (IN == IN_KV64) v = buf_load_u2(rv, loc0 * 8u, (uint32_t)j * 512u).x;
+                else v = (uint32_t)(tb + loc0 + (uint32_t)j * 64);
                 word[j] = (((k >> f.lo) & f.fmask) << 32) | v;
             } else {
                 word[j] = k;
@@ -340,13 +419,21 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
             if constexpr (CARRY != X_NONE) pos[j] = slot;   // the payload takes the same slot later
         }
     }
-    if constexpr (CARRY != X_NONE) {   // the payloads load into the words' registers, in flight during the write-out
+    // the payloads load into the words' registers (a 32-bit one into registers of its own), in
+    // flight during the write-out
+    constexpr bool P32 = CARRY == X32 || CARRY == XCOL;
+    uint32_t xw[P32 ? ITEMS : 1];
+    if constexpr (CARRY != X_NONE) {
+        const auto ra = CARRY == XCOL ? buf_rsrc(reinterpret_cast<const uint64_t*>(xa) + tb, tcount * 8u)
+                                      : buf_rsrc(xa + tb, tcount * 4u);
+        const auto rb = buf_rsrc(xb ? xb + tb : xa, xb ? tcount * 4u : 0u);   // (no xb: reads 0)
 #pragma unroll
         for (int j = 0; j < ITEMS; j++) {
-            const uint64_t i = wave_base + (uint64_t)j * 64 + l;
-            if constexpr (CARRY == X64) word[j] = i < n ? ((uint64_t)xa[i] | (xb ? (uint64_t)xb[i] << 32 : 0ull)) : 0ull;
-            else if constexpr (CARRY == X32) word[j] = i < n ? xa[i] : 0u;
-            else word[j] = i < n ? (uint32_t)reinterpret_cast<const uint64_t*>(xa)[i] : 0u;
+            if constexpr (CARRY == X64)
+                word[j] = (uint64_t)buf_load_u32(ra, loc0 * 4u, (uint32_t)j * 256u) |
+                          (uint64_t)buf_load_u32(rb, loc0 * 4u, (uint32_t)j * 256u) << 32;
+            else if constexpr (CARRY == X32) xw[j] = buf_load_u32(ra, loc0 * 4u, (uint32_t)j * 256u);
+            else xw[j] = buf_load_u2(ra, loc0 * 8u, (uint32_t)j * 512u).x;
         }
     }
 #pragma unroll
@@ -354,7 +441,7 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
         const uint32_t d = threadIdx.x * DPT + q;
         if (!owner) continue;
         if constexpr (PRE) {
-            gofs[d] = offs[(uint64_t)tile * BINS + d] - bexcl[d];
+            gofs[d] = pre_off[q] - bexcl[d];
             continue;
         }
         // the predecessors' counts: by this time most have published their inclusive prefix
@@ -399,34 +486,37 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
             // (p >= n: never with consistent offsets; keeps stores in bounds)
             const bool ok = i < tn && (uint64_t)p < n;
             if constexpr (CARRY != X_NONE) pk[k] = ok ? p : 0xFFFFFFFFu;
-            if (!ok) continue;
             const uint64_t x = wd[q];
+            // every store issued (a lane with nothing to write stores to g_store_sink): no branch
             if (OUT == OUT_WORD) {
-                QE_ST(&wout[p], x);
+                QE_STS(ok, &wout[p], &g_store_sink[l], x);
             } else if (OUT == OUT_W32) {
-                QE_ST(&reinterpret_cast<uint32_t*>(wout)[p], (uint32_t)(x >> 32));
+                QE_STS(ok, &reinterpret_cast<uint32_t*>(wout)[p], reinterpret_cast<uint32_t*>(&g_store_sink[l]), (uint32_t)(x >> 32));
             } else if (PACK) {
-                kout[p] = (K)(f.kconst | ((x >> 32) << f.lo));
-                vout[p] = (uint32_t)x;
+                QE_STP(ok, &kout[p], reinterpret_cast<K*>(&g_store_sink[l]), (K)(f.kconst | ((x >> 32) << f.lo)));
+                QE_STP(ok, &vout[p], reinterpret_cast<uint32_t*>(&g_store_sink[l]), (uint32_t)x);
             } else {
-                kout[p] = (K)x;
+                QE_STP(ok, &kout[p], reinterpret_cast<K*>(&g_store_sink[l]), (K)x);
             }
         }
         __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (CARRY != X_NONE) {
         __syncthreads();   // every word is out of the stage
+        uint32_t* st32 = reinterpret_cast<uint32_t*>(stage);   // (32-bit payloads: 4-B slots)
 #pragma unroll
         for (int j = 0; j < ITEMS; j++)
-            if (wave_base + (uint64_t)j * 64 + l < n) stage[pos[j]] = word[j];
+            if (wave_base + (uint64_t)j * 64 + l < n) {
+                if constexpr (P32) st32[pos[j]] = xw[j];
+                else stage[pos[j]] = word[j];
+            }
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < ITEMS; k++) {
             const uint32_t i = (uint32_t)k * NT + threadIdx.x;
-            if (i < tn && pk[k] != 0xFFFFFFFFu) {
-                if constexpr (CARRY == X64) QE_ST(&xout[pk[k]], stage[i]);
-                else QE_ST(&reinterpret_cast<uint32_t*>(xout)[pk[k]], (uint32_t)stage[i]);
-            }
+            const bool ok = pk[k] != 0xFFFFFFFFu;   // (set only for i < tn)
+            if constexpr (CARRY == X64) QE_STS(ok, &xout[pk[k]], &g_store_sink[l], stage[i]);
+            else QE_STS(ok, &reinterpret_cast<uint32_t*>(xout)[pk[k]], reinterpret_cast<uint32_t*>(&g_store_sink[l]), st32[i]);
         }
     }
     QE_SORT_STAMP(tile, 6);
@@ -457,15 +547,9 @@ __global__ void __launch_bounds__(1024) tl_hist_kernel(const K* __restrict__ key
     __shared__ uint32_t h[TL_BUCKETS];   // 128 KiB: one block per CU, 16 waves
     for (int i = threadIdx.x; i < TL_BUCKETS; i += 1024) h[i] = 0;
     __syncthreads();
-    const uint64_t stride = (uint64_t)gridDim.x * 1024 * 4;
-    for (uint64_t i0 = ((uint64_t)blockIdx.x * 1024 + threadIdx.x) * 4; i0 < n; i0 += stride) {
-        uint64_t k[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) k[q] = i0 + q < n ? (uint64_t)keys[i0 + q] : 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            if (i0 + q < n) atomicAdd(&h[(uint32_t)((((k[q] >> f.lo) & f.fmask) >> L) & (TL_BUCKETS - 1))], 1u);
-    }
+    for_each_key<8>(keys, n, [&](K k) {
+        atomicAdd(&h[(uint32_t)(((((uint64_t)k >> f.lo) & f.fmask) >> L) & (TL_BUCKETS - 1))], 1u);
+    });
     __syncthreads();
     for (int i = threadIdx.x; i < TL_BUCKETS; i += 1024)
         if (h[i]) atomicAdd(&hist[i], h[i]);
@@ -543,28 +627,45 @@ __global__ void __launch_bounds__(1024) tl_scan_kernel(const uint32_t* __restric
         for (int w = 0; w < 16; w++) m = wmax[w] > m ? wmax[w] : m;
         *maxb = m;
     }
-    // marginals: pass 1 sorts by the bucket's low 8 bits, pass 2 by its high 7
-    if (t < 256) {
+    // marginals: pass 1 sorts by the bucket's low 8 bits, pass 2 by its high 7.  All in parallel
+    // (the serial form -- a 64-way bank conflict down each row, one thread scanning 512 values --
+    // took ~30 us per sort: 212 ms per C4 batch profile, profiles/r04f_c4_kernel_stats.csv)
+    __shared__ uint32_t part[4][256];
+    {   // c1[d1]: four partial column sums of 32 rows each (consecutive threads, consecutive banks)
+        const int d1 = t & 255, q = t >> 8;
         uint32_t a = 0;
-        for (int d2 = 0; d2 < 128; d2++) a += h[d2 * 256 + t];
-        c1[t] = a;
-    } else if (t < 384) {
-        const int d2 = t - 256;
-        uint32_t a = 0;
-        for (int d1 = 0; d1 < 256; d1++) a += h[d2 * 256 + d1];
-        c2[d2] = a;
+#pragma unroll 8
+        for (int d2 = q * 32; d2 < q * 32 + 32; d2++) a += h[d2 * 256 + d1];
+        part[q][d1] = a;
     }
+    // c2[d2]: row d2 = the 256 buckets of threads 8*d2 .. 8*d2 + 7 (their `mine`), one shuffle tree
+    uint32_t r8 = mine;
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) r8 += (uint32_t)__shfl_xor((int)r8, m, 64);
+    if ((t & 7) == 0) c2[t >> 3] = r8;
     __syncthreads();
-    if (t == 0) {
-        uint32_t r1 = 0, r2 = 0;
-        for (int d = 0; d < 256; d++) {
-            base1[d] = r1;
-            r1 += c1[d];
+    if (t < 256) c1[t] = part[0][t] + part[1][t] + part[2][t] + part[3][t];
+    __syncthreads();
+    if (t < 64) {   // one wave scans both: 4 digits of base1 and 2 of base2 per lane
+        uint32_t a[4], sa = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            a[k] = c1[t * 4 + k];
+            sa += a[k];
         }
-        for (int d = 0; d < 256; d++) {
-            base2[d] = r2;
-            r2 += d < 128 ? c2[d] : 0u;
+        uint32_t run1 = wave_incl_scan_u32(sa) - sa;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            base1[t * 4 + k] = run1;
+            run1 += a[k];
         }
+        const uint32_t b0 = c2[t * 2], b1 = c2[t * 2 + 1];
+        uint32_t run2 = wave_incl_scan_u32(b0 + b1) - b0 - b1;
+        base2[t * 2] = run2;
+        base2[t * 2 + 1] = run2 + b0;
+        const uint32_t tot2 = (uint32_t)__shfl((int)(run2 + b0 + b1), 63, 64);
+        base2[128 + t * 2] = tot2;   // (digits 128..255 of the second pass are empty)
+        base2[128 + t * 2 + 1] = tot2;
     }
 }
 
@@ -577,9 +678,7 @@ __global__ void __launch_bounds__(256) tl_hist8_kernel(const K* __restrict__ key
     __shared__ uint32_t h[256];
     h[threadIdx.x] = 0;
     __syncthreads();
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
-        atomicAdd(&h[(uint32_t)((((uint64_t)keys[i] >> f.lo) & f.fmask) >> L) & 255u], 1u);
+    for_each_key<8>(keys, n, [&](K k) { atomicAdd(&h[(uint32_t)((((uint64_t)k >> f.lo) & f.fmask) >> L) & 255u], 1u); });
     __syncthreads();
     if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
 }
@@ -1177,13 +1276,10 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
 #pragma unroll
             for (int k = 0; k < TL2_ITEMS; k++) {
                 const uint32_t i = (uint32_t)k * TL2_NT + threadIdx.x;
-                uint32_t dd = 0;
-                if (i < m) {
-                    const uint64_t wd = stage[i];
-                    dd = (uint32_t)(wd >> dsh) & (BINS - 1);
-                    const uint32_t p = gofs[dd] + i;
-                    if ((uint64_t)p < n) QE_ST(&wout[p], wd);
-                }
+                const uint64_t wd = stage[i];   // (a slot past m: a stale word, not stored)
+                const uint32_t dd = i < m ? (uint32_t)(wd >> dsh) & (BINS - 1) : 0u;
+                const uint32_t p = gofs[dd] + i;
+                QE_STS(i < m && (uint64_t)p < n, &wout[p], &g_store_sink[l], wd);
                 if (k & 3) dg[k >> 2] |= dd << (8 * (k & 3));
                 else dg[k >> 2] = dd;
                 if (k % 6 == 5) __builtin_amdgcn_sched_barrier(0);   // six slots' LDS reads in flight, not 18
@@ -1196,10 +1292,8 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
 #pragma unroll
             for (int k = 0; k < TL2_ITEMS; k++) {
                 const uint32_t i = (uint32_t)k * TL2_NT + threadIdx.x;
-                if (i < m) {
-                    const uint32_t p = gofs[(dg[k >> 2] >> (8 * (k & 3))) & 0xFFu] + i;
-                    if ((uint64_t)p < n) QE_ST(&xout[p], stage[i]);
-                }
+                const uint32_t p = gofs[(dg[k >> 2] >> (8 * (k & 3))) & 0xFFu] + i;
+                QE_STS(i < m && (uint64_t)p < n, &xout[p], &g_store_sink[l], stage[i]);
                 if (k % 6 == 5) __builtin_amdgcn_sched_barrier(0);
             }
         } else if constexpr (CARRY != X_NONE) {
@@ -1219,10 +1313,9 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
 #pragma unroll
                 for (int q = 0; q < TL2_WCH; q++) {
                     const uint32_t i = (uint32_t)(k0 + q) * TL2_NT + threadIdx.x;
-                    if (i < m) {
-                        if ((uint64_t)p[q] < n) QE_ST(&wout[p[q]], wd[q]);
-                        reinterpret_cast<uint32_t*>(stage)[2 * i] = p[q];   // slot i now holds its destination
-                    }
+                    const bool ok = i < m && (uint64_t)p[q] < n;
+                    QE_STS(ok, &wout[p[q]], &g_store_sink[l], wd[q]);   // (every store issued: counted waits)
+                    if (i < m) reinterpret_cast<uint32_t*>(stage)[2 * i] = p[q];   // slot i now holds its destination
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -1231,11 +1324,9 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
             if constexpr (CARRY == X64) {
 #pragma unroll
                 for (int j = 0; j < TL2_ITEMS; j++) {   // payload j goes straight to its slot's destination
-                    if (j * 64 < lim) {
-                        const uint32_t sl = (pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-                        const uint32_t dst = reinterpret_cast<const uint32_t*>(stage)[2 * sl];
-                        if ((uint64_t)dst < n) QE_ST(&xout[dst], word[j]);
-                    }
+                    const uint32_t sl = (pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                    const uint32_t dst = reinterpret_cast<const uint32_t*>(stage)[2 * sl];
+                    QE_STS(j * 64 < lim && (uint64_t)dst < n, &xout[dst], &g_store_sink[l], word[j]);
                 }
             } else {
                 // a 32-bit payload joins its destination in the slot's other half, and the slots
@@ -1254,8 +1345,7 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
                         dv[q] = reinterpret_cast<const uint2*>(stage)[(uint32_t)(k0 + q) * TL2_NT + threadIdx.x];
 #pragma unroll
                     for (int q = 0; q < TL2_WCH; q++)
-                        if ((uint32_t)(k0 + q) * TL2_NT + threadIdx.x < m && (uint64_t)dv[q].x < n)
-                            QE_ST(&xo[dv[q].x], dv[q].y);
+                        QE_STS((uint32_t)(k0 + q) * TL2_NT + threadIdx.x < m && (uint64_t)dv[q].x < n, &xo[dv[q].x], reinterpret_cast<uint32_t*>(&g_store_sink[l]), dv[q].y);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
@@ -1272,10 +1362,10 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
 #pragma unroll
                 for (int q = 0; q < TL2_WCH; q++) {
                     const uint32_t i = (uint32_t)(k0 + q) * TL2_NT + threadIdx.x;
-                    if (i < m && (uint64_t)p[q] < n) {   // (p < n: never false with consistent offsets)
-                        if constexpr (W32) QE_ST(&reinterpret_cast<uint32_t*>(wout)[p[q]], (uint32_t)(wd[q] >> 32));
-                        else QE_ST(&wout[p[q]], wd[q]);
-                    }
+                    const bool ok = i < m && (uint64_t)p[q] < n;   // (p < n: never false with consistent offsets)
+                    if constexpr (W32)
+                        QE_STS(ok, &reinterpret_cast<uint32_t*>(wout)[p[q]], reinterpret_cast<uint32_t*>(&g_store_sink[l]), (uint32_t)(wd[q] >> 32));
+                    else QE_STS(ok, &wout[p[q]], &g_store_sink[l], wd[q]);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
