@@ -544,7 +544,7 @@ constexpr int TL_NT = QE_TL_NT, TL_ITEMS = QE_TL_ITEMS, TL_CAP = TL_NT * TL_ITEM
 template <typename K>
 __global__ void __launch_bounds__(1024) tl_hist_kernel(const K* __restrict__ keys, uint64_t n, Field f, int L,
                                                        uint32_t* __restrict__ hist) {
-    __shared__ uint32_t h[TL_BUCKETS];   // 128 KiB: one block per CU, 16 waves
+    __shared__ alignas(16) uint32_t h[TL_BUCKETS];   // 128 KiB: one block per CU, 16 waves
     for (int i = threadIdx.x; i < TL_BUCKETS; i += 1024) h[i] = 0;
     __syncthreads();
     for_each_key<8>(keys, n, [&](K k) {
@@ -596,7 +596,7 @@ __global__ void __launch_bounds__(1024) tl_scan_kernel(const uint32_t* __restric
                                                        uint32_t* __restrict__ base1, uint32_t* __restrict__ base2,
                                                        uint64_t* __restrict__ maxb) {
     constexpr int PER = TL_BUCKETS / 1024;
-    __shared__ uint32_t h[TL_BUCKETS];
+    __shared__ alignas(16) uint32_t h[TL_BUCKETS];
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t c1[256], c2[128];
     __shared__ uint32_t wmax[16];
@@ -860,11 +860,23 @@ __global__ void __launch_bounds__(NT) tl_local_kernel(const uint64_t* __restrict
 constexpr uint32_t TL_TPG = QE_TL_TPG;   // first-pass tiles per group
 static_assert(RTILE == 8192, "tl_hist_tiles_kernel counts 8192-key first-pass tiles (1024 threads x 8)");
 
+// The end of a histogram block: its group's 32 K bucket counts stored PLAINLY, each of a group's Q
+// blocks into its own slice gout + q * nseg * 128 (gcnt's layout), folded by tl_gfold_kernel.  Round
+// 3 added them into gcnt with device-scope atomics: those execute at the memory side, one 256-B wave
+// instruction per ~50 ns per CU (MI355X_MICROARCH "Global float atomics") = ~25 us for a block's
+// 128 KiB, every block at once at the end of the pass, and gcnt needed a memset first.
+__device__ inline void tl_store_counts(const uint32_t* h, uint32_t g, uint32_t q, uint32_t G, uint32_t* gout) {
+    uint32_t* o = gout + (uint64_t)q * 256u * G * 128u;
+    for (uint32_t i = threadIdx.x * 4u; i < TL_BUCKETS; i += blockDim.x * 4u)   // 16-B stores, 512-B runs
+        *reinterpret_cast<uint4*>(o + ((uint64_t)(i >> 7) * G + g) * 128u + (i & 127u)) =
+            *reinterpret_cast<const uint4*>(h + i);
+}
+
 template <typename K>
 __global__ void __launch_bounds__(1024) tl_hist_tiles_kernel(const K* __restrict__ keys, uint64_t n, Field f, int L,
                                                              uint32_t nt, uint32_t G, uint32_t Q,
-                                                             uint32_t* __restrict__ tcnt, uint32_t* __restrict__ gcnt) {
-    __shared__ uint32_t h[TL_BUCKETS];   // index d1 * 128 + d2: 128 KiB, one block per CU
+                                                             uint32_t* __restrict__ tcnt, uint32_t* __restrict__ gout) {
+    __shared__ alignas(16) uint32_t h[TL_BUCKETS];   // index d1 * 128 + d2: 128 KiB, one block per CU
     __shared__ uint32_t th[2][256];      // the tile's d1 counts, double-buffered: one barrier per tile
     for (int i = threadIdx.x; i < TL_BUCKETS; i += 1024) h[i] = 0;
     if (threadIdx.x < 512) (&th[0][0])[threadIdx.x] = 0;
@@ -925,8 +937,7 @@ __global__ void __launch_bounds__(1024) tl_hist_tiles_kernel(const K* __restrict
     }
     if (g * TL_TPG + q < t_end && threadIdx.x < 256) tcnt[(uint64_t)prev * 256 + threadIdx.x] = th[par ^ 1u][threadIdx.x];
     __syncthreads();
-    for (int i = threadIdx.x; i < TL_BUCKETS; i += 1024)
-        if (h[i]) atomicAdd(&gcnt[((uint64_t)(i >> 7) * G + g) * 128 + (i & 127)], h[i]);
+    tl_store_counts(h, g, q, G, gout);
 }
 
 // tl_hist_tiles_kernel fused into the gather that produces the keys: keys = col[rows] in list
@@ -938,9 +949,9 @@ __global__ void __launch_bounds__(1024) tl_gather_hist_kernel(const uint64_t* __
                                                               const uint32_t* __restrict__ rows, uint64_t n,
                                                               uint64_t* __restrict__ keys, Field f, int L, uint32_t nt,
                                                               uint32_t G, uint32_t Q, uint32_t* __restrict__ tcnt,
-                                                              uint32_t* __restrict__ gcnt,
+                                                              uint32_t* __restrict__ gout,
                                                               const uint32_t* __restrict__ col32 = nullptr) {
-    __shared__ uint32_t h[TL_BUCKETS];
+    __shared__ alignas(16) uint32_t h[TL_BUCKETS];
     __shared__ uint32_t th[2][256];
     for (int i = threadIdx.x; i < TL_BUCKETS; i += 1024) h[i] = 0;
     if (threadIdx.x < 512) (&th[0][0])[threadIdx.x] = 0;
@@ -991,25 +1002,36 @@ __global__ void __launch_bounds__(1024) tl_gather_hist_kernel(const uint64_t* __
     }
     if (g * TL_TPG + q < t_end && threadIdx.x < 256) tcnt[(uint64_t)prev * 256 + threadIdx.x] = th[par ^ 1u][threadIdx.x];
     __syncthreads();
-    for (int i = threadIdx.x; i < TL_BUCKETS; i += 1024)
-        if (h[i]) atomicAdd(&gcnt[((uint64_t)(i >> 7) * G + g) * 128 + (i & 127)], h[i]);
+    tl_store_counts(h, g, q, G, gout);
 }
 
-// the bucket histogram in natural order (bucket = d2 << 8 | d1) from the segment counts
-__global__ void __launch_bounds__(128) tl_gsum_kernel(const uint32_t* __restrict__ gcnt, uint32_t G,
-                                                      uint32_t* __restrict__ hist) {
-    const uint32_t d1 = blockIdx.x, d2 = threadIdx.x;
-    const uint32_t* p = gcnt + (uint64_t)d1 * G * 128 + d2;
-    uint32_t s = 0, g = 0;
-    for (; g + 8 <= G; g += 8) {   // 8 independent loads in flight
-        uint32_t v[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) v[j] = p[(uint64_t)(g + j) * 128];
-#pragma unroll
-        for (int j = 0; j < 8; j++) s += v[j];
+// gcnt = the sum of a histogram's Q slices (src != dst), and with `hist` the bucket histogram in
+// natural order (bucket = d2 << 8 | d1) from the segment counts.  Block = (d1, 32 d2's) x 8 group
+// lanes, G x Q / 8 (~32) independent loads per thread; the lanes' sums meet in LDS.
+__global__ void __launch_bounds__(256) tl_gfold_kernel(const uint32_t* __restrict__ src, uint32_t Q, uint32_t G,
+                                                       uint32_t* __restrict__ dst, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t part[8][32];
+    const uint32_t d1 = blockIdx.x >> 2, d2 = (blockIdx.x & 3u) * 32u + (threadIdx.x & 31u), gl = threadIdx.x >> 5;
+    const uint64_t S = (uint64_t)256u * G * 128u;
+    uint32_t acc = 0;
+#pragma unroll 2
+    for (uint32_t g = gl; g < G; g += 8) {
+        const uint64_t o = ((uint64_t)d1 * G + g) * 128u + d2;
+        uint32_t s = 0;
+#pragma unroll 4
+        for (uint32_t q = 0; q < Q; q++) s += src[q * S + o];
+        if (dst != src) dst[o] = s;
+        acc += s;
     }
-    for (; g < G; g++) s += p[(uint64_t)g * 128];
-    hist[(d2 << 8) | d1] = s;
+    if (!hist) return;   // (grid-uniform)
+    part[gl][threadIdx.x & 31u] = acc;
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) t += part[j][threadIdx.x];
+        hist[(d2 << 8) | d1] = t;
+    }
 }
 
 // Column-wise exclusive scan of a rows x C matrix of u32 counts, in place: m[r][c] <- base[c] +
@@ -2034,6 +2056,21 @@ static bool prof_split() {   // tuning aid: QE_PROF_SPLIT=1 times the second pas
     return on;
 }
 
+// blocks of tl_hist_kernel.  Each block zeroes a 32 K-bucket LDS table and adds it out with device-
+// scope atomics (executed at the memory side: ~0.1 us of chip time per block, on 32 K words every
+// block shares), against ~2.7 keys per CU cycle of LDS atomics while counting: B ~ sqrt(n / 720)
+// balances the two (round 3 used one block per 4096 keys up to 256: a 1e6-key sort paid 256
+// flushes for 4 K keys each).  QE_HIST_C tunes the constant; 0 restores round 3's grid.
+static unsigned hist_blocks(uint64_t n) {
+    static const double C = [] {
+        const char* s = getenv("QE_HIST_C");
+        return s ? atof(s) : 720.0;
+    }();
+    if (C <= 0) return grid_for((n + 3) / 4, 1024, 256);
+    const double b = sqrt((double)n / C);
+    return b < 8 ? 8u : b > 256 ? 256u : (unsigned)b;
+}
+
 static uint64_t sort_pre_min() {   // tuning knob: QE_SORT_PRE_MIN = smallest n for the lookback-free form
     static uint64_t v = [] {
         const char* s = getenv("QE_SORT_PRE_MIN");
@@ -2073,6 +2110,20 @@ static void local_sort_buckets(qe_ctx* c, const uint64_t* words, K* kout, uint32
         hipLaunchKernelGGL((tl_local_kernel<K, IN_WORD>), dim3(nbuckets), dim3(TL_NT), 0, c->stream, words, nullptr,
                            nullptr, kout, vout, bstart, 0u, f, lr);
     QE_HIP(hipGetLastError());
+}
+
+// where a histogram kernel stores its group counts: gcnt itself when every group has one block, else
+// Q slices that hist_fold adds into gcnt (and frees), also writing the bucket histogram when asked
+static uint32_t* hist_slices(qe_ctx* c, uint32_t* gcnt, uint32_t Q, uint32_t nseg) {
+    return Q > 1 ? dalloc_t<uint32_t>(c, (size_t)Q * nseg * 128) : gcnt;
+}
+static void hist_fold(qe_ctx* c, uint32_t* gout, uint32_t Q, uint32_t G, uint32_t* gcnt, uint32_t* hist) {
+    if (gout != gcnt || hist) {
+        hipLaunchKernelGGL(tl_gfold_kernel, dim3(1024), dim3(256), 0, c->stream, gout, gout != gcnt ? Q : 1u, G, gcnt,
+                           hist);
+        QE_HIP(hipGetLastError());
+    }
+    if (gout != gcnt) dfree(c, gout);
 }
 
 // the two-level sort (H = TL_H) with both global passes lookback-free (see tl_hist_tiles_kernel)
@@ -2117,20 +2168,18 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
         tcnt = ph->second.tcnt;
         gcnt = ph->second.gcnt;
         c->prehist.erase(ph);
-    } else {
-        QE_HIP(hipMemsetAsync(gcnt, 0, (size_t)nseg * 128 * sizeof(uint32_t), c->stream));
     }
     {
         Timed t(c, "sort_hist", have ? 0.0 : (kn ? 4.0 : (double)sizeof(K)) * n);
+        uint32_t* gout = have ? gcnt : hist_slices(c, gcnt, Q, nseg);
         if (!have && kn)
             hipLaunchKernelGGL((tl_hist_tiles_kernel<uint32_t>), dim3(G * Q), dim3(1024), 0, c->stream, kn, n, f, L, nt,
-                               G, Q, tcnt, gcnt);
+                               G, Q, tcnt, gout);
         else if (!have)
             hipLaunchKernelGGL((tl_hist_tiles_kernel<K>), dim3(G * Q), dim3(1024), 0, c->stream, keys, n, f, L, nt, G,
-                               Q, tcnt, gcnt);
+                               Q, tcnt, gout);
         QE_HIP(hipGetLastError());
-        hipLaunchKernelGGL(tl_gsum_kernel, dim3(256), dim3(128), 0, c->stream, gcnt, G, hist);
-        QE_HIP(hipGetLastError());
+        hist_fold(c, gout, have ? 1u : Q, G, gcnt, hist);
         hipLaunchKernelGGL(tl_bstart_kernel, dim3(1), dim3(1024), 0, c->stream, hist, bstart, d_max);
         QE_HIP(hipGetLastError());
     }
@@ -2332,8 +2381,7 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
     } else {
         QE_HIP(hipMemsetAsync(hist, 0, TL_BUCKETS * sizeof(uint32_t), c->stream));
         Timed t(c, "sort_hist", (double)sizeof(K) * n);
-        hipLaunchKernelGGL((tl_hist_kernel<K>), dim3(grid_for((n + 3) / 4, 1024, 256)), dim3(1024), 0, c->stream, keys,
-                           n, f, L, hist);
+        hipLaunchKernelGGL((tl_hist_kernel<K>), dim3(hist_blocks(n)), dim3(1024), 0, c->stream, keys, n, f, L, hist);
         QE_HIP(hipGetLastError());
         hipLaunchKernelGGL(tl_scan_kernel, dim3(1), dim3(1024), 0, c->stream, hist, bstart, base1, base2, d_max);
         QE_HIP(hipGetLastError());
@@ -2679,21 +2727,20 @@ void partition_words_kv(qe_ctx* c, const uint64_t* keys, const uint64_t* v64, co
     uint32_t* hist = dalloc_t<uint32_t>(c, TL_BUCKETS);
     uint32_t* bstart = dalloc_t<uint32_t>(c, TL_BUCKETS + 1);
     uint32_t* seg = dalloc_t<uint32_t>(c, (size_t)nseg + 1);
-    QE_HIP(hipMemsetAsync(gcnt, 0, (size_t)nseg * 128 * sizeof(uint32_t), c->stream));
     // base columns with u32 copies (Relation::cols32): the histogram and the first pass read those
     const uint32_t* kn = narrow_of(c, keys, n);
     const uint32_t* vn = v64 ? narrow_of(c, v64, n) : nullptr;
     {
         Timed t(c, "sort_hist", (kn ? 4.0 : 8.0) * n);
+        uint32_t* gout = hist_slices(c, gcnt, Q, nseg);
         if (kn)
             hipLaunchKernelGGL((tl_hist_tiles_kernel<uint32_t>), dim3(G * Q), dim3(1024), 0, c->stream, kn, n, f, L, nt,
-                               G, Q, tcnt, gcnt);
+                               G, Q, tcnt, gout);
         else
             hipLaunchKernelGGL((tl_hist_tiles_kernel<uint64_t>), dim3(G * Q), dim3(1024), 0, c->stream, keys, n, f, L, nt,
-                               G, Q, tcnt, gcnt);
+                               G, Q, tcnt, gout);
         QE_HIP(hipGetLastError());
-        hipLaunchKernelGGL(tl_gsum_kernel, dim3(256), dim3(128), 0, c->stream, gcnt, G, hist);
-        QE_HIP(hipGetLastError());
+        hist_fold(c, gout, Q, G, gcnt, hist);
         hipLaunchKernelGGL(tl_bstart_kernel, dim3(1), dim3(1024), 0, c->stream, hist, bstart, c->d_scratch + 34);
         QE_HIP(hipGetLastError());
     }
@@ -2787,18 +2834,19 @@ static bool gather_hist_impl(qe_ctx* c, const uint64_t* col, const uint32_t* row
     const uint32_t nseg = 256u * G;
     uint32_t* tcnt = dalloc_t<uint32_t>(c, (size_t)nt * 256);
     uint32_t* gcnt = dalloc_t<uint32_t>(c, (size_t)nseg * 128);
-    QE_HIP(hipMemsetAsync(gcnt, 0, (size_t)nseg * 128 * sizeof(uint32_t), c->stream));
+    uint32_t* gout = hist_slices(c, gcnt, Q, nseg);
     if (col) {
         Timed t(c, "gather_keys", (col32 ? 8.0 : 12.0) * n + 8.0 * n);
         hipLaunchKernelGGL(tl_gather_hist_kernel<false>, dim3(G * Q), dim3(1024), 0, c->stream, col, rows, n, keys, f, L,
-                           nt, G, Q, tcnt, gcnt, col32);
+                           nt, G, Q, tcnt, gout, col32);
         QE_HIP(hipGetLastError());
     } else {
         Timed t(c, "widen_keys", 12.0 * n);
         hipLaunchKernelGGL(tl_gather_hist_kernel<true>, dim3(G * Q), dim3(1024), 0, c->stream, nullptr, rows, n, keys, f,
-                           L, nt, G, Q, tcnt, gcnt);
+                           L, nt, G, Q, tcnt, gout);
         QE_HIP(hipGetLastError());
     }
+    hist_fold(c, gout, Q, G, gcnt, nullptr);   // (the sort that reads these counts makes the histogram)
     PreHist ph;
     ph.tcnt = tcnt;
     ph.gcnt = gcnt;
