@@ -53,6 +53,12 @@ __device__ __forceinline__ uint2 buf_load_u2(__amdgpu_buffer_rsrc_t r, uint32_t 
 __device__ __forceinline__ uint32_t buf_load_u32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
 }
+typedef unsigned int qe_v4u __attribute__((ext_vector_type(4)));
+// (a 16-B load that crosses the end of the range: use it only where the range is whole 16-B units)
+__device__ __forceinline__ uint4 buf_load_u4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    const qe_v4u x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0);
+    return make_uint4(x.x, x.y, x.z, x.w);
+}
 
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll

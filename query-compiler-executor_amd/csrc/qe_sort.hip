@@ -278,8 +278,11 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
     constexpr int NW = NT / 64;
     constexpr int TILE = NT * ITEMS, WT = 64 * ITEMS;
     const bool owner = DPT > 1 || (int)threadIdx.x < BINS;   // this thread owns digits
+    // per-wave digit counts -> exclusive over waves; UNSTABLE ranks on ONE block-wide row (no order
+    // to keep between waves), which leaves a 1024-thread tile in 2 workgroups' LDS per CU
+    constexpr int NWH = UNSTABLE ? 1 : NW;
     __shared__ uint64_t stage[TILE];
-    __shared__ uint32_t whist[NW][BINS];   // per-wave digit counts -> exclusive over waves
+    __shared__ uint32_t whist[NWH][BINS];
     __shared__ uint32_t bexcl[BINS];        // tile-local exclusive offset of each digit
     __shared__ uint32_t gofs[BINS];         // global position of the digit's run - bexcl
     __shared__ uint32_t wsum[NW];
@@ -302,11 +305,10 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
 #pragma unroll
         for (int q = 0; q < DPT; q++) pre_off[q] = owner ? offs[(uint64_t)tile * BINS + threadIdx.x * DPT + q] : 0u;
     }
-    for (int i = threadIdx.x; i < NW * BINS; i += NT) (&whist[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < NWH * BINS; i += NT) (&whist[0][0])[i] = 0;
     __syncthreads();
     QE_SORT_STAMP(tile, 1);
 
-    const uint64_t wave_base = (uint64_t)tile * TILE + (uint64_t)w * WT;
     uint64_t word[ITEMS];
     uint32_t pos[ITEMS];
     // every load unconditional, through buffer descriptors over this tile's elements (those past
@@ -314,6 +316,31 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
     const uint64_t tb = (uint64_t)tile * TILE;
     const uint32_t tcount = (uint32_t)((n - tb) < (uint64_t)TILE ? (n - tb) : (uint64_t)TILE);
     const uint32_t loc0 = (uint32_t)w * WT + (uint32_t)l;   // this lane's first tile-local element
+    // V4 (unstable ranks, u32 keys and u32 side arrays): a lane loads 16 B = 4 consecutive elements
+    // of each array (1 KiB per wave instruction instead of 256 B) -- element j of lane l is then
+    // tile-local w * WT + (j / 4) * 256 + 4 l + j % 4.  A partial tile loads them one by one.
+    constexpr bool V4 = UNSTABLE && sizeof(K) == 4 && (IN == IN_KIOTA || IN == IN_KV) && CARRY != XCOL && ITEMS % 4 == 0;
+    auto loc_of = [&](int j) -> uint32_t {
+        return V4 ? (uint32_t)w * WT + (uint32_t)(j >> 2) * 256u + (uint32_t)l * 4u + (uint32_t)(j & 3)
+                  : loc0 + (uint32_t)j * 64u;
+    };
+    const bool full = tcount == (uint32_t)TILE;   // (block-uniform)
+    // u32 elements j of one array at the V4 mapping
+    auto load_v4 = [&](const __amdgpu_buffer_rsrc_t& r, uint32_t (&x)[ITEMS]) {
+        if (full) {
+#pragma unroll
+            for (int g = 0; g < ITEMS / 4; g++) {
+                const uint4 a = buf_load_u4(r, ((uint32_t)w * WT + (uint32_t)l * 4u) * 4u, (uint32_t)g * 1024u);
+                x[4 * g] = a.x;
+                x[4 * g + 1] = a.y;
+                x[4 * g + 2] = a.z;
+                x[4 * g + 3] = a.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < ITEMS; j++) x[j] = buf_load_u32(r, loc_of(j) * 4u, 0u);
+        }
+    };
     if constexpr (IN == IN_WORD) {
         const auto rw = buf_rsrc(win + tb, tcount * 8u);
 #pragma unroll
@@ -321,6 +348,14 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
             const uint2 v = buf_load_u2(rw, loc0 * 8u, (uint32_t)j * 512u);
             word[j] = (uint64_t)v.y << 32 | v.x;
         }
+    } else if constexpr (V4) {
+        uint32_t kk[ITEMS], vv[ITEMS];
+        load_v4(buf_rsrc(kin + tb, tcount * 4u), kk);
+        if constexpr (IN == IN_KV) load_v4(buf_rsrc(vin + tb, tcount * 4u), vv);
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++)
+            word[j] = ((((uint64_t)kk[j] >> f.lo) & f.fmask) << 32) |
+                      (IN == IN_KV ? vv[j] : (uint32_t)(tb + loc_of(j)));
     } else {
         const auto rk = buf_rsrc(kin + tb, tcount * (uint32_t)sizeof(K));
         const auto rv = IN == IN_KV64 ? buf_rsrc(reinterpret_cast<const uint64_t*>(vin) + tb, tcount * 8u)
@@ -348,11 +383,10 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
     // stable rank inside the wave: element order is (j, lane)
 #pragma unroll
     for (int j = 0; j < ITEMS; j++) {
-        uint64_t i = wave_base + (uint64_t)j * 64 + l;
-        bool ok = i < n;
+        const bool ok = loc_of(j) < tcount;
         uint32_t d = (uint32_t)(word[j] >> dsh) & mask;
         if constexpr (UNSTABLE) {
-            pos[j] = ok ? atomicAdd(&whist[w][d], 1u) : 0u;
+            pos[j] = ok ? atomicAdd(&whist[0][d], 1u) : 0u;
             continue;
         }
 #ifdef QE_DIAG_SORT_NORANK   // ablation only: LDS-atomic ranks instead of match-any (unstable, in range)
@@ -387,7 +421,7 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
         if (!owner) continue;
         uint32_t t = 0;
 #pragma unroll
-        for (int ww = 0; ww < NW; ww++) {
+        for (int ww = 0; ww < NWH; ww++) {
             uint32_t c = whist[ww][d];
             whist[ww][d] = t;
             t += c;
@@ -411,10 +445,9 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
     // stage the tile in digit order (tile-local offsets only)
 #pragma unroll
     for (int j = 0; j < ITEMS; j++) {
-        uint64_t i = wave_base + (uint64_t)j * 64 + l;
-        if (i < n) {
+        if (loc_of(j) < tcount) {
             uint32_t dd = (uint32_t)(word[j] >> dsh) & mask;
-            const uint32_t slot = bexcl[dd] + whist[w][dd] + pos[j];
+            const uint32_t slot = bexcl[dd] + whist[UNSTABLE ? 0 : w][dd] + pos[j];
             stage[slot] = word[j];
             if constexpr (CARRY != X_NONE) pos[j] = slot;   // the payload takes the same slot later
         }
@@ -427,13 +460,23 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
         const auto ra = CARRY == XCOL ? buf_rsrc(reinterpret_cast<const uint64_t*>(xa) + tb, tcount * 8u)
                                       : buf_rsrc(xa + tb, tcount * 4u);
         const auto rb = buf_rsrc(xb ? xb + tb : xa, xb ? tcount * 4u : 0u);   // (no xb: reads 0)
+        if constexpr (V4 && CARRY == X64) {
+            uint32_t xa4[ITEMS], xb4[ITEMS];
+            load_v4(ra, xa4);
+            load_v4(rb, xb4);
 #pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            if constexpr (CARRY == X64)
-                word[j] = (uint64_t)buf_load_u32(ra, loc0 * 4u, (uint32_t)j * 256u) |
-                          (uint64_t)buf_load_u32(rb, loc0 * 4u, (uint32_t)j * 256u) << 32;
-            else if constexpr (CARRY == X32) xw[j] = buf_load_u32(ra, loc0 * 4u, (uint32_t)j * 256u);
-            else xw[j] = buf_load_u2(ra, loc0 * 8u, (uint32_t)j * 512u).x;
+            for (int j = 0; j < ITEMS; j++) word[j] = (uint64_t)xa4[j] | (uint64_t)xb4[j] << 32;
+        } else if constexpr (V4) {
+            load_v4(ra, xw);
+        } else {
+#pragma unroll
+            for (int j = 0; j < ITEMS; j++) {
+                if constexpr (CARRY == X64)
+                    word[j] = (uint64_t)buf_load_u32(ra, loc0 * 4u, (uint32_t)j * 256u) |
+                              (uint64_t)buf_load_u32(rb, loc0 * 4u, (uint32_t)j * 256u) << 32;
+                else if constexpr (CARRY == X32) xw[j] = buf_load_u32(ra, loc0 * 4u, (uint32_t)j * 256u);
+                else xw[j] = buf_load_u2(ra, loc0 * 8u, (uint32_t)j * 512u).x;
+            }
         }
     }
 #pragma unroll
@@ -506,7 +549,7 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
         uint32_t* st32 = reinterpret_cast<uint32_t*>(stage);   // (32-bit payloads: 4-B slots)
 #pragma unroll
         for (int j = 0; j < ITEMS; j++)
-            if (wave_base + (uint64_t)j * 64 + l < n) {
+            if (loc_of(j) < tcount) {
                 if constexpr (P32) st32[pos[j]] = xw[j];
                 else stage[pos[j]] = word[j];
             }
@@ -1660,7 +1703,13 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
     __shared__ uint32_t tab[HJ_I * NW];
     __shared__ uint64_t s_excl;
     __shared__ uint32_t s_total, s_long;
+#ifdef QE_DIAG_STAMPS
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint32_t b = blockIdx.x;
+#ifdef QE_DIAG_STAMPS
+    if (threadIdx.x == 0 && b < STAMP_TILES) g_hj_stamps[(uint64_t)b * STAMP_SLOTS] = t_start;
+#endif
     const uint32_t r0 = bsR[b], mR = bsR[b + 1] - r0, s0 = bsS[b], mS = bsS[b + 1] - s0;
     if (mR > (uint32_t)(NT * HJ_I) || mS > (uint32_t)(NT * HJ_I)) {   // beyond LDS (the sorts were not checked): flag it
         if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(total_out + 1), 1ull);
@@ -1698,6 +1747,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
     for (uint32_t v = threadIdx.x; v < D; v += NT) head[v] = HJ_NONE;
     if (threadIdx.x == 0) s_long = 0;
     __syncthreads();
+    QE_STAMP(g_hj_stamps, b, 1);
 #pragma unroll
     for (int j = 0; j < HJ_I; j++) {
         const uint32_t i = (uint32_t)j * NT + threadIdx.x;
@@ -1708,9 +1758,16 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
         }
     }
     __syncthreads();
+    QE_STAMP(g_hj_stamps, b, 2);
     uint32_t pre[HJ_I], hd[HJ_I], tot[HJ_I];
 #pragma unroll
     for (int j = 0; j < HJ_I; j++) {
+        if ((uint32_t)j * NT + (uint32_t)w * 64u >= mS) {   // (wave-uniform) no S row of this item in this
+            hd[j] = HJ_NONE;                                  // wave: skip its walk and scan (a C3 bucket
+            pre[j] = tot[j] = 0;                              // fills 1.4 of the 5 items)
+            if (l == 63) tab[j * NW + w] = 0;
+            continue;
+        }
         uint32_t cnt = 0, h = HJ_NONE;
         if ((uint32_t)j * NT + threadIdx.x < mS) {
             h = head[fld(ws[j]) & dmask];
@@ -1724,6 +1781,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
         if (l == 63) tab[j * NW + w] = inc;
     }
     __syncthreads();
+    QE_STAMP(g_hj_stamps, b, 3);
     if (s_long) {   // block-uniform: a chain too long to emit by walking (the sorts + merge take the join)
         if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(total_out + 1), 1ull);
         return;
@@ -1742,6 +1800,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
         }
     }
     __syncthreads();
+    QE_STAMP(g_hj_stamps, b, 4);
     const uint64_t gofs = s_excl;
     if (gofs + s_total > cap) return;   // outgrew the buffers: the host re-runs with the exact size
 #pragma unroll
@@ -1778,6 +1837,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
             }
         }
     }
+    QE_STAMP(g_hj_stamps, b, 5);
 }
 
 static bool hj_chain_on() {
@@ -2044,9 +2104,14 @@ static void column_scans(qe_ctx* c, uint32_t* m0, uint32_t rows0, uint32_t* m1, 
 #ifndef QE_PRE_NT
 #define QE_PRE_NT 512
 #endif
+#ifndef QE_PRE_NTU
+#define QE_PRE_NTU 512
+#endif
 // threads of the lookback-free first pass (its tile stays RTILE): 1024 x 8 measured 25 % slower
-// than 512 x 16 (fewer loads in flight per thread)
-constexpr int PRE_NT = QE_PRE_NT;
+// than 512 x 16 (fewer loads in flight per thread) when its per-wave rank counters (16 KiB) left
+// one workgroup per CU.  The unstable ranks count on one block-wide row: QE_PRE_NTU threads there.
+constexpr int PRE_NT = QE_PRE_NT, PRE_NTU = QE_PRE_NTU;
+constexpr int pre_nt(bool unstable) { return unstable ? PRE_NTU : PRE_NT; }
 
 static bool prof_split() {   // tuning aid: QE_PROF_SPLIT=1 times the second pass under its own name
     static bool on = [] {
@@ -2215,12 +2280,12 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     // a deferred sort's consumer needs its buckets, not an order inside them: unstable ranks
     const bool uns = dfr && sort_unstable_on();
 #define QE_P1(IN, CR, UN, XA, XB, XO)                                                                                   \
-    hipLaunchKernelGGL((radix_pass_kernel<K, IN, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, CR, UN>),            \
-                       dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, \
+    hipLaunchKernelGGL((radix_pass_kernel<K, IN, OUT_WORD, true, 8, RTILE / pre_nt(UN), pre_nt(UN), true, CR, UN>),            \
+                       dim3(xcd_grid(nt)), dim3(pre_nt(UN)), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, \
                        255u, f, tcnt, nullptr, nullptr, 0u, XA, XB, XO)
 #define QE_P1N(IN, CR, VIN, XA)                                                                                         \
-    hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, CR, true>),      \
-                       dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, kn, nullptr, VIN, nullptr, w1, vout, n, 32 + L,     \
+    hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true), true, CR, true>),      \
+                       dim3(xcd_grid(nt)), dim3(pre_nt(true)), 0, c->stream, kn, nullptr, VIN, nullptr, w1, vout, n, 32 + L,     \
                        255u, f, tcnt, nullptr, nullptr, 0u, XA, nullptr, x1)
 #ifdef QE_DIAG_STAMPS
     stamp_select(c, "p1", n);
@@ -2232,8 +2297,8 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
         Timed t(c, xm ? "sort_pass_carry" : name, (4.0 + (vt ? 4.0 : 0.0) + (xt ? 4.0 : 0.0) + (w32 ? 4.0 : 8.0) +
                                                    (xt ? 4.0 : 0.0)) * n);
         if (w32)
-            hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN_KIOTA, OUT_W32, true, 8, RTILE / PRE_NT, PRE_NT, true, X_NONE, true>),
-                               dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, kn, nullptr, nullptr, nullptr, w1, vout, n,
+            hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN_KIOTA, OUT_W32, true, 8, RTILE / pre_nt(true), pre_nt(true), true, X_NONE, true>),
+                               dim3(xcd_grid(nt)), dim3(pre_nt(true)), 0, c->stream, kn, nullptr, nullptr, nullptr, w1, vout, n,
                                32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr);
         else if (vt && xt) QE_P1N(IN_KV, X32, vt, xt);
         else if (vt) QE_P1N(IN_KV, X_NONE, vt, nullptr);
@@ -2242,19 +2307,19 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
         QE_HIP(hipGetLastError());
     } else if (w32) {
         Timed t(c, name, ((double)sizeof(K) + 4.0) * n);
-        hipLaunchKernelGGL((radix_pass_kernel<K, IN_KIOTA, OUT_W32, true, 8, RTILE / PRE_NT, PRE_NT, true, X_NONE, true>),
-                           dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, nullptr, kout, w1, vout, n,
+        hipLaunchKernelGGL((radix_pass_kernel<K, IN_KIOTA, OUT_W32, true, 8, RTILE / pre_nt(true), pre_nt(true), true, X_NONE, true>),
+                           dim3(xcd_grid(nt)), dim3(pre_nt(true)), 0, c->stream, keys, nullptr, nullptr, kout, w1, vout, n,
                            32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr);
         QE_HIP(hipGetLastError());
     } else if (cv64) {
         Timed t(c, xm ? "sort_pass_carry" : name, ((double)sizeof(K) + 8.0 + (xm ? 8.0 : 0.0) + 8.0 + (xm ? 4.0 : 0.0)) * n);
         if (xm)
-            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV64, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, XCOL, true>),
-                               dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, v64w, kout, w1, vout, n,
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV64, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true), true, XCOL, true>),
+                               dim3(xcd_grid(nt)), dim3(pre_nt(true)), 0, c->stream, keys, nullptr, v64w, kout, w1, vout, n,
                                32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, cxa, nullptr, x1);
         else
-            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV64, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, X_NONE, true>),
-                               dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, keys, nullptr, v64w, kout, w1, vout, n,
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV64, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true), true, X_NONE, true>),
+                               dim3(xcd_grid(nt)), dim3(pre_nt(true)), 0, c->stream, keys, nullptr, v64w, kout, w1, vout, n,
                                32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr);
         QE_HIP(hipGetLastError());
     } else if (xm == X64) {
@@ -2753,8 +2818,8 @@ void partition_words_kv(qe_ctx* c, const uint64_t* keys, const uint64_t* v64, co
     {
         Timed t(c, "sort_pass_agg", ((kn ? 4.0 : 8.0) + (vn ? 4.0 : v64 ? 8.0 : v32 ? 4.0 : 0.0) + 8.0) * n);
 #define QE_PW1(KT, KP, IN, V)                                                                                            \
-    hipLaunchKernelGGL((radix_pass_kernel<KT, IN, OUT_WORD, true, 8, RTILE / PRE_NT, PRE_NT, true, X_NONE, true>),        \
-                       dim3(xcd_grid(nt)), dim3(PRE_NT), 0, c->stream, KP, nullptr, V, nullptr, w1, nullptr, n,         \
+    hipLaunchKernelGGL((radix_pass_kernel<KT, IN, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true), true, X_NONE, true>),        \
+                       dim3(xcd_grid(nt)), dim3(pre_nt(true)), 0, c->stream, KP, nullptr, V, nullptr, w1, nullptr, n,         \
                        32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr)
         if (kn && (vn || v32)) QE_PW1(uint32_t, kn, IN_KV, vn ? vn : v32);
         else if (kn && !v64) QE_PW1(uint32_t, kn, IN_KIOTA, nullptr);

@@ -27,6 +27,7 @@ PHASES = {
     "ws": ["ticket", "loads+ballots", "lookback", "stores"],
     "wsp": ["lookback (next loads in flight)", "stores"],
     "hj": ["bounds+loads issued", "R loaded+hist", "scan+scatter", "S counts+wave scans", "slice atomic", "emit (t0)"],
+    "hjc": ["bounds+loads issued+head init", "R chained (loads landed)", "S counts+wave scans", "slice atomic", "emit (t0)"],
     "p2": ["zero+loads issued", "rank (loads landed)", "digit scan", "stage+payload loads", "words out", "payloads out"],
 }
 
@@ -35,7 +36,7 @@ def report(ctx, which, ntiles):
     buf = np.zeros(ntiles * SLOTS, dtype=np.uint64)
     fn = ctx.lib.qe_diag_stamps
     fn.argtypes = [C.c_char_p, C.c_void_p, C.c_uint64]
-    src = "cp" if which in ("cpp", "ws", "wsp") else "sort" if which == "p2" else which
+    src = "cp" if which in ("cpp", "ws", "wsp") else "sort" if which == "p2" else "hj" if which == "hjc" else which
     rc = fn(src.encode(), buf.ctypes.data, buf.size)   # "hj", "p2": the sort file
     assert rc == 0, rc
     st = buf.reshape(ntiles, SLOTS).astype(np.int64)
@@ -107,7 +108,7 @@ def main():
         for _ in range(2):
             ctx.run_dist(q, None)
         ctx.sync()
-        report(ctx, "hj", 32768)
+        report(ctx, "hjc" if os.environ.get("QE_HJ_CHAIN", "1") != "0" else "hj", 32768)
         ctx.close()
         return
     kinds = [("mod", n), ("mod", n), ("hi32",)]
