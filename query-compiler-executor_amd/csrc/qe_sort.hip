@@ -1187,6 +1187,12 @@ constexpr int TL2_NT = QE_TL2_NT, TL2_ITEMS = QE_TL2_ITEMS, TL2_TILE = TL2_NT * 
 #define QE_TL2_WCH 6
 #endif
 constexpr int TL2_WCH = QE_TL2_WCH;   // write-out chunk (slots whose LDS reads are in flight together)
+// waves per SIMD the kernel is compiled for: 4 (128 VGPRs) at 18 words per thread, whose 75 KB of
+// LDS leave two workgroups per CU anyway; 8 (64 VGPRs) for sub-tiles small enough for four
+#ifndef QE_TL2_WPE
+#define QE_TL2_WPE (QE_TL2_ITEMS <= 9 ? 8 : 2048 / QE_TL2_NT)
+#endif
+constexpr int TL2_WPE = QE_TL2_WPE;
 static_assert(TL2_ITEMS % TL2_WCH == 0, "whole chunks");
 
 // CARRY: the payloads of pass 1 (xin, in pass-1 order; X64: 64-bit, X32: 32-bit) follow the words
@@ -1196,14 +1202,15 @@ static_assert(TL2_ITEMS % TL2_WCH == 0, "whole chunks");
 // byte of a register while its word leaves, the payloads then take the words' slots and leave as
 // the same runs (coalesced), instead of every lane storing its payload at its slot's destination.
 template <typename K, int CARRY = X_NONE, bool UNSTABLE = false, bool W32 = false, bool XS = false>
-__global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const uint64_t* __restrict__ win, uint64_t* __restrict__ wout,
+__global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_t* __restrict__ win, uint64_t* __restrict__ wout,
                                                          uint64_t n, int dsh, const uint32_t* __restrict__ seg,
                                                          const uint32_t* __restrict__ off2, uint32_t G,
                                                          const uint64_t* __restrict__ xin = nullptr,
                                                          uint64_t* __restrict__ xout = nullptr) {
     constexpr int BINS = 128, NW = TL2_NT / 64, WT = 64 * TL2_ITEMS;
+    constexpr int NWH = UNSTABLE ? 1 : NW;   // unstable ranks: one block-wide counter row
     __shared__ uint64_t stage[TL2_TILE];
-    __shared__ uint32_t whist[NW][BINS];
+    __shared__ uint32_t whist[NWH][BINS];
     __shared__ uint32_t bexcl[BINS];
     __shared__ uint32_t gofs[BINS];
     __shared__ uint32_t wsum[NW];
@@ -1223,7 +1230,7 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
     const uint32_t* runp = off2 + (uint64_t)s * BINS + (d < BINS ? d : BINS - 1);
     for (uint32_t base = start; base < end; base += TL2_TILE) {   // block-uniform
         const uint32_t m = end - base < (uint32_t)TL2_TILE ? end - base : (uint32_t)TL2_TILE;
-        for (int i = threadIdx.x; i < NW * BINS; i += TL2_NT) (&whist[0][0])[i] = 0;
+        for (int i = threadIdx.x; i < NWH * BINS; i += TL2_NT) (&whist[0][0])[i] = 0;
         uint64_t word[TL2_ITEMS];
         uint32_t pos2[(TL2_ITEMS + 1) / 2];   // ranks < TL2_TILE: two u16 per register
         const int lim = (int)m - (int)((uint32_t)w * WT + l);   // element j valid iff j * 64 < lim
@@ -1251,7 +1258,7 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
             const uint32_t dd = (uint32_t)(word[j] >> dsh) & (BINS - 1);
             uint32_t r;
             if constexpr (UNSTABLE) {
-                r = ok ? atomicAdd(&whist[w][dd], 1u) : 0u;
+                r = ok ? atomicAdd(&whist[0][dd], 1u) : 0u;
             } else {
                 uint64_t peers = __ballot(ok);
 #pragma unroll
@@ -1278,7 +1285,7 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
         uint32_t tot = 0;
         if (d < BINS) {
 #pragma unroll
-            for (int ww = 0; ww < NW; ww++) {
+            for (int ww = 0; ww < NWH; ww++) {
                 const uint32_t cc = whist[ww][d];
                 whist[ww][d] = tot;
                 tot += cc;
@@ -1305,7 +1312,7 @@ __global__ void __launch_bounds__(TL2_NT, 2048 / TL2_NT) tl_pass2_kernel(const u
             for (int q = 0; q < TL2_WCH; q++) {
                 const int j = j0 + q;
                 const uint32_t dd = (uint32_t)(word[j] >> dsh) & (BINS - 1);
-                sl[q] = bexcl[dd] + whist[w][dd] + ((pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
+                sl[q] = bexcl[dd] + whist[UNSTABLE ? 0 : w][dd] + ((pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
             }
 #pragma unroll
             for (int q = 0; q < TL2_WCH; q++) {
@@ -1677,6 +1684,9 @@ constexpr uint32_t HJ_CHAIN_MAX = 64;
 #ifndef QE_HJ_RR_GLOBAL
 #define QE_HJ_RR_GLOBAL 0
 #endif
+#ifndef QE_HJ_SKIP
+#define QE_HJ_SKIP 1   // (build knob, A/B: 0 walks and scans every item of every wave)
+#endif
 static_assert(TL_CAP < HJ_NONE, "chain links are 16-bit row indices");
 
 // S32: S's payload is 32-bit (xS32: one carried binding), outX0 only.
@@ -1762,7 +1772,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
     uint32_t pre[HJ_I], hd[HJ_I], tot[HJ_I];
 #pragma unroll
     for (int j = 0; j < HJ_I; j++) {
-        if ((uint32_t)j * NT + (uint32_t)w * 64u >= mS) {   // (wave-uniform) no S row of this item in this
+        if (QE_HJ_SKIP && (uint32_t)j * NT + (uint32_t)w * 64u >= mS) {   // (wave-uniform) no S row of this item in this
             hd[j] = HJ_NONE;                                  // wave: skip its walk and scan (a C3 bucket
             pre[j] = tot[j] = 0;                              // fills 1.4 of the 5 items)
             if (l == 63) tab[j * NW + w] = 0;
