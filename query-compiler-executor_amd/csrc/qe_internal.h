@@ -126,6 +126,7 @@ struct qe_ctx {
 
     // small device scratch + pinned host mirror for scalar results
     uint64_t* d_scratch = nullptr;   // 64 words
+    uint32_t* d_zhist = nullptr;     // the lookback-form sorts' histograms (32 K + 256 words), left zeroed by their scans
     uint64_t* h_scratch = nullptr;   // pinned, 64 words
     hipEvent_t wait_ev = nullptr;    // polled for scalar results (read_u64 / read_words, QE_WAIT=event)
     // device blocks a batch's shared sort holds (qe_sort_cache): dfree of one of them is a bug

@@ -635,7 +635,8 @@ __global__ void __launch_bounds__(1024) tl_bstart_kernel(const uint32_t* __restr
 
 // one block: bucket starts (exclusive scan, plus the end), the two global passes' digit bases (the
 // histogram's marginals over the low 8 / high 7 bucket bits) and the largest bucket
-__global__ void __launch_bounds__(1024) tl_scan_kernel(const uint32_t* __restrict__ hist, uint32_t* __restrict__ bstart,
+// (hist is left zeroed for the next sort on this stream: no memset launch per sort)
+__global__ void __launch_bounds__(1024) tl_scan_kernel(uint32_t* __restrict__ hist, uint32_t* __restrict__ bstart,
                                                        uint32_t* __restrict__ base1, uint32_t* __restrict__ base2,
                                                        uint64_t* __restrict__ maxb) {
     constexpr int PER = TL_BUCKETS / 1024;
@@ -652,6 +653,8 @@ __global__ void __launch_bounds__(1024) tl_scan_kernel(const uint32_t* __restric
         mine += v[k];
         mx = v[k] > mx ? v[k] : mx;
     }
+#pragma unroll
+    for (int k = 0; k < PER; k++) hist[t * PER + k] = 0;
     uint32_t inc = wave_incl_scan_u32(mine);
     mx = wave_max_u32(mx);
     if (lane_id() == 63) wsum[wave_id()] = inc;
@@ -728,10 +731,12 @@ __global__ void __launch_bounds__(256) tl_hist8_kernel(const K* __restrict__ key
 
 // one block: the 256 bucket starts (+ the end), which are also the pass's digit bases, and the
 // largest bucket
-__global__ void __launch_bounds__(256) tl_scan8_kernel(const uint32_t* __restrict__ hist, uint32_t* __restrict__ bstart,
+// (hist is left zeroed for the next sort on this stream: no memset launch per sort)
+__global__ void __launch_bounds__(256) tl_scan8_kernel(uint32_t* __restrict__ hist, uint32_t* __restrict__ bstart,
                                                        uint64_t* __restrict__ maxb) {
     __shared__ uint32_t wsum[4], wmax[4];
     const uint32_t v = hist[threadIdx.x];
+    hist[threadIdx.x] = 0;
     const uint32_t inc = wave_incl_scan_u32(v);
     const uint32_t mx = wave_max_u32(v);
     if (lane_id() == 63) wsum[wave_id()] = inc;
@@ -762,7 +767,10 @@ struct LocalRounds {
 // NT: threads per bucket -- TL_NT, or 64 (one wave, TL_ITEMS x 64 words) for the many small buckets
 // of a two-level sort over a few million keys (32 K buckets of tens to hundreds of words: 512 threads
 // and their barriers per bucket were most of the C4 batch's local-sort time)
-template <typename K, int IN, int NT = TL_NT>
+// UN0: the first round ranks unstably (one LDS atomic per element instead of up to 8 ballots) -- a
+// deferred sort's completion, whose consumer (the plan's merge) needs no order among equal keys;
+// later rounds stay stable (they must keep the earlier rounds' order)
+template <typename K, int IN, int NT = TL_NT, bool UN0 = false>
 __global__ void __launch_bounds__(NT) tl_local_kernel(const uint64_t* __restrict__ win, const K* __restrict__ kin,
                                                          const uint32_t* __restrict__ vin, K* __restrict__ kout,
                                                          uint32_t* __restrict__ vout,
@@ -808,6 +816,10 @@ __global__ void __launch_bounds__(NT) tl_local_kernel(const uint64_t* __restrict
             const uint32_t i = wbase + (uint32_t)j * 64 + l;
             const bool ok = i < m;
             const uint32_t d = (uint32_t)(word[j] >> dsh) & mask;
+            if (UN0 && r == 0) {   // (block-uniform)
+                pos[j] = ok ? atomicAdd(&whist[w][d], 1u) : 0u;
+                continue;
+            }
             uint64_t peers = __ballot(ok);
 #pragma unroll
             for (int b = 0; b < 8; b++) {
@@ -2176,14 +2188,17 @@ static bool sort_pre_on() {
 // keeps TL_NT threads everywhere.
 template <typename K>
 static void local_sort_buckets(qe_ctx* c, const uint64_t* words, K* kout, uint32_t* vout, const uint32_t* bstart,
-                               unsigned nbuckets, Field f, LocalRounds lr, uint64_t maxb) {
+                               unsigned nbuckets, Field f, LocalRounds lr, uint64_t maxb, bool unstable0 = false) {
     static const bool wave_on = !(getenv("QE_LOCAL_WAVE") && getenv("QE_LOCAL_WAVE")[0] == '0');
-    if (wave_on && maxb <= 64u * TL_ITEMS)
-        hipLaunchKernelGGL((tl_local_kernel<K, IN_WORD, 64>), dim3(nbuckets), dim3(64), 0, c->stream, words, nullptr,
-                           nullptr, kout, vout, bstart, 0u, f, lr);
-    else
-        hipLaunchKernelGGL((tl_local_kernel<K, IN_WORD>), dim3(nbuckets), dim3(TL_NT), 0, c->stream, words, nullptr,
-                           nullptr, kout, vout, bstart, 0u, f, lr);
+    const bool one_wave = wave_on && maxb <= 64u * TL_ITEMS;
+#define QE_LOCAL(NTH, UN)                                                                                                \
+    hipLaunchKernelGGL((tl_local_kernel<K, IN_WORD, NTH, UN>), dim3(nbuckets), dim3(NTH), 0, c->stream, words, nullptr, \
+                       nullptr, kout, vout, bstart, 0u, f, lr)
+    if (one_wave && unstable0) QE_LOCAL(64, true);
+    else if (one_wave) QE_LOCAL(64, false);
+    else if (unstable0) QE_LOCAL(TL_NT, true);
+    else QE_LOCAL(TL_NT, false);
+#undef QE_LOCAL
     QE_HIP(hipGetLastError());
 }
 
@@ -2437,7 +2452,11 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
         return sort_two_level_pre<K>(c, keys, vals, n, bits, f, name, out, defer);
     const int L = bits - H;   // low bits sorted in LDS (<= 24)
     const LocalRounds lr = local_rounds(L);
-    uint32_t* hist = dalloc_t<uint32_t>(c, TL_BUCKETS);
+    if (!c->d_zhist) {   // once per context; every scan below leaves it zeroed again
+        QE_HIP(hipMalloc(&c->d_zhist, (TL_BUCKETS + 256) * sizeof(uint32_t)));
+        QE_HIP(hipMemsetAsync(c->d_zhist, 0, (TL_BUCKETS + 256) * sizeof(uint32_t), c->stream));
+    }
+    uint32_t* hist = H == 8 ? c->d_zhist + TL_BUCKETS : c->d_zhist;
     // digit bases: 256 entries each (the pass kernel reads one per possible 8-bit digit)
     uint32_t* bstart = dalloc_t<uint32_t>(c, TL_BUCKETS + 1 + 512);
     uint32_t* base1 = bstart + TL_BUCKETS + 1;
@@ -2446,7 +2465,6 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
     uint64_t* d_max = dfr ? dalloc_t<uint64_t>(c, 1) : c->d_scratch + 34;
     if (H == 8) {
         base1 = bstart;   // one pass: its digit IS the bucket
-        QE_HIP(hipMemsetAsync(hist, 0, 256 * sizeof(uint32_t), c->stream));
         Timed t(c, "sort_hist", (double)sizeof(K) * n);
         hipLaunchKernelGGL((tl_hist8_kernel<K>), dim3(grid_for(n, 256 * 16, 1024)), dim3(256), 0, c->stream, keys, n, f,
                            L, hist);
@@ -2454,7 +2472,6 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
         hipLaunchKernelGGL(tl_scan8_kernel, dim3(1), dim3(256), 0, c->stream, hist, bstart, d_max);
         QE_HIP(hipGetLastError());
     } else {
-        QE_HIP(hipMemsetAsync(hist, 0, TL_BUCKETS * sizeof(uint32_t), c->stream));
         Timed t(c, "sort_hist", (double)sizeof(K) * n);
         hipLaunchKernelGGL((tl_hist_kernel<K>), dim3(hist_blocks(n)), dim3(1024), 0, c->stream, keys, n, f, L, hist);
         QE_HIP(hipGetLastError());
@@ -2463,7 +2480,6 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
     }
     const uint64_t maxb = dfr ? 0 : read_u64(c, d_max);
     if (!dfr && maxb > (uint64_t)TL_CAP) {
-        dfree(c, hist);
         dfree(c, bstart);
         return false;
     }
@@ -2472,6 +2488,11 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
     uint64_t* w2 = H == TL_H ? dalloc_t<uint64_t>(c, n) : nullptr;
     K* kout = dalloc_t<K>(c, n);
     uint32_t* vout = dalloc_t<uint32_t>(c, n);
+    // a deferred sort's consumer (the plan's join) needs buckets, not an order inside them: the
+    // first pass ranks unstably (one LDS atomic per element instead of 8 ballots).  The second
+    // stays stable -- in this lookback form a tile holds several first digits, and an unstable
+    // rank would interleave their buckets
+    const bool uns = dfr && sort_unstable_on() && H == TL_H;
     for (int p = 0; p < (H == TL_H ? 2 : 1); p++) {
         const int dsh = 32 + L + 8 * p;
         const uint32_t pmask = p == 0 ? 255u : 127u;
@@ -2481,10 +2502,18 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
             hipLaunchKernelGGL((radix_pass_kernel<K, IN_WORD, OUT_WORD, true, 8, R_ITEMS, R_NT>), dim3((unsigned)nt),
                                dim3(R_NT), 0, c->stream, keys, w1, vals, kout, w2, vout, n, dsh, pmask, f, base2,
                                sl.status, sl.ticket, sl.epoch);
+        else if (vals && uns)
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV, OUT_WORD, true, 8, R_ITEMS, R_NT, false, X_NONE, true>),
+                               dim3((unsigned)nt), dim3(R_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, dsh,
+                               pmask, f, base1, sl.status, sl.ticket, sl.epoch);
         else if (vals)
             hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV, OUT_WORD, true, 8, R_ITEMS, R_NT>), dim3((unsigned)nt),
                                dim3(R_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, dsh, pmask, f, base1,
                                sl.status, sl.ticket, sl.epoch);
+        else if (uns)
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KIOTA, OUT_WORD, true, 8, R_ITEMS, R_NT, false, X_NONE, true>),
+                               dim3((unsigned)nt), dim3(R_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, dsh,
+                               pmask, f, base1, sl.status, sl.ticket, sl.epoch);
         else
             hipLaunchKernelGGL((radix_pass_kernel<K, IN_KIOTA, OUT_WORD, true, 8, R_ITEMS, R_NT>), dim3((unsigned)nt),
                                dim3(R_NT), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, dsh, pmask, f, base1,
@@ -2507,7 +2536,6 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
             for (int r = 0; r < 4; r++) d.lr_bits[r] = lr.bits[r];
             c->deferred[kout] = d;
             dfree(c, w1);
-            dfree(c, hist);
             *out = SortOut{kout, vout, true, true};
             return true;
         }
@@ -2518,7 +2546,6 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
     }
     dfree(c, w1);
     if (w2) dfree(c, w2);
-    dfree(c, hist);
     dfree(c, bstart);
     *out = SortOut{kout, vout, true, true};
     return true;
@@ -2867,7 +2894,9 @@ void pairs_need_keys(qe_ctx* c, const qe_pairs* p) {
         complete_lsd(c, d, p->n);
     } else {
         Timed t(c, "sort_local", 8.0 * p->n + 12.0 * p->n);
-        local_sort_buckets<uint64_t>(c, d.words, d.kout, d.vout, d.bstart, TL_BUCKETS, f, rounds_of(d), maxb);
+        // (a deferred sort is the plan's: no order among equal keys is needed)
+        local_sort_buckets<uint64_t>(c, d.words, d.kout, d.vout, d.bstart, TL_BUCKETS, f, rounds_of(d), maxb,
+                                     sort_unstable_on());
     }
     drop(c, d);
 }

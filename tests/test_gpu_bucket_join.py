@@ -69,6 +69,25 @@ def test_bucket_join_uniform(ctx, n):
     _check(ctx, rk, sk, gathered=True, expect=True)
 
 
+def test_bucket_join_segments_beyond_one_pass2_tile(ctx):
+    """lookback-free form with the first-pass digits skewed 3:1 (buckets stay small): a second-pass
+    segment then holds ~12 K words, more than one 9216-word sub-tile, so pass 2 walks a segment in
+    sub-tiles with running digit offsets (uniform keys never do: ~8192 +- 90 words)"""
+    rng = np.random.default_rng(29)
+    n = (1 << 25) + 777
+
+    def keys(m):
+        p = np.where(np.arange(256) < 128, 1.5, 0.5)
+        d1 = rng.choice(256, m, p=p / p.sum()).astype(np.uint64)
+        d2 = rng.integers(0, 128, m, dtype=np.uint64)
+        low = rng.integers(0, 1 << 10, m, dtype=np.uint64)
+        return (((d2 << np.uint64(8)) | d1) << np.uint64(10)) | low   # 25 varying bits, L = 10
+
+    rk, sk = keys(n), keys(n // 2 + 3)
+    _check(ctx, rk, sk, gathered=True, expect=True)
+    _check(ctx, rk, sk, gathered=False, expect=True)
+
+
 def test_bucket_join_base_columns_and_fanout(ctx):
     """both sides base columns (rowids generated); ~4 partners per row: the optimistic nR + nS
     buffers are outgrown and the kernel re-runs with the exact size"""
