@@ -60,6 +60,15 @@ __device__ __forceinline__ uint4 buf_load_u4(__amdgpu_buffer_rsrc_t r, uint32_t 
     return make_uint4(x.x, x.y, x.z, x.w);
 }
 
+// two device words set from kernel arguments: an [OR, AND] accumulator's start, instead of an
+// async copy from a host stack buffer (pageable: the runtime stages it on every call)
+static __global__ void __launch_bounds__(64) __attribute__((unused)) set2_kernel(uint64_t* d, uint64_t a, uint64_t b) {
+    if (threadIdx.x == 0) {
+        d[0] = a;
+        d[1] = b;
+    }
+}
+
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) v += shfl_xor_u64(v, m);

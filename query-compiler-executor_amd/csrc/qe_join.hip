@@ -1619,8 +1619,8 @@ int qe_gather_pairs(qe_ctx* c, qe_col col, const qe_list* rows, qe_pairs* out) {
                 return 0;
             }
     uint64_t* d_bits = c->d_scratch + 44;
-    uint64_t init[2] = {0ull, ~0ull};
-    QE_HIP(hipMemcpyAsync(d_bits, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(set2_kernel, dim3(1), dim3(64), 0, c->stream, d_bits, 0ull, ~0ull);
+    QE_HIP(hipGetLastError());
     if (n) {
         Timed t(c, "gather_keys", 12.0 * n + 8.0 * n);
         hipLaunchKernelGGL(gather_keys_kernel<true>, dim3(grid_for((n + 3) / 4, 256, 4096)), dim3(256), 0, c->stream,

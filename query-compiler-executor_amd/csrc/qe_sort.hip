@@ -2023,8 +2023,8 @@ static PassDesc plan_passes(uint64_t kor, uint64_t kand, int maxbits, int* width
 template <typename K>
 static void key_bits_impl(qe_ctx* c, const K* keys, uint64_t n, uint64_t* out) {
     uint64_t* d_bits = c->d_scratch + 8;   // [or, and]
-    uint64_t init[2] = {0ull, ~0ull};
-    QE_HIP(hipMemcpyAsync(d_bits, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(set2_kernel, dim3(1), dim3(64), 0, c->stream, d_bits, 0ull, ~0ull);
+    QE_HIP(hipGetLastError());
     if (n) {
         Timed t(c, "sort_keybits", (double)sizeof(K) * n);
         hipLaunchKernelGGL(key_bits_kernel<K>, dim3(grid_for(n, 256 * 16, 4096)), dim3(256), 0, c->stream, keys,

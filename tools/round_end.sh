@@ -3,6 +3,7 @@
 #   tools/round_end.sh TAG c3     -> C3 rocprofv3 trace + PMC passes, then `python bench.py` (the line
 #                                    picks the fresh per-query traffic: copied to profiles/ first)
 #   tools/round_end.sh TAG c45    -> the same for C5, then for C4
+#   tools/round_end.sh TAG c4     -> the C4 line, then its trace + PMC passes (best effort)
 #   tools/round_end.sh TAG check  -> every -m gpu test, smoke(), the goldens (tools/gpu_check_ab.sh)
 set -o pipefail
 mkdir -p gpurun_out
@@ -21,9 +22,15 @@ c45)
   cp gpurun_out/${T}c4_traffic.json profiles/${T}c4_traffic.json || exit 1
   timeout -k 10 400 python bench.py --workload c4 > gpurun_out/${T}_c4_bench.json 2> gpurun_out/${T}_c4_bench.err || exit 1
   ;;
+c4)
+  # the bench line first (no profiler), then the trace + PMC passes as best effort: the 8 lanes'
+  # HIP calls under rocprofv3's kernel trace have crashed inside the runtime
+  timeout -k 10 400 python bench.py --workload c4 > gpurun_out/${T}_c4_bench.json 2> gpurun_out/${T}_c4_bench.err || exit 1
+  timeout -k 10 600 bash tools/profile_workload.sh ${T}c4 c4 || echo "c4 profile failed (rc $?)"
+  ;;
 check)
   bash tools/gpu_check_ab.sh || exit 1
   ;;
-*) echo "usage: $0 TAG c3|c45|check"; exit 2 ;;
+*) echo "usage: $0 TAG c3|c45|c4|check"; exit 2 ;;
 esac
 echo round-end-$2-done
