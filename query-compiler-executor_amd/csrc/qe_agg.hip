@@ -492,7 +492,8 @@ static void join_aggregate_buckets(qe_ctx* c, const AggSide& R, const AggSide& S
     uint64_t* part = dalloc_t<uint64_t>(c, (size_t)NB * 3);
     uint32_t* big = dalloc_t<uint32_t>(c, (size_t)NB * 3);
     uint64_t* d = dalloc_t<uint64_t>(c, 4);   // [pairs, sumR, sumS, giant buckets]
-    QE_HIP(hipMemsetAsync(d, 0, 4 * sizeof(uint64_t), c->stream));
+    hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(64), 0, c->stream, (uint64_t*)d, 4);
+    QE_HIP(hipGetLastError());
     {
         Timed t(c, "agg_count", 8.0 * 2.0 * (double)(R.n + S.n));
         hipLaunchKernelGGL(ab_bucket_kernel, dim3(NB), dim3(AB_NT), 0, c->stream, wR, bsR, wS, bsS, L, part, big,

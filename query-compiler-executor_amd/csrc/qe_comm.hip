@@ -735,7 +735,8 @@ int e_checksums(void* u, int n, const uint32_t* rels, const uint32_t* cols, cons
         }
         if (!vat.empty()) {
             unsigned long long* d = (unsigned long long*)dalloc_t<uint64_t>(c, vat.size());
-            QE_HIP(hipMemsetAsync(d, 0, vat.size() * 8, c->stream));
+            hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(64), 0, c->stream, (uint64_t*)d, (int)vat.size());
+            QE_HIP(hipGetLastError());
             for (size_t k = 0; k < vat.size(); k++) {
                 const qe_list& l = ls[vat[k]];
                 if (!l.n) continue;

@@ -60,6 +60,12 @@ __device__ __forceinline__ uint4 buf_load_u4(__amdgpu_buffer_rsrc_t r, uint32_t 
     return make_uint4(x.x, x.y, x.z, x.w);
 }
 
+// a few device words zeroed by a kernel of ours instead of a runtime memset (hipMemsetAsync is a
+// separate fill launch through the runtime's own path; the small scalar-result words need none)
+static __global__ void __launch_bounds__(64) __attribute__((unused)) zero_words_kernel(uint64_t* d, int n) {
+    for (int i = threadIdx.x; i < n; i += 64) d[i] = 0;
+}
+
 // two device words set from kernel arguments: an [OR, AND] accumulator's start, instead of an
 // async copy from a host stack buffer (pageable: the runtime stages it on every call)
 static __global__ void __launch_bounds__(64) __attribute__((unused)) set2_kernel(uint64_t* d, uint64_t a, uint64_t b) {

@@ -586,7 +586,8 @@ std::vector<uint64_t> heavy_keys_dev(qe_ctx* c, const qe_col* cols, int ncols, u
         const uint64_t* sorted = static_cast<const uint64_t*>(so.keys);
         uint64_t* d = dalloc_t<uint64_t>(c, 2 * (uint64_t)CAP + 1);
         unsigned long long* d_cnt = reinterpret_cast<unsigned long long*>(d + 2 * CAP);
-        QE_HIP(hipMemsetAsync(d_cnt, 0, 8, c->stream));
+        hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(64), 0, c->stream, (uint64_t*)d_cnt, 1);
+        QE_HIP(hipGetLastError());
         hipLaunchKernelGGL(heavy_runs_kernel, dim3(grid_for(m, 256)), dim3(256), 0, c->stream, sorted, m, thr, d_cnt, d,
                            d + CAP, CAP);
         QE_HIP(hipGetLastError());
@@ -645,7 +646,8 @@ void bucket_select_dev(qe_ctx* c, qe_col col, uint32_t nparts, uint32_t part, co
     for (int attempt = 0; attempt < 2; attempt++) {
         out->key = dalloc_t<uint64_t>(c, std::max<uint64_t>(cap, 1));
         out->val = dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1));
-        QE_HIP(hipMemsetAsync(d_cnt, 0, sizeof(uint64_t), c->stream));
+        hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(64), 0, c->stream, (uint64_t*)d_cnt, 1);
+        QE_HIP(hipGetLastError());
         if (n) {
             Timed t(c, "bucket_select", 8.0 * n);
             hipLaunchKernelGGL(bucket_select_kernel, dim3(nb), dim3(BS_B), dyn, c->stream, col.d, n, nparts, part,

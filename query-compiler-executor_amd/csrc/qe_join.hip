@@ -1976,7 +1976,8 @@ int qe_checksum_weighted(qe_ctx* c, qe_col col, const qe_pairs* p, uint64_t* sum
     if (p->n && !p->match) throw Error(QE_EINVAL, "qe_checksum_weighted needs match counts");
     pairs_need_vals(c, p);
     unsigned long long* d = (unsigned long long*)(c->d_scratch + 40);
-    QE_HIP(hipMemsetAsync(d, 0, 8, c->stream));
+    hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(64), 0, c->stream, (uint64_t*)d, 1);
+    QE_HIP(hipGetLastError());
     if (p->n) {
         Timed t(c, "checksum_weighted", (p->val ? 8.0 : 4.0) * p->n);
         hipLaunchKernelGGL(checksum_weighted_kernel, dim3(grid_for(p->n, 256 * 16, 8192)), dim3(256), 0, c->stream,
@@ -2141,7 +2142,8 @@ int qe_checksum(qe_ctx* c, qe_col col, const qe_list* rows, uint64_t* sum) {
     QE_API_BEGIN(c)
     uint64_t n = rows ? rows->n : col.n;
     unsigned long long* d = (unsigned long long*)(c->d_scratch + 40);
-    QE_HIP(hipMemsetAsync(d, 0, 8, c->stream));
+    hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(64), 0, c->stream, (uint64_t*)d, 1);
+    QE_HIP(hipGetLastError());
     if (n) {
         Timed t(c, "checksum", rows ? 12.0 * n : 8.0 * n);
         hipLaunchKernelGGL(checksum_kernel, dim3(grid_for(n, 256 * 16, 8192)), dim3(256), 0, c->stream, col.d,
@@ -2159,7 +2161,8 @@ int qe_checksums(qe_ctx* c, int n, const qe_col* cols, const qe_list* const* row
     for (int k0 = 0; k0 < n; k0 += 32) {   // 32 sums per round trip (the pinned scratch holds 64 words)
         const int m = std::min(32, n - k0);
         unsigned long long* d = (unsigned long long*)dalloc_t<uint64_t>(c, 32);
-        QE_HIP(hipMemsetAsync(d, 0, 32 * 8, c->stream));
+        hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(64), 0, c->stream, (uint64_t*)d, 32);
+        QE_HIP(hipGetLastError());
         for (int k = 0; k < m; k++) {
             const qe_list* r = rows[k0 + k];
             const uint64_t len = r ? r->n : cols[k0 + k].n;

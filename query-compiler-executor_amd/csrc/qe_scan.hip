@@ -594,7 +594,8 @@ uint64_t filter_scan2_unordered(qe_ctx* c, const uint64_t* c1, char op1, uint64_
     const uint64_t nt = (n + TILE - 1) / TILE;
     if (nt >= (1ull << 31)) throw Error(QE_EINVAL, "input too large");
     unsigned long long* d_cnt = reinterpret_cast<unsigned long long*>(c->d_scratch);
-    QE_HIP(hipMemsetAsync(d_cnt, 0, sizeof(uint64_t), c->stream));
+    hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(64), 0, c->stream, (uint64_t*)d_cnt, 1);
+    QE_HIP(hipGetLastError());
     const unsigned grid = (unsigned)nt;
     {
         Timed t(c, "filter_scan", (two ? 16.0 : 8.0) * n);
