@@ -912,9 +912,6 @@ __global__ void __launch_bounds__(NT) tl_local_kernel(const uint64_t* __restrict
 #ifndef QE_TL_TPG
 #define QE_TL_TPG 256
 #endif
-#ifndef QE_HIST_ROWSUM
-#define QE_HIST_ROWSUM 0   // (build knob) tile digit counts from row sums instead of LDS counters
-#endif
 constexpr uint32_t TL_TPG = QE_TL_TPG;   // first-pass tiles per group
 static_assert(RTILE == 8192, "tl_hist_tiles_kernel counts 8192-key first-pass tiles (1024 threads x 8)");
 
@@ -976,42 +973,6 @@ __global__ void __launch_bounds__(1024) tl_hist_tiles_kernel(const K* __restrict
     };
     uint64_t k[8];
     uint32_t t = g * TL_TPG + q, prev = 0, par = 0;
-#if QE_HIST_ROWSUM
-    // (A/B build) no per-tile digit counters: one LDS atomic per key into the group table, then the
-    // tile's first-digit counts as differences of that table's row sums (row d1 = 128 counters, read
-    // as 4 x 8 16-B chunks per row by 4 lanes, chunk order rotated per lane to spread the banks) --
-    // at the price of a second barrier per tile
-    uint32_t rowsum = 0;   // row (threadIdx.x >> 2)'s total before this tile (lanes with x % 4 == 0)
-    for (; t < t_end; t += Q) {
-        load(t, k);
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            if ((vm >> j) & 1u) {
-                const uint32_t b = (uint32_t)((((k[j] >> f.lo) & f.fmask) >> L) & (TL_BUCKETS - 1));
-                atomicAdd(&h[((b & 255u) << 7) | (b >> 8)], 1u);
-            }
-        }
-        __syncthreads();
-        const uint32_t r = threadIdx.x >> 2;
-        const uint4* rp = reinterpret_cast<const uint4*>(h + r * 128u + (threadIdx.x & 3u) * 32u);
-        uint32_t sum = 0;
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const uint4 v = rp[(i + threadIdx.x + (threadIdx.x >> 3)) & 7u];
-            sum += v.x + v.y + v.z + v.w;
-        }
-        sum += (uint32_t)__shfl_xor((int)sum, 1, 64);
-        sum += (uint32_t)__shfl_xor((int)sum, 2, 64);
-        if ((threadIdx.x & 3u) == 0) {
-            tcnt[(uint64_t)t * 256 + r] = sum - rowsum;
-            rowsum = sum;
-        }
-        __syncthreads();   // every row read before the next tile's atomics
-    }
-    (void)prev;
-    (void)par;
-    (void)th;
-#else
     for (; t < t_end; t += Q, par ^= 1u) {
         load(t, k);
         if (t != g * TL_TPG + q && threadIdx.x < 256) {   // the previous tile's counts (its barrier passed)
@@ -1030,7 +991,6 @@ __global__ void __launch_bounds__(1024) tl_hist_tiles_kernel(const K* __restrict
         prev = t;
     }
     if (g * TL_TPG + q < t_end && threadIdx.x < 256) tcnt[(uint64_t)prev * 256 + threadIdx.x] = th[par ^ 1u][threadIdx.x];
-#endif
     __syncthreads();
     tl_store_counts(h, g, q, G, gout);
 }
