@@ -2161,7 +2161,7 @@ static unsigned hist_blocks(uint64_t n) {
 static uint64_t sort_pre_min() {   // tuning knob: QE_SORT_PRE_MIN = smallest n for the lookback-free form
     static uint64_t v = [] {
         const char* s = getenv("QE_SORT_PRE_MIN");
-        return s ? strtoull(s, nullptr, 0) : (1ull << 25);
+        return s ? strtoull(s, nullptr, 0) : (1ull << 22);   // (round 3: 2^25; see sort_two_level)
     }();
     return v;
 }
@@ -2445,9 +2445,10 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
 template <typename K>
 static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint64_t n, int bits, Field f,
                            const char* name, SortOut* out, int H = TL_H, bool defer = false) {
-    // the lookback-free form saves ~1 us per million keys per pass but adds ~30 us of count
-    // scans: it pays from a few 10^7 keys (measured on MI355X: C3's 0.5-1e8-key sorts 2 % faster,
-    // the C4 batch's 1-10 M-key sorts slower)
+    // the lookback-free form saves ~1 us per million keys per pass but adds the count scans: round
+    // 3 measured it paying from a few 10^7 keys (C4's 1-10 M-key sorts slower); with round 4's
+    // cheaper scans and histograms it pays from 2^22 keys (C4 3724 -> 3748 q/s averaged over four
+    // same-box pairs, 2^21 and 2^23 no better: profiles/r04q_c4_knobs_ab.log, r04r_c4_knobs_ab.log)
     if (H == TL_H && sort_pre_on() && n >= sort_pre_min())
         return sort_two_level_pre<K>(c, keys, vals, n, bits, f, name, out, defer);
     const int L = bits - H;   // low bits sorted in LDS (<= 24)
