@@ -2,7 +2,7 @@
 only, then each 15-bit bucket joined in LDS (bucket_join, csrc/qe_sort.hip) -- against numpy: the
 multiset of (R val, S val) pairs must be exactly the equi-join's (join_relations,
 src/join.c:325-392, emits every matching pair once; the plan needs no order).  Covers both forms of
-the deferred two-level sort (lookback and lookback-free, around 2^25 rows), base columns (rowids
+the deferred two-level sort (lookback and lookback-free: below / from 2^22 rows), base columns (rowids
 generated) and gathered lists, fan-out above 1 (the optimistic buffers outgrown: exact re-run),
 two sides of different key bounds (both sorted over the union bounds: one bucket geometry), and
 every fallback to the ordinary sort + merge (an in-bucket domain beyond LDS, skewed buckets, small
@@ -74,7 +74,7 @@ def test_bucket_join_segments_beyond_one_pass2_tile(ctx):
     segment then holds ~12 K words, more than one 9216-word sub-tile, so pass 2 walks a segment in
     sub-tiles with running digit offsets (uniform keys never do: ~8192 +- 90 words)"""
     rng = np.random.default_rng(29)
-    n = (1 << 25) + 777
+    n = (1 << 22) + 777   # the lookback-free form from 2^22 keys; a full group's segments average 8 K words
 
     def keys(m):
         p = np.where(np.arange(256) < 128, 1.5, 0.5)

@@ -151,7 +151,8 @@ def _keys_for(case, n, rng):
 @pytest.mark.parametrize("case", ["27bit", "20bit", "31bit", "19bit", "const_hi", "stride8", "skew"])
 def test_sort_pairs_two_level_sizes(ctx, case):
     """n >= 2^22 takes the two-level sort (15 high bits by global passes, the rest in LDS per
-    bucket) when 20..31 bits vary; skew or fewer bits fall back to the LSD passes."""
+    bucket; at 5 M keys its lookback-free form) when 20..31 bits vary; skew or fewer bits fall
+    back to the LSD passes."""
     n = 5_000_000
     rng = np.random.default_rng(len(case))
     k = _keys_for(case, n, rng)
@@ -167,9 +168,9 @@ def test_sort_pairs_two_level_sizes(ctx, case):
 
 @pytest.mark.parametrize("case,with_vals", [("27bit", True), ("27bit", False), ("31bit", True), ("skew", True)])
 def test_sort_pairs_lookback_free_two_level(ctx, case, with_vals):
-    """n >= 2^25: the two-level sort whose global passes take their offsets from the histogram
-    read (per-tile and per-segment digit counts) instead of a lookback; 'skew' runs both passes
-    and then falls back to the LSD passes"""
+    """n >= 2^22 (QE_SORT_PRE_MIN): the two-level sort whose global passes take their offsets from
+    the histogram read (per-tile and per-segment digit counts) instead of a lookback; 'skew' runs
+    both passes and then falls back to the LSD passes"""
     n = (1 << 25) + 4_321
     rng = np.random.default_rng(99 + len(case))
     k = _keys_for(case, n, rng)
