@@ -38,7 +38,7 @@ STAGES = [
     (r"radix_pass_kv_kernel<unsigned int", "sort_pass_k32v32"),
     (r"tl_pass2_kernel<unsigned long(, 0\b[^>]*)?>", "sort_pass_k64v32"),
     (r"tl_pass2_kernel<unsigned int(, 0\b[^>]*)?>", "sort_pass_k32v32"),
-    (r"digit_hist_kernel|digit_scan_kernel|tl_hist_kernel|tl_hist8_kernel|tl_hist_tiles_kernel|tl_gsum_kernel|tl_scan_kernel|tl_scan8_kernel", "sort_hist"),
+    (r"digit_hist_kernel|digit_scan_kernel|tl_hist_kernel|tl_hist8_kernel|tl_hist_tiles_kernel|tl_gfold_kernel|tl_bstart_kernel|tl_scan_kernel|tl_scan8_kernel", "sort_hist"),
     (r"cs_reduce_kernel|cs_top_kernel|cs_apply_kernel", "sort_scan"),
     (r"tl_local_kernel", "sort_local"),
     (r"bucket_select_kernel", "bucket_select"),
