@@ -1093,6 +1093,9 @@ __global__ void __launch_bounds__(256) tl_gfold_kernel(const uint32_t* __restric
 // sum of m[<r][c], with base[c] = sum of all counts of the columns before c (the digit's global
 // start).  Three launches for BOTH matrices of a sort (tile counts, C = 256; segment counts,
 // C = 128): chunk sums, a one-block-per-matrix scan of the chunk sums, apply.
+#ifndef QE_CS_TOP_REG
+#define QE_CS_TOP_REG 1   // (build knob, 0 = round 3's two walks) the chunk-sum scan holds its sums in registers
+#endif
 constexpr uint32_t CS_CH = 64;
 struct CSJob {
     uint32_t* m;
@@ -1135,9 +1138,23 @@ __global__ void __launch_bounds__(1024) cs_top_kernel(CSJobs js) {
     __shared__ uint32_t wsum[16];
     const uint32_t c = threadIdx.x % C, q = threadIdx.x / C;
     const uint32_t per = (nb + QN - 1) / QN, b0 = q * per < nb ? q * per : nb, b1 = b0 + per < nb ? b0 + per : nb;
+    // up to CS_TOP_REG chunk sums per thread are read ONCE, all in flight together (buffer loads,
+    // past the matrix read 0), and kept in registers for the rewrite: one global round trip each
+    // way instead of a chain of them (~10 us of this one-block kernel per sort)
+    constexpr uint32_t CS_TOP_REG = 48;   // (C3: 191 chunks of the tile matrix over 4 row groups)
+    const bool reg = QE_CS_TOP_REG && per <= CS_TOP_REG;   // (block-uniform)
+    uint32_t v[CS_TOP_REG];
     uint32_t s = 0;
+    if (reg) {
+        const auto rp = buf_rsrc(J.part, nb * C * 4u);
+#pragma unroll
+        for (uint32_t i = 0; i < CS_TOP_REG; i++) v[i] = buf_load_u32(rp, ((b0 + i) * C + c) * 4u, 0u);
+#pragma unroll
+        for (uint32_t i = 0; i < CS_TOP_REG; i++) s += b0 + i < b1 ? v[i] : 0u;
+    } else {
 #pragma unroll 8
-    for (uint32_t b = b0; b < b1; b++) s += J.part[(uint64_t)b * C + c];
+        for (uint32_t b = b0; b < b1; b++) s += J.part[(uint64_t)b * C + c];
+    }
     tot[q * C + c] = s;
     __syncthreads();
     uint32_t T = 0;
@@ -1154,11 +1171,19 @@ __global__ void __launch_bounds__(1024) cs_top_kernel(CSJobs js) {
     __syncthreads();
     uint32_t run = colbase[c];
     for (uint32_t k = 0; k < q; k++) run += tot[k * C + c];
+    if (reg) {
+#pragma unroll
+        for (uint32_t i = 0; i < CS_TOP_REG; i++) {
+            if (b0 + i < b1) J.part[(uint64_t)(b0 + i) * C + c] = run;
+            run += b0 + i < b1 ? v[i] : 0u;
+        }
+        return;
+    }
 #pragma unroll 8
     for (uint32_t b = b0; b < b1; b++) {
-        const uint32_t v = J.part[(uint64_t)b * C + c];
+        const uint32_t x = J.part[(uint64_t)b * C + c];
         J.part[(uint64_t)b * C + c] = run;
-        run += v;
+        run += x;
     }
 }
 
