@@ -192,8 +192,14 @@ def run_dist(args):
     t0 = time.time()
     gen_chain(ctx, total, args.seed, total)       # replicated on every rank
     ctx.sync()
+    t_part = None
+    if multi:   # load-time layout: this rank's hash bucket of every base column (qe_partition_columns)
+        t1 = time.time()
+        ctx.partition_columns(world, rank)
+        t_part = time.time() - t1
     if rank == 0:
-        log(f"[bench] {world} rank(s): 4 x {total} rows x 3 cols in HBM per GPU in {time.time() - t0:.2f}s")
+        log(f"[bench] {world} rank(s): 4 x {total} rows x 3 cols in HBM per GPU in {time.time() - t0:.2f}s"
+            + (f" (partitioned in {t_part:.3f}s)" if t_part is not None else ""))
     out = None
     for i in range(args.warmup):
         out, _, refused = ctx.run_dist(QUERY, comm)
@@ -273,7 +279,8 @@ def run_dist(args):
                        "executor": "qe_run_queries_dist: host-C partitioned plan (include/qe_plan.h), "
                                    "RCCL grouped send/recv per exchange, all-reduced sums",
                        "refused_queries": refused, "exchanges_per_step": exchanges / max(1, args.steps + args.warmup),
-                       "parallelism": f"hash-partitioned dp{world}" if multi else "partitioned plan, one rank"},
+                       "parallelism": f"hash-partitioned dp{world}" if multi else "partitioned plan, one rank",
+                       "load_partition_s": round(t_part, 4) if t_part is not None else None},
             "faithful_executor": faithful_line,
             "roofline": roofline({dominant: stats[dominant]} if dominant in stats else stats,
                                  traffic, args.steps),

@@ -77,6 +77,16 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
     # faithful executor on the lanes
     workers = int(os.environ.get("QE_WORKERS", "8"))
     plan = getattr(args, "plan", "auto") != "faithful"
+    # QE_CRASH_MAPS=FILE: on SIGSEGV / SIGBUS append the fault address, PC and /proc/self/maps to
+    # FILE before the previous handler reports (tools/crashmaps.c; the profiled C4 runs' crash)
+    if os.environ.get("QE_CRASH_MAPS"):
+        import ctypes
+        cm = ctypes.CDLL(os.path.join(ROOT, "query-compiler-executor_amd", "build", "libqecrash.so"))
+        cm.qecrash_install.argtypes = [ctypes.c_char_p]
+        if cm.qecrash_install(os.environ["QE_CRASH_MAPS"].encode()) != 0:
+            raise RuntimeError("qecrash_install failed")
+    # QE_BENCH_EVENTS=0: no HIP-event stage table on the lanes (the off switch ADVICE r4 asked to keep)
+    events = os.environ.get("QE_BENCH_EVENTS", "1") != "0"
 
     def run_batch():
         return ctx.run_lanes(text, workers, plan=plan)
@@ -87,7 +97,7 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
     # the HIP-event stage table on every lane (round 3 switched it off under rocprofv3, where the
     # lanes' event-query spins crashed inside the runtime; results now come back through a pinned
     # flag -- qe_runtime.hip read_words -- with no runtime call in the wait)
-    ctx.set_profiling(True)
+    ctx.set_profiling(events)
     ctx.reset_stats()
     torch.cuda.synchronize()
     hits0, builds0 = ctx.sort_cache_stats()

@@ -381,6 +381,18 @@ int e_base_side(void* u, uint32_t rel, uint32_t col, qe_h* keys, qe_h* rowids) {
             *rowids = 0;
             return;
         }
+        if (c->bparts_n == (uint32_t)e->world && c->bparts_p == (uint32_t)e->rank) {
+            auto it = c->bparts.find(q.d);     // partitioned at load (qe_partition_columns): no scan
+            if (it != c->bparts.end()) {
+                DArr* k = new_arr(c, it->second.key, it->second.n, true, false);
+                k->bits = true;
+                k->kor = kor;
+                k->kand = kand;
+                *keys = H(k);
+                *rowids = H(new_arr(c, it->second.val, it->second.n, false, false));
+                return;
+            }
+        }
         qe_pairs p{};                          // this rank's hash bucket of the replicated column
         ck(qe_bucket_select(c, q, (uint32_t)e->world, (uint32_t)e->rank, nullptr, 0, &p), c);
         DArr* k = new_arr(c, p.key, p.n, true);
@@ -1062,6 +1074,11 @@ int qe_run_queries_local(qe_ctx* c, int nranks, const char* text, char** out, si
     if (nranks < 1 || nranks > 16) throw Error(QE_EINVAL, "1..16 in-process ranks");
     qe_ctx* w[16];
     ck(qe_workers(c, nranks, w), c);
+    // each rank's buckets of the base columns, as the RCCL ranks take them at load (kept in the
+    // worker contexts until the relations are dropped)
+    for (int r = 0; r < nranks; r++)
+        if (nranks > 1 && (w[r]->bparts_n != (uint32_t)nranks || w[r]->bparts_p != (uint32_t)r))
+            ck(qe_partition_columns(w[r], (uint32_t)nranks, (uint32_t)r), w[r]);
     qe_comm* m[16];
     ck(qe_comm_init_local(w, nranks, m), w[0]);
     std::vector<char*> outs(nranks, nullptr);

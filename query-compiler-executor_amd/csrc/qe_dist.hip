@@ -11,6 +11,8 @@
 #include <algorithm>
 #include <vector>
 
+#include <chrono>
+
 #include "qe_device.h"
 #include "qe_internal.h"
 
@@ -544,6 +546,30 @@ int qe_bucket_select(qe_ctx* c, qe_col col, uint32_t nparts, uint32_t part, cons
                      qe_pairs* out) {
     QE_API_BEGIN(c)
     bucket_select_dev(c, col, nparts, part, heavy, nheavy, nullptr, out);
+    return 0;
+    QE_API_END(c)
+}
+
+int qe_partition_columns(qe_ctx* c, uint32_t nparts, uint32_t part) {
+    QE_API_BEGIN(c)
+    if (nparts < 1 || part >= nparts) throw Error(QE_EINVAL, "part out of range");
+    drop_partitions(c);
+    if (nparts == 1) return 0;   // (one rank reads the columns themselves)
+    const auto t0 = std::chrono::steady_clock::now();
+    double bytes = 0;
+    for (const auto& r : c->rels)
+        for (size_t k = 0; k < r.cols.size(); k++) {
+            qe_col q{r.cols[k], r.rows};
+            qe_pairs p{};
+            bucket_select_dev(c, q, nparts, part, nullptr, 0, nullptr, &p);
+            c->bparts[r.cols[k]] = p;
+            bytes += 8.0 * (double)r.rows + 12.0 * (double)p.n;
+        }
+    c->bparts_n = nparts;
+    c->bparts_p = part;
+    sync(c);
+    c->load_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    c->load_bytes += bytes;
     return 0;
     QE_API_END(c)
 }

@@ -100,10 +100,16 @@ struct qe_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
+    std::string late_err;   // an internal violation found where no throw is allowed (dfree), surfaced later
 
     // caching device allocator: exact size classes, stream-ordered reuse on the one stream
     std::multimap<size_t, void*> free_blocks;
     std::unordered_map<void*, size_t> live;
+    std::unordered_map<void*, void*> pad_base;   // QE_ALLOC_PAD: offset block -> its hipMalloc base
+    uint64_t* d_hj8 = nullptr;                   // the chain bucket join's eight stream counters (qe_sort.hip)
+    // qe_partition_columns: every base column's hash bucket `bparts_p` of `bparts_n`, by column
+    std::unordered_map<const uint64_t*, qe_pairs> bparts;
+    uint32_t bparts_n = 0, bparts_p = 0;
     uint64_t in_use = 0, cached = 0;
 
     std::vector<qe::Relation> rels;
@@ -127,6 +133,7 @@ struct qe_ctx {
     // small device scratch + pinned host mirror for scalar results
     uint64_t* d_scratch = nullptr;   // 64 words
     uint32_t* d_zhist = nullptr;     // the lookback-form sorts' histograms (32 K + 256 words), left zeroed by their scans
+    bool zhist_dirty = false;        // set from a histogram launch until its scan is queued (a throw between: clear first)
     uint64_t* h_scratch = nullptr;   // pinned, 64 words
     hipEvent_t wait_ev = nullptr;    // polled for scalar results (read_u64 / read_words, QE_WAIT=event)
     // device blocks a batch's shared sort holds (qe_sort_cache): dfree of one of them is a bug
@@ -186,7 +193,12 @@ inline const uint32_t* narrow_of(const qe_ctx* c, const void* col, uint64_t n) {
     return nullptr;
 }
 
+// every dalloc block is followed by DALLOC_SLACK allocated bytes: the soffset-strided buffer
+// loads (buf_load_*_sl, qe_device.h) may read that far past a block's end
+constexpr size_t DALLOC_SLACK = 64u << 10;
 void* dalloc(qe_ctx* c, size_t bytes);
+bool alloc_log_on();   // QE_ALLOC_LOG=1 (placement A/Bs)
+void drop_partitions(qe_ctx* c);   // qe_partition_columns' buckets freed
 void dfree(qe_ctx* c, void* p);
 template <class T>
 T* dalloc_t(qe_ctx* c, size_t n) { return static_cast<T*>(dalloc(c, n * sizeof(T))); }

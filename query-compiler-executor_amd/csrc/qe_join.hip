@@ -1815,6 +1815,19 @@ int qe_sort_cache(qe_ctx* c, int on) {
     c->scache_hits += sc->hits;
     c->scache_builds += sc->builds;
     delete sc;
+    // a lane that tried to return a shared sort's buffer to its allocator (dfree records it, it
+    // cannot throw from the destructors it runs in): the batch fails loudly here
+    for (qe_ctx* x : c->workers)
+        if (!x->late_err.empty()) {
+            const std::string m = x->late_err;
+            x->late_err.clear();
+            throw Error(QE_EINVAL, m);
+        }
+    if (!c->late_err.empty()) {
+        const std::string m = c->late_err;
+        c->late_err.clear();
+        throw Error(QE_EINVAL, m);
+    }
     return 0;
     QE_API_END(c)
 }

@@ -29,6 +29,43 @@ static size_t round_size(size_t b) {
     return ((b + g - 1) / g) * g;
 }
 
+// placement knobs for A/Bs: QE_ALLOC_PAD=B offsets every new block of >= 16 MiB
+// by B bytes inside a larger hipMalloc (the base kept for hipFree); QE_ALLOC_LOG=1 prints each new
+// large block's address
+static size_t alloc_pad() {
+    static const size_t v = [] {
+        const char* e = getenv("QE_ALLOC_PAD");
+        return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)0;
+    }();
+    return v;
+}
+bool alloc_log_on() {
+    static const bool v = [] {
+        const char* e = getenv("QE_ALLOC_LOG");
+        return e && *e == '1';
+    }();
+    return v;
+}
+static hipError_t hmalloc(qe_ctx* c, void** p, size_t sz) {
+    const size_t pad = sz >= (16u << 20) ? alloc_pad() : 0;
+    void* b = nullptr;
+    hipError_t e = hipMalloc(&b, sz + pad + DALLOC_SLACK);
+    if (e != hipSuccess) return e;
+    *p = (char*)b + pad;
+    if (pad) c->pad_base[*p] = b;
+    if (alloc_log_on() && sz >= (16u << 20))
+        fprintf(stderr, "[qe alloc] %zu MiB at %p (base %p)\n", sz >> 20, *p, b);
+    return e;
+}
+static void hfree(qe_ctx* c, void* p) {
+    auto it = c->pad_base.find(p);
+    if (it != c->pad_base.end()) {
+        p = it->second;
+        c->pad_base.erase(it);
+    }
+    (void)hipFree(p);
+}
+
 void* dalloc(qe_ctx* c, size_t bytes) {
     size_t sz = round_size(bytes);
     auto it = c->free_blocks.lower_bound(sz);
@@ -42,15 +79,15 @@ void* dalloc(qe_ctx* c, size_t bytes) {
         return p;
     }
     void* p = nullptr;
-    hipError_t e = hipMalloc(&p, sz);
+    hipError_t e = hmalloc(c, &p, sz);
     if (e != hipSuccess) {
         (void)hipGetLastError();
         // release the cache and retry once
         QE_HIP(hipStreamSynchronize(c->stream));
-        for (auto& kv : c->free_blocks) (void)hipFree(kv.second);
+        for (auto& kv : c->free_blocks) hfree(c, kv.second);
         c->free_blocks.clear();
         c->cached = 0;
-        e = hipMalloc(&p, sz);
+        e = hmalloc(c, &p, sz);
         if (e != hipSuccess) {
             (void)hipGetLastError();
             throw Error(QE_ENOMEM, "hipMalloc(" + std::to_string(sz) + ") failed");
@@ -63,7 +100,13 @@ void* dalloc(qe_ctx* c, size_t bytes) {
 
 void dfree(qe_ctx* c, void* p) {
     if (!p) return;
-    if (!c->pinned.empty() && c->pinned.count(p)) throw Error(QE_EINVAL, "internal: dfree of a shared sort's buffer");
+    // a shared sort's buffer (pinned while this lane reads it) is never recycled: the violation is
+    // recorded -- dfree runs inside destructors and qe_pairs_free, where a throw would terminate --
+    // and qe_sort_cache(ctx, 0) fails the batch with it
+    if (!c->pinned.empty() && c->pinned.count(p)) {
+        if (c->late_err.empty()) c->late_err = "internal: dfree of a shared sort's buffer";
+        return;
+    }
     auto it = c->live.find(p);
     if (it == c->live.end()) return;   // not ours (e.g. a relation column)
     size_t sz = it->second;
@@ -71,6 +114,17 @@ void dfree(qe_ctx* c, void* p) {
     c->in_use -= sz;
     c->free_blocks.emplace(sz, p);
     c->cached += sz;
+}
+
+void drop_partitions(qe_ctx* c) {
+    if (c->bparts.empty()) return;
+    QE_HIP(hipStreamSynchronize(c->stream));
+    for (auto& kv : c->bparts) {
+        dfree(c, kv.second.key);
+        dfree(c, kv.second.val);
+    }
+    c->bparts.clear();
+    c->bparts_n = c->bparts_p = 0;
 }
 
 LBSlot lb_acquire(qe_ctx* c, size_t words) {
@@ -540,8 +594,8 @@ void qe_fini(qe_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     for (auto& r : c->rels) free_relation(r);
-    for (auto& kv : c->free_blocks) (void)hipFree(kv.second);
-    for (auto& kv : c->live) (void)hipFree(kv.first);
+    for (auto& kv : c->free_blocks) hfree(c, kv.second);
+    for (auto& kv : c->live) hfree(c, kv.first);
     for (auto& p : c->pending) {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
@@ -551,6 +605,7 @@ void qe_fini(qe_ctx* c) {
     if (c->lb_tickets) (void)hipFree(c->lb_tickets);
     if (c->d_scratch) (void)hipFree(c->d_scratch);
     if (c->d_zhist) (void)hipFree(c->d_zhist);
+    if (c->d_hj8) (void)hipFree(c->d_hj8);
     if (c->h_scratch) (void)hipHostFree(c->h_scratch);
     if (c->h_ret) (void)hipHostFree(c->h_ret);
     if (c->wait_ev) (void)hipEventDestroy(c->wait_ev);
@@ -752,7 +807,9 @@ int qe_drop_relations(qe_ctx* c) {
     for (qe_ctx* w : c->workers) {             // workers may still read them
         sync(w);
         w->rels.clear();
+        qe::drop_partitions(w);
     }
+    qe::drop_partitions(c);
     sync(c);
     for (auto& r : c->rels) free_relation(r);
     c->rels.clear();
@@ -910,7 +967,7 @@ int qe_mem_stats(qe_ctx* c, uint64_t* in_use, uint64_t* cached) {
 int qe_mem_trim(qe_ctx* c) {
     QE_API_BEGIN(c)
     sync(c);
-    for (auto& kv : c->free_blocks) QE_HIP(hipFree(kv.second));
+    for (auto& kv : c->free_blocks) hfree(c, kv.second);
     c->free_blocks.clear();
     c->cached = 0;
     return 0;

@@ -261,6 +261,21 @@ static inline uint32_t xcd_grid(uint64_t items) {
 // match-any -- equal digits keep no order.  For the partitioned plan's deferred sorts (their
 // consumer, bucket_join, needs the buckets, not an order inside them) and the first LSD pass of
 // the aggregate join's sorts (no earlier order to keep, none needed among equal keys).
+// PRERANK (PRE + UNSTABLE, round 5): the tile's digit counts are known before the pass -- the
+// difference of two rows of the scanned tile-count matrix (the next tile's offsets, or the next
+// digit's column start) -- so the tile-local digit starts are scanned while the element loads are
+// in flight, and ONE LDS atomic per element returns its stage slot directly: no barrier + scan
+// after ranking, no per-element reads of the digit start and wave offset when staging.
+// (QE_PRERANK=0: build knob, the round-4 rank -> scan -> stage order.)
+#ifndef QE_PRERANK
+#define QE_PRERANK 0   // (default off: measured slower in round 5, see HISTORY.md)
+#endif
+#ifndef QE_PRERANK2   // (build knob: the second pass's PRERANK form alone)
+#define QE_PRERANK2 QE_PRERANK
+#endif
+#ifndef QE_P1_EARLY_X   // (build knob: PRERANK's 32-bit payload loads issued with the elements')
+#define QE_P1_EARLY_X 1
+#endif
 enum { X_NONE = 0, X64 = 1, X32 = 2, XCOL = 3 };
 template <typename K, int IN, int OUT, bool PACK, int RBITS, int ITEMS, int NT, bool PRE = false, int CARRY = X_NONE,
           bool UNSTABLE = false>
@@ -281,8 +296,8 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
     // per-wave digit counts -> exclusive over waves; UNSTABLE ranks on ONE block-wide row (no order
     // to keep between waves), which leaves a 1024-thread tile in 2 workgroups' LDS per CU
     constexpr int NWH = UNSTABLE ? 1 : NW;
-    __shared__ uint64_t stage[TILE];
-    __shared__ uint32_t whist[NWH][BINS];
+    __shared__ uint64_t stage[TILE + 1];     // (+1: PRERANK's spare slot)
+    __shared__ uint32_t whist[NWH][BINS + 1];
     __shared__ uint32_t bexcl[BINS];        // tile-local exclusive offset of each digit
     __shared__ uint32_t gofs[BINS];         // global position of the digit's run - bexcl
     __shared__ uint32_t wsum[NW];
@@ -305,8 +320,19 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
 #pragma unroll
         for (int q = 0; q < DPT; q++) pre_off[q] = owner ? offs[(uint64_t)tile * BINS + threadIdx.x * DPT + q] : 0u;
     }
-    for (int i = threadIdx.x; i < NWH * BINS; i += NT) (&whist[0][0])[i] = 0;
-    __syncthreads();
+    constexpr bool PRERANK = PRE && UNSTABLE && DPT == 1 && QE_PRERANK;
+    uint32_t nxt_off = 0;   // PRERANK: where this tile's run of the digit ends (its count = nxt_off - pre_off)
+    if constexpr (PRERANK) {
+        const uint32_t ntl = (uint32_t)((n + TILE - 1) / TILE), d = threadIdx.x;
+        // one unconditional load: the next tile's row, or for the last tile the next column's start
+        // (row 0); the last tile's last digit ends at n
+        const bool last = tile + 1 >= ntl;
+        const uint32_t v = offs[last ? (d < (uint32_t)BINS - 1 ? d + 1 : 0u) : (tile + 1) * (uint32_t)BINS + (d < (uint32_t)BINS ? d : 0u)];
+        nxt_off = last && d == (uint32_t)BINS - 1 ? (uint32_t)n : v;
+    } else {
+        for (int i = threadIdx.x; i < NWH * (BINS + 1); i += NT) (&whist[0][0])[i] = 0;
+        __syncthreads();
+    }
     QE_SORT_STAMP(tile, 1);
 
     uint64_t word[ITEMS];
@@ -324,23 +350,22 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
         return V4 ? (uint32_t)w * WT + (uint32_t)(j >> 2) * 256u + (uint32_t)l * 4u + (uint32_t)(j & 3)
                   : loc0 + (uint32_t)j * 64u;
     };
-    const bool full = tcount == (uint32_t)TILE;   // (block-uniform)
-    // u32 elements j of one array at the V4 mapping
+    // u32 elements j of one array at the V4 mapping, every tile alike (no branch: the compiler's
+    // waits stay counted).  The descriptors of V4 arrays cover the tile rounded up to whole 16-B
+    // units (v4_bytes): the last unit of a partial tile reads up to 3 elements past n -- inside the
+    // allocation, whose size granule is a multiple of 16 B (the V4 arrays are hipMalloc'd u32 column
+    // copies or dalloc'd lists, 256-B aligned) -- and they are masked by `ok` like the rest.
     auto load_v4 = [&](const __amdgpu_buffer_rsrc_t& r, uint32_t (&x)[ITEMS]) {
-        if (full) {
 #pragma unroll
-            for (int g = 0; g < ITEMS / 4; g++) {
-                const uint4 a = buf_load_u4(r, ((uint32_t)w * WT + (uint32_t)l * 4u) * 4u, (uint32_t)g * 1024u);
-                x[4 * g] = a.x;
-                x[4 * g + 1] = a.y;
-                x[4 * g + 2] = a.z;
-                x[4 * g + 3] = a.w;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < ITEMS; j++) x[j] = buf_load_u32(r, loc_of(j) * 4u, 0u);
+        for (int g = 0; g < ITEMS / 4; g++) {
+            const uint4 a = buf_load_u4(r, ((uint32_t)w * WT + (uint32_t)l * 4u) * 4u, (uint32_t)g * 1024u);
+            x[4 * g] = a.x;
+            x[4 * g + 1] = a.y;
+            x[4 * g + 2] = a.z;
+            x[4 * g + 3] = a.w;
         }
     };
+    const uint32_t v4_bytes = (tcount * 4u + 15u) & ~15u;
     if constexpr (IN == IN_WORD) {
         const auto rw = buf_rsrc(win + tb, tcount * 8u);
 #pragma unroll
@@ -350,8 +375,8 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
         }
     } else if constexpr (V4) {
         uint32_t kk[ITEMS], vv[ITEMS];
-        load_v4(buf_rsrc(kin + tb, tcount * 4u), kk);
-        if constexpr (IN == IN_KV) load_v4(buf_rsrc(vin + tb, tcount * 4u), vv);
+        load_v4(buf_rsrc(kin + tb, v4_bytes), kk);
+        if constexpr (IN == IN_KV) load_v4(buf_rsrc(vin + tb, v4_bytes), vv);
 #pragma unroll
         for (int j = 0; j < ITEMS; j++)
             word[j] = ((((uint64_t)kk[j] >> f.lo) & f.fmask) << 32) |
@@ -380,9 +405,67 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
             }
         }
     }
+    constexpr bool P32 = CARRY == X32 || CARRY == XCOL;
+    uint32_t xw[P32 ? ITEMS : 1];
+    auto load_payloads = [&]() {
+        if constexpr (CARRY != X_NONE) {
+            const auto ra = CARRY == XCOL ? buf_rsrc(reinterpret_cast<const uint64_t*>(xa) + tb, tcount * 8u)
+                                          : buf_rsrc(xa + tb, V4 ? v4_bytes : tcount * 4u);
+            const auto rb = buf_rsrc(xb ? xb + tb : xa, xb ? (V4 ? v4_bytes : tcount * 4u) : 0u);   // (no xb: reads 0)
+            if constexpr (V4 && CARRY == X64) {
+                uint32_t xa4[ITEMS], xb4[ITEMS];
+                load_v4(ra, xa4);
+                load_v4(rb, xb4);
+#pragma unroll
+                for (int j = 0; j < ITEMS; j++) word[j] = (uint64_t)xa4[j] | (uint64_t)xb4[j] << 32;
+            } else if constexpr (V4) {
+                load_v4(ra, xw);
+            } else {
+#pragma unroll
+                for (int j = 0; j < ITEMS; j++) {
+                    if constexpr (CARRY == X64)
+                        word[j] = (uint64_t)buf_load_u32(ra, loc0 * 4u, (uint32_t)j * 256u) |
+                                  (uint64_t)buf_load_u32(rb, loc0 * 4u, (uint32_t)j * 256u) << 32;
+                    else if constexpr (CARRY == X32) xw[j] = buf_load_u32(ra, loc0 * 4u, (uint32_t)j * 256u);
+                    else xw[j] = buf_load_u2(ra, loc0 * 8u, (uint32_t)j * 512u).x;
+                }
+            }
+        }
+    };
+    if constexpr (PRERANK && P32 && QE_P1_EARLY_X) load_payloads();
+    if constexpr (PRERANK) {
+        // the tile-local digit starts (scanned while the loads are in flight), then rank + stage
+        const uint32_t cnt = owner ? nxt_off - pre_off[0] : 0u;
+        const uint32_t inc = wave_incl_scan_u32(cnt);
+        if (l == 63) wsum[w] = inc;
+        __syncthreads();
+        if (owner) {
+            uint32_t ex = inc - cnt;
+            for (int ww = 0; ww < w; ww++) ex += wsum[ww];
+            whist[0][threadIdx.x] = ex;            // the digit's next free stage slot
+            gofs[threadIdx.x] = pre_off[0] - ex;   // global position of the digit's run - its tile-local start
+        }
+        __syncthreads();
+        QE_SORT_STAMP(tile, 2);
+        // branch-free: an element past the tile counts on a spare counter and lands in a spare slot
+        // (partial tiles only), so every atomic of the thread is in flight before the first store
+        uint32_t sl[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const bool ok = loc_of(j) < tcount;
+            sl[j] = atomicAdd(&whist[0][ok ? (uint32_t)(word[j] >> dsh) & mask : (uint32_t)BINS], 1u);
+            sl[j] = ok ? sl[j] : (uint32_t)TILE;
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            stage[sl[j]] = word[j];
+            if constexpr (CARRY != X_NONE) pos[j] = sl[j];   // the payload takes the same slot later
+        }
+        QE_SORT_STAMP(tile, 3);
+    }
     // stable rank inside the wave: element order is (j, lane)
 #pragma unroll
-    for (int j = 0; j < ITEMS; j++) {
+    for (int j = 0; j < (PRERANK ? 0 : ITEMS); j++) {
         const bool ok = loc_of(j) < tcount;
         uint32_t d = (uint32_t)(word[j] >> dsh) & mask;
         if constexpr (UNSTABLE) {
@@ -410,10 +493,11 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
         pos[j] = old + (uint32_t)__popcll(peers & lt);
 #endif
     }
+    uint32_t tot[DPT], tsum = 0;
+    if constexpr (!PRERANK) {
     __syncthreads();
     QE_SORT_STAMP(tile, 2);
     // thread t owns digits t*DPT .. t*DPT+DPT-1: totals, exclusive over waves, publish aggregate
-    uint32_t tot[DPT], tsum = 0;
 #pragma unroll
     for (int q = 0; q < DPT; q++) {
         const uint32_t d = threadIdx.x * DPT + q;
@@ -452,39 +536,17 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
             if constexpr (CARRY != X_NONE) pos[j] = slot;   // the payload takes the same slot later
         }
     }
+    }   // !PRERANK
     // the payloads load into the words' registers (a 32-bit one into registers of its own), in
-    // flight during the write-out
-    constexpr bool P32 = CARRY == X32 || CARRY == XCOL;
-    uint32_t xw[P32 ? ITEMS : 1];
-    if constexpr (CARRY != X_NONE) {
-        const auto ra = CARRY == XCOL ? buf_rsrc(reinterpret_cast<const uint64_t*>(xa) + tb, tcount * 8u)
-                                      : buf_rsrc(xa + tb, tcount * 4u);
-        const auto rb = buf_rsrc(xb ? xb + tb : xa, xb ? tcount * 4u : 0u);   // (no xb: reads 0)
-        if constexpr (V4 && CARRY == X64) {
-            uint32_t xa4[ITEMS], xb4[ITEMS];
-            load_v4(ra, xa4);
-            load_v4(rb, xb4);
-#pragma unroll
-            for (int j = 0; j < ITEMS; j++) word[j] = (uint64_t)xa4[j] | (uint64_t)xb4[j] << 32;
-        } else if constexpr (V4) {
-            load_v4(ra, xw);
-        } else {
-#pragma unroll
-            for (int j = 0; j < ITEMS; j++) {
-                if constexpr (CARRY == X64)
-                    word[j] = (uint64_t)buf_load_u32(ra, loc0 * 4u, (uint32_t)j * 256u) |
-                              (uint64_t)buf_load_u32(rb, loc0 * 4u, (uint32_t)j * 256u) << 32;
-                else if constexpr (CARRY == X32) xw[j] = buf_load_u32(ra, loc0 * 4u, (uint32_t)j * 256u);
-                else xw[j] = buf_load_u2(ra, loc0 * 8u, (uint32_t)j * 512u).x;
-            }
-        }
-    }
+    // flight during the write-out (PRERANK, 32-bit payloads: issued with the elements' loads, so
+    // the tile's whole read is in flight at once)
+    if constexpr (!(PRERANK && P32 && QE_P1_EARLY_X)) load_payloads();
 #pragma unroll
     for (int q = 0; q < DPT; q++) {
         const uint32_t d = threadIdx.x * DPT + q;
         if (!owner) continue;
         if constexpr (PRE) {
-            gofs[d] = pre_off[q] - bexcl[d];
+            if constexpr (!PRERANK) gofs[d] = pre_off[q] - bexcl[d];   // (PRERANK: set before ranking)
             continue;
         }
         // the predecessors' counts: by this time most have published their inclusive prefix
@@ -1246,8 +1308,9 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
                                                          uint64_t* __restrict__ xout = nullptr) {
     constexpr int BINS = 128, NW = TL2_NT / 64, WT = 64 * TL2_ITEMS;
     constexpr int NWH = UNSTABLE ? 1 : NW;   // unstable ranks: one block-wide counter row
-    __shared__ uint64_t stage[TL2_TILE];
-    __shared__ uint32_t whist[NWH][BINS];
+    constexpr int SP = UNSTABLE ? 1 : 0;   // the PRERANK spare slot / counter (unstable ranks only)
+    __shared__ uint64_t stage[TL2_TILE + SP];
+    __shared__ uint32_t whist[NWH][BINS + SP];
     __shared__ uint32_t bexcl[BINS];
     __shared__ uint32_t gofs[BINS];
     __shared__ uint32_t wsum[NW];
@@ -1264,28 +1327,83 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
     const uint64_t lt = lanemask_lt();
     const uint32_t d = threadIdx.x;   // threads 0..127 own one digit each
     uint32_t run = 0;
-    const uint32_t* runp = off2 + (uint64_t)s * BINS + (d < BINS ? d : BINS - 1);
+    const uint32_t dcl = d < BINS ? d : BINS - 1;
+    const uint32_t* runp = off2 + (uint64_t)s * BINS + dcl;
+    // PRERANK (unstable ranks, a segment that fits one sub-tile -- nearly all of them): the segment's
+    // digit counts are the difference of two rows of the scanned segment-count matrix, so the
+    // digit starts are scanned while the words load and one LDS atomic per word returns its slot
+    // (see radix_pass_kernel's PRERANK)
+    const bool one = UNSTABLE && QE_PRERANK2 && end - start <= (uint32_t)TL2_TILE;   // (block-uniform)
     for (uint32_t base = start; base < end; base += TL2_TILE) {   // block-uniform
         const uint32_t m = end - base < (uint32_t)TL2_TILE ? end - base : (uint32_t)TL2_TILE;
-        for (int i = threadIdx.x; i < NWH * BINS; i += TL2_NT) (&whist[0][0])[i] = 0;
+        if (!one)
+            for (int i = threadIdx.x; i < NWH * (BINS + SP); i += TL2_NT) (&whist[0][0])[i] = 0;
         uint64_t word[TL2_ITEMS];
         uint32_t pos2[(TL2_ITEMS + 1) / 2];   // ranks < TL2_TILE: two u16 per register
         const int lim = (int)m - (int)((uint32_t)w * WT + l);   // element j valid iff j * 64 < lim
+        uint32_t nrun = 0;   // (one) where the segment's run of the digit ends
+        if (one) {   // issued before the words: their wait is a counted one
+            run = *runp;
+            const bool last = s + 1 >= 256u * G;   // (the last segment: the next column's start, or n)
+            const uint32_t v = off2[last ? (dcl + 1 < (uint32_t)BINS ? dcl + 1 : 0u) : (s + 1) * (uint32_t)BINS + dcl];
+            nrun = v;   // (the select against n happens at the scan, behind the words' loads)
+        }
         // every load unconditional, all 18 in flight at once, through a buffer descriptor over the
         // sub-tile: one 32-bit lane offset + a constant per element (18 64-bit clamped addresses
-        // held 36 VGPRs and made the kernel spill), elements past the segment read as 0
+        // held 36 VGPRs and made the kernel spill; the stride in soffset: no VGPR per element).
+        // Elements past the segment are masked by `lim`; the strided reads stay inside the
+        // dalloc block's slack (win and xin are always dalloc'd: DALLOC_SLACK > 18 x 512 B)
         const uint32_t o0 = (uint32_t)w * WT + l;
         {
             const auto rw = W32 ? buf_rsrc(reinterpret_cast<const uint32_t*>(win) + base, m * 4u) : buf_rsrc(win + base, m * 8u);
 #pragma unroll
             for (int j = 0; j < TL2_ITEMS; j++) {
-                if constexpr (W32) word[j] = (uint64_t)buf_load_u32(rw, o0 * 4u, (uint32_t)j * 256u) << 32;
+                if constexpr (W32) word[j] = (uint64_t)buf_load_u32_sl(rw, o0 * 4u, (uint32_t)j * 256u) << 32;
                 else {
-                    const uint2 v = buf_load_u2(rw, o0 * 8u, (uint32_t)j * 512u);
+                    const uint2 v = buf_load_u2_sl(rw, o0 * 8u, (uint32_t)j * 512u);
                     word[j] = (uint64_t)v.y << 32 | v.x;
                 }
             }
         }
+        if (one) {
+            const uint32_t ne = s + 1 >= 256u * G && dcl == (uint32_t)BINS - 1 ? (uint32_t)n : nrun;
+            const uint32_t cnt = d < BINS ? ne - run : 0u;
+            const uint32_t inc = wave_incl_scan_u32(cnt);
+            if (l == 63) wsum[w] = inc;
+            __syncthreads();
+            if (d < BINS) {
+                uint32_t ex = inc - cnt;
+                for (int ww = 0; ww < w; ww++) ex += wsum[ww];
+                whist[0][d] = ex;       // the digit's next free stage slot
+                gofs[d] = run - ex;     // global position of the digit's run - its sub-tile start
+            }
+            __syncthreads();
+            QE_SORT_STAMP(s, 1);
+            // in chunks of TL2_WCH (a chunk's atomics in flight together, registers within budget);
+            // branch-free: a word past the segment counts on the spare counter, lands in the spare slot
+#pragma unroll
+            for (int j0 = 0; j0 < TL2_ITEMS; j0 += TL2_WCH) {
+                uint32_t sl[TL2_WCH];
+#pragma unroll
+                for (int q = 0; q < TL2_WCH; q++) {
+                    const int j = j0 + q;
+                    const bool ok = j * 64 < lim;
+                    sl[q] = atomicAdd(&whist[0][ok ? (uint32_t)(word[j] >> dsh) & (BINS - 1) : (uint32_t)BINS], 1u);
+                    sl[q] = ok ? sl[q] : (uint32_t)TL2_TILE;
+                }
+#pragma unroll
+                for (int q = 0; q < TL2_WCH; q++) {
+                    const int j = j0 + q;
+                    stage[sl[q]] = word[j];
+                    if constexpr (CARRY != X_NONE) {   // pos2 holds the slot (<= TL2_TILE: 16 bits)
+                        if (j & 1) pos2[j >> 1] |= sl[q] << 16;
+                        else pos2[j >> 1] = sl[q];
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            QE_SORT_STAMP(s, 3);
+        } else {
         if (base == start) run = *runp;   // the digit offsets, behind the words (clamped: no branch)
         __syncthreads();   // whist zeroed
         if (base == start) QE_SORT_STAMP(s, 1);
@@ -1362,6 +1480,7 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+        }   // !one
         // the payloads load into the words' registers (a 32-bit one into registers of its own),
         // in flight during the write-out
         uint32_t xw[CARRY == X32 ? TL2_ITEMS : 1];
@@ -1371,10 +1490,10 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
 #pragma unroll
             for (int j = 0; j < TL2_ITEMS; j++) {
                 if constexpr (CARRY == X64) {
-                    const uint2 v = buf_load_u2(rx, o0 * 8u, (uint32_t)j * 512u);
+                    const uint2 v = buf_load_u2_sl(rx, o0 * 8u, (uint32_t)j * 512u);
                     word[j] = (uint64_t)v.y << 32 | v.x;
                 } else {
-                    xw[j] = buf_load_u32(rx, o0 * 4u, (uint32_t)j * 256u);
+                    xw[j] = buf_load_u32_sl(rx, o0 * 4u, (uint32_t)j * 256u);
                 }
             }
         }
@@ -1718,6 +1837,12 @@ constexpr uint32_t HJ_NONE = 0xFFFFu;
 // a chain longer than HJ_CHAIN_MAX is flagged like one beyond LDS, and the join takes the sorts +
 // merge path (linear in the pairs) instead.
 constexpr uint32_t HJ_CHAIN_MAX = 64;
+// XCD-stream output reservation (round 5): the chain join's blocks reserve their
+// pairs on eight counters (HJ8_STRIDE words apart: different channels), stream x = block % 8.  A
+// stream is laid out in chunks of 2^HJ8_CHB pairs: stream x's chunk k is output chunk 8 k + x, so
+// every chunk row below the shortest stream is dense, and hj8_fixup moves the few pairs past P (the
+// streams' ragged ends) into the holes below it -- the plan's pairs need no order.
+constexpr uint32_t HJ8_CHB = 12, HJ8_STRIDE = 544;   // 4096-pair chunks; counters 4352 B apart
 #ifndef QE_HJ_RR_GLOBAL
 #define QE_HJ_RR_GLOBAL 0
 #endif
@@ -1737,7 +1862,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
                       uint64_t cap, uint64_t* total_out, const uint64_t* __restrict__ xS = nullptr,
                       uint32_t* __restrict__ outX0 = nullptr, uint32_t* __restrict__ outX1 = nullptr,
                       const uint32_t* __restrict__ xR = nullptr, uint32_t* __restrict__ outRX = nullptr,
-                      const uint32_t* __restrict__ xS32 = nullptr) {
+                      const uint32_t* __restrict__ xS32 = nullptr, uint64_t* __restrict__ x8 = nullptr) {
     __shared__ uint32_t head[1 << DBITS];   // per key value: the last R row inserted (HJ_NONE: none)
     __shared__ uint16_t nxt[NT * HJ_I];        // per R row: the previous row of its value
 #if QE_HJ_RR_GLOBAL
@@ -1818,7 +1943,10 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
         uint32_t cnt = 0, h = HJ_NONE;
         if ((uint32_t)j * NT + threadIdx.x < mS) {
             h = head[fld(ws[j]) & dmask];
-            for (uint32_t p = h; p != HJ_NONE; p = nxt[p]) cnt++;   // (linear in the pairs: cnt of them)
+            // (linear in the pairs: cnt of them) -- and bounded: the walk stops one link past
+            // HJ_CHAIN_MAX whatever nxt[] holds, so no chain (a long one, or a cycle through stale
+            // links) can keep a wave here (the looped emission that hung in round 4)
+            for (uint32_t p = h; p != HJ_NONE && cnt <= HJ_CHAIN_MAX; p = nxt[p]) cnt++;
             if (cnt > HJ_CHAIN_MAX) s_long = 1;
         }
         hd[j] = h;
@@ -1841,15 +1969,24 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
         if (2u * l < E) tab[2 * l] = inc - a0 - a1;
         if (2u * l + 1 < E) tab[2 * l + 1] = inc - a1;
         if (l == 0) {
-            s_excl = total ? atomicAdd(reinterpret_cast<unsigned long long*>(total_out), (unsigned long long)total)
-                           : 0ull;
+            // x8: eight counters, one per XCD stream (block b -> stream b % 8), instead of one word
+            // that every bucket's reservation queues on (~55 returning atomics per us on one address
+            // bounded the kernel: 32 K buckets in ~0.55 ms)
+            uint64_t* ctr = x8 ? x8 + (uint64_t)HJ8_STRIDE * (b & 7u) : total_out;
+            s_excl = total ? atomicAdd(reinterpret_cast<unsigned long long*>(ctr), (unsigned long long)total) : 0ull;
             s_total = total;
         }
     }
     __syncthreads();
     QE_STAMP(g_hj_stamps, b, 4);
     const uint64_t gofs = s_excl;
-    if (gofs + s_total > cap) return;   // outgrew the buffers: the host re-runs with the exact size
+    // outgrew the buffers (a stream's whole chunks, or the one run): the host re-runs with the size
+    if (gofs + s_total > (x8 ? (((cap >> HJ8_CHB) / 8) << HJ8_CHB) : cap)) return;
+    const uint32_t xs = x8 ? (b & 7u) : 0u;
+    // stream offset -> output position: stream x's chunk k is the output's chunk 8 k + x (hj8_place)
+    auto place = [&](uint64_t o) -> uint64_t {
+        return x8 ? ((((o >> HJ8_CHB) << 3) | xs) << HJ8_CHB) | (o & ((1u << HJ8_CHB) - 1u)) : o;
+    };
 #pragma unroll
     for (int j = 0; j < HJ_I; j++) {   // wave-cooperative emission, as tl_hjoin_kernel's
         const uint32_t pj = pre[j], all = tot[j];
@@ -1874,12 +2011,13 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
             }
             if (q < all) {
                 for (uint32_t s = 0; s < k; s++) p = nxt[p];   // the k-th partner on the chain
-                outR[ob + q] = QE_HJ_RR_GLOBAL ? (uint32_t)wR[r0 + p] : rr[p];
-                outS[ob + q] = sr;
-                if constexpr (RX) outRX[ob + q] = rx[p];
+                const uint64_t o = place(ob + q);
+                outR[o] = QE_HJ_RR_GLOBAL ? (uint32_t)wR[r0 + p] : rr[p];
+                outS[o] = sr;
+                if constexpr (RX) outRX[o] = rx[p];
                 if constexpr (CARRY) {
-                    outX0[ob + q] = x0;
-                    if (!S32 && outX1) outX1[ob + q] = x1;
+                    outX0[o] = x0;
+                    if (!S32 && outX1) outX1[o] = x1;
                 }
             }
         }
@@ -2327,6 +2465,9 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     const size_t xsz = xm == X64 ? 8 : 4;
     uint64_t* x1 = xm ? static_cast<uint64_t*>(dalloc(c, n * xsz)) : nullptr;
     uint64_t* x2 = xm ? static_cast<uint64_t*>(dalloc(c, n * xsz)) : nullptr;
+    if (xm && alloc_log_on())
+        fprintf(stderr, "[qe sort_pass_carry] n=%llu w1=%p w2=%p x1=%p x2=%p keys=%p\n", (unsigned long long)n,
+                (void*)w1, (void*)w2, (void*)x1, (void*)x2, (const void*)keys);
     // a deferred sort's consumer needs its buckets, not an order inside them: unstable ranks
     const bool uns = dfr && sort_unstable_on();
 #define QE_P1(IN, CR, UN, XA, XB, XO)                                                                                   \
@@ -2480,8 +2621,12 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
     const LocalRounds lr = local_rounds(L);
     if (!c->d_zhist) {   // once per context; every scan below leaves it zeroed again
         QE_HIP(hipMalloc(&c->d_zhist, (TL_BUCKETS + 256) * sizeof(uint32_t)));
-        QE_HIP(hipMemsetAsync(c->d_zhist, 0, (TL_BUCKETS + 256) * sizeof(uint32_t), c->stream));
+        c->zhist_dirty = true;
     }
+    // a throw between a histogram launch and its scan's (which re-zeroes the table) leaves counts
+    // behind: the flag, set from the one to the other, makes the next sort clear the table first
+    if (c->zhist_dirty) QE_HIP(hipMemsetAsync(c->d_zhist, 0, (TL_BUCKETS + 256) * sizeof(uint32_t), c->stream));
+    c->zhist_dirty = true;
     uint32_t* hist = H == 8 ? c->d_zhist + TL_BUCKETS : c->d_zhist;
     // digit bases: 256 entries each (the pass kernel reads one per possible 8-bit digit)
     uint32_t* bstart = dalloc_t<uint32_t>(c, TL_BUCKETS + 1 + 512);
@@ -2497,12 +2642,14 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
         QE_HIP(hipGetLastError());
         hipLaunchKernelGGL(tl_scan8_kernel, dim3(1), dim3(256), 0, c->stream, hist, bstart, d_max);
         QE_HIP(hipGetLastError());
+        c->zhist_dirty = false;
     } else {
         Timed t(c, "sort_hist", (double)sizeof(K) * n);
         hipLaunchKernelGGL((tl_hist_kernel<K>), dim3(hist_blocks(n)), dim3(1024), 0, c->stream, keys, n, f, L, hist);
         QE_HIP(hipGetLastError());
         hipLaunchKernelGGL(tl_scan_kernel, dim3(1), dim3(1024), 0, c->stream, hist, bstart, base1, base2, d_max);
         QE_HIP(hipGetLastError());
+        c->zhist_dirty = false;
     }
     const uint64_t maxb = dfr ? 0 : read_u64(c, d_max);
     if (!dfr && maxb > (uint64_t)TL_CAP) {
@@ -3043,6 +3190,76 @@ bool carry_eligible(const qe_pairs* R, const qe_pairs* S, bool rpay) {
     return loR == loS && nbR == nbS && kcR == kcS && nbR - TL_H <= HJ_DBITS;
 }
 
+// XCD-stream mode of the chain join (see HJ8_CHB): on by default, QE_HJ8=0 keeps the one counter
+static bool hj8_on() {
+    static const bool on = !(getenv("QE_HJ8") && getenv("QE_HJ8")[0] == '0');
+    return on;
+}
+// before a join: the [pairs, oversize] words and the eight stream counters zeroed (one launch)
+static __global__ void __launch_bounds__(64) hj8_zero_kernel(uint64_t* w2, uint64_t* x8) {
+    if (threadIdx.x < 2) w2[threadIdx.x] = 0;
+    if (x8 && threadIdx.x < 8) x8[(uint64_t)HJ8_STRIDE * threadIdx.x] = 0;
+}
+// after it: the eight stream totals next to the oversize flag, so one read brings all of them
+static __global__ void __launch_bounds__(64) hj8_collect_kernel(const uint64_t* x8, uint64_t* dst) {
+    if (threadIdx.x < 8) dst[threadIdx.x] = x8[(uint64_t)HJ8_STRIDE * threadIdx.x];
+}
+// the streams' ragged ends: op k copies len pairs (and every carried column) from src to dst
+constexpr int HJ8_MAXOPS = 160;
+struct HJ8Ops {
+    uint64_t src[HJ8_MAXOPS], dst[HJ8_MAXOPS];
+    uint32_t len[HJ8_MAXOPS];
+};
+static __global__ void __launch_bounds__(256) hj8_fixup_kernel(HJ8Ops ops, uint32_t* a0, uint32_t* a1, uint32_t* a2,
+                                                              uint32_t* a3, uint32_t* a4) {
+    const uint64_t s = ops.src[blockIdx.x], d = ops.dst[blockIdx.x];
+    const uint32_t len = ops.len[blockIdx.x];
+    for (uint32_t i = threadIdx.x; i < len; i += 256) {   // src >= P > dst: no op reads what another writes
+        a0[d + i] = a0[s + i];
+        a1[d + i] = a1[s + i];
+        if (a2) a2[d + i] = a2[s + i];
+        if (a3) a3[d + i] = a3[s + i];
+        if (a4) a4[d + i] = a4[s + i];
+    }
+}
+// The copies that make [0, P) dense from the streams' totals Px[8] (stream x's pairs fill output
+// chunks 8 k + x, k = 0, 1, ...): the filled positions at or past P go, in order, into the holes
+// below P.  Returns false when more than HJ8_MAXOPS copies would be needed (heavy skew).
+static bool hj8_plan(const uint64_t* Px, uint64_t P, HJ8Ops* ops, int* nops) {
+    const uint64_t CH = 1ull << HJ8_CHB;
+    uint64_t kmin = ~0ull, kmax = 0;
+    for (int x = 0; x < 8; x++) {
+        kmin = std::min(kmin, Px[x] / CH);
+        kmax = std::max(kmax, (Px[x] + CH - 1) / CH);
+    }
+    std::vector<std::pair<uint64_t, uint64_t>> holes, srcs;   // [a, b) in position order
+    for (uint64_t k = kmin; k < kmax; k++)
+        for (int x = 0; x < 8; x++) {
+            const uint64_t base = (8 * k + (uint64_t)x) * CH;
+            const uint64_t f = Px[x] > k * CH ? std::min(CH, Px[x] - k * CH) : 0;
+            const uint64_t fa = base, fb = base + f, ea = base + f, eb = base + CH;
+            if (fb > std::max(fa, P)) srcs.push_back({std::max(fa, P), fb});
+            if (std::min(eb, P) > ea) holes.push_back({ea, std::min(eb, P)});
+        }
+    *nops = 0;
+    size_t hi = 0, si = 0;
+    uint64_t ho = 0, so = 0;   // consumed within the current hole / source
+    while (hi < holes.size() && si < srcs.size()) {
+        const uint64_t hl = holes[hi].second - holes[hi].first - ho, sl = srcs[si].second - srcs[si].first - so;
+        const uint64_t len = std::min(hl, sl);
+        if (*nops == HJ8_MAXOPS || len > 0xFFFFFFFFull) return false;
+        ops->src[*nops] = srcs[si].first + so;
+        ops->dst[*nops] = holes[hi].first + ho;
+        ops->len[*nops] = (uint32_t)len;
+        (*nops)++;
+        ho += len;
+        so += len;
+        if (ho == holes[hi].second - holes[hi].first) hi++, ho = 0;
+        if (so == srcs[si].second - srcs[si].first) si++, so = 0;
+    }
+    return hi == holes.size() && si == srcs.size();   // (every hole filled by exactly the pairs past P)
+}
+
 bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS, qe_list* outX0,
                  qe_list* outX1, qe_list* outRX) {
     auto iR = c->deferred.find(R->key), iS = c->deferred.find(S->key);
@@ -3060,13 +3277,20 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
     if (rx && (!dR.x32 || !hj_chain_on() || dR.L > 12)) return false;
     const uint64_t nR = R->n, nS = S->n;
     uint64_t cap = nR + nS;   // optimistic (fan-out ~1); an outgrown launch re-runs with the exact size
+    // the XCD streams (chain kernel only; the re-run of an outgrown launch takes the one counter)
+    bool x8m = hj_chain_on() && hj8_on();
+    if (x8m && !c->d_hj8) {
+        QE_HIP(hipMalloc(&c->d_hj8, (size_t)HJ8_STRIDE * 8 * sizeof(uint64_t)));
+        QE_HIP(hipMemsetAsync(c->d_hj8, 0, (size_t)HJ8_STRIDE * 8 * sizeof(uint64_t), c->stream));
+    }
     for (int attempt = 0; attempt < 2; attempt++) {
+        uint64_t* x8 = x8m ? c->d_hj8 : nullptr;
         uint32_t* oR = dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1));
         uint32_t* oS = dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1));
         uint32_t* x0 = carry ? dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1)) : nullptr;
         uint32_t* x1 = carry && outX1 ? dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1)) : nullptr;
         uint32_t* xr = rx ? dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1)) : nullptr;
-        hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(64), 0, c->stream, c->d_scratch + 17, 2);   // [pairs, oversize]
+        hipLaunchKernelGGL(hj8_zero_kernel, dim3(1), dim3(64), 0, c->stream, c->d_scratch + 17, x8);   // [pairs, oversize] (+ streams)
         QE_HIP(hipGetLastError());
         {
             // algorithmic bytes: both sides' words in (+ 8 B per pair below; + the payloads)
@@ -3075,36 +3299,38 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
             if (s32 && rx) {
                 hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, true, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
                                    c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
-                                   c->d_scratch + 17, nullptr, x0, nullptr, dR.x32, xr, dS.x32);
+                                   c->d_scratch + 17, nullptr, x0, nullptr, dR.x32, xr, dS.x32, x8);
             } else if (s32) {
                 hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, false, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
                                    c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
-                                   c->d_scratch + 17, nullptr, x0, nullptr, nullptr, nullptr, dS.x32);
+                                   c->d_scratch + 17, nullptr, x0, nullptr, nullptr, nullptr, dS.x32, x8);
             } else if (rx) {
                 const uint64_t* xs = carry ? dS.x : nullptr;
                 if (carry)
                     hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
                                        c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
-                                       c->d_scratch + 17, xs, x0, x1, dR.x32, xr);
+                                       c->d_scratch + 17, xs, x0, x1, dR.x32, xr, nullptr, x8);
                 else
                     hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, false, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
                                        c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
-                                       c->d_scratch + 17, nullptr, nullptr, nullptr, dR.x32, xr);
+                                       c->d_scratch + 17, nullptr, nullptr, nullptr, dR.x32, xr, nullptr, x8);
             } else if (hj_chain_on()) {
                 if (carry && dR.L <= 12)
                     hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream,
                                        dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17,
-                                       dS.x, x0, x1);
+                                       dS.x, x0, x1, nullptr, nullptr, nullptr, x8);
                 else if (carry)
                     hipLaunchKernelGGL((tl_hjoin_chain_kernel<HJ_DBITS, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
                                        c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
-                                       c->d_scratch + 17, dS.x, x0, x1);
+                                       c->d_scratch + 17, dS.x, x0, x1, nullptr, nullptr, nullptr, x8);
                 else if (dR.L <= 12)
                     hipLaunchKernelGGL(tl_hjoin_chain_kernel<12>, dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream, dR.words,
-                                       dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17);
+                                       dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17, nullptr,
+                                       nullptr, nullptr, nullptr, nullptr, nullptr, x8);
                 else
                     hipLaunchKernelGGL(tl_hjoin_chain_kernel<HJ_DBITS>, dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream,
-                                       dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17);
+                                       dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17,
+                                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, x8);
             } else if (carry && dR.L <= 12)
                 hipLaunchKernelGGL((tl_hjoin_kernel<12, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream, dR.words,
                                    dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17, dS.x, x0, x1);
@@ -3120,9 +3346,23 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
                                    dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17);
             QE_HIP(hipGetLastError());
         }
-        uint64_t h[2];
-        read_words(c, c->d_scratch + 17, h, 2);   // the ONE round trip of the join
-        const uint64_t P = h[0];
+        if (x8) {
+            hipLaunchKernelGGL(hj8_collect_kernel, dim3(1), dim3(64), 0, c->stream, x8, c->d_scratch + 19);
+            QE_HIP(hipGetLastError());
+        }
+        uint64_t h[10];
+        read_words(c, c->d_scratch + 17, h, x8 ? 10 : 2);   // the ONE round trip of the join
+        uint64_t P = h[0];
+        bool fits = P <= cap;
+        if (x8) {   // the streams' totals; each must fit its whole chunks of the buffers
+            const uint64_t cx = ((cap >> HJ8_CHB) / 8) << HJ8_CHB;
+            P = 0;
+            fits = true;
+            for (int x = 0; x < 8; x++) {
+                P += h[2 + x];
+                fits = fits && h[2 + x] <= cx;
+            }
+        }
         if (h[1]) {   // a bucket beyond LDS (skew): the sides complete their sorts, the merge joins them
             dfree(c, oR);
             dfree(c, oS);
@@ -3131,7 +3371,18 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
             dfree(c, xr);
             return false;
         }
-        if (P <= cap) {
+        if (fits && x8) {   // close the streams' ragged ends (no order among the plan's pairs)
+            HJ8Ops ops;
+            int nops = 0;
+            if (!hj8_plan(h + 2, P, &ops, &nops)) {
+                fits = false;   // (heavy skew between the streams: the one-counter re-run below)
+            } else if (nops) {
+                Timed t(c, "bucket_join", 0.0);
+                hipLaunchKernelGGL(hj8_fixup_kernel, dim3(nops), dim3(256), 0, c->stream, ops, oR, oS, x0, x1, xr);
+                QE_HIP(hipGetLastError());
+            }
+        }
+        if (fits) {
             // the pairs (4 + 4 B) and every carried output column (4 B each) written per pair
             add_bytes(c, "bucket_join", (8.0 + (carry ? 4.0 : 0.0) + (outX1 ? 4.0 : 0.0) + (rx ? 4.0 : 0.0)) * (double)P);
             if (P > c->mat_limit) {   // the reference's DArray cannot hold it either (src/DArray.h:14-15)
@@ -3164,7 +3415,9 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
         dfree(c, x0);
         dfree(c, x1);
         dfree(c, xr);
-        cap = P;
+        if (x8m) cap = std::max(P, cap);   // (a stream outgrew its share: the one counter, no larger buffers)
+        else cap = P;
+        x8m = false;
     }
     throw Error(QE_EINVAL, "internal: bucket join outgrew its exact size");
 }
@@ -3218,21 +3471,21 @@ tl_hjoin_sums_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict
         uint32_t xl[XK ? HJ_I : 1], xh[XK == 2 ? HJ_I : 1];   // S's payload halves
 #pragma unroll
         for (int j = 0; j < HJ_I; j++) {
-            fr[j] = buf_load_u32(rR, oR, (uint32_t)j * HJ_NT * rstride);
-            const uint2 ws = buf_load_u2(rS, o8, (uint32_t)j * HJ_NT * 8u);
+            fr[j] = buf_load_u32_sl(rR, oR, (uint32_t)j * HJ_NT * rstride);
+            const uint2 ws = buf_load_u2_sl(rS, o8, (uint32_t)j * HJ_NT * 8u);
             fs[j] = ws.y;
             sl[j] = ws.x;
         }
         if constexpr (XK == 1) {
             const auto rX = buf_rsrc(xS32 + s0, mS * 4u);
 #pragma unroll
-            for (int j = 0; j < HJ_I; j++) xl[j] = buf_load_u32(rX, o4, (uint32_t)j * HJ_NT * 4u);
+            for (int j = 0; j < HJ_I; j++) xl[j] = buf_load_u32_sl(rX, o4, (uint32_t)j * HJ_NT * 4u);
         }
         if constexpr (XK == 2) {
             const auto rX = buf_rsrc(xS + s0, mS * 8u);
 #pragma unroll
             for (int j = 0; j < HJ_I; j++) {
-                const uint2 x = buf_load_u2(rX, o8, (uint32_t)j * HJ_NT * 8u);
+                const uint2 x = buf_load_u2_sl(rX, o8, (uint32_t)j * HJ_NT * 8u);
                 xl[j] = x.x;
                 xh[j] = x.y;
             }

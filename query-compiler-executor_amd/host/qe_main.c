@@ -152,6 +152,11 @@ static int run_rank(const input_t* in, int rank, int world, int* to_peers, int f
         return EXIT_FAILURE;
     }
     if (load_relations(c, in) != 0) return EXIT_FAILURE;
+    /* this rank's hash buckets of the base columns (load-time layout, include/qe.h) */
+    if (qe_partition_columns(c, (uint32_t)world, (uint32_t)rank) != 0) {
+        fprintf(stderr, "[ERROR] rank %d: %s\n", rank, qe_last_error(c));
+        return EXIT_FAILURE;
+    }
     qe_comm* m = NULL;
     if (qe_comm_init(c, world, rank, id, &m) != 0) {
         fprintf(stderr, "[ERROR] rank %d: %s\n", rank, qe_last_error(c));

@@ -118,6 +118,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "qe_counts_to_host": (I, [P, C.c_void_p, U64, VP]),
         "qe_mem_stats": (I, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "qe_load_stats": (I, [P, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+        "qe_partition_columns": (I, [P, C.c_uint32, C.c_uint32]),
         "qe_mem_trim": (I, [P]),
         "qe_set_profiling": (I, [P, I]),
         "qe_set_profiling_only": (I, [P, C.c_char_p]),
@@ -498,6 +499,11 @@ class Ctx:
         self._chk(self.lib.qe_bucket_select(self.h, col, nparts, part, h.ctypes.data if h.size else None, h.size,
                                             C.byref(p)))
         return p
+
+    def partition_columns(self, nparts: int, part: int):
+        """keep this rank's hash bucket of every loaded base column (qe_partition_columns: load-time
+        layout for the partitioned plan at nparts ranks; counted in load_stats)"""
+        self._chk(self.lib.qe_partition_columns(self.h, nparts, part))
 
     def heavy_stats(self, keys: Col, start: int, end: int, heavy, vals: Col | None = None, weights=None):
         """-> (counts per heavy key over rows [start, end), weighted value sum mod 2^64 or None)"""

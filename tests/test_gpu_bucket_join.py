@@ -143,17 +143,16 @@ def test_bucket_join_long_chain_in_one_bucket_is_linear(ctx):
     """~3000 equal keys on BOTH sides of one bucket that still fits LDS (9 M pairs from one key):
     the chain join would emit each pair k links down the chain (quadratic: minutes in one
     workgroup); a chain past HJ_CHAIN_MAX flags the bucket and the sorts + merge join take it"""
-    import time
     rng = np.random.default_rng(11)
     n = 3_000_000
     rk = rng.integers(0, 1 << 24, n, dtype=np.uint64)
     sk = rng.integers(0, 1 << 24, n, dtype=np.uint64)
     rk[:3000] = 12345
     sk[:3000] = 12345
-    t0 = time.time()
-    P = _check(ctx, rk, sk, gathered=True, expect=True)
+    # the path taken, not the wall time (ADVICE r4): the bucket join ran, flagged the long chain
+    # and the sorts + merge join took the join (its kernel ran: stage mj_fused)
+    P = _check(ctx, rk, sk, gathered=True, expect=True, stage="mj_fused")
     assert P >= 9_000_000
-    assert time.time() - t0 < 30
 
 
 def test_bucket_join_materialisation_limit(ctx):

@@ -10,6 +10,8 @@ O=$R/gpurun_out
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 A="--workload $W --steps 2 --warmup 1 --no-cpu $PROFILE_EXTRA"
+# C4: a crash under the profiler leaves the fault address, PC and /proc/self/maps here (tools/crashmaps.c)
+[ "$W" = c4 ] && export QE_CRASH_MAPS=$O/${TAG}_crashmaps.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${TAG}_trace -o run -- python3 $R/bench.py $A > $O/${TAG}_trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/${TAG}_fetch -o run -- python3 $R/bench.py $A > $O/${TAG}_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/${TAG}_write -o run -- python3 $R/bench.py $A > $O/${TAG}_write.log 2>&1
