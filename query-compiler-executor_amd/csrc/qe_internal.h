@@ -106,7 +106,6 @@ struct qe_ctx {
     std::multimap<size_t, void*> free_blocks;
     std::unordered_map<void*, size_t> live;
     std::unordered_map<void*, void*> pad_base;   // QE_ALLOC_PAD: offset block -> its hipMalloc base
-    uint64_t* d_hj8 = nullptr;                   // the chain bucket join's eight stream counters (qe_sort.hip)
     // qe_partition_columns: every base column's hash bucket `bparts_p` of `bparts_n`, by column
     std::unordered_map<const uint64_t*, qe_pairs> bparts;
     uint32_t bparts_n = 0, bparts_p = 0;

@@ -605,7 +605,6 @@ void qe_fini(qe_ctx* c) {
     if (c->lb_tickets) (void)hipFree(c->lb_tickets);
     if (c->d_scratch) (void)hipFree(c->d_scratch);
     if (c->d_zhist) (void)hipFree(c->d_zhist);
-    if (c->d_hj8) (void)hipFree(c->d_hj8);
     if (c->h_scratch) (void)hipHostFree(c->h_scratch);
     if (c->h_ret) (void)hipHostFree(c->h_ret);
     if (c->wait_ev) (void)hipEventDestroy(c->wait_ev);

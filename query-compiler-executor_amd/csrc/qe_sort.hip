@@ -273,6 +273,9 @@ static inline uint32_t xcd_grid(uint64_t items) {
 #ifndef QE_PRERANK2   // (build knob: the second pass's PRERANK form alone)
 #define QE_PRERANK2 QE_PRERANK
 #endif
+#ifndef QE_STAGE_FLAT   // (build knob, 0 = round 4's guarded per-element staging in pass 1)
+#define QE_STAGE_FLAT 1
+#endif
 #ifndef QE_P1_EARLY_X   // (build knob: PRERANK's 32-bit payload loads issued with the elements')
 #define QE_P1_EARLY_X 1
 #endif
@@ -526,7 +529,20 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
     }
     __syncthreads();
     QE_SORT_STAMP(tile, 3);
-    // stage the tile in digit order (tile-local offsets only)
+    // stage the tile in digit order (tile-local offsets only).  QE_STAGE_FLAT (round 5): every
+    // slot's offset read issued before the first store, no branch per element (an element past
+    // the tile goes to the spare slot), and unstable ranks read one table, not two (their wave
+    // row is all zeros after the scan); else the round-4 form, one guarded round trip per element
+    if constexpr (QE_STAGE_FLAT) {
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint32_t dd = (uint32_t)(word[j] >> dsh) & mask;
+            const uint32_t b = bexcl[dd] + (UNSTABLE ? 0u : whist[w][dd]);
+            pos[j] = loc_of(j) < tcount ? b + pos[j] : (uint32_t)TILE;
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) stage[pos[j]] = word[j];   // (pos: the slot from here on)
+    } else {
 #pragma unroll
     for (int j = 0; j < ITEMS; j++) {
         if (loc_of(j) < tcount) {
@@ -535,6 +551,7 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
             stage[slot] = word[j];
             if constexpr (CARRY != X_NONE) pos[j] = slot;   // the payload takes the same slot later
         }
+    }
     }
     }   // !PRERANK
     // the payloads load into the words' registers (a 32-bit one into registers of its own), in
@@ -611,7 +628,7 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
         uint32_t* st32 = reinterpret_cast<uint32_t*>(stage);   // (32-bit payloads: 4-B slots)
 #pragma unroll
         for (int j = 0; j < ITEMS; j++)
-            if (loc_of(j) < tcount) {
+            if (QE_STAGE_FLAT || PRERANK || loc_of(j) < tcount) {   // (flat: past the tile, the spare slot)
                 if constexpr (P32) st32[pos[j]] = xw[j];
                 else stage[pos[j]] = word[j];
             }
@@ -1467,7 +1484,8 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
             for (int q = 0; q < TL2_WCH; q++) {
                 const int j = j0 + q;
                 const uint32_t dd = (uint32_t)(word[j] >> dsh) & (BINS - 1);
-                sl[q] = bexcl[dd] + whist[UNSTABLE ? 0 : w][dd] + ((pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
+                // (unstable ranks: the wave row is all zeros after the scan -- one table read)
+                sl[q] = bexcl[dd] + (UNSTABLE ? 0u : whist[w][dd]) + ((pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
             }
 #pragma unroll
             for (int q = 0; q < TL2_WCH; q++) {
@@ -1837,12 +1855,6 @@ constexpr uint32_t HJ_NONE = 0xFFFFu;
 // a chain longer than HJ_CHAIN_MAX is flagged like one beyond LDS, and the join takes the sorts +
 // merge path (linear in the pairs) instead.
 constexpr uint32_t HJ_CHAIN_MAX = 64;
-// XCD-stream output reservation (round 5): the chain join's blocks reserve their
-// pairs on eight counters (HJ8_STRIDE words apart: different channels), stream x = block % 8.  A
-// stream is laid out in chunks of 2^HJ8_CHB pairs: stream x's chunk k is output chunk 8 k + x, so
-// every chunk row below the shortest stream is dense, and hj8_fixup moves the few pairs past P (the
-// streams' ragged ends) into the holes below it -- the plan's pairs need no order.
-constexpr uint32_t HJ8_CHB = 12, HJ8_STRIDE = 544;   // 4096-pair chunks; counters 4352 B apart
 #ifndef QE_HJ_RR_GLOBAL
 #define QE_HJ_RR_GLOBAL 0
 #endif
@@ -1862,7 +1874,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
                       uint64_t cap, uint64_t* total_out, const uint64_t* __restrict__ xS = nullptr,
                       uint32_t* __restrict__ outX0 = nullptr, uint32_t* __restrict__ outX1 = nullptr,
                       const uint32_t* __restrict__ xR = nullptr, uint32_t* __restrict__ outRX = nullptr,
-                      const uint32_t* __restrict__ xS32 = nullptr, uint64_t* __restrict__ x8 = nullptr) {
+                      const uint32_t* __restrict__ xS32 = nullptr) {
     __shared__ uint32_t head[1 << DBITS];   // per key value: the last R row inserted (HJ_NONE: none)
     __shared__ uint16_t nxt[NT * HJ_I];        // per R row: the previous row of its value
 #if QE_HJ_RR_GLOBAL
@@ -1969,24 +1981,15 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
         if (2u * l < E) tab[2 * l] = inc - a0 - a1;
         if (2u * l + 1 < E) tab[2 * l + 1] = inc - a1;
         if (l == 0) {
-            // x8: eight counters, one per XCD stream (block b -> stream b % 8), instead of one word
-            // that every bucket's reservation queues on (~55 returning atomics per us on one address
-            // bounded the kernel: 32 K buckets in ~0.55 ms)
-            uint64_t* ctr = x8 ? x8 + (uint64_t)HJ8_STRIDE * (b & 7u) : total_out;
-            s_excl = total ? atomicAdd(reinterpret_cast<unsigned long long*>(ctr), (unsigned long long)total) : 0ull;
+            s_excl = total ? atomicAdd(reinterpret_cast<unsigned long long*>(total_out), (unsigned long long)total)
+                           : 0ull;
             s_total = total;
         }
     }
     __syncthreads();
     QE_STAMP(g_hj_stamps, b, 4);
     const uint64_t gofs = s_excl;
-    // outgrew the buffers (a stream's whole chunks, or the one run): the host re-runs with the size
-    if (gofs + s_total > (x8 ? (((cap >> HJ8_CHB) / 8) << HJ8_CHB) : cap)) return;
-    const uint32_t xs = x8 ? (b & 7u) : 0u;
-    // stream offset -> output position: stream x's chunk k is the output's chunk 8 k + x (hj8_place)
-    auto place = [&](uint64_t o) -> uint64_t {
-        return x8 ? ((((o >> HJ8_CHB) << 3) | xs) << HJ8_CHB) | (o & ((1u << HJ8_CHB) - 1u)) : o;
-    };
+    if (gofs + s_total > cap) return;   // outgrew the buffers: the host re-runs with the exact size
 #pragma unroll
     for (int j = 0; j < HJ_I; j++) {   // wave-cooperative emission, as tl_hjoin_kernel's
         const uint32_t pj = pre[j], all = tot[j];
@@ -2011,13 +2014,12 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
             }
             if (q < all) {
                 for (uint32_t s = 0; s < k; s++) p = nxt[p];   // the k-th partner on the chain
-                const uint64_t o = place(ob + q);
-                outR[o] = QE_HJ_RR_GLOBAL ? (uint32_t)wR[r0 + p] : rr[p];
-                outS[o] = sr;
-                if constexpr (RX) outRX[o] = rx[p];
+                outR[ob + q] = QE_HJ_RR_GLOBAL ? (uint32_t)wR[r0 + p] : rr[p];
+                outS[ob + q] = sr;
+                if constexpr (RX) outRX[ob + q] = rx[p];
                 if constexpr (CARRY) {
-                    outX0[o] = x0;
-                    if (!S32 && outX1) outX1[o] = x1;
+                    outX0[ob + q] = x0;
+                    if (!S32 && outX1) outX1[ob + q] = x1;
                 }
             }
         }
@@ -3190,76 +3192,6 @@ bool carry_eligible(const qe_pairs* R, const qe_pairs* S, bool rpay) {
     return loR == loS && nbR == nbS && kcR == kcS && nbR - TL_H <= HJ_DBITS;
 }
 
-// XCD-stream mode of the chain join (see HJ8_CHB): on by default, QE_HJ8=0 keeps the one counter
-static bool hj8_on() {
-    static const bool on = !(getenv("QE_HJ8") && getenv("QE_HJ8")[0] == '0');
-    return on;
-}
-// before a join: the [pairs, oversize] words and the eight stream counters zeroed (one launch)
-static __global__ void __launch_bounds__(64) hj8_zero_kernel(uint64_t* w2, uint64_t* x8) {
-    if (threadIdx.x < 2) w2[threadIdx.x] = 0;
-    if (x8 && threadIdx.x < 8) x8[(uint64_t)HJ8_STRIDE * threadIdx.x] = 0;
-}
-// after it: the eight stream totals next to the oversize flag, so one read brings all of them
-static __global__ void __launch_bounds__(64) hj8_collect_kernel(const uint64_t* x8, uint64_t* dst) {
-    if (threadIdx.x < 8) dst[threadIdx.x] = x8[(uint64_t)HJ8_STRIDE * threadIdx.x];
-}
-// the streams' ragged ends: op k copies len pairs (and every carried column) from src to dst
-constexpr int HJ8_MAXOPS = 160;
-struct HJ8Ops {
-    uint64_t src[HJ8_MAXOPS], dst[HJ8_MAXOPS];
-    uint32_t len[HJ8_MAXOPS];
-};
-static __global__ void __launch_bounds__(256) hj8_fixup_kernel(HJ8Ops ops, uint32_t* a0, uint32_t* a1, uint32_t* a2,
-                                                              uint32_t* a3, uint32_t* a4) {
-    const uint64_t s = ops.src[blockIdx.x], d = ops.dst[blockIdx.x];
-    const uint32_t len = ops.len[blockIdx.x];
-    for (uint32_t i = threadIdx.x; i < len; i += 256) {   // src >= P > dst: no op reads what another writes
-        a0[d + i] = a0[s + i];
-        a1[d + i] = a1[s + i];
-        if (a2) a2[d + i] = a2[s + i];
-        if (a3) a3[d + i] = a3[s + i];
-        if (a4) a4[d + i] = a4[s + i];
-    }
-}
-// The copies that make [0, P) dense from the streams' totals Px[8] (stream x's pairs fill output
-// chunks 8 k + x, k = 0, 1, ...): the filled positions at or past P go, in order, into the holes
-// below P.  Returns false when more than HJ8_MAXOPS copies would be needed (heavy skew).
-static bool hj8_plan(const uint64_t* Px, uint64_t P, HJ8Ops* ops, int* nops) {
-    const uint64_t CH = 1ull << HJ8_CHB;
-    uint64_t kmin = ~0ull, kmax = 0;
-    for (int x = 0; x < 8; x++) {
-        kmin = std::min(kmin, Px[x] / CH);
-        kmax = std::max(kmax, (Px[x] + CH - 1) / CH);
-    }
-    std::vector<std::pair<uint64_t, uint64_t>> holes, srcs;   // [a, b) in position order
-    for (uint64_t k = kmin; k < kmax; k++)
-        for (int x = 0; x < 8; x++) {
-            const uint64_t base = (8 * k + (uint64_t)x) * CH;
-            const uint64_t f = Px[x] > k * CH ? std::min(CH, Px[x] - k * CH) : 0;
-            const uint64_t fa = base, fb = base + f, ea = base + f, eb = base + CH;
-            if (fb > std::max(fa, P)) srcs.push_back({std::max(fa, P), fb});
-            if (std::min(eb, P) > ea) holes.push_back({ea, std::min(eb, P)});
-        }
-    *nops = 0;
-    size_t hi = 0, si = 0;
-    uint64_t ho = 0, so = 0;   // consumed within the current hole / source
-    while (hi < holes.size() && si < srcs.size()) {
-        const uint64_t hl = holes[hi].second - holes[hi].first - ho, sl = srcs[si].second - srcs[si].first - so;
-        const uint64_t len = std::min(hl, sl);
-        if (*nops == HJ8_MAXOPS || len > 0xFFFFFFFFull) return false;
-        ops->src[*nops] = srcs[si].first + so;
-        ops->dst[*nops] = holes[hi].first + ho;
-        ops->len[*nops] = (uint32_t)len;
-        (*nops)++;
-        ho += len;
-        so += len;
-        if (ho == holes[hi].second - holes[hi].first) hi++, ho = 0;
-        if (so == srcs[si].second - srcs[si].first) si++, so = 0;
-    }
-    return hi == holes.size() && si == srcs.size();   // (every hole filled by exactly the pairs past P)
-}
-
 bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR, qe_list* outS, qe_list* outX0,
                  qe_list* outX1, qe_list* outRX) {
     auto iR = c->deferred.find(R->key), iS = c->deferred.find(S->key);
@@ -3277,20 +3209,13 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
     if (rx && (!dR.x32 || !hj_chain_on() || dR.L > 12)) return false;
     const uint64_t nR = R->n, nS = S->n;
     uint64_t cap = nR + nS;   // optimistic (fan-out ~1); an outgrown launch re-runs with the exact size
-    // the XCD streams (chain kernel only; the re-run of an outgrown launch takes the one counter)
-    bool x8m = hj_chain_on() && hj8_on();
-    if (x8m && !c->d_hj8) {
-        QE_HIP(hipMalloc(&c->d_hj8, (size_t)HJ8_STRIDE * 8 * sizeof(uint64_t)));
-        QE_HIP(hipMemsetAsync(c->d_hj8, 0, (size_t)HJ8_STRIDE * 8 * sizeof(uint64_t), c->stream));
-    }
     for (int attempt = 0; attempt < 2; attempt++) {
-        uint64_t* x8 = x8m ? c->d_hj8 : nullptr;
         uint32_t* oR = dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1));
         uint32_t* oS = dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1));
         uint32_t* x0 = carry ? dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1)) : nullptr;
         uint32_t* x1 = carry && outX1 ? dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1)) : nullptr;
         uint32_t* xr = rx ? dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1)) : nullptr;
-        hipLaunchKernelGGL(hj8_zero_kernel, dim3(1), dim3(64), 0, c->stream, c->d_scratch + 17, x8);   // [pairs, oversize] (+ streams)
+        hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(64), 0, c->stream, c->d_scratch + 17, 2);   // [pairs, oversize]
         QE_HIP(hipGetLastError());
         {
             // algorithmic bytes: both sides' words in (+ 8 B per pair below; + the payloads)
@@ -3299,38 +3224,36 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
             if (s32 && rx) {
                 hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, true, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
                                    c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
-                                   c->d_scratch + 17, nullptr, x0, nullptr, dR.x32, xr, dS.x32, x8);
+                                   c->d_scratch + 17, nullptr, x0, nullptr, dR.x32, xr, dS.x32);
             } else if (s32) {
                 hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, false, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
                                    c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
-                                   c->d_scratch + 17, nullptr, x0, nullptr, nullptr, nullptr, dS.x32, x8);
+                                   c->d_scratch + 17, nullptr, x0, nullptr, nullptr, nullptr, dS.x32);
             } else if (rx) {
                 const uint64_t* xs = carry ? dS.x : nullptr;
                 if (carry)
                     hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
                                        c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
-                                       c->d_scratch + 17, xs, x0, x1, dR.x32, xr, nullptr, x8);
+                                       c->d_scratch + 17, xs, x0, x1, dR.x32, xr);
                 else
                     hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, false, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
                                        c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
-                                       c->d_scratch + 17, nullptr, nullptr, nullptr, dR.x32, xr, nullptr, x8);
+                                       c->d_scratch + 17, nullptr, nullptr, nullptr, dR.x32, xr);
             } else if (hj_chain_on()) {
                 if (carry && dR.L <= 12)
                     hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream,
                                        dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17,
-                                       dS.x, x0, x1, nullptr, nullptr, nullptr, x8);
+                                       dS.x, x0, x1);
                 else if (carry)
                     hipLaunchKernelGGL((tl_hjoin_chain_kernel<HJ_DBITS, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
                                        c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
-                                       c->d_scratch + 17, dS.x, x0, x1, nullptr, nullptr, nullptr, x8);
+                                       c->d_scratch + 17, dS.x, x0, x1);
                 else if (dR.L <= 12)
                     hipLaunchKernelGGL(tl_hjoin_chain_kernel<12>, dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream, dR.words,
-                                       dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17, nullptr,
-                                       nullptr, nullptr, nullptr, nullptr, nullptr, x8);
+                                       dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17);
                 else
                     hipLaunchKernelGGL(tl_hjoin_chain_kernel<HJ_DBITS>, dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream,
-                                       dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17,
-                                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, x8);
+                                       dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17);
             } else if (carry && dR.L <= 12)
                 hipLaunchKernelGGL((tl_hjoin_kernel<12, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream, dR.words,
                                    dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17, dS.x, x0, x1);
@@ -3346,23 +3269,9 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
                                    dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17);
             QE_HIP(hipGetLastError());
         }
-        if (x8) {
-            hipLaunchKernelGGL(hj8_collect_kernel, dim3(1), dim3(64), 0, c->stream, x8, c->d_scratch + 19);
-            QE_HIP(hipGetLastError());
-        }
-        uint64_t h[10];
-        read_words(c, c->d_scratch + 17, h, x8 ? 10 : 2);   // the ONE round trip of the join
-        uint64_t P = h[0];
-        bool fits = P <= cap;
-        if (x8) {   // the streams' totals; each must fit its whole chunks of the buffers
-            const uint64_t cx = ((cap >> HJ8_CHB) / 8) << HJ8_CHB;
-            P = 0;
-            fits = true;
-            for (int x = 0; x < 8; x++) {
-                P += h[2 + x];
-                fits = fits && h[2 + x] <= cx;
-            }
-        }
+        uint64_t h[2];
+        read_words(c, c->d_scratch + 17, h, 2);   // the ONE round trip of the join
+        const uint64_t P = h[0];
         if (h[1]) {   // a bucket beyond LDS (skew): the sides complete their sorts, the merge joins them
             dfree(c, oR);
             dfree(c, oS);
@@ -3371,18 +3280,7 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
             dfree(c, xr);
             return false;
         }
-        if (fits && x8) {   // close the streams' ragged ends (no order among the plan's pairs)
-            HJ8Ops ops;
-            int nops = 0;
-            if (!hj8_plan(h + 2, P, &ops, &nops)) {
-                fits = false;   // (heavy skew between the streams: the one-counter re-run below)
-            } else if (nops) {
-                Timed t(c, "bucket_join", 0.0);
-                hipLaunchKernelGGL(hj8_fixup_kernel, dim3(nops), dim3(256), 0, c->stream, ops, oR, oS, x0, x1, xr);
-                QE_HIP(hipGetLastError());
-            }
-        }
-        if (fits) {
+        if (P <= cap) {
             // the pairs (4 + 4 B) and every carried output column (4 B each) written per pair
             add_bytes(c, "bucket_join", (8.0 + (carry ? 4.0 : 0.0) + (outX1 ? 4.0 : 0.0) + (rx ? 4.0 : 0.0)) * (double)P);
             if (P > c->mat_limit) {   // the reference's DArray cannot hold it either (src/DArray.h:14-15)
@@ -3415,9 +3313,7 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
         dfree(c, x0);
         dfree(c, x1);
         dfree(c, xr);
-        if (x8m) cap = std::max(P, cap);   // (a stream outgrew its share: the one counter, no larger buffers)
-        else cap = P;
-        x8m = false;
+        cap = P;
     }
     throw Error(QE_EINVAL, "internal: bucket join outgrew its exact size");
 }
