@@ -261,23 +261,11 @@ static inline uint32_t xcd_grid(uint64_t items) {
 // match-any -- equal digits keep no order.  For the partitioned plan's deferred sorts (their
 // consumer, bucket_join, needs the buckets, not an order inside them) and the first LSD pass of
 // the aggregate join's sorts (no earlier order to keep, none needed among equal keys).
-// PRERANK (PRE + UNSTABLE, round 5): the tile's digit counts are known before the pass -- the
-// difference of two rows of the scanned tile-count matrix (the next tile's offsets, or the next
-// digit's column start) -- so the tile-local digit starts are scanned while the element loads are
-// in flight, and ONE LDS atomic per element returns its stage slot directly: no barrier + scan
-// after ranking, no per-element reads of the digit start and wave offset when staging.
-// (QE_PRERANK=0: build knob, the round-4 rank -> scan -> stage order.)
-#ifndef QE_PRERANK
-#define QE_PRERANK 0   // (default off: measured slower in round 5, see HISTORY.md)
-#endif
-#ifndef QE_PRERANK2   // (build knob: the second pass's PRERANK form alone)
-#define QE_PRERANK2 QE_PRERANK
+#ifndef QE_P1_EARLY
+#define QE_P1_EARLY 1
 #endif
 #ifndef QE_STAGE_FLAT   // (build knob, 0 = round 4's guarded per-element staging in pass 1)
 #define QE_STAGE_FLAT 1
-#endif
-#ifndef QE_P1_EARLY_X   // (build knob: PRERANK's 32-bit payload loads issued with the elements')
-#define QE_P1_EARLY_X 1
 #endif
 enum { X_NONE = 0, X64 = 1, X32 = 2, XCOL = 3 };
 template <typename K, int IN, int OUT, bool PACK, int RBITS, int ITEMS, int NT, bool PRE = false, int CARRY = X_NONE,
@@ -299,8 +287,8 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
     // per-wave digit counts -> exclusive over waves; UNSTABLE ranks on ONE block-wide row (no order
     // to keep between waves), which leaves a 1024-thread tile in 2 workgroups' LDS per CU
     constexpr int NWH = UNSTABLE ? 1 : NW;
-    __shared__ uint64_t stage[TILE + 1];     // (+1: PRERANK's spare slot)
-    __shared__ uint32_t whist[NWH][BINS + 1];
+    __shared__ uint64_t stage[TILE + 1];     // (+1: the flat staging's spare slot)
+    __shared__ uint32_t whist[NWH][BINS];
     __shared__ uint32_t bexcl[BINS];        // tile-local exclusive offset of each digit
     __shared__ uint32_t gofs[BINS];         // global position of the digit's run - bexcl
     __shared__ uint32_t wsum[NW];
@@ -323,17 +311,11 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
 #pragma unroll
         for (int q = 0; q < DPT; q++) pre_off[q] = owner ? offs[(uint64_t)tile * BINS + threadIdx.x * DPT + q] : 0u;
     }
-    constexpr bool PRERANK = PRE && UNSTABLE && DPT == 1 && QE_PRERANK;
-    uint32_t nxt_off = 0;   // PRERANK: where this tile's run of the digit ends (its count = nxt_off - pre_off)
-    if constexpr (PRERANK) {
-        const uint32_t ntl = (uint32_t)((n + TILE - 1) / TILE), d = threadIdx.x;
-        // one unconditional load: the next tile's row, or for the last tile the next column's start
-        // (row 0); the last tile's last digit ends at n
-        const bool last = tile + 1 >= ntl;
-        const uint32_t v = offs[last ? (d < (uint32_t)BINS - 1 ? d + 1 : 0u) : (tile + 1) * (uint32_t)BINS + (d < (uint32_t)BINS ? d : 0u)];
-        nxt_off = last && d == (uint32_t)BINS - 1 ? (uint32_t)n : v;
-    } else {
-        for (int i = threadIdx.x; i < NWH * (BINS + 1); i += NT) (&whist[0][0])[i] = 0;
+    // the rank counters are zeroed AFTER the element loads are issued (below, for PRE tiles): a
+    // barrier first would hold every wave's loads until the block's last wave has launched
+    // (QE_P1_EARLY=0: build knob, round 4's zero -> barrier -> loads)
+    if constexpr (!PRE || !QE_P1_EARLY) {
+        for (int i = threadIdx.x; i < NWH * BINS; i += NT) (&whist[0][0])[i] = 0;
         __syncthreads();
     }
     QE_SORT_STAMP(tile, 1);
@@ -435,40 +417,13 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
             }
         }
     };
-    if constexpr (PRERANK && P32 && QE_P1_EARLY_X) load_payloads();
-    if constexpr (PRERANK) {
-        // the tile-local digit starts (scanned while the loads are in flight), then rank + stage
-        const uint32_t cnt = owner ? nxt_off - pre_off[0] : 0u;
-        const uint32_t inc = wave_incl_scan_u32(cnt);
-        if (l == 63) wsum[w] = inc;
+    if constexpr (PRE && QE_P1_EARLY) {   // (the loads above are in flight across this barrier)
+        for (int i = threadIdx.x; i < NWH * BINS; i += NT) (&whist[0][0])[i] = 0;
         __syncthreads();
-        if (owner) {
-            uint32_t ex = inc - cnt;
-            for (int ww = 0; ww < w; ww++) ex += wsum[ww];
-            whist[0][threadIdx.x] = ex;            // the digit's next free stage slot
-            gofs[threadIdx.x] = pre_off[0] - ex;   // global position of the digit's run - its tile-local start
-        }
-        __syncthreads();
-        QE_SORT_STAMP(tile, 2);
-        // branch-free: an element past the tile counts on a spare counter and lands in a spare slot
-        // (partial tiles only), so every atomic of the thread is in flight before the first store
-        uint32_t sl[ITEMS];
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const bool ok = loc_of(j) < tcount;
-            sl[j] = atomicAdd(&whist[0][ok ? (uint32_t)(word[j] >> dsh) & mask : (uint32_t)BINS], 1u);
-            sl[j] = ok ? sl[j] : (uint32_t)TILE;
-        }
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            stage[sl[j]] = word[j];
-            if constexpr (CARRY != X_NONE) pos[j] = sl[j];   // the payload takes the same slot later
-        }
-        QE_SORT_STAMP(tile, 3);
     }
     // stable rank inside the wave: element order is (j, lane)
 #pragma unroll
-    for (int j = 0; j < (PRERANK ? 0 : ITEMS); j++) {
+    for (int j = 0; j < ITEMS; j++) {
         const bool ok = loc_of(j) < tcount;
         uint32_t d = (uint32_t)(word[j] >> dsh) & mask;
         if constexpr (UNSTABLE) {
@@ -497,7 +452,6 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
 #endif
     }
     uint32_t tot[DPT], tsum = 0;
-    if constexpr (!PRERANK) {
     __syncthreads();
     QE_SORT_STAMP(tile, 2);
     // thread t owns digits t*DPT .. t*DPT+DPT-1: totals, exclusive over waves, publish aggregate
@@ -553,17 +507,15 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
         }
     }
     }
-    }   // !PRERANK
     // the payloads load into the words' registers (a 32-bit one into registers of its own), in
-    // flight during the write-out (PRERANK, 32-bit payloads: issued with the elements' loads, so
-    // the tile's whole read is in flight at once)
-    if constexpr (!(PRERANK && P32 && QE_P1_EARLY_X)) load_payloads();
+    // flight during the write-out
+    load_payloads();
 #pragma unroll
     for (int q = 0; q < DPT; q++) {
         const uint32_t d = threadIdx.x * DPT + q;
         if (!owner) continue;
         if constexpr (PRE) {
-            if constexpr (!PRERANK) gofs[d] = pre_off[q] - bexcl[d];   // (PRERANK: set before ranking)
+            gofs[d] = pre_off[q] - bexcl[d];
             continue;
         }
         // the predecessors' counts: by this time most have published their inclusive prefix
@@ -628,7 +580,7 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
         uint32_t* st32 = reinterpret_cast<uint32_t*>(stage);   // (32-bit payloads: 4-B slots)
 #pragma unroll
         for (int j = 0; j < ITEMS; j++)
-            if (QE_STAGE_FLAT || PRERANK || loc_of(j) < tcount) {   // (flat: past the tile, the spare slot)
+            if (QE_STAGE_FLAT || loc_of(j) < tcount) {   // (flat: past the tile, the spare slot)
                 if constexpr (P32) st32[pos[j]] = xw[j];
                 else stage[pos[j]] = word[j];
             }
@@ -1325,9 +1277,8 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
                                                          uint64_t* __restrict__ xout = nullptr) {
     constexpr int BINS = 128, NW = TL2_NT / 64, WT = 64 * TL2_ITEMS;
     constexpr int NWH = UNSTABLE ? 1 : NW;   // unstable ranks: one block-wide counter row
-    constexpr int SP = UNSTABLE ? 1 : 0;   // the PRERANK spare slot / counter (unstable ranks only)
-    __shared__ uint64_t stage[TL2_TILE + SP];
-    __shared__ uint32_t whist[NWH][BINS + SP];
+    __shared__ uint64_t stage[TL2_TILE];
+    __shared__ uint32_t whist[NWH][BINS];
     __shared__ uint32_t bexcl[BINS];
     __shared__ uint32_t gofs[BINS];
     __shared__ uint32_t wsum[NW];
@@ -1344,27 +1295,13 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
     const uint64_t lt = lanemask_lt();
     const uint32_t d = threadIdx.x;   // threads 0..127 own one digit each
     uint32_t run = 0;
-    const uint32_t dcl = d < BINS ? d : BINS - 1;
-    const uint32_t* runp = off2 + (uint64_t)s * BINS + dcl;
-    // PRERANK (unstable ranks, a segment that fits one sub-tile -- nearly all of them): the segment's
-    // digit counts are the difference of two rows of the scanned segment-count matrix, so the
-    // digit starts are scanned while the words load and one LDS atomic per word returns its slot
-    // (see radix_pass_kernel's PRERANK)
-    const bool one = UNSTABLE && QE_PRERANK2 && end - start <= (uint32_t)TL2_TILE;   // (block-uniform)
+    const uint32_t* runp = off2 + (uint64_t)s * BINS + (d < BINS ? d : BINS - 1);
     for (uint32_t base = start; base < end; base += TL2_TILE) {   // block-uniform
         const uint32_t m = end - base < (uint32_t)TL2_TILE ? end - base : (uint32_t)TL2_TILE;
-        if (!one)
-            for (int i = threadIdx.x; i < NWH * (BINS + SP); i += TL2_NT) (&whist[0][0])[i] = 0;
+        for (int i = threadIdx.x; i < NWH * BINS; i += TL2_NT) (&whist[0][0])[i] = 0;
         uint64_t word[TL2_ITEMS];
         uint32_t pos2[(TL2_ITEMS + 1) / 2];   // ranks < TL2_TILE: two u16 per register
         const int lim = (int)m - (int)((uint32_t)w * WT + l);   // element j valid iff j * 64 < lim
-        uint32_t nrun = 0;   // (one) where the segment's run of the digit ends
-        if (one) {   // issued before the words: their wait is a counted one
-            run = *runp;
-            const bool last = s + 1 >= 256u * G;   // (the last segment: the next column's start, or n)
-            const uint32_t v = off2[last ? (dcl + 1 < (uint32_t)BINS ? dcl + 1 : 0u) : (s + 1) * (uint32_t)BINS + dcl];
-            nrun = v;   // (the select against n happens at the scan, behind the words' loads)
-        }
         // every load unconditional, all 18 in flight at once, through a buffer descriptor over the
         // sub-tile: one 32-bit lane offset + a constant per element (18 64-bit clamped addresses
         // held 36 VGPRs and made the kernel spill; the stride in soffset: no VGPR per element).
@@ -1382,45 +1319,6 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
                 }
             }
         }
-        if (one) {
-            const uint32_t ne = s + 1 >= 256u * G && dcl == (uint32_t)BINS - 1 ? (uint32_t)n : nrun;
-            const uint32_t cnt = d < BINS ? ne - run : 0u;
-            const uint32_t inc = wave_incl_scan_u32(cnt);
-            if (l == 63) wsum[w] = inc;
-            __syncthreads();
-            if (d < BINS) {
-                uint32_t ex = inc - cnt;
-                for (int ww = 0; ww < w; ww++) ex += wsum[ww];
-                whist[0][d] = ex;       // the digit's next free stage slot
-                gofs[d] = run - ex;     // global position of the digit's run - its sub-tile start
-            }
-            __syncthreads();
-            QE_SORT_STAMP(s, 1);
-            // in chunks of TL2_WCH (a chunk's atomics in flight together, registers within budget);
-            // branch-free: a word past the segment counts on the spare counter, lands in the spare slot
-#pragma unroll
-            for (int j0 = 0; j0 < TL2_ITEMS; j0 += TL2_WCH) {
-                uint32_t sl[TL2_WCH];
-#pragma unroll
-                for (int q = 0; q < TL2_WCH; q++) {
-                    const int j = j0 + q;
-                    const bool ok = j * 64 < lim;
-                    sl[q] = atomicAdd(&whist[0][ok ? (uint32_t)(word[j] >> dsh) & (BINS - 1) : (uint32_t)BINS], 1u);
-                    sl[q] = ok ? sl[q] : (uint32_t)TL2_TILE;
-                }
-#pragma unroll
-                for (int q = 0; q < TL2_WCH; q++) {
-                    const int j = j0 + q;
-                    stage[sl[q]] = word[j];
-                    if constexpr (CARRY != X_NONE) {   // pos2 holds the slot (<= TL2_TILE: 16 bits)
-                        if (j & 1) pos2[j >> 1] |= sl[q] << 16;
-                        else pos2[j >> 1] = sl[q];
-                    }
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            QE_SORT_STAMP(s, 3);
-        } else {
         if (base == start) run = *runp;   // the digit offsets, behind the words (clamped: no branch)
         __syncthreads();   // whist zeroed
         if (base == start) QE_SORT_STAMP(s, 1);
@@ -1498,7 +1396,6 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
             }
             __builtin_amdgcn_sched_barrier(0);
         }
-        }   // !one
         // the payloads load into the words' registers (a 32-bit one into registers of its own),
         // in flight during the write-out
         uint32_t xw[CARRY == X32 ? TL2_ITEMS : 1];
@@ -1524,7 +1421,11 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
                 const uint32_t i = (uint32_t)k * TL2_NT + threadIdx.x;
                 const uint64_t wd = stage[i];   // (a slot past m: a stale word, not stored)
                 const uint32_t dd = i < m ? (uint32_t)(wd >> dsh) & (BINS - 1) : 0u;
+#ifdef QE_DIAG_SORT_LINEAR
+                const uint32_t p = base + i;
+#else
                 const uint32_t p = gofs[dd] + i;
+#endif
                 QE_STS(i < m && (uint64_t)p < n, &wout[p], &g_store_sink[l], wd);
                 if (k & 3) dg[k >> 2] |= dd << (8 * (k & 3));
                 else dg[k >> 2] = dd;
@@ -1555,7 +1456,11 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
                 for (int q = 0; q < TL2_WCH; q++) wd[q] = stage[(uint32_t)(k0 + q) * TL2_NT + threadIdx.x];
 #pragma unroll
                 for (int q = 0; q < TL2_WCH; q++)
+#ifdef QE_DIAG_SORT_LINEAR   // ablation only: contiguous output instead of the digit scatter
+                    p[q] = base + (uint32_t)(k0 + q) * TL2_NT + threadIdx.x;
+#else
                     p[q] = gofs[(uint32_t)(wd[q] >> dsh) & (BINS - 1)] + (uint32_t)(k0 + q) * TL2_NT + threadIdx.x;
+#endif
 #pragma unroll
                 for (int q = 0; q < TL2_WCH; q++) {
                     const uint32_t i = (uint32_t)(k0 + q) * TL2_NT + threadIdx.x;
@@ -1604,7 +1509,11 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
                 for (int q = 0; q < TL2_WCH; q++) wd[q] = stage[(uint32_t)(k0 + q) * TL2_NT + threadIdx.x];
 #pragma unroll
                 for (int q = 0; q < TL2_WCH; q++)
+#ifdef QE_DIAG_SORT_LINEAR   // ablation only: contiguous output instead of the digit scatter
+                    p[q] = base + (uint32_t)(k0 + q) * TL2_NT + threadIdx.x;
+#else
                     p[q] = gofs[(uint32_t)(wd[q] >> dsh) & (BINS - 1)] + (uint32_t)(k0 + q) * TL2_NT + threadIdx.x;
+#endif
 #pragma unroll
                 for (int q = 0; q < TL2_WCH; q++) {
                     const uint32_t i = (uint32_t)(k0 + q) * TL2_NT + threadIdx.x;

@@ -1,6 +1,13 @@
 set -o pipefail
 mkdir -p gpurun_out
-export QE_LIB_PATH=$PWD/query-compiler-executor_amd/build/ab/libqe_STAMPS.so
-timeout -k 10 600 bash tools/stamps_c3.sh r05d || exit 1
-QE_LIB_PATH=$PWD/query-compiler-executor_amd/build/ab/libqe_STAMPS.so timeout -k 10 120 python tools/stamps.py --what hj > gpurun_out/r05d_hj_stamps.log 2>&1 || exit 1
+AB=$PWD/query-compiler-executor_amd/build/ab
+( for lib in STAMPS STAMPSLIN; do
+    for sel in p1:1 p2:1 p1:4 p2:4; do
+      echo "=== $lib $sel"
+      w=c3p1; [ "${sel%%:*}" = p2 ] && w=c3p2
+      QE_LIB_PATH=$AB/libqe_$lib.so QE_STAMP_SEL=$sel timeout -k 10 120 python tools/stamps.py --what $w 2>&1 | grep -v "^\[stamps\]" || exit 1
+    done
+  done ) > gpurun_out/r05d_stamps.log 2>&1 || exit 1
+QE_LIB_PATH=$AB/libqe_STAMPS.so timeout -k 10 120 python tools/stamps.py --what hj > gpurun_out/r05d_hj_stamps.log 2>&1 || exit 1
+REPS=3 bash tools/gpu_lib_ab.sh r05d_c3 "prev:QE_LIB_PATH=$AB/libqe_PREV.so" "late:QE_LIB_PATH=$AB/libqe_late.so" "noflat:QE_LIB_PATH=$AB/libqe_noflat.so" "new:QE_NOTHING=1" "loadnt:QE_LIB_PATH=$AB/libqe_loadnt.so" "tpg128:QE_LIB_PATH=$AB/libqe_tpg128.so" || exit 1
 echo all-done

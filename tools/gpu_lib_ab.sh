@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 T=$1; shift
-( for rep in 1 2; do for spec in "$@"; do
+( for rep in $(seq ${REPS:-2}); do for spec in "$@"; do
     label=${spec%%:*}; envs=${spec#*:}
     echo "== $label"
     env $envs timeout -k 10 240 python bench.py --no-cpu --no-faithful --steps 10 --warmup 2 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); s=d['stages']; print(d['ms_per_step'], d['kernel_ms_per_step'], d['parity'], {k: v['ms_per_step'] for k, v in s.items()})" || exit 1

@@ -45,6 +45,9 @@ def report(ctx, which, ntiles):
     st = st[:, :k]
     ok = (st > 0).all(axis=1)
     st = st[ok]
+    if not len(st):   # (a kernel form that does not stamp every phase)
+        print(f"== {which}: no tile with all {k} stamps")
+        return
     d = np.diff(st, axis=1) * 10.0 / 1000.0   # ticks of 10 ns -> us
     span = (st[:, -1].max() - st[:, 0].min()) * 10.0 / 1000.0
     busy = (st[:, -1] - st[:, 0]).sum() * 10.0 / 1000.0
