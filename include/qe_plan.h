@@ -124,6 +124,13 @@ typedef struct qe_engine {
     /* keys from a list of the key column's values (nullable; join_carry's outxa): the keys `keys`
      * would gather through the rowids, without the gather (`vals` borrowed) */
     int (*keys_of)(void* u, uint32_t rel, uint32_t col, qe_h vals, qe_h* out);
+    /* a WHOLE base relation as a join side at any rank count (nullable): the column itself,
+     * *rowids = 0 (row i), as base_side gives it at one rank.  The plan's broadcast joins use it:
+     * at N ranks a join of a derived side with a whole (replicated) base relation may leave the
+     * derived side where it lies and join it against the whole column on every rank -- each pair
+     * is still made on exactly one rank -- instead of exchanging the derived side and joining
+     * bucket against bucket; the plan picks the cheaper by its cost model (QE_PLAN_BCAST). */
+    int (*base_side_all)(void* u, uint32_t rel, uint32_t col, qe_h* keys, qe_h* rowids);
 } qe_engine;
 
 /* Replay the reference's variant choice and list bookkeeping for every query of `text` on the

@@ -365,6 +365,23 @@ int e_keys_of(void* u, uint32_t rel, uint32_t col, qe_h vals, qe_h* out) {
     });
 }
 
+// the whole column at any rank count (the plan's broadcast joins): as e_base_side at one rank
+int e_base_side_all(void* u, uint32_t rel, uint32_t col, qe_h* keys, qe_h* rowids) {
+    Eng* e = E(u);
+    return guard(e, [&] {
+        qe_ctx* c = e->c;
+        const qe_col q = column(c, rel, col);
+        uint64_t kor = 0, kand = 0;
+        ck(qe_relation_column_bits(c, (int)rel, (int)col, &kor, &kand), c);
+        DArr* k = new_arr(c, const_cast<uint64_t*>(q.d), q.n, true, false);
+        k->bits = true;
+        k->kor = kor;
+        k->kand = kand;
+        *keys = H(k);
+        *rowids = 0;
+    });
+}
+
 int e_base_side(void* u, uint32_t rel, uint32_t col, qe_h* keys, qe_h* rowids) {
     Eng* e = E(u);
     return guard(e, [&] {
@@ -964,6 +981,7 @@ qe_engine make_engine(Eng* e) {
     g.scan2 = e_scan2;
     g.keys = e_keys;
     g.base_side = e_base_side;
+    g.base_side_all = e_base_side_all;
     g.exchange_start = e_exchange_start;
     g.exchange_finish = e_exchange_finish;
     g.join = e_join;

@@ -429,13 +429,16 @@ typedef struct {
 
 static int is_whole(const comp_t* c) { return c->n == 1 && c->m[0].whole; }
 
+/* local: a broadcast join (bcast_join below) -- a whole base side is the whole column, a derived
+ * side stays where it lies (no exchange), as at one rank */
 static int side_start(plan_t* P, int cid, int b, uint32_t col, const uint8_t* need, const int* sel1, const int* kcol1,
-                      const int* vok, side_t* s) {
+                      const int* vok, side_t* s, int local) {
     const qe_engine* e = P->e;
     comp_t* c = &P->C[cid];
     memset(s, 0, sizeof *s);
     if (is_whole(c) && c->m[0].b == b) {                     /* a whole base relation: never exchanged */
-        ECHK(e->base_side(e->u, P->q->rels[b], col, &s->keys, &s->vals));
+        if (local) ECHK(e->base_side_all(e->u, P->q->rels[b], col, &s->keys, &s->vals));
+        else ECHK(e->base_side(e->u, P->q->rels[b], col, &s->keys, &s->vals));
         s->base = 1;
         if (need[b]) {
             s->ncar = 1;
@@ -504,7 +507,7 @@ static int side_start(plan_t* P, int cid, int b, uint32_t col, const uint8_t* ne
         cols[nk++] = c->m[mi].rows;
     }
     s->keep_n = nk;
-    if (e->world > 1) {
+    if (e->world > 1 && !local) {
         /* the carried lists travel with the keys (consumed); the others are dropped */
         for (int i = 0; i < c->n; i++) {
             int kept = 0;
@@ -565,6 +568,30 @@ static void free_comp(plan_t* P, int cid) {
     c->alive = 0;
 }
 
+/* Broadcast or partitioned, for a join of a derived side D with a whole base relation of R rows at
+ * G > 1 ranks (DESIGN §5's per-rank budget).  Partitioned (the default plan): D
+ * is exchanged -- per rank D/G rows hash-partitioned (~13 ps a row) and 1/G of them to each peer
+ * over its own xGMI link (16 B a row at ~150 GB/s: D*16/(G^2 * 150 GB/s)) -- and joined with the
+ * rank's bucket of the base column (R/G rows).  Broadcast: D stays where it lies and is joined with
+ * the WHOLE column, so the base side's sort does not shrink with G: (1 - 1/G) * R rows more at
+ * ~10 ps a row (a two-level sort of 1e8 keys ~1 ms).  Broadcast wins at G = 2 (one link between the
+ * two GPUs carries a quarter of D), partitioned from G = 4.  QE_PLAN_BCAST: 0 never, 2 always
+ * (tests), otherwise this model.  Every rank decides on the same global sizes. */
+static int bcast_join(const plan_t* P, int A, int B) {
+    const qe_engine* e = P->e;
+    if (e->world <= 1 || !e->base_side_all) return 0;
+    const int wa = is_whole(&P->C[A]), wb = is_whole(&P->C[B]);
+    if (wa == wb) return 0;                                  /* both derived, or both whole: no */
+    const char* m = getenv("QE_PLAN_BCAST");   /* (read per join: tests switch it) */
+    const int mode = m && (m[0] == '0' || m[0] == '2') ? m[0] - '0' : 1;
+    if (mode != 1) return mode == 2;
+    const double G = (double)e->world;
+    const double R = (double)(wa ? P->C[A].size : P->C[B].size), D = (double)(wa ? P->C[B].size : P->C[A].size);
+    const double bcast_ps = (1.0 - 1.0 / G) * R * 10.0;
+    const double part_ps = D / G * 13.0 + D * 16.0 / (G * G) / 150e9 * 1e12;
+    return bcast_ps < part_ps;
+}
+
 static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* sel1, const int* kcol1, const int* vok,
                    int last) {
     const qe_engine* e = P->e;
@@ -600,13 +627,14 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* s
         }
     }
     side_t sa, sb;
+    const int bc = bcast_join(P, A, B);
     /* derived sides first, so their exchanges overlap the base side's local bucket scan */
     if (is_whole(&P->C[A])) {
-        ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, sel1, kcol1, vok, &sb));
-        ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, sel1, kcol1, vok, &sa));
+        ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, sel1, kcol1, vok, &sb, bc));
+        ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, sel1, kcol1, vok, &sa, bc));
     } else {
-        ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, sel1, kcol1, vok, &sa));
-        ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, sel1, kcol1, vok, &sb));
+        ECHK(side_start(P, A, ba, (uint32_t)p->fcol, need, sel1, kcol1, vok, &sa, bc));
+        ECHK(side_start(P, B, bb, (uint32_t)p->scol, need, sel1, kcol1, vok, &sb, bc));
     }
     if (sa.pay && sb.pay) {                                  /* one payload column per join */
         rel(P, sb.pay);

@@ -44,11 +44,13 @@ VALUES, VALUES_SRC = 0xFFFFFFFF, 4   # include/qe_plan.h: QE_PLAN_VALUES, QE_PLA
 JOIN_AGG = C.CFUNCTYPE(I, VP, U32, U32, U32, U32, I, P(I), P(U32), P(U64), P(U64))
 COLUMN = C.CFUNCTYPE(I, VP, U32, U32, P(H))
 KEYS_OF = C.CFUNCTYPE(I, VP, U32, U32, H, P(H))
+BASE_SIDE_ALL = C.CFUNCTYPE(I, VP, U32, U32, P(H), P(H))
 
 
 class Engine(C.Structure):
     _fields_ = [("u", VP), ("rank", U32), ("world", U32)] + FIELDS + [("mat_limit", P(U64)), ("join_agg", JOIN_AGG),
-                                                                      ("column", COLUMN), ("keys_of", KEYS_OF)]
+                                                                      ("column", COLUMN), ("keys_of", KEYS_OF),
+                                                                      ("base_side_all", BASE_SIDE_ALL)]
 
 
 def part_of(k: np.ndarray, nparts: int) -> np.ndarray:
@@ -109,6 +111,9 @@ class NumpyPlanEngine:
         self.agg_calls = 0                       # last joins of two base relations in aggregate form
         self.keys_of_calls = 0                   # join keys that rode with their rows (no gather)
         self.values_rows = 0                     # base sides whose rows rode as a column's values
+        self.bcast_sides = 0                     # whole base sides taken by broadcast joins
+        self._bsa_cb = BASE_SIDE_ALL(self._wrap(self.cb_base_side_all, False))
+        e.base_side_all = self._bsa_cb
         if key_carry:
             self._col_cb = COLUMN(self._wrap(self.cb_column, False))
             self._ko_cb = KEYS_OF(self._wrap(self.cb_keys_of, False))
@@ -209,6 +214,12 @@ class NumpyPlanEngine:
         rows = np.random.default_rng(self.rank + 17).permutation(rows).astype(np.uint32)
         keys[0] = self.put(c[rows])
         rowids[0] = self.put(rows)
+
+    def cb_base_side_all(self, u, rel, col, keys, rowids):
+        """the whole column at any rank count (the plan's broadcast joins), as at one rank"""
+        self.bcast_sides += 1
+        keys[0] = self.put(self.rels[rel][col], borrowed=True)
+        rowids[0] = 0
 
     def cb_exchange_start(self, u, keys, cols, ncols, ticket):
         import torch

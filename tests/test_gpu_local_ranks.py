@@ -25,11 +25,14 @@ def _load(ctx, ds):
         ctx.load_relation(cols)
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("world,bcast", [(2, "0"), (3, "0"), (8, "0"), (2, "2"), (3, "2"), (8, "1")])
 @pytest.mark.parametrize("fixture", [f.split("/")[-1][:-5] for f in goldens.golden_files()])
-def test_local_ranks_match_every_golden(ctx, fixture, world):
+def test_local_ranks_match_every_golden(ctx, fixture, world, bcast, monkeypatch):
     """every golden at W ranks: exit-0 well-formed queries as one batch (one line per query, so the
-    batch's bytes are the concatenation), the others one by one; rows really moved between ranks"""
+    batch's bytes are the concatenation), the others one by one; rows really moved between ranks.
+    QE_PLAN_BCAST: 0 every join partitioned, 2 every join of a derived side with a whole base
+    relation broadcast (the derived side stays, the whole column joins it), 1 the cost model"""
+    monkeypatch.setenv("QE_PLAN_BCAST", bcast)
     doc = goldens.load(f"{goldens.GOLDEN_DIR}/{fixture}.json")
     _load(ctx, doc["dataset"])
     batch = [c for c in doc["cases"] if c["rc"] == 0 and WELL_FORMED.fullmatch(c["input"])]
@@ -49,14 +52,15 @@ def test_local_ranks_match_every_golden(ctx, fixture, world):
         out, rc, _, b = ctx.run_local(c["input"], world)
         sent += b
         assert (out, rc) == (c["stdout"], c["rc"]), c["input"]
-    if fixture in ("c4", "fuzz_a", "headline"):
+    if fixture in ("c4", "fuzz_a", "headline") and bcast == "0":
         assert sent > 0                                   # derived join sides crossed ranks
 
 
-def test_one_rank_too_large_stops_every_rank(ctx):
+def test_one_rank_too_large_stops_every_rank(ctx, monkeypatch):
     """a join past the materialisation limit on ONE rank only: every rank leaves the planned query
     together (one all-reduce), the query re-runs on rank 0's faithful executor, the bytes are the
     reference's; nobody waits in a later exchange"""
+    monkeypatch.setenv("QE_PLAN_BCAST", "0")
     doc = goldens.load(f"{goldens.GOLDEN_DIR}/headline.json")
     _load(ctx, doc["dataset"])
     case = next(c for c in doc["cases"] if c["input"] == C3)
@@ -99,7 +103,8 @@ def test_limit_bounds_the_global_pair_count(ctx):
 def test_local_ranks_c3_100m(ctx, world):
     """the headline query at its size (4 x 100 M rows) on W in-process ranks: the faithful
     executor's bytes (pinned to the aggregate truth by test_gpu_fullsize), the same row count, no
-    fallback, and the three derived sides exchanged"""
+    fallback; at 8 ranks the three derived sides exchanged, at 2 the cost model's broadcast joins
+    (no derived side moves: each rank joins its rows with the whole base columns)"""
     N = 100_000_000
     ctx.drop_relations()
     try:
@@ -111,6 +116,6 @@ def test_local_ranks_c3_100m(ctx, world):
         out, rc, refused, sent = ctx.run_local(C3, world)
         assert (out, rc, refused) == (want, 0, 0)
         assert ctx.last_result_rows() == rows
-        assert sent > 0
+        assert (sent > 0) == (world == 8)
     finally:
         ctx.drop_relations()

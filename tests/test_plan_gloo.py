@@ -77,8 +77,9 @@ def test_check_names_the_reason():
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_c3_chain_on_ranks_equals_one_rank_and_truth(world):
+def test_c3_chain_on_ranks_equals_one_rank_and_truth(world, monkeypatch):
     import agg_truth
+    monkeypatch.setenv("QE_PLAN_BCAST", "0")   # the partitioned form of every join (exchanges)
     rows = 60_000
     rels = dg.make_relations(dg.chain_spec(4, rows), 1)
     one = pe.NumpyPlanEngine(rels, 0, 1).run(C3)
@@ -97,15 +98,45 @@ def test_c3_chain_on_ranks_equals_one_rank_and_truth(world):
     assert live == 0
 
 
-def test_two_ranks_match_goldens():
+@pytest.mark.parametrize("bcast", ["0", "1", "2"])
+def test_two_ranks_match_goldens(bcast, monkeypatch):
+    """QE_PLAN_BCAST: 0 every join partitioned (derived sides exchanged), 2 every join of a derived
+    side with a whole base relation broadcast (the derived side stays, the base side is the whole
+    column), 1 the plan's cost model -- the bytes are the reference's in every form"""
+    monkeypatch.setenv("QE_PLAN_BCAST", bcast)
     doc = goldens.load(f"{goldens.GOLDEN_DIR}/fuzz_a.json")
     rels, _ = goldens.dataset(doc["dataset"])
     one = pe.NumpyPlanEngine(rels, 0, 1)
     cases = [c for c in doc["cases"] if one.run(c["input"])[1] == 0][:60]
     res, nex, _ = _run_world(rels, [c["input"] for c in cases], 2)
-    assert nex > 0 and len(cases) >= 40
+    assert len(cases) >= 40
+    if bcast == "0":
+        assert nex > 0
     for c, (out, rc, _, _) in zip(cases, res):
         assert (out, rc) == (c["stdout"], 0), c["input"]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_c3_broadcast_joins(world, monkeypatch):
+    """C3 with every join broadcast: R2, R1 and R0 are whole base relations, so no derived side
+    moves (0 exchanges) and the output is still the aggregate truth; the cost model picks the
+    broadcast form at 2 ranks for C3's shape (one link between two GPUs) and never for a join of
+    two derived sides"""
+    import agg_truth
+    rows = 60_000
+    rels = dg.make_relations(dg.chain_spec(4, rows), 1)
+    c2 = rels[3][2]
+    mask = (c2 > np.uint64(1000000000)) & (c2 < np.uint64(3000000000))
+    cnt, nrows, sums = agg_truth.chain4_sums(rels, rows, mask)
+    want = f"{cnt}\n" + "".join(f"{s} " for s in sums) + "\n"
+    monkeypatch.setenv("QE_PLAN_BCAST", "2")
+    res, nex, live = _run_world(rels, [C3], world)
+    assert res[0][:3] == (want, 0, nrows)
+    assert nex == 0 and live == 0
+    monkeypatch.setenv("QE_PLAN_BCAST", "1")
+    res, nex, _ = _run_world(rels, [C3], 2)
+    assert res[0][:3] == (want, 0, nrows)
+    assert nex == 0                                   # the model: broadcast at 2 ranks
 
 
 def test_one_rank_too_large_stops_every_rank():
