@@ -36,12 +36,13 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
 
 // A buffer descriptor over [p, p + bytes) built from wave-uniform inputs (readfirstlane'd so the
 // compiler can prove it: no waterfall loop around the loads).  Loads through it take a 32-bit
-// per-lane byte offset (one VGPR of addressing per stream instead of a 64-bit address per load)
-// and return 0 past `bytes` (the range check replaces the `i < n` guards).  The raw-buffer range
-// check covers the VGPR offset + the instruction's immediate offset but NOT the scalar soffset
-// (ADVICE r4), so the helpers' second offset is added to the per-lane one: a compile-time
-// stride (j * 512) folds into the range-checked immediate, and a lane past the end of an
-// exactly-sized allocation reads 0 instead of the next page.
+// per-lane byte offset + a scalar one (one VGPR of addressing per stream instead of a 64-bit
+// address per load); elements past `bytes` are masked by their kernels.  The raw-buffer range
+// check covers the per-lane offset + the instruction's immediate but NOT the scalar soffset
+// (ADVICE r4), so a lane may read up to its stride past `bytes`: allowed because every buffer a
+// kernel reads is libqe-allocated with DALLOC_SLACK bytes of slack (qe_internal.h).  (Folding
+// the stride into the checked offset instead cost pass 1 up to 6 VGPRs and ~2 % of
+// sort_pass_carry: profiles/r05d_c3_bench.log.)
 typedef unsigned int qe_v2u __attribute__((ext_vector_type(2)));
 // cache policy of the streaming buffer loads (build knob, A/B: QE_LOAD_NT=1 marks them
 // non-temporal, aux = 2 -- MI355X_MICROARCH "nt-weights": read-once streams land earlier)
@@ -57,27 +58,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, uint32
     return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, (int)n, 0x00020000);
 }
 __device__ __forceinline__ uint2 buf_load_u2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    const qe_v2u x = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(voff + soff), 0, QE_LOAD_AUX);
-    return make_uint2(x.x, x.y);
-}
-__device__ __forceinline__ uint32_t buf_load_u32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)(voff + soff), 0, QE_LOAD_AUX);
-}
-// The same loads with the stride in soffset, for the kernels whose address registers are tight
-// (pass 2, the aggregate join): soffset is not range-checked, so these read up to a stride's
-// worth past the range -- allowed ONLY on buffers from dalloc(), whose blocks all end with
-// DALLOC_SLACK bytes of allocated slack (qe_runtime.hip), and for soff < DALLOC_SLACK.
-__device__ __forceinline__ uint2 buf_load_u2_sl(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     const qe_v2u x = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, QE_LOAD_AUX);
     return make_uint2(x.x, x.y);
 }
-__device__ __forceinline__ uint32_t buf_load_u32_sl(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+__device__ __forceinline__ uint32_t buf_load_u32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, QE_LOAD_AUX);
 }
 typedef unsigned int qe_v4u __attribute__((ext_vector_type(4)));
 // (a 16-B load that crosses the end of the range: use it only where the range is whole 16-B units)
 __device__ __forceinline__ uint4 buf_load_u4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    const qe_v4u x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(voff + soff), 0, QE_LOAD_AUX);
+    const qe_v4u x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, QE_LOAD_AUX);
     return make_uint4(x.x, x.y, x.z, x.w);
 }
 
@@ -117,8 +107,35 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return v;
 }
 
-// inclusive wave scan (u32)
+// Inclusive wave scans.  QE_DPP_SCAN (default): six DPP adds -- row_shr 1/2/4/8 inside each
+// 16-lane row, then row_bcast:15 (rows 1, 3 take row 0's / row 2's total) and row_bcast:31 (rows
+// 2, 3 take rows 0-1's total), GFX9's wave64 broadcasts -- no LDS round trip per step; the
+// __shfl_up form was six dependent ds_bpermute + waits (~100 cycles each).  A source lane out of
+// its row reads 0 (bound_ctrl), a row masked off keeps its value.
+#ifndef QE_DPP_SCAN
+#define QE_DPP_SCAN 1
+#endif
+__device__ __forceinline__ uint32_t dpp_add_u32(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);   // row_bcast:31
+    return v;
+}
+#define QE_DPP64(v, CTRL, RM)                                                                                   \
+    do {                                                                                                        \
+        const uint32_t lo_ = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v), CTRL, RM, 0xf, false);  \
+        const uint32_t hi_ = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)((v) >> 32), CTRL, RM, 0xf, false); \
+        (v) += ((uint64_t)hi_ << 32) | lo_;                                                                     \
+    } while (0)
+
+// inclusive wave scan (u32); DPP = false: the ds_bpermute form (a kernel at its register limit
+// may allocate better around it)
+template <bool DPP = (QE_DPP_SCAN != 0)>
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+    if (DPP) return dpp_add_u32(v);
     int l = lane_id();
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -129,6 +146,15 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
 }
 
 __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
+    if (QE_DPP_SCAN) {
+        QE_DPP64(v, 0x111, 0xf);
+        QE_DPP64(v, 0x112, 0xf);
+        QE_DPP64(v, 0x114, 0xf);
+        QE_DPP64(v, 0x118, 0xf);
+        QE_DPP64(v, 0x142, 0xa);
+        QE_DPP64(v, 0x143, 0xc);
+        return v;
+    }
     int l = lane_id();
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {

@@ -192,8 +192,10 @@ inline const uint32_t* narrow_of(const qe_ctx* c, const void* col, uint64_t n) {
     return nullptr;
 }
 
-// every dalloc block is followed by DALLOC_SLACK allocated bytes: the soffset-strided buffer
-// loads (buf_load_*_sl, qe_device.h) may read that far past a block's end
+// every device buffer a kernel reads is libqe's own -- a dalloc block, a relation column or its
+// u32 copy (no entry point takes a caller's device pointer) -- and each is followed by
+// DALLOC_SLACK allocated bytes: the soffset-strided buffer loads (qe_device.h) may read up to a
+// tile's stride past a buffer's end, never past its allocation
 constexpr size_t DALLOC_SLACK = 64u << 10;
 void* dalloc(qe_ctx* c, size_t bytes);
 bool alloc_log_on();   // QE_ALLOC_LOG=1 (placement A/Bs)

@@ -500,7 +500,7 @@ static void column_stats(qe_ctx* c, Relation& r) {
         for (size_t j = 0; j < r.cols.size(); j++) {
             if ((r.kor[j] >> 32) || !r.rows) continue;
             uint32_t* d = nullptr;
-            if (hipMalloc(&d, r.rows * sizeof(uint32_t)) != hipSuccess) {
+            if (hipMalloc(&d, r.rows * sizeof(uint32_t) + DALLOC_SLACK) != hipSuccess) {   // (slack: as dalloc's)
                 // best effort: a relation near the memory limit loads without its u32 copies
                 // (every reader of cols32 takes the u64 column when the copy is null)
                 (void)hipGetLastError();
@@ -656,7 +656,7 @@ int qe_load_relation(qe_ctx* c, uint64_t rows, uint64_t ncols, const uint64_t* c
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t j = 0; j < ncols; j++) {
         uint64_t* d = nullptr;
-        QE_HIP(hipMalloc(&d, std::max<uint64_t>(rows, 1) * sizeof(uint64_t)));
+        QE_HIP(hipMalloc(&d, std::max<uint64_t>(rows, 1) * sizeof(uint64_t) + DALLOC_SLACK));   // (slack: as dalloc's)
         r.cols.push_back(d);
         if (!rows) continue;
         if (getenv("QE_LOAD_DIRECT"))   // A/B only: the runtime's own pageable copy
@@ -689,7 +689,7 @@ int qe_gen_relation(qe_ctx* c, uint64_t rows, uint64_t ncols, const int* kinds, 
     ColsGuard guard(r.cols);
     for (uint64_t j = 0; j < ncols; j++) {
         uint64_t* d = nullptr;
-        QE_HIP(hipMalloc(&d, std::max<uint64_t>(rows, 1) * sizeof(uint64_t)));
+        QE_HIP(hipMalloc(&d, std::max<uint64_t>(rows, 1) * sizeof(uint64_t) + DALLOC_SLACK));   // (slack: as dalloc's)
         r.cols.push_back(d);
         uint64_t base = (seed << 40) | ((uint64_t)gen_rel << 36) | ((uint64_t)j << 32);
         if (kinds[j] == 2) {

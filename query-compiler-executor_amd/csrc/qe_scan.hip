@@ -247,7 +247,7 @@ __global__ void __launch_bounds__(CB) compact_kernel(Op op, uint64_t n, uint32_t
         constexpr uint32_t E = ITEMS * CNW;
         const uint32_t c0 = 2u * l < E ? s_cnt[2 * l] : 0u, c1 = 2u * l + 1 < E ? s_cnt[2 * l + 1] : 0u;
         uint32_t inc = wave_incl_scan_u32(c0 + c1);
-        uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
+        uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
         if (2u * l < E) s_cnt[2 * l] = inc - c0 - c1;
         if (2u * l + 1 < E) s_cnt[2 * l + 1] = inc - c1;
         uint64_t excl = lookback_wave(status, epoch, tile, total);
@@ -346,7 +346,7 @@ __global__ void __launch_bounds__(CB) compact_pipe_kernel(Op op, uint64_t n, uin
             constexpr uint32_t E = ITEMS * CNW;
             const uint32_t c0 = 2u * l < E ? s_cnt[2 * l] : 0u, c1 = 2u * l + 1 < E ? s_cnt[2 * l + 1] : 0u;
             const uint32_t inc = wave_incl_scan_u32(c0 + c1);
-            const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
+            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
             if (2u * l < E) s_cnt[2 * l] = inc - c0 - c1;
             if (2u * l + 1 < E) s_cnt[2 * l + 1] = inc - c1;
             lookback_publish(status, epoch, tile, total);
@@ -562,7 +562,7 @@ __global__ void __launch_bounds__(US_B) uscan_kernel(FilterScan2Op op, uint64_t 
     if (w == 0) {   // the waves' exclusive offsets inside the workgroup's run; one atomic for the run
         const uint32_t c = l < NW ? s_wtot[l] : 0u;
         const uint32_t inc = wave_incl_scan_u32(c);
-        const uint32_t sum = (uint32_t)__shfl((int)inc, 63, 64);
+        const uint32_t sum = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
         if (l < NW) s_wtot[l] = inc - c;
         if (l == 0) s_base = sum ? atomicAdd(counter, (unsigned long long)sum) : 0ull;
     }

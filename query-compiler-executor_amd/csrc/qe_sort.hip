@@ -264,8 +264,8 @@ static inline uint32_t xcd_grid(uint64_t items) {
 #ifndef QE_P1_EARLY
 #define QE_P1_EARLY 1
 #endif
-#ifndef QE_STAGE_FLAT   // (build knob, 0 = round 4's guarded per-element staging in pass 1)
-#define QE_STAGE_FLAT 1
+#ifndef QE_STAGE_FLAT   // (build knob: 1 = branch-free staging in pass 1, measured ~1 % slower)
+#define QE_STAGE_FLAT 0
 #endif
 enum { X_NONE = 0, X64 = 1, X32 = 2, XCOL = 3 };
 template <typename K, int IN, int OUT, bool PACK, int RBITS, int ITEMS, int NT, bool PRE = false, int CARRY = X_NONE,
@@ -740,7 +740,7 @@ __global__ void __launch_bounds__(1024) tl_scan_kernel(uint32_t* __restrict__ hi
         uint32_t run2 = wave_incl_scan_u32(b0 + b1) - b0 - b1;
         base2[t * 2] = run2;
         base2[t * 2 + 1] = run2 + b0;
-        const uint32_t tot2 = (uint32_t)__shfl((int)(run2 + b0 + b1), 63, 64);
+        const uint32_t tot2 = (uint32_t)__builtin_amdgcn_readlane((int)(run2 + b0 + b1), 63);
         base2[128 + t * 2] = tot2;   // (digits 128..255 of the second pass are empty)
         base2[128 + t * 2 + 1] = tot2;
     }
@@ -1312,9 +1312,9 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
             const auto rw = W32 ? buf_rsrc(reinterpret_cast<const uint32_t*>(win) + base, m * 4u) : buf_rsrc(win + base, m * 8u);
 #pragma unroll
             for (int j = 0; j < TL2_ITEMS; j++) {
-                if constexpr (W32) word[j] = (uint64_t)buf_load_u32_sl(rw, o0 * 4u, (uint32_t)j * 256u) << 32;
+                if constexpr (W32) word[j] = (uint64_t)buf_load_u32(rw, o0 * 4u, (uint32_t)j * 256u) << 32;
                 else {
-                    const uint2 v = buf_load_u2_sl(rw, o0 * 8u, (uint32_t)j * 512u);
+                    const uint2 v = buf_load_u2(rw, o0 * 8u, (uint32_t)j * 512u);
                     word[j] = (uint64_t)v.y << 32 | v.x;
                 }
             }
@@ -1361,7 +1361,7 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
                 tot += cc;
             }
         }
-        const uint32_t inc = wave_incl_scan_u32(tot);
+        const uint32_t inc = wave_incl_scan_u32<UNSTABLE>(tot);
         if (l == 63) wsum[w] = inc;
         __syncthreads();
         if (d < BINS) {
@@ -1405,10 +1405,10 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
 #pragma unroll
             for (int j = 0; j < TL2_ITEMS; j++) {
                 if constexpr (CARRY == X64) {
-                    const uint2 v = buf_load_u2_sl(rx, o0 * 8u, (uint32_t)j * 512u);
+                    const uint2 v = buf_load_u2(rx, o0 * 8u, (uint32_t)j * 512u);
                     word[j] = (uint64_t)v.y << 32 | v.x;
                 } else {
-                    xw[j] = buf_load_u32_sl(rx, o0 * 4u, (uint32_t)j * 256u);
+                    xw[j] = buf_load_u32(rx, o0 * 4u, (uint32_t)j * 256u);
                 }
             }
         }
@@ -1660,7 +1660,7 @@ __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
         constexpr uint32_t E = HJ_I * HJ_NW;
         const uint32_t a0 = 2u * l < E ? tab[2 * l] : 0u, a1 = 2u * l + 1 < E ? tab[2 * l + 1] : 0u;
         const uint32_t inc = wave_incl_scan_u32(a0 + a1);
-        const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
         if (2u * l < E) tab[2 * l] = inc - a0 - a1;
         if (2u * l + 1 < E) tab[2 * l + 1] = inc - a1;
         if (l == 0) {   // the pairs need no order: a bucket reserves its output slice with one atomic
@@ -1686,7 +1686,7 @@ __global__ void __launch_bounds__(HJ_NT) __attribute__((amdgpu_waves_per_eu(8)))
         const uint32_t st = live ? (v ? bnd[v - 1] : 0u) : 0u;
         const uint32_t cnt = live ? bnd[v] - st : 0u;
         const uint32_t pj = pre[j];
-        const uint32_t tot = (uint32_t)__shfl((int)(pj + cnt), 63, 64);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)(pj + cnt), 63);
         const uint64_t ob = gofs + tab[j * HJ_NW + w];
         const uint32_t srow = (uint32_t)ws[j];
         for (uint32_t q0 = 0; q0 < tot; q0 += 64) {   // wave-uniform
@@ -1873,7 +1873,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
         hd[j] = h;
         const uint32_t inc = wave_incl_scan_u32(cnt);
         pre[j] = inc - cnt;
-        tot[j] = (uint32_t)__shfl((int)inc, 63, 64);   // the item's pairs in this wave
+        tot[j] = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);   // the item's pairs in this wave
         if (l == 63) tab[j * NW + w] = inc;
     }
     __syncthreads();
@@ -1886,7 +1886,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
         constexpr uint32_t E = HJ_I * NW;
         const uint32_t a0 = 2u * l < E ? tab[2 * l] : 0u, a1 = 2u * l + 1 < E ? tab[2 * l + 1] : 0u;
         const uint32_t inc = wave_incl_scan_u32(a0 + a1);
-        const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
         if (2u * l < E) tab[2 * l] = inc - a0 - a1;
         if (2u * l + 1 < E) tab[2 * l + 1] = inc - a1;
         if (l == 0) {
@@ -3276,21 +3276,21 @@ tl_hjoin_sums_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict
         uint32_t xl[XK ? HJ_I : 1], xh[XK == 2 ? HJ_I : 1];   // S's payload halves
 #pragma unroll
         for (int j = 0; j < HJ_I; j++) {
-            fr[j] = buf_load_u32_sl(rR, oR, (uint32_t)j * HJ_NT * rstride);
-            const uint2 ws = buf_load_u2_sl(rS, o8, (uint32_t)j * HJ_NT * 8u);
+            fr[j] = buf_load_u32(rR, oR, (uint32_t)j * HJ_NT * rstride);
+            const uint2 ws = buf_load_u2(rS, o8, (uint32_t)j * HJ_NT * 8u);
             fs[j] = ws.y;
             sl[j] = ws.x;
         }
         if constexpr (XK == 1) {
             const auto rX = buf_rsrc(xS32 + s0, mS * 4u);
 #pragma unroll
-            for (int j = 0; j < HJ_I; j++) xl[j] = buf_load_u32_sl(rX, o4, (uint32_t)j * HJ_NT * 4u);
+            for (int j = 0; j < HJ_I; j++) xl[j] = buf_load_u32(rX, o4, (uint32_t)j * HJ_NT * 4u);
         }
         if constexpr (XK == 2) {
             const auto rX = buf_rsrc(xS + s0, mS * 8u);
 #pragma unroll
             for (int j = 0; j < HJ_I; j++) {
-                const uint2 x = buf_load_u2_sl(rX, o8, (uint32_t)j * HJ_NT * 8u);
+                const uint2 x = buf_load_u2(rX, o8, (uint32_t)j * HJ_NT * 8u);
                 xl[j] = x.x;
                 xh[j] = x.y;
             }

@@ -566,3 +566,23 @@ def test_checksums_batched(ctx):
         assert ctx.checksum(rels[k % 3], lists[k]) == want[k]
     for l in hosts:
         ctx.list_free(l)
+
+
+@pytest.mark.parametrize("extra", [13, 4096 + 3, 8191])
+def test_partial_last_tile_at_the_end_of_exact_allocations(ctx, extra):
+    """relations of 2^22 + extra rows (the lookback-free two-level sort's floor, a partial last
+    tile): every column and its u32 copy is an exactly-sized hipMalloc, so the last tile's strided
+    buffer loads end at an allocation's end (the stride rides in the range-checked
+    offset) -- the planned C3 query equals the faithful executor's bytes"""
+    rows = (1 << 22) + extra
+    q = "0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>1000000000&3.2<3000000000|1.2 2.2 3.2\n"
+    ctx.drop_relations()
+    try:
+        kinds = [("mod", rows), ("mod", rows), ("hi32",)]
+        for r in range(4):
+            ctx.gen_relation(rows, kinds, seed=3, gen_rel=r)
+        want, rc0 = ctx.run(q)
+        got, rc, refused = ctx.run_dist(q)
+        assert (got, rc, refused) == (want, 0, 0) and rc0 == 0
+    finally:
+        ctx.drop_relations()
