@@ -257,6 +257,9 @@ static inline uint32_t xcd_grid(uint64_t items) {
 // word of the u64 column xa points to (a base relation's next join key riding with its rows).  The
 // words are written first; the same LDS stage then takes the payloads in the words' slots, so
 // they leave in the same runs.
+// TM (PRE only): one workgroup takes TM consecutive counted tiles -- its run of digit d starts at
+// the first one's offset and is the TM tiles' runs back to back (the column scan orders a group's
+// tiles consecutively), so nothing else changes (see P1_TM).
 // UNSTABLE: ranks from per-wave LDS counters (one ds_add_rtn per element) instead of the 8-ballot
 // match-any -- equal digits keep no order.  For the partitioned plan's deferred sorts (their
 // consumer, bucket_join, needs the buckets, not an order inside them) and the first LSD pass of
@@ -269,7 +272,7 @@ static inline uint32_t xcd_grid(uint64_t items) {
 #endif
 enum { X_NONE = 0, X64 = 1, X32 = 2, XCOL = 3 };
 template <typename K, int IN, int OUT, bool PACK, int RBITS, int ITEMS, int NT, bool PRE = false, int CARRY = X_NONE,
-          bool UNSTABLE = false>
+          bool UNSTABLE = false, int TM = 1>
 __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ kin, const uint64_t* __restrict__ win,
                                                         const uint32_t* __restrict__ vin, K* __restrict__ kout,
                                                         uint64_t* __restrict__ wout, uint32_t* __restrict__ vout,
@@ -280,6 +283,7 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
                                                         const uint32_t* __restrict__ xb = nullptr,
                                                         uint64_t* __restrict__ xout = nullptr) {
     static_assert(CARRY == X_NONE || (PRE && OUT == OUT_WORD), "payload carry: the lookback-free first pass only");
+    static_assert(TM == 1 || PRE, "a tile of TM counted tiles: the lookback-free first pass only");
     constexpr int BINS = 1 << RBITS, DPT = BINS >= NT ? BINS / NT : 1;   // digits per thread
     constexpr int NW = NT / 64;
     constexpr int TILE = NT * ITEMS, WT = 64 * ITEMS;
@@ -309,7 +313,7 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
     uint32_t pre_off[PRE ? DPT : 1];
     if constexpr (PRE) {
 #pragma unroll
-        for (int q = 0; q < DPT; q++) pre_off[q] = owner ? offs[(uint64_t)tile * BINS + threadIdx.x * DPT + q] : 0u;
+        for (int q = 0; q < DPT; q++) pre_off[q] = owner ? offs[(uint64_t)tile * TM * BINS + threadIdx.x * DPT + q] : 0u;
     }
     // the rank counters are zeroed AFTER the element loads are issued (below, for PRE tiles): a
     // barrier first would hold every wave's loads until the block's last wave has launched
@@ -632,17 +636,27 @@ __global__ void __launch_bounds__(1024) tl_hist_kernel(const K* __restrict__ key
 // one block: bucket starts (+ the end) and the largest bucket only -- the lookback-free form
 // computes its digit bases in the count scans, so it needs none of tl_scan_kernel's marginals
 // (whose serial loops made that kernel ~22 us per sort)
+// cbase (nullable): the two count scans' column bases, 256 + 128 words -- cbase[d1] = the keys with
+// a smaller first-pass digit (d1 = bucket bits 0-7), cbase[256 + d2] = bstart[d2 << 8]
 __global__ void __launch_bounds__(1024) tl_bstart_kernel(const uint32_t* __restrict__ hist, uint32_t* __restrict__ bstart,
-                                                         uint64_t* __restrict__ maxb) {
+                                                         uint64_t* __restrict__ maxb, uint32_t* __restrict__ cbase = nullptr) {
     constexpr int PER = TL_BUCKETS / 1024;
-    __shared__ uint32_t wsum[16], wmax[16];
+    static_assert(PER == 32 && TL_BUCKETS == 128 * 256, "thread t holds d2 = t / 8, d1 = (t % 8) * 32 + k");
+    __shared__ uint32_t wsum[16], wmax[16], d1tot[256];
     const int t = threadIdx.x;
+    if (cbase && t < 256) d1tot[t] = 0;
     uint32_t v[PER], mine = 0, mx = 0;
 #pragma unroll
     for (int k = 0; k < PER; k++) {
         v[k] = hist[t * PER + k];
         mine += v[k];
         mx = v[k] > mx ? v[k] : mx;
+    }
+    if (cbase) {   // (grid-uniform)
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PER; k++)
+            if (v[k]) atomicAdd(&d1tot[(t & 7) * PER + k], v[k]);
     }
     const uint32_t inc = wave_incl_scan_u32(mine);
     mx = wave_max_u32(mx);
@@ -651,6 +665,7 @@ __global__ void __launch_bounds__(1024) tl_bstart_kernel(const uint32_t* __restr
     __syncthreads();
     uint32_t run = inc - mine;
     for (int w = 0; w < wave_id(); w++) run += wsum[w];
+    const uint32_t bstart_first = run;
 #pragma unroll
     for (int k = 0; k < PER; k++) {
         bstart[t * PER + k] = run;
@@ -661,6 +676,17 @@ __global__ void __launch_bounds__(1024) tl_bstart_kernel(const uint32_t* __restr
         uint32_t m = 0;
         for (int w = 0; w < 16; w++) m = wmax[w] > m ? wmax[w] : m;
         *maxb = m;
+    }
+    if (!cbase) return;   // (grid-uniform)
+    if ((t & 7) == 0) cbase[256 + (t >> 3)] = bstart_first;   // (bucket t * PER = d2 << 8)
+    __syncthreads();   // d1tot complete (and wmax read)
+    const uint32_t x = t < 256 ? d1tot[t] : 0u, i1 = wave_incl_scan_u32(x);
+    if (t < 256 && lane_id() == 63) wmax[wave_id()] = i1;   // (wmax reused: the first 4 waves' totals)
+    __syncthreads();
+    if (t < 256) {
+        uint32_t r = i1 - x;
+        for (int w = 0; w < wave_id(); w++) r += wmax[w];
+        cbase[t] = r;
     }
 }
 
@@ -975,38 +1001,45 @@ __global__ void __launch_bounds__(1024) tl_hist_tiles_kernel(const K* __restrict
     // compiled to a branch and a vmcnt(0) wait per load -- 12 of the 16 loads of a tile served one
     // after another (round 3: 0.20 ms per 1e8 u32 keys).  A full tile takes 8-B loads of two u32
     // keys; the last, partial tile clamps its indices and masks the surplus.
-    uint32_t vm = 0;   // valid keys of this thread
-    auto load = [&](uint32_t t, uint64_t (&k)[8]) {
-        const uint64_t base = (uint64_t)t * RTILE;
-        if (base + RTILE <= n) {   // block-uniform
-            vm = 0xFFu;
-            if (sizeof(K) == 4 && !(reinterpret_cast<uintptr_t>(keys) & 7)) {
-                const uint2* k2 = reinterpret_cast<const uint2*>(reinterpret_cast<const uint32_t*>(keys) + base);
+    // The next tile's keys are loaded before this tile's atomics (two register buffers, the loop
+    // unrolled by two so neither is copied): one block per CU has no other block to hide the load
+    // round trip behind its atomics and barrier (round 4: load -> wait -> atomics -> barrier).
+    // Every load is a buffer load over the tile's keys (those past n read 0 and are masked): no
+    // branch between a full and a partial tile, whose register merge made the compiler wait for
+    // the loads right where they were issued.  A u32 tile takes 8-B loads of two keys.
+    // (live = false: a tile past the group -- no keys, the loads return 0 -- so the next tile's
+    // load is unconditional too; a guarded one merged registers and waited the same way)
+    auto load = [&](uint32_t t, uint64_t (&k)[8], bool live) -> uint32_t {   // -> the valid-key mask
+        const uint64_t base = live ? (uint64_t)t * RTILE : 0u;
+        const uint32_t tc = !live ? 0u : (uint32_t)((n - base) < (uint64_t)RTILE ? (n - base) : (uint64_t)RTILE);
+        uint32_t vm = 0;
+        if constexpr (sizeof(K) == 4) {
+            const auto r = buf_rsrc(keys + base, (tc * 4u + 7u) & ~7u);
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const uint2 v = k2[j * 1024 + threadIdx.x];
-                    k[2 * j] = v.x;
-                    k[2 * j + 1] = v.y;
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; j++) k[j] = (uint64_t)keys[base + (uint64_t)j * 1024 + threadIdx.x];
+            for (int j = 0; j < 4; j++) {
+                const uint32_t e = 2u * ((uint32_t)j * 1024u + threadIdx.x);
+                const uint2 v = buf_load_u2(r, e * 4u, 0u);
+                k[2 * j] = v.x;
+                k[2 * j + 1] = v.y;
+                vm |= (e < tc ? 1u : 0u) << (2 * j) | (e + 1u < tc ? 1u : 0u) << (2 * j + 1);
             }
-            return;
-        }
-        vm = 0;
+        } else {
+            const auto r = buf_rsrc(keys + base, tc * 8u);
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const uint64_t i = base + (uint64_t)j * 1024 + threadIdx.x;
-            k[j] = (uint64_t)keys[i < n ? i : n - 1];
-            vm |= (i < n ? 1u : 0u) << j;
+            for (int j = 0; j < 8; j++) {
+                const uint32_t e = (uint32_t)j * 1024u + threadIdx.x;
+                const uint2 v = buf_load_u2(r, e * 8u, 0u);
+                k[j] = (uint64_t)v.y << 32 | v.x;
+                vm |= (e < tc ? 1u : 0u) << j;
+            }
         }
+        return vm;
     };
-    uint64_t k[8];
-    uint32_t t = g * TL_TPG + q, prev = 0, par = 0;
-    for (; t < t_end; t += Q, par ^= 1u) {
-        load(t, k);
-        if (t != g * TL_TPG + q && threadIdx.x < 256) {   // the previous tile's counts (its barrier passed)
+    const uint32_t t0 = g * TL_TPG + q;
+    uint32_t prev = 0, par = 0;
+    // count tile t (keys k, mask vm): flush the previous tile's d1 counts first (its barrier passed)
+    auto count = [&](uint32_t t, const uint64_t (&k)[8], uint32_t vm) {
+        if (t != t0 && threadIdx.x < 256) {
             tcnt[(uint64_t)prev * 256 + threadIdx.x] = th[par ^ 1u][threadIdx.x];
             th[par ^ 1u][threadIdx.x] = 0;
         }
@@ -1020,6 +1053,16 @@ __global__ void __launch_bounds__(1024) tl_hist_tiles_kernel(const K* __restrict
         }
         __syncthreads();
         prev = t;
+        par ^= 1u;
+    };
+    uint64_t ka[8], kb[8];
+    uint32_t va = load(t0, ka, t0 < t_end), vb;
+    for (uint32_t t = t0; t < t_end; t += 2 * Q) {   // (block-uniform trip count)
+        vb = load(t + Q, kb, t + Q < t_end);
+        count(t, ka, va);
+        if (t + Q >= t_end) break;
+        va = load(t + 2 * Q, ka, t + 2 * Q < t_end);
+        count(t + Q, kb, vb);
     }
     if (g * TL_TPG + q < t_end && threadIdx.x < 256) tcnt[(uint64_t)prev * 256 + threadIdx.x] = th[par ^ 1u][threadIdx.x];
     __syncthreads();
@@ -1230,6 +1273,46 @@ __global__ void __launch_bounds__(256) cs_apply_kernel(CSJobs js) {
 #pragma unroll
     for (uint32_t r = 0; r < CS_CH; r++) {
         if (r0 + r < J.rows) {
+            J.m[(uint64_t)(r0 + r) * J.C + c] = run;
+            if (J.seg && (r0 + r) % TL_TPG == 0) J.seg[c * J.G + (r0 + r) / TL_TPG] = run;
+        }
+        run += v[r];
+    }
+    if (J.seg && blk == 0 && c == 0) J.seg[J.C * J.G] = J.ntot;
+}
+
+// The same scans in ONE pass (round 5): the column bases come from the bucket histogram
+// (tl_bstart_kernel's cbase), so a chunk needs only the sums of the chunks above it -- a decoupled
+// lookback per column (thread c walks column c's status words), as the sort passes do per digit.
+// Every count is read once and written once (the three-launch form read them twice: 1.54x the
+// algorithmic bytes in PMC, round 4), and the one-block middle launch is gone.
+__global__ void __launch_bounds__(256) cs_single_kernel(CSJobs js, const uint32_t* __restrict__ cbase,
+                                                        uint64_t* status, uint32_t* ticket, uint32_t epoch) {
+    __shared__ uint32_t s_ticket;
+    const uint32_t gb = take_ticket(ticket, &s_ticket);   // predecessors in ticket order are resident
+    uint32_t blk = gb;
+    const CSJob& J = cs_job(js, blk);
+    const uint32_t c = threadIdx.x, r0 = blk * CS_CH;
+    if (c >= J.C) return;
+    const uint32_t nrow = J.rows - r0 < CS_CH ? J.rows - r0 : CS_CH;
+    const auto rm = buf_rsrc(J.m + (uint64_t)r0 * J.C, nrow * J.C * 4u);
+    uint32_t v[CS_CH];
+#pragma unroll
+    for (uint32_t r = 0; r < CS_CH; r++) v[r] = buf_load_u32(rm, (r * J.C + c) * 4u, 0u);   // (past the matrix: 0)
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < CS_CH; r++) sum += v[r];
+    // a job's first chunk publishes its inclusive sum at once and ends every walk of that job
+    st_agent(&status[(uint64_t)gb * 256u + c], lb_word(epoch, blk == 0 ? LB_FLAG_INC : LB_FLAG_AGG, sum));
+    uint32_t run = 0;
+    if (blk > 0) {
+        run = (uint32_t)lookback_serial(status, epoch, gb, 256u, c);
+        st_agent(&status[(uint64_t)gb * 256u + c], lb_word(epoch, LB_FLAG_INC, (uint64_t)run + sum));
+    }
+    run += cbase[(J.C == 256u ? 0u : 256u) + c];
+#pragma unroll
+    for (uint32_t r = 0; r < CS_CH; r++) {
+        if (r < nrow) {
             J.m[(uint64_t)(r0 + r) * J.C + c] = run;
             if (J.seg && (r0 + r) % TL_TPG == 0) J.seg[c * J.G + (r0 + r) / TL_TPG] = run;
         }
@@ -2179,15 +2262,23 @@ static LocalRounds local_rounds(int L) {   // L low bits in rounds of <= 8
 }
 
 // both column scans of a two-level sort: m0 (rows0 x 256), m1 (rows1 x 128)
+// cbase (nullable): tl_bstart_kernel's column bases -> the one-pass form
 static void column_scans(qe_ctx* c, uint32_t* m0, uint32_t rows0, uint32_t* m1, uint32_t rows1, uint32_t* seg,
-                         uint32_t G, uint32_t ntot) {
+                         uint32_t G, uint32_t ntot, const uint32_t* cbase = nullptr) {
     CSJobs js;
     js.j[0] = CSJob{m0, nullptr, rows0, 256u, (rows0 + CS_CH - 1) / CS_CH, seg, G, ntot};
     js.j[1] = CSJob{m1, nullptr, rows1, 128u, (rows1 + CS_CH - 1) / CS_CH, nullptr, 0u, 0u};
+    const unsigned nblk = js.j[0].nb + js.j[1].nb;
+    if (cbase) {   // one pass (cs_single_kernel)
+        LBSlot sl = lb_acquire(c, (size_t)nblk * 256);
+        hipLaunchKernelGGL(cs_single_kernel, dim3(nblk), dim3(256), 0, c->stream, js, cbase, sl.status, sl.ticket,
+                           sl.epoch);
+        QE_HIP(hipGetLastError());
+        return;
+    }
     uint32_t* part = dalloc_t<uint32_t>(c, (size_t)js.j[0].nb * 256 + (size_t)js.j[1].nb * 128);
     js.j[0].part = part;
     js.j[1].part = part + (size_t)js.j[0].nb * 256;
-    const unsigned nblk = js.j[0].nb + js.j[1].nb;
     hipLaunchKernelGGL(cs_reduce_kernel, dim3(nblk), dim3(256), 0, c->stream, js);
     QE_HIP(hipGetLastError());
     hipLaunchKernelGGL(cs_top_kernel, dim3(2), dim3(1024), 0, c->stream, js);
@@ -2208,6 +2299,26 @@ static void column_scans(qe_ctx* c, uint32_t* m0, uint32_t rows0, uint32_t* m1, 
 // one workgroup per CU.  The unstable ranks count on one block-wide row: QE_PRE_NTU threads there.
 constexpr int PRE_NT = QE_PRE_NT, PRE_NTU = QE_PRE_NTU;
 constexpr int pre_nt(bool unstable) { return unstable ? PRE_NTU : PRE_NT; }
+// The unstable first pass's workgroup takes P1_TM = 2 consecutive counted tiles (1024 threads x
+// 16 words, a 128 KiB LDS stage: one workgroup per CU): each digit run it writes is twice as long
+// (~64 words).  Round 5 on MI355X (C3, 1e8 carried rows): the digit scatter cost pass 1 a third of
+// its time (a contiguous-write ablation: 598 -> 400 us); paired tiles 598 -> 449 us, sort_pass_carry
+// 3.19 -> 3.08 ms per step.  The stable first pass keeps one tile (its 16 per-wave rank rows at
+// 1024 threads measured 0.66 -> 0.74 ms per step).  QE_P1_TM=1 (build knob): single tiles.
+#ifndef QE_P1_TM
+#define QE_P1_TM 2
+#endif
+constexpr int P1_TM = QE_P1_TM;
+static_assert(P1_TM == 1 || (P1_TM == 2 && TL_TPG % 2 == 0), "paired tiles stay inside one group");
+constexpr int p1_tm(bool unstable) { return unstable ? P1_TM : 1; }
+
+static bool cs_single_on() {   // A/B knob: QE_CS_SINGLE=0 keeps the three-launch count scans
+    static bool on = [] {
+        const char* s = getenv("QE_CS_SINGLE");
+        return !(s && s[0] == '0');
+    }();
+    return on;
+}
 
 static bool prof_split() {   // tuning aid: QE_PROF_SPLIT=1 times the second pass under its own name
     static bool on = [] {
@@ -2303,7 +2414,8 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     uint32_t* tcnt = dalloc_t<uint32_t>(c, (size_t)nt * 256);
     uint32_t* gcnt = dalloc_t<uint32_t>(c, (size_t)nseg * 128);
     uint32_t* hist = dalloc_t<uint32_t>(c, TL_BUCKETS);
-    uint32_t* bstart = dalloc_t<uint32_t>(c, TL_BUCKETS + 1);
+    uint32_t* bstart = dalloc_t<uint32_t>(c, TL_BUCKETS + 1 + (cs_single_on() ? 384 : 0));
+    uint32_t* cbase = cs_single_on() ? bstart + TL_BUCKETS + 1 : nullptr;   // the count scans' column bases
     uint32_t* seg = dalloc_t<uint32_t>(c, (size_t)nseg + 1);   // the second pass's segment starts
     // a deferred sort keeps its largest bucket on the device: the consumer checks it there
     // (bucket_join) or reads it when it completes the sort (pairs_need_keys) -- no round trip here
@@ -2344,12 +2456,12 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
                                Q, tcnt, gout);
         QE_HIP(hipGetLastError());
         hist_fold(c, gout, have ? 1u : Q, G, gcnt, hist);
-        hipLaunchKernelGGL(tl_bstart_kernel, dim3(1), dim3(1024), 0, c->stream, hist, bstart, d_max);
+        hipLaunchKernelGGL(tl_bstart_kernel, dim3(1), dim3(1024), 0, c->stream, hist, bstart, d_max, cbase);
         QE_HIP(hipGetLastError());
     }
     {
         Timed t(c, "sort_scan", 8.0 * ((double)nt * 256 + (double)nseg * 128));
-        column_scans(c, tcnt, nt, gcnt, nseg, seg, G, (uint32_t)n);
+        column_scans(c, tcnt, nt, gcnt, nseg, seg, G, (uint32_t)n, cbase);
     }
     uint64_t* w1 = dalloc_t<uint64_t>(c, n);
     uint64_t* w2 = dalloc_t<uint64_t>(c, n);
@@ -2382,12 +2494,12 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     // a deferred sort's consumer needs its buckets, not an order inside them: unstable ranks
     const bool uns = dfr && sort_unstable_on();
 #define QE_P1(IN, CR, UN, XA, XB, XO)                                                                                   \
-    hipLaunchKernelGGL((radix_pass_kernel<K, IN, OUT_WORD, true, 8, RTILE / pre_nt(UN), pre_nt(UN), true, CR, UN>),            \
-                       dim3(xcd_grid(nt)), dim3(pre_nt(UN)), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, \
+    hipLaunchKernelGGL((radix_pass_kernel<K, IN, OUT_WORD, true, 8, RTILE / pre_nt(UN), pre_nt(UN) * p1_tm(UN), true, CR, UN, p1_tm(UN)>),  \
+                       dim3(xcd_grid((nt + p1_tm(UN) - 1) / p1_tm(UN))), dim3(pre_nt(UN) * p1_tm(UN)), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, \
                        255u, f, tcnt, nullptr, nullptr, 0u, XA, XB, XO)
 #define QE_P1N(IN, CR, VIN, XA)                                                                                         \
-    hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true), true, CR, true>),      \
-                       dim3(xcd_grid(nt)), dim3(pre_nt(true)), 0, c->stream, kn, nullptr, VIN, nullptr, w1, vout, n, 32 + L,     \
+    hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true) * P1_TM, true, CR, true, P1_TM>),      \
+                       dim3(xcd_grid((nt + P1_TM - 1) / P1_TM)), dim3(pre_nt(true) * P1_TM), 0, c->stream, kn, nullptr, VIN, nullptr, w1, vout, n, 32 + L,     \
                        255u, f, tcnt, nullptr, nullptr, 0u, XA, nullptr, x1)
 #ifdef QE_DIAG_STAMPS
     stamp_select(c, "p1", n);
@@ -2399,8 +2511,8 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
         Timed t(c, xm ? "sort_pass_carry" : name, (4.0 + (vt ? 4.0 : 0.0) + (xt ? 4.0 : 0.0) + (w32 ? 4.0 : 8.0) +
                                                    (xt ? 4.0 : 0.0)) * n);
         if (w32)
-            hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN_KIOTA, OUT_W32, true, 8, RTILE / pre_nt(true), pre_nt(true), true, X_NONE, true>),
-                               dim3(xcd_grid(nt)), dim3(pre_nt(true)), 0, c->stream, kn, nullptr, nullptr, nullptr, w1, vout, n,
+            hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN_KIOTA, OUT_W32, true, 8, RTILE / pre_nt(true), pre_nt(true) * P1_TM, true, X_NONE, true, P1_TM>),
+                               dim3(xcd_grid((nt + P1_TM - 1) / P1_TM)), dim3(pre_nt(true) * P1_TM), 0, c->stream, kn, nullptr, nullptr, nullptr, w1, vout, n,
                                32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr);
         else if (vt && xt) QE_P1N(IN_KV, X32, vt, xt);
         else if (vt) QE_P1N(IN_KV, X_NONE, vt, nullptr);
@@ -2409,19 +2521,19 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
         QE_HIP(hipGetLastError());
     } else if (w32) {
         Timed t(c, name, ((double)sizeof(K) + 4.0) * n);
-        hipLaunchKernelGGL((radix_pass_kernel<K, IN_KIOTA, OUT_W32, true, 8, RTILE / pre_nt(true), pre_nt(true), true, X_NONE, true>),
-                           dim3(xcd_grid(nt)), dim3(pre_nt(true)), 0, c->stream, keys, nullptr, nullptr, kout, w1, vout, n,
+        hipLaunchKernelGGL((radix_pass_kernel<K, IN_KIOTA, OUT_W32, true, 8, RTILE / pre_nt(true), pre_nt(true) * P1_TM, true, X_NONE, true, P1_TM>),
+                           dim3(xcd_grid((nt + P1_TM - 1) / P1_TM)), dim3(pre_nt(true) * P1_TM), 0, c->stream, keys, nullptr, nullptr, kout, w1, vout, n,
                            32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr);
         QE_HIP(hipGetLastError());
     } else if (cv64) {
         Timed t(c, xm ? "sort_pass_carry" : name, ((double)sizeof(K) + 8.0 + (xm ? 8.0 : 0.0) + 8.0 + (xm ? 4.0 : 0.0)) * n);
         if (xm)
-            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV64, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true), true, XCOL, true>),
-                               dim3(xcd_grid(nt)), dim3(pre_nt(true)), 0, c->stream, keys, nullptr, v64w, kout, w1, vout, n,
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV64, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true) * P1_TM, true, XCOL, true, P1_TM>),
+                               dim3(xcd_grid((nt + P1_TM - 1) / P1_TM)), dim3(pre_nt(true) * P1_TM), 0, c->stream, keys, nullptr, v64w, kout, w1, vout, n,
                                32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, cxa, nullptr, x1);
         else
-            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV64, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true), true, X_NONE, true>),
-                               dim3(xcd_grid(nt)), dim3(pre_nt(true)), 0, c->stream, keys, nullptr, v64w, kout, w1, vout, n,
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV64, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true) * P1_TM, true, X_NONE, true, P1_TM>),
+                               dim3(xcd_grid((nt + P1_TM - 1) / P1_TM)), dim3(pre_nt(true) * P1_TM), 0, c->stream, keys, nullptr, v64w, kout, w1, vout, n,
                                32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr);
         QE_HIP(hipGetLastError());
     } else if (xm == X64) {
@@ -2939,8 +3051,8 @@ void partition_words_kv(qe_ctx* c, const uint64_t* keys, const uint64_t* v64, co
     {
         Timed t(c, "sort_pass_agg", ((kn ? 4.0 : 8.0) + (vn ? 4.0 : v64 ? 8.0 : v32 ? 4.0 : 0.0) + 8.0) * n);
 #define QE_PW1(KT, KP, IN, V)                                                                                            \
-    hipLaunchKernelGGL((radix_pass_kernel<KT, IN, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true), true, X_NONE, true>),        \
-                       dim3(xcd_grid(nt)), dim3(pre_nt(true)), 0, c->stream, KP, nullptr, V, nullptr, w1, nullptr, n,         \
+    hipLaunchKernelGGL((radix_pass_kernel<KT, IN, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true) * P1_TM, true, X_NONE, true, P1_TM>),        \
+                       dim3(xcd_grid((nt + P1_TM - 1) / P1_TM)), dim3(pre_nt(true) * P1_TM), 0, c->stream, KP, nullptr, V, nullptr, w1, nullptr, n,         \
                        32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr)
         if (kn && (vn || v32)) QE_PW1(uint32_t, kn, IN_KV, vn ? vn : v32);
         else if (kn && !v64) QE_PW1(uint32_t, kn, IN_KIOTA, nullptr);
