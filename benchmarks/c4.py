@@ -60,6 +60,17 @@ def cpu_sample(queries: list[str], gpu_ctx, budget_s: float = 20.0) -> dict:
             "seconds": round(t_cpu, 3), "queries": done, "cpu_model": cpu_model(), "parity_with_gpu": cpu_outs == gpu_outs}
 
 
+def install_crash_maps():
+    """QE_CRASH_MAPS=FILE: on SIGSEGV / SIGBUS append the fault address, PC and /proc/self/maps to
+    FILE before the previous handler reports (tools/crashmaps.c; the profiled C4 runs' crash)."""
+    if os.environ.get("QE_CRASH_MAPS"):
+        import ctypes
+        cm = ctypes.CDLL(os.path.join(ROOT, "query-compiler-executor_amd", "build", "libqecrash.so"))
+        cm.qecrash_install.argtypes = [ctypes.c_char_p]
+        if cm.qecrash_install(os.environ["QE_CRASH_MAPS"].encode()) != 0:
+            raise RuntimeError("qecrash_install failed")
+
+
 def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
     import torch
 
@@ -77,14 +88,7 @@ def run_single(args, log, roofline_fn=None, traffic_fn=None) -> dict:
     # faithful executor on the lanes
     workers = int(os.environ.get("QE_WORKERS", "8"))
     plan = getattr(args, "plan", "auto") != "faithful"
-    # QE_CRASH_MAPS=FILE: on SIGSEGV / SIGBUS append the fault address, PC and /proc/self/maps to
-    # FILE before the previous handler reports (tools/crashmaps.c; the profiled C4 runs' crash)
-    if os.environ.get("QE_CRASH_MAPS"):
-        import ctypes
-        cm = ctypes.CDLL(os.path.join(ROOT, "query-compiler-executor_amd", "build", "libqecrash.so"))
-        cm.qecrash_install.argtypes = [ctypes.c_char_p]
-        if cm.qecrash_install(os.environ["QE_CRASH_MAPS"].encode()) != 0:
-            raise RuntimeError("qecrash_install failed")
+    install_crash_maps()
     # QE_BENCH_EVENTS=0: no HIP-event stage table on the lanes (the off switch ADVICE r4 asked to keep)
     events = os.environ.get("QE_BENCH_EVENTS", "1") != "0"
 

@@ -272,6 +272,7 @@ __device__ __forceinline__ uint64_t lookback_wave(uint64_t* status, uint32_t epo
 #define QE_LB_WIN 8
 #endif
 constexpr int LB_WIN = QE_LB_WIN;
+template <int WIN = LB_WIN>
 __device__ __forceinline__ uint64_t lookback_serial(uint64_t* status, uint32_t epoch, uint32_t tile,
                                                     uint32_t stride, uint32_t col, uint32_t* diag = nullptr) {
     uint64_t excl = 0;
@@ -279,15 +280,15 @@ __device__ __forceinline__ uint64_t lookback_serial(uint64_t* status, uint32_t e
     uint32_t spins = 0, rounds = 0;
     while (idx >= 0) {
         rounds++;
-        uint64_t w[LB_WIN];
+        uint64_t w[WIN];
 #pragma unroll
-        for (int q = 0; q < LB_WIN; q++)
+        for (int q = 0; q < WIN; q++)
             w[q] = idx - q >= 0 ? ld_agent(&status[(uint64_t)(idx - q) * stride + col])
                                 : lb_word(epoch, LB_FLAG_INC, 0);
         int used = 0;
         bool done = false, stall = false;
 #pragma unroll
-        for (int q = 0; q < LB_WIN; q++) {
+        for (int q = 0; q < WIN; q++) {
             if (done || stall) continue;
             uint32_t f = lb_flag(w[q], epoch);
             if (f == 0) {

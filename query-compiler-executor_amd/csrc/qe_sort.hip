@@ -652,11 +652,21 @@ __global__ void __launch_bounds__(1024) tl_bstart_kernel(const uint32_t* __restr
         mine += v[k];
         mx = v[k] > mx ? v[k] : mx;
     }
-    if (cbase) {   // (grid-uniform)
-        __syncthreads();
+    if (cbase) {   // (grid-uniform) d1 totals: the 8 lanes of a wave with one t % 8 sum by butterfly
+        uint32_t r[PER];
 #pragma unroll
-        for (int k = 0; k < PER; k++)
-            if (v[k]) atomicAdd(&d1tot[(t & 7) * PER + k], v[k]);
+        for (int k = 0; k < PER; k++) {
+            uint32_t x = v[k];
+            x += __shfl_xor(x, 8, 64);
+            x += __shfl_xor(x, 16, 64);
+            x += __shfl_xor(x, 32, 64);
+            r[k] = x;
+        }
+        __syncthreads();   // (d1tot zeroed)
+        if (lane_id() < 8) {   // 16 waves add their sums: 16-way, not 128-way, per counter
+#pragma unroll
+            for (int k = 0; k < PER; k++) atomicAdd(&d1tot[(t & 7) * PER + k], r[k]);
+        }
     }
     const uint32_t inc = wave_incl_scan_u32(mine);
     mx = wave_max_u32(mx);
@@ -1306,7 +1316,7 @@ __global__ void __launch_bounds__(256) cs_single_kernel(CSJobs js, const uint32_
     st_agent(&status[(uint64_t)gb * 256u + c], lb_word(epoch, blk == 0 ? LB_FLAG_INC : LB_FLAG_AGG, sum));
     uint32_t run = 0;
     if (blk > 0) {
-        run = (uint32_t)lookback_serial(status, epoch, gb, 256u, c);
+        run = (uint32_t)lookback_serial<32>(status, epoch, gb, 256u, c);   // (~190 chunks: <= 6 rounds)
         st_agent(&status[(uint64_t)gb * 256u + c], lb_word(epoch, LB_FLAG_INC, (uint64_t)run + sum));
     }
     run += cbase[(J.C == 256u ? 0u : 256u) + c];
@@ -2299,18 +2309,19 @@ static void column_scans(qe_ctx* c, uint32_t* m0, uint32_t rows0, uint32_t* m1, 
 // one workgroup per CU.  The unstable ranks count on one block-wide row: QE_PRE_NTU threads there.
 constexpr int PRE_NT = QE_PRE_NT, PRE_NTU = QE_PRE_NTU;
 constexpr int pre_nt(bool unstable) { return unstable ? PRE_NTU : PRE_NT; }
-// The unstable first pass's workgroup takes P1_TM = 2 consecutive counted tiles (1024 threads x
-// 16 words, a 128 KiB LDS stage: one workgroup per CU): each digit run it writes is twice as long
-// (~64 words).  Round 5 on MI355X (C3, 1e8 carried rows): the digit scatter cost pass 1 a third of
-// its time (a contiguous-write ablation: 598 -> 400 us); paired tiles 598 -> 449 us, sort_pass_carry
-// 3.19 -> 3.08 ms per step.  The stable first pass keeps one tile (its 16 per-wave rank rows at
-// 1024 threads measured 0.66 -> 0.74 ms per step).  QE_P1_TM=1 (build knob): single tiles.
+// The unstable first pass with a carried payload takes P1_TM = 2 consecutive counted tiles per
+// workgroup (1024 threads x 16 words, a 128 KiB LDS stage: one workgroup per CU): each digit run
+// it writes is twice as long (~64 words).  Round 5 on MI355X (C3, 1e8 carried rows): the digit
+// scatter cost pass 1 a third of its time (a contiguous-write ablation: 598 -> 400 us); paired
+// tiles 598 -> 449 us, sort_pass_carry 3.28 -> 3.12 ms per step.  Passes without a payload (half
+// the bytes per element, the LDS phases a larger share) measured slower paired, 0.67 -> 0.745 ms
+// per step, and keep one tile, as does the stable pass.  QE_P1_TM=1 (build knob): single tiles.
 #ifndef QE_P1_TM
 #define QE_P1_TM 2
 #endif
 constexpr int P1_TM = QE_P1_TM;
 static_assert(P1_TM == 1 || (P1_TM == 2 && TL_TPG % 2 == 0), "paired tiles stay inside one group");
-constexpr int p1_tm(bool unstable) { return unstable ? P1_TM : 1; }
+constexpr int p1_tm(bool unstable, int carry) { return unstable && carry != X_NONE ? P1_TM : 1; }
 
 static bool cs_single_on() {   // A/B knob: QE_CS_SINGLE=0 keeps the three-launch count scans
     static bool on = [] {
@@ -2494,12 +2505,12 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     // a deferred sort's consumer needs its buckets, not an order inside them: unstable ranks
     const bool uns = dfr && sort_unstable_on();
 #define QE_P1(IN, CR, UN, XA, XB, XO)                                                                                   \
-    hipLaunchKernelGGL((radix_pass_kernel<K, IN, OUT_WORD, true, 8, RTILE / pre_nt(UN), pre_nt(UN) * p1_tm(UN), true, CR, UN, p1_tm(UN)>),  \
-                       dim3(xcd_grid((nt + p1_tm(UN) - 1) / p1_tm(UN))), dim3(pre_nt(UN) * p1_tm(UN)), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, \
+    hipLaunchKernelGGL((radix_pass_kernel<K, IN, OUT_WORD, true, 8, RTILE / pre_nt(UN), pre_nt(UN) * p1_tm(UN, CR), true, CR, UN, p1_tm(UN, CR)>),  \
+                       dim3(xcd_grid((nt + p1_tm(UN, CR) - 1) / p1_tm(UN, CR))), dim3(pre_nt(UN) * p1_tm(UN, CR)), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, \
                        255u, f, tcnt, nullptr, nullptr, 0u, XA, XB, XO)
 #define QE_P1N(IN, CR, VIN, XA)                                                                                         \
-    hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true) * P1_TM, true, CR, true, P1_TM>),      \
-                       dim3(xcd_grid((nt + P1_TM - 1) / P1_TM)), dim3(pre_nt(true) * P1_TM), 0, c->stream, kn, nullptr, VIN, nullptr, w1, vout, n, 32 + L,     \
+    hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true) * p1_tm(true, CR), true, CR, true, p1_tm(true, CR)>),      \
+                       dim3(xcd_grid((nt + p1_tm(true, CR) - 1) / p1_tm(true, CR))), dim3(pre_nt(true) * p1_tm(true, CR)), 0, c->stream, kn, nullptr, VIN, nullptr, w1, vout, n, 32 + L,     \
                        255u, f, tcnt, nullptr, nullptr, 0u, XA, nullptr, x1)
 #ifdef QE_DIAG_STAMPS
     stamp_select(c, "p1", n);
@@ -2511,8 +2522,8 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
         Timed t(c, xm ? "sort_pass_carry" : name, (4.0 + (vt ? 4.0 : 0.0) + (xt ? 4.0 : 0.0) + (w32 ? 4.0 : 8.0) +
                                                    (xt ? 4.0 : 0.0)) * n);
         if (w32)
-            hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN_KIOTA, OUT_W32, true, 8, RTILE / pre_nt(true), pre_nt(true) * P1_TM, true, X_NONE, true, P1_TM>),
-                               dim3(xcd_grid((nt + P1_TM - 1) / P1_TM)), dim3(pre_nt(true) * P1_TM), 0, c->stream, kn, nullptr, nullptr, nullptr, w1, vout, n,
+            hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN_KIOTA, OUT_W32, true, 8, RTILE / pre_nt(true), pre_nt(true) * p1_tm(true, X_NONE), true, X_NONE, true, p1_tm(true, X_NONE)>),
+                               dim3(xcd_grid((nt + p1_tm(true, X_NONE) - 1) / p1_tm(true, X_NONE))), dim3(pre_nt(true) * p1_tm(true, X_NONE)), 0, c->stream, kn, nullptr, nullptr, nullptr, w1, vout, n,
                                32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr);
         else if (vt && xt) QE_P1N(IN_KV, X32, vt, xt);
         else if (vt) QE_P1N(IN_KV, X_NONE, vt, nullptr);
@@ -2521,19 +2532,19 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
         QE_HIP(hipGetLastError());
     } else if (w32) {
         Timed t(c, name, ((double)sizeof(K) + 4.0) * n);
-        hipLaunchKernelGGL((radix_pass_kernel<K, IN_KIOTA, OUT_W32, true, 8, RTILE / pre_nt(true), pre_nt(true) * P1_TM, true, X_NONE, true, P1_TM>),
-                           dim3(xcd_grid((nt + P1_TM - 1) / P1_TM)), dim3(pre_nt(true) * P1_TM), 0, c->stream, keys, nullptr, nullptr, kout, w1, vout, n,
+        hipLaunchKernelGGL((radix_pass_kernel<K, IN_KIOTA, OUT_W32, true, 8, RTILE / pre_nt(true), pre_nt(true) * p1_tm(true, X_NONE), true, X_NONE, true, p1_tm(true, X_NONE)>),
+                           dim3(xcd_grid((nt + p1_tm(true, X_NONE) - 1) / p1_tm(true, X_NONE))), dim3(pre_nt(true) * p1_tm(true, X_NONE)), 0, c->stream, keys, nullptr, nullptr, kout, w1, vout, n,
                            32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr);
         QE_HIP(hipGetLastError());
     } else if (cv64) {
         Timed t(c, xm ? "sort_pass_carry" : name, ((double)sizeof(K) + 8.0 + (xm ? 8.0 : 0.0) + 8.0 + (xm ? 4.0 : 0.0)) * n);
         if (xm)
-            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV64, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true) * P1_TM, true, XCOL, true, P1_TM>),
-                               dim3(xcd_grid((nt + P1_TM - 1) / P1_TM)), dim3(pre_nt(true) * P1_TM), 0, c->stream, keys, nullptr, v64w, kout, w1, vout, n,
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV64, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true) * p1_tm(true, XCOL), true, XCOL, true, p1_tm(true, XCOL)>),
+                               dim3(xcd_grid((nt + p1_tm(true, XCOL) - 1) / p1_tm(true, XCOL))), dim3(pre_nt(true) * p1_tm(true, XCOL)), 0, c->stream, keys, nullptr, v64w, kout, w1, vout, n,
                                32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, cxa, nullptr, x1);
         else
-            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV64, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true) * P1_TM, true, X_NONE, true, P1_TM>),
-                               dim3(xcd_grid((nt + P1_TM - 1) / P1_TM)), dim3(pre_nt(true) * P1_TM), 0, c->stream, keys, nullptr, v64w, kout, w1, vout, n,
+            hipLaunchKernelGGL((radix_pass_kernel<K, IN_KV64, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true) * p1_tm(true, X_NONE), true, X_NONE, true, p1_tm(true, X_NONE)>),
+                               dim3(xcd_grid((nt + p1_tm(true, X_NONE) - 1) / p1_tm(true, X_NONE))), dim3(pre_nt(true) * p1_tm(true, X_NONE)), 0, c->stream, keys, nullptr, v64w, kout, w1, vout, n,
                                32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr);
         QE_HIP(hipGetLastError());
     } else if (xm == X64) {
@@ -3051,8 +3062,8 @@ void partition_words_kv(qe_ctx* c, const uint64_t* keys, const uint64_t* v64, co
     {
         Timed t(c, "sort_pass_agg", ((kn ? 4.0 : 8.0) + (vn ? 4.0 : v64 ? 8.0 : v32 ? 4.0 : 0.0) + 8.0) * n);
 #define QE_PW1(KT, KP, IN, V)                                                                                            \
-    hipLaunchKernelGGL((radix_pass_kernel<KT, IN, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true) * P1_TM, true, X_NONE, true, P1_TM>),        \
-                       dim3(xcd_grid((nt + P1_TM - 1) / P1_TM)), dim3(pre_nt(true) * P1_TM), 0, c->stream, KP, nullptr, V, nullptr, w1, nullptr, n,         \
+    hipLaunchKernelGGL((radix_pass_kernel<KT, IN, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true) * p1_tm(true, X_NONE), true, X_NONE, true, p1_tm(true, X_NONE)>),        \
+                       dim3(xcd_grid((nt + p1_tm(true, X_NONE) - 1) / p1_tm(true, X_NONE))), dim3(pre_nt(true) * p1_tm(true, X_NONE)), 0, c->stream, KP, nullptr, V, nullptr, w1, nullptr, n,         \
                        32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr)
         if (kn && (vn || v32)) QE_PW1(uint32_t, kn, IN_KV, vn ? vn : v32);
         else if (kn && !v64) QE_PW1(uint32_t, kn, IN_KIOTA, nullptr);

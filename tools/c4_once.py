@@ -17,6 +17,7 @@ stamp = sys.argv[1]
 plan = (sys.argv[2] if len(sys.argv) > 2 else "plan") == "plan"
 workers = int(sys.argv[3]) if len(sys.argv) > 3 else 8
 torch.cuda.init()
+c4.install_crash_maps()
 ctx = lib.Ctx(0)
 queries = c4.load_queries()
 text = dg.c4_batches(queries)

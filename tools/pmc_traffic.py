@@ -29,8 +29,8 @@ STAGES = [
     (r"radix_pass_kernel<unsigned long, \d, \d, true, \d+, \d+, \d+, true, [123]\b", "sort_pass_carry"),
     (r"tl_pass2_kernel<unsigned long, [12]\b", "sort_pass_carry"),
     # a 64-bit key sort's first pass reading the base column's u32 copy (unstable: deferred sorts only)
-    (r"radix_pass_kernel<unsigned int, \d, \d, true, \d+, \d+, \d+, true, [123], true>", "sort_pass_carry"),
-    (r"radix_pass_kernel<unsigned int, \d, \d, true, \d+, \d+, \d+, true, 0, true>", "sort_pass_k64v32"),
+    (r"radix_pass_kernel<unsigned int, \d, \d, true, \d+, \d+, \d+, true, [123], true(, \d+)?>", "sort_pass_carry"),
+    (r"radix_pass_kernel<unsigned int, \d, \d, true, \d+, \d+, \d+, true, 0, true(, \d+)?>", "sort_pass_k64v32"),
     (r"radix_pass_kernel<unsigned long, \d, \d, true", "sort_pass_k64v32"),
     (r"radix_pass_kernel<unsigned int, \d, \d, true", "sort_pass_k32v32"),
     (r"radix_pass_kernel<unsigned long, \d, \d, false", "sort_pass_k64"),
@@ -39,7 +39,7 @@ STAGES = [
     (r"tl_pass2_kernel<unsigned long(, 0\b[^>]*)?>", "sort_pass_k64v32"),
     (r"tl_pass2_kernel<unsigned int(, 0\b[^>]*)?>", "sort_pass_k32v32"),
     (r"digit_hist_kernel|digit_scan_kernel|tl_hist_kernel|tl_hist8_kernel|tl_hist_tiles_kernel|tl_gfold_kernel|tl_bstart_kernel|tl_scan_kernel|tl_scan8_kernel", "sort_hist"),
-    (r"cs_reduce_kernel|cs_top_kernel|cs_apply_kernel", "sort_scan"),
+    (r"cs_reduce_kernel|cs_top_kernel|cs_apply_kernel|cs_single_kernel", "sort_scan"),
     (r"tl_local_kernel", "sort_local"),
     (r"bucket_select_kernel", "bucket_select"),
     (r"part_count_kernel", "partition_count"),
