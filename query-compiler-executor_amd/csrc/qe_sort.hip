@@ -600,6 +600,142 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
     QE_SORT_STAMP(tile, 6);
 }
 
+// The same first pass (PRE, unstable, paired tiles) for u32 keys (+ u32 values) with a u32 payload,
+// as a RESIDENT grid: one 1024-thread workgroup per CU walks its tiles, and the next tile's keys
+// (+ values) are loaded as soon as this tile's words are staged in LDS -- into the registers the
+// words leave -- so their load latency runs under this tile's offset phase and write-out instead
+// of opening the next tile (round-5 stamps of the one-tile-per-workgroup form: 6.5 of a 17.4 us
+// tile from the first load to the last rank, the memory idle through ~5 us of LDS phases).
+// XCD x (blockIdx % 8) walks a contiguous eighth of the tiles, its workgroups interleaved, so
+// neighbouring tiles still run on one XCD at the same time (their digit runs share lines in L2).
+// (IN_KIOTA compiles too but spills: its 16 generated row indices are hoisted out of the loop)
+template <int IN>
+__global__ void __launch_bounds__(1024) p1_resident_kernel(const uint32_t* __restrict__ kin,
+                                                           const uint32_t* __restrict__ vin, uint64_t* __restrict__ wout,
+                                                           uint64_t n, int dsh, Field f,
+                                                           const uint32_t* __restrict__ offs,
+                                                           const uint32_t* __restrict__ xa, uint32_t* __restrict__ xout) {
+    static_assert(IN == IN_KV || IN == IN_KIOTA, "u32 keys, with or without u32 values");
+    constexpr int NT = 1024, ITEMS = 16, TILE = NT * ITEMS, BINS = 256, WT = 64 * ITEMS, TMC = TILE / RTILE;
+    __shared__ uint64_t stage[TILE];
+    __shared__ uint8_t sdig[TILE];   // each slot's digit: the payload write-out finds its destination
+    __shared__ uint32_t whist[BINS], bexcl[BINS], gofs[BINS], wsum[4];
+    const int w = wave_id(), l = lane_id();
+    const bool owner = threadIdx.x < (unsigned)BINS;
+    const uint32_t ntile = (uint32_t)((n + TILE - 1) / TILE);
+    const uint32_t x8 = blockIdx.x & 7u, G8 = gridDim.x >> 3, per = (ntile + 7u) / 8u;
+    const uint32_t t_lo = x8 * per, t_hi = t_lo + per < ntile ? t_lo + per : ntile;
+    auto loc_of = [&](int j) -> uint32_t {   // element j of this lane: 4 consecutive per 16-B load
+        return (uint32_t)w * WT + (uint32_t)(j >> 2) * 256u + (uint32_t)l * 4u + (uint32_t)(j & 3);
+    };
+    auto load_v4 = [&](const uint32_t* a, uint64_t tb, uint32_t bytes, uint32_t (&v)[ITEMS]) {
+        const auto r = buf_rsrc(a + tb, bytes);   // (past `bytes`: 0)
+#pragma unroll
+        for (int g = 0; g < ITEMS / 4; g++) {
+            const uint4 q = buf_load_u4(r, ((uint32_t)w * WT + (uint32_t)l * 4u + (uint32_t)g * 256u) * 4u, 0u);
+            v[4 * g] = q.x;
+            v[4 * g + 1] = q.y;
+            v[4 * g + 2] = q.z;
+            v[4 * g + 3] = q.w;
+        }
+    };
+    uint32_t kk[ITEMS], vv[ITEMS];
+    auto load_tile = [&](uint32_t t) {   // t >= t_hi: an empty range (every load returns 0)
+        const bool live = t < t_hi;
+        const uint64_t tb = live ? (uint64_t)t * TILE : 0u;
+        const uint32_t tc = !live ? 0u : (uint32_t)((n - tb) < (uint64_t)TILE ? (n - tb) : (uint64_t)TILE);
+        const uint32_t bytes = (tc * 4u + 15u) & ~15u;
+        load_v4(kin, tb, bytes, kk);
+        if constexpr (IN == IN_KV) load_v4(vin, tb, bytes, vv);
+    };
+    // (the next tile's digit offsets are loaded with its keys: a load issued after this tile's
+    // stores would wait for them -- gfx9 counts loads and stores on one in-order counter)
+    auto load_off = [&](uint32_t t) -> uint32_t {
+        return owner && t < t_hi ? offs[(uint64_t)t * TMC * BINS + threadIdx.x] : 0u;
+    };
+    uint32_t tile = t_lo + (blockIdx.x >> 3);
+    load_tile(tile);
+    uint32_t pre_next = load_off(tile);
+    for (; tile < t_hi; tile += G8) {   // (block-uniform)
+        const uint64_t tb = (uint64_t)tile * TILE;
+        const uint32_t tcount = (uint32_t)((n - tb) < (uint64_t)TILE ? (n - tb) : (uint64_t)TILE);
+        const uint32_t pre_off = pre_next;
+        if (owner) whist[threadIdx.x] = 0;
+        __syncthreads();
+        uint64_t word[ITEMS];
+        uint32_t pos[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++)
+            word[j] = ((((uint64_t)kk[j] >> f.lo) & f.fmask) << 32) | (IN == IN_KV ? vv[j] : (uint32_t)(tb + loc_of(j)));
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint32_t d = (uint32_t)(word[j] >> dsh) & 255u;
+            pos[j] = loc_of(j) < tcount ? atomicAdd(&whist[d], 1u) : 0u;
+        }
+        __syncthreads();
+        const uint32_t tot = owner ? whist[threadIdx.x] : 0u, inc = wave_incl_scan_u32(tot);
+        if (w < 4 && l == 63) wsum[w] = inc;
+        __syncthreads();
+        if (owner) {
+            uint32_t ex = inc - tot;
+            for (int ww = 0; ww < w; ww++) ex += wsum[ww];
+            bexcl[threadIdx.x] = ex;
+            gofs[threadIdx.x] = pre_off - ex;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            if (loc_of(j) < tcount) {
+                const uint32_t d = (uint32_t)(word[j] >> dsh) & 255u, slot = bexcl[d] + pos[j];
+                stage[slot] = word[j];
+                sdig[slot] = (uint8_t)d;
+                pos[j] = slot;   // the payload takes the same slot later
+            }
+        }
+        // this tile's payloads, then the next tile's keys (+ values): in flight during the write-out
+        uint32_t xw[ITEMS];
+        load_v4(xa, tb, (tcount * 4u + 15u) & ~15u, xw);
+        load_tile(tile + G8);
+        pre_next = load_off(tile + G8);
+        __syncthreads();
+#ifndef QE_P1R_CH
+#define QE_P1R_CH 4
+#endif
+        constexpr int RW_CH = QE_P1R_CH;   // (8 spilled: the next tile's loads hold 32 registers)
+#pragma unroll
+        for (int k0 = 0; k0 < ITEMS; k0 += RW_CH) {
+            uint64_t wd[RW_CH];
+            uint32_t pp[RW_CH];
+#pragma unroll
+            for (int q = 0; q < RW_CH; q++) wd[q] = stage[(uint32_t)(k0 + q) * NT + threadIdx.x];
+#pragma unroll
+            for (int q = 0; q < RW_CH; q++)
+                pp[q] = gofs[(uint32_t)(wd[q] >> dsh) & 255u] + (uint32_t)(k0 + q) * NT + threadIdx.x;
+#pragma unroll
+            for (int q = 0; q < RW_CH; q++) {
+                const uint32_t i = (uint32_t)(k0 + q) * NT + threadIdx.x, p = pp[q];
+                const bool ok = i < tcount && (uint64_t)p < n;
+                QE_ST(ok ? &wout[p] : &g_store_sink[l], wd[q]);   // (every store issued: no branch)
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();   // every word is out of the stage
+        uint32_t* st32 = reinterpret_cast<uint32_t*>(stage);
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++)
+            if (loc_of(j) < tcount) st32[pos[j]] = xw[j];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < ITEMS; k++) {
+            const uint32_t i = (uint32_t)k * NT + threadIdx.x, p = gofs[sdig[i]] + i;
+            const bool ok = i < tcount && (uint64_t)p < n;
+            QE_ST(ok ? &xout[p] : reinterpret_cast<uint32_t*>(&g_store_sink[l]), st32[i]);
+        }
+        // (the next iteration's first LDS writes -- whist -- come before two barriers that every
+        // thread reaches only after this write-out: no barrier needed here)
+    }
+}
+
 // ---- two-level sort: 14 high bits by two global passes, the rest inside LDS per bucket ---------
 // For 20..31 varying bits: the top H = 15 bits split the array into 32768 buckets (~4 K words
 // each at 10^8 keys below 10^8 -- keys rarely fill their top bit's range, so H leaves room);
@@ -637,36 +773,23 @@ __global__ void __launch_bounds__(1024) tl_hist_kernel(const K* __restrict__ key
 // computes its digit bases in the count scans, so it needs none of tl_scan_kernel's marginals
 // (whose serial loops made that kernel ~22 us per sort)
 // cbase (nullable): the two count scans' column bases, 256 + 128 words -- cbase[d1] = the keys with
-// a smaller first-pass digit (d1 = bucket bits 0-7), cbase[256 + d2] = bstart[d2 << 8]
+// a smaller first-pass digit (d1 = bucket bits 0-7; from d1part, tl_gfold_kernel's four partial
+// sums per d1), cbase[256 + d2] = bstart[d2 << 8]
 __global__ void __launch_bounds__(1024) tl_bstart_kernel(const uint32_t* __restrict__ hist, uint32_t* __restrict__ bstart,
-                                                         uint64_t* __restrict__ maxb, uint32_t* __restrict__ cbase = nullptr) {
+                                                         uint64_t* __restrict__ maxb, uint32_t* __restrict__ cbase = nullptr,
+                                                         const uint32_t* __restrict__ d1part = nullptr) {
     constexpr int PER = TL_BUCKETS / 1024;
-    static_assert(PER == 32 && TL_BUCKETS == 128 * 256, "thread t holds d2 = t / 8, d1 = (t % 8) * 32 + k");
-    __shared__ uint32_t wsum[16], wmax[16], d1tot[256];
+    static_assert(PER == 32 && TL_BUCKETS == 128 * 256, "thread t holds buckets t * 32 .. t * 32 + 31");
+    __shared__ uint32_t wsum[16], wmax[16];
     const int t = threadIdx.x;
-    if (cbase && t < 256) d1tot[t] = 0;
+    uint4 dp = make_uint4(0, 0, 0, 0);
+    if (cbase && t < 256) dp = reinterpret_cast<const uint4*>(d1part)[t];
     uint32_t v[PER], mine = 0, mx = 0;
 #pragma unroll
     for (int k = 0; k < PER; k++) {
         v[k] = hist[t * PER + k];
         mine += v[k];
         mx = v[k] > mx ? v[k] : mx;
-    }
-    if (cbase) {   // (grid-uniform) d1 totals: the 8 lanes of a wave with one t % 8 sum by butterfly
-        uint32_t r[PER];
-#pragma unroll
-        for (int k = 0; k < PER; k++) {
-            uint32_t x = v[k];
-            x += __shfl_xor(x, 8, 64);
-            x += __shfl_xor(x, 16, 64);
-            x += __shfl_xor(x, 32, 64);
-            r[k] = x;
-        }
-        __syncthreads();   // (d1tot zeroed)
-        if (lane_id() < 8) {   // 16 waves add their sums: 16-way, not 128-way, per counter
-#pragma unroll
-            for (int k = 0; k < PER; k++) atomicAdd(&d1tot[(t & 7) * PER + k], r[k]);
-        }
     }
     const uint32_t inc = wave_incl_scan_u32(mine);
     mx = wave_max_u32(mx);
@@ -689,8 +812,8 @@ __global__ void __launch_bounds__(1024) tl_bstart_kernel(const uint32_t* __restr
     }
     if (!cbase) return;   // (grid-uniform)
     if ((t & 7) == 0) cbase[256 + (t >> 3)] = bstart_first;   // (bucket t * PER = d2 << 8)
-    __syncthreads();   // d1tot complete (and wmax read)
-    const uint32_t x = t < 256 ? d1tot[t] : 0u, i1 = wave_incl_scan_u32(x);
+    __syncthreads();   // (wmax read)
+    const uint32_t x = dp.x + dp.y + dp.z + dp.w, i1 = wave_incl_scan_u32(x);
     if (t < 256 && lane_id() == 63) wmax[wave_id()] = i1;   // (wmax reused: the first 4 waves' totals)
     __syncthreads();
     if (t < 256) {
@@ -1148,7 +1271,8 @@ __global__ void __launch_bounds__(1024) tl_gather_hist_kernel(const uint64_t* __
 // natural order (bucket = d2 << 8 | d1) from the segment counts.  Block = (d1, 32 d2's) x 8 group
 // lanes, G x Q / 8 (~32) independent loads per thread; the lanes' sums meet in LDS.
 __global__ void __launch_bounds__(256) tl_gfold_kernel(const uint32_t* __restrict__ src, uint32_t Q, uint32_t G,
-                                                       uint32_t* __restrict__ dst, uint32_t* __restrict__ hist) {
+                                                       uint32_t* __restrict__ dst, uint32_t* __restrict__ hist,
+                                                       uint32_t* __restrict__ d1part = nullptr) {
     __shared__ uint32_t part[8][32];
     const uint32_t d1 = blockIdx.x >> 2, d2 = (blockIdx.x & 3u) * 32u + (threadIdx.x & 31u), gl = threadIdx.x >> 5;
     const uint64_t S = (uint64_t)256u * G * 128u;
@@ -1170,6 +1294,11 @@ __global__ void __launch_bounds__(256) tl_gfold_kernel(const uint32_t* __restric
 #pragma unroll
         for (int j = 0; j < 8; j++) t += part[j][threadIdx.x];
         hist[(d2 << 8) | d1] = t;
+        if (d1part) {   // (grid-uniform) this block's 32 d2's summed: d1part[d1 * 4 + quarter]
+#pragma unroll
+            for (int m = 16; m >= 1; m >>= 1) t += (uint32_t)__shfl_xor((int)t, m, 32);
+            if (threadIdx.x == 0) d1part[blockIdx.x] = t;
+        }
     }
 }
 
@@ -1296,39 +1425,54 @@ __global__ void __launch_bounds__(256) cs_apply_kernel(CSJobs js) {
 // lookback per column (thread c walks column c's status words), as the sort passes do per digit.
 // Every count is read once and written once (the three-launch form read them twice: 1.54x the
 // algorithmic bytes in PMC, round 4), and the one-block middle launch is gone.
-__global__ void __launch_bounds__(256) cs_single_kernel(CSJobs js, const uint32_t* __restrict__ cbase,
-                                                        uint64_t* status, uint32_t* ticket, uint32_t epoch) {
+// 1024 threads per block: thread (q, c) owns CS_CH rows of column c (q < 1024 / C row groups), so a
+// block covers 256 (C = 256) or 512 (C = 128) rows and the lookback chain is that much shorter
+// (~48 links at 1e8 keys instead of ~190: with 64-row blocks the walks, 8 status words a round,
+// cost more than the reads -- 17.6 us per sort, and 21 us with 32-word rounds).
+__global__ void __launch_bounds__(1024) cs_single_kernel(CSJobs js, const uint32_t* __restrict__ cbase,
+                                                         uint64_t* status, uint32_t* ticket, uint32_t epoch) {
     __shared__ uint32_t s_ticket;
+    __shared__ uint32_t gsum[1024];   // per (row group, column): the group's sum
+    __shared__ uint32_t spre[256];    // per column: the rows above this block
     const uint32_t gb = take_ticket(ticket, &s_ticket);   // predecessors in ticket order are resident
     uint32_t blk = gb;
     const CSJob& J = cs_job(js, blk);
-    const uint32_t c = threadIdx.x, r0 = blk * CS_CH;
-    if (c >= J.C) return;
-    const uint32_t nrow = J.rows - r0 < CS_CH ? J.rows - r0 : CS_CH;
-    const auto rm = buf_rsrc(J.m + (uint64_t)r0 * J.C, nrow * J.C * 4u);
+    const uint32_t C = J.C, QN = 1024u / C, c = threadIdx.x % C, q = threadIdx.x / C;
+    const uint32_t r0 = (blk * QN + q) * CS_CH;
+    const uint32_t nrow = r0 >= J.rows ? 0u : (J.rows - r0 < CS_CH ? J.rows - r0 : CS_CH);
+    const auto rm = buf_rsrc(J.m + (uint64_t)(nrow ? r0 : 0u) * C, nrow * C * 4u);
     uint32_t v[CS_CH];
 #pragma unroll
-    for (uint32_t r = 0; r < CS_CH; r++) v[r] = buf_load_u32(rm, (r * J.C + c) * 4u, 0u);   // (past the matrix: 0)
+    for (uint32_t r = 0; r < CS_CH; r++) v[r] = buf_load_u32(rm, (r * C + c) * 4u, 0u);   // (past the matrix: 0)
     uint32_t sum = 0;
 #pragma unroll
     for (uint32_t r = 0; r < CS_CH; r++) sum += v[r];
-    // a job's first chunk publishes its inclusive sum at once and ends every walk of that job
-    st_agent(&status[(uint64_t)gb * 256u + c], lb_word(epoch, blk == 0 ? LB_FLAG_INC : LB_FLAG_AGG, sum));
-    uint32_t run = 0;
-    if (blk > 0) {
-        run = (uint32_t)lookback_serial<32>(status, epoch, gb, 256u, c);   // (~190 chunks: <= 6 rounds)
-        st_agent(&status[(uint64_t)gb * 256u + c], lb_word(epoch, LB_FLAG_INC, (uint64_t)run + sum));
+    gsum[threadIdx.x] = sum;   // (= gsum[q * C + c])
+    __syncthreads();
+    if (q == 0) {
+        uint32_t tot = 0;
+        for (uint32_t k = 0; k < QN; k++) tot += gsum[k * C + c];
+        // a job's first block publishes its inclusive sum at once and ends every walk of that job
+        st_agent(&status[(uint64_t)gb * 256u + c], lb_word(epoch, blk == 0 ? LB_FLAG_INC : LB_FLAG_AGG, tot));
+        uint32_t ex = 0;
+        if (blk > 0) {
+            ex = (uint32_t)lookback_serial(status, epoch, gb, 256u, c);
+            st_agent(&status[(uint64_t)gb * 256u + c], lb_word(epoch, LB_FLAG_INC, (uint64_t)ex + tot));
+        }
+        spre[c] = ex;
     }
-    run += cbase[(J.C == 256u ? 0u : 256u) + c];
+    __syncthreads();
+    uint32_t run = cbase[(C == 256u ? 0u : 256u) + c] + spre[c];
+    for (uint32_t k = 0; k < q; k++) run += gsum[k * C + c];
 #pragma unroll
     for (uint32_t r = 0; r < CS_CH; r++) {
         if (r < nrow) {
-            J.m[(uint64_t)(r0 + r) * J.C + c] = run;
+            J.m[(uint64_t)(r0 + r) * C + c] = run;
             if (J.seg && (r0 + r) % TL_TPG == 0) J.seg[c * J.G + (r0 + r) / TL_TPG] = run;
         }
         run += v[r];
     }
-    if (J.seg && blk == 0 && c == 0) J.seg[J.C * J.G] = J.ntot;
+    if (J.seg && gb == 0 && threadIdx.x == 0) J.seg[C * J.G] = J.ntot;
 }
 
 // pass 2: one workgroup per segment s = d1 * G + g (the run of group g's keys with first-pass
@@ -2279,9 +2423,13 @@ static void column_scans(qe_ctx* c, uint32_t* m0, uint32_t rows0, uint32_t* m1, 
     js.j[0] = CSJob{m0, nullptr, rows0, 256u, (rows0 + CS_CH - 1) / CS_CH, seg, G, ntot};
     js.j[1] = CSJob{m1, nullptr, rows1, 128u, (rows1 + CS_CH - 1) / CS_CH, nullptr, 0u, 0u};
     const unsigned nblk = js.j[0].nb + js.j[1].nb;
-    if (cbase) {   // one pass (cs_single_kernel)
-        LBSlot sl = lb_acquire(c, (size_t)nblk * 256);
-        hipLaunchKernelGGL(cs_single_kernel, dim3(nblk), dim3(256), 0, c->stream, js, cbase, sl.status, sl.ticket,
+    if (cbase) {   // one pass (cs_single_kernel): blocks of 1024 / C row groups of CS_CH rows
+        CSJobs j1 = js;
+        j1.j[0].nb = (rows0 + 4 * CS_CH - 1) / (4 * CS_CH);
+        j1.j[1].nb = (rows1 + 8 * CS_CH - 1) / (8 * CS_CH);
+        const unsigned nb1 = j1.j[0].nb + j1.j[1].nb;
+        LBSlot sl = lb_acquire(c, (size_t)nb1 * 256);
+        hipLaunchKernelGGL(cs_single_kernel, dim3(nb1), dim3(1024), 0, c->stream, j1, cbase, sl.status, sl.ticket,
                            sl.epoch);
         QE_HIP(hipGetLastError());
         return;
@@ -2322,6 +2470,14 @@ constexpr int pre_nt(bool unstable) { return unstable ? PRE_NTU : PRE_NT; }
 constexpr int P1_TM = QE_P1_TM;
 static_assert(P1_TM == 1 || (P1_TM == 2 && TL_TPG % 2 == 0), "paired tiles stay inside one group");
 constexpr int p1_tm(bool unstable, int carry) { return unstable && carry != X_NONE ? P1_TM : 1; }
+
+static bool p1_resident_on() {   // A/B knob: QE_P1_RESIDENT=0 launches a workgroup per tile pair
+    static bool on = [] {
+        const char* s = getenv("QE_P1_RESIDENT");
+        return !(s && s[0] == '0');
+    }();
+    return on;
+}
 
 static bool cs_single_on() {   // A/B knob: QE_CS_SINGLE=0 keeps the three-launch count scans
     static bool on = [] {
@@ -2403,10 +2559,11 @@ static void local_sort_buckets(qe_ctx* c, const uint64_t* words, K* kout, uint32
 static uint32_t* hist_slices(qe_ctx* c, uint32_t* gcnt, uint32_t Q, uint32_t nseg) {
     return Q > 1 ? dalloc_t<uint32_t>(c, (size_t)Q * nseg * 128) : gcnt;
 }
-static void hist_fold(qe_ctx* c, uint32_t* gout, uint32_t Q, uint32_t G, uint32_t* gcnt, uint32_t* hist) {
+static void hist_fold(qe_ctx* c, uint32_t* gout, uint32_t Q, uint32_t G, uint32_t* gcnt, uint32_t* hist,
+                      uint32_t* d1part = nullptr) {
     if (gout != gcnt || hist) {
         hipLaunchKernelGGL(tl_gfold_kernel, dim3(1024), dim3(256), 0, c->stream, gout, gout != gcnt ? Q : 1u, G, gcnt,
-                           hist);
+                           hist, d1part);
         QE_HIP(hipGetLastError());
     }
     if (gout != gcnt) dfree(c, gout);
@@ -2425,8 +2582,10 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     uint32_t* tcnt = dalloc_t<uint32_t>(c, (size_t)nt * 256);
     uint32_t* gcnt = dalloc_t<uint32_t>(c, (size_t)nseg * 128);
     uint32_t* hist = dalloc_t<uint32_t>(c, TL_BUCKETS);
-    uint32_t* bstart = dalloc_t<uint32_t>(c, TL_BUCKETS + 1 + (cs_single_on() ? 384 : 0));
-    uint32_t* cbase = cs_single_on() ? bstart + TL_BUCKETS + 1 : nullptr;   // the count scans' column bases
+    // (+ the count scans' column bases and the d1 partial sums they come from, 16-B aligned)
+    uint32_t* bstart = dalloc_t<uint32_t>(c, TL_BUCKETS + 4 + (cs_single_on() ? 384 + 1024 : 0));
+    uint32_t* cbase = cs_single_on() ? bstart + TL_BUCKETS + 4 : nullptr;
+    uint32_t* d1part = cs_single_on() ? cbase + 384 : nullptr;
     uint32_t* seg = dalloc_t<uint32_t>(c, (size_t)nseg + 1);   // the second pass's segment starts
     // a deferred sort keeps its largest bucket on the device: the consumer checks it there
     // (bucket_join) or reads it when it completes the sort (pairs_need_keys) -- no round trip here
@@ -2466,8 +2625,8 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
             hipLaunchKernelGGL((tl_hist_tiles_kernel<K>), dim3(G * Q), dim3(1024), 0, c->stream, keys, n, f, L, nt, G,
                                Q, tcnt, gout);
         QE_HIP(hipGetLastError());
-        hist_fold(c, gout, have ? 1u : Q, G, gcnt, hist);
-        hipLaunchKernelGGL(tl_bstart_kernel, dim3(1), dim3(1024), 0, c->stream, hist, bstart, d_max, cbase);
+        hist_fold(c, gout, have ? 1u : Q, G, gcnt, hist, d1part);
+        hipLaunchKernelGGL(tl_bstart_kernel, dim3(1), dim3(1024), 0, c->stream, hist, bstart, d_max, cbase, d1part);
         QE_HIP(hipGetLastError());
     }
     {
@@ -2525,6 +2684,15 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
             hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN_KIOTA, OUT_W32, true, 8, RTILE / pre_nt(true), pre_nt(true) * p1_tm(true, X_NONE), true, X_NONE, true, p1_tm(true, X_NONE)>),
                                dim3(xcd_grid((nt + p1_tm(true, X_NONE) - 1) / p1_tm(true, X_NONE))), dim3(pre_nt(true) * p1_tm(true, X_NONE)), 0, c->stream, kn, nullptr, nullptr, nullptr, w1, vout, n,
                                32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr);
+        else if (vt && xt && p1_resident_on()) {   // the resident form (p1_resident_kernel)
+            static const uint32_t grid = [&] {
+                int ncu = 0;
+                QE_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
+                return (uint32_t)std::max(8, ncu / 8 * 8);   // one workgroup per CU (its 144 KiB of LDS)
+            }();
+            hipLaunchKernelGGL(p1_resident_kernel<IN_KV>, dim3(grid), dim3(1024), 0, c->stream, kn, vt, w1, n, 32 + L, f,
+                               tcnt, xt, reinterpret_cast<uint32_t*>(x1));
+        }
         else if (vt && xt) QE_P1N(IN_KV, X32, vt, xt);
         else if (vt) QE_P1N(IN_KV, X_NONE, vt, nullptr);
         else if (xt) QE_P1N(IN_KIOTA, X32, nullptr, xt);
