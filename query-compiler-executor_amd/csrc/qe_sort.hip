@@ -600,142 +600,6 @@ __global__ void __launch_bounds__(NT) radix_pass_kernel(const K* __restrict__ ki
     QE_SORT_STAMP(tile, 6);
 }
 
-// The same first pass (PRE, unstable, paired tiles) for u32 keys (+ u32 values) with a u32 payload,
-// as a RESIDENT grid: one 1024-thread workgroup per CU walks its tiles, and the next tile's keys
-// (+ values) are loaded as soon as this tile's words are staged in LDS -- into the registers the
-// words leave -- so their load latency runs under this tile's offset phase and write-out instead
-// of opening the next tile (round-5 stamps of the one-tile-per-workgroup form: 6.5 of a 17.4 us
-// tile from the first load to the last rank, the memory idle through ~5 us of LDS phases).
-// XCD x (blockIdx % 8) walks a contiguous eighth of the tiles, its workgroups interleaved, so
-// neighbouring tiles still run on one XCD at the same time (their digit runs share lines in L2).
-// (IN_KIOTA compiles too but spills: its 16 generated row indices are hoisted out of the loop)
-template <int IN>
-__global__ void __launch_bounds__(1024) p1_resident_kernel(const uint32_t* __restrict__ kin,
-                                                           const uint32_t* __restrict__ vin, uint64_t* __restrict__ wout,
-                                                           uint64_t n, int dsh, Field f,
-                                                           const uint32_t* __restrict__ offs,
-                                                           const uint32_t* __restrict__ xa, uint32_t* __restrict__ xout) {
-    static_assert(IN == IN_KV || IN == IN_KIOTA, "u32 keys, with or without u32 values");
-    constexpr int NT = 1024, ITEMS = 16, TILE = NT * ITEMS, BINS = 256, WT = 64 * ITEMS, TMC = TILE / RTILE;
-    __shared__ uint64_t stage[TILE];
-    __shared__ uint8_t sdig[TILE];   // each slot's digit: the payload write-out finds its destination
-    __shared__ uint32_t whist[BINS], bexcl[BINS], gofs[BINS], wsum[4];
-    const int w = wave_id(), l = lane_id();
-    const bool owner = threadIdx.x < (unsigned)BINS;
-    const uint32_t ntile = (uint32_t)((n + TILE - 1) / TILE);
-    const uint32_t x8 = blockIdx.x & 7u, G8 = gridDim.x >> 3, per = (ntile + 7u) / 8u;
-    const uint32_t t_lo = x8 * per, t_hi = t_lo + per < ntile ? t_lo + per : ntile;
-    auto loc_of = [&](int j) -> uint32_t {   // element j of this lane: 4 consecutive per 16-B load
-        return (uint32_t)w * WT + (uint32_t)(j >> 2) * 256u + (uint32_t)l * 4u + (uint32_t)(j & 3);
-    };
-    auto load_v4 = [&](const uint32_t* a, uint64_t tb, uint32_t bytes, uint32_t (&v)[ITEMS]) {
-        const auto r = buf_rsrc(a + tb, bytes);   // (past `bytes`: 0)
-#pragma unroll
-        for (int g = 0; g < ITEMS / 4; g++) {
-            const uint4 q = buf_load_u4(r, ((uint32_t)w * WT + (uint32_t)l * 4u + (uint32_t)g * 256u) * 4u, 0u);
-            v[4 * g] = q.x;
-            v[4 * g + 1] = q.y;
-            v[4 * g + 2] = q.z;
-            v[4 * g + 3] = q.w;
-        }
-    };
-    uint32_t kk[ITEMS], vv[ITEMS];
-    auto load_tile = [&](uint32_t t) {   // t >= t_hi: an empty range (every load returns 0)
-        const bool live = t < t_hi;
-        const uint64_t tb = live ? (uint64_t)t * TILE : 0u;
-        const uint32_t tc = !live ? 0u : (uint32_t)((n - tb) < (uint64_t)TILE ? (n - tb) : (uint64_t)TILE);
-        const uint32_t bytes = (tc * 4u + 15u) & ~15u;
-        load_v4(kin, tb, bytes, kk);
-        if constexpr (IN == IN_KV) load_v4(vin, tb, bytes, vv);
-    };
-    // (the next tile's digit offsets are loaded with its keys: a load issued after this tile's
-    // stores would wait for them -- gfx9 counts loads and stores on one in-order counter)
-    auto load_off = [&](uint32_t t) -> uint32_t {
-        return owner && t < t_hi ? offs[(uint64_t)t * TMC * BINS + threadIdx.x] : 0u;
-    };
-    uint32_t tile = t_lo + (blockIdx.x >> 3);
-    load_tile(tile);
-    uint32_t pre_next = load_off(tile);
-    for (; tile < t_hi; tile += G8) {   // (block-uniform)
-        const uint64_t tb = (uint64_t)tile * TILE;
-        const uint32_t tcount = (uint32_t)((n - tb) < (uint64_t)TILE ? (n - tb) : (uint64_t)TILE);
-        const uint32_t pre_off = pre_next;
-        if (owner) whist[threadIdx.x] = 0;
-        __syncthreads();
-        uint64_t word[ITEMS];
-        uint32_t pos[ITEMS];
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++)
-            word[j] = ((((uint64_t)kk[j] >> f.lo) & f.fmask) << 32) | (IN == IN_KV ? vv[j] : (uint32_t)(tb + loc_of(j)));
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const uint32_t d = (uint32_t)(word[j] >> dsh) & 255u;
-            pos[j] = loc_of(j) < tcount ? atomicAdd(&whist[d], 1u) : 0u;
-        }
-        __syncthreads();
-        const uint32_t tot = owner ? whist[threadIdx.x] : 0u, inc = wave_incl_scan_u32(tot);
-        if (w < 4 && l == 63) wsum[w] = inc;
-        __syncthreads();
-        if (owner) {
-            uint32_t ex = inc - tot;
-            for (int ww = 0; ww < w; ww++) ex += wsum[ww];
-            bexcl[threadIdx.x] = ex;
-            gofs[threadIdx.x] = pre_off - ex;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            if (loc_of(j) < tcount) {
-                const uint32_t d = (uint32_t)(word[j] >> dsh) & 255u, slot = bexcl[d] + pos[j];
-                stage[slot] = word[j];
-                sdig[slot] = (uint8_t)d;
-                pos[j] = slot;   // the payload takes the same slot later
-            }
-        }
-        // this tile's payloads, then the next tile's keys (+ values): in flight during the write-out
-        uint32_t xw[ITEMS];
-        load_v4(xa, tb, (tcount * 4u + 15u) & ~15u, xw);
-        load_tile(tile + G8);
-        pre_next = load_off(tile + G8);
-        __syncthreads();
-#ifndef QE_P1R_CH
-#define QE_P1R_CH 4
-#endif
-        constexpr int RW_CH = QE_P1R_CH;   // (8 spilled: the next tile's loads hold 32 registers)
-#pragma unroll
-        for (int k0 = 0; k0 < ITEMS; k0 += RW_CH) {
-            uint64_t wd[RW_CH];
-            uint32_t pp[RW_CH];
-#pragma unroll
-            for (int q = 0; q < RW_CH; q++) wd[q] = stage[(uint32_t)(k0 + q) * NT + threadIdx.x];
-#pragma unroll
-            for (int q = 0; q < RW_CH; q++)
-                pp[q] = gofs[(uint32_t)(wd[q] >> dsh) & 255u] + (uint32_t)(k0 + q) * NT + threadIdx.x;
-#pragma unroll
-            for (int q = 0; q < RW_CH; q++) {
-                const uint32_t i = (uint32_t)(k0 + q) * NT + threadIdx.x, p = pp[q];
-                const bool ok = i < tcount && (uint64_t)p < n;
-                QE_ST(ok ? &wout[p] : &g_store_sink[l], wd[q]);   // (every store issued: no branch)
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        __syncthreads();   // every word is out of the stage
-        uint32_t* st32 = reinterpret_cast<uint32_t*>(stage);
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++)
-            if (loc_of(j) < tcount) st32[pos[j]] = xw[j];
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < ITEMS; k++) {
-            const uint32_t i = (uint32_t)k * NT + threadIdx.x, p = gofs[sdig[i]] + i;
-            const bool ok = i < tcount && (uint64_t)p < n;
-            QE_ST(ok ? &xout[p] : reinterpret_cast<uint32_t*>(&g_store_sink[l]), st32[i]);
-        }
-        // (the next iteration's first LDS writes -- whist -- come before two barriers that every
-        // thread reaches only after this write-out: no barrier needed here)
-    }
-}
-
 // ---- two-level sort: 14 high bits by two global passes, the rest inside LDS per bucket ---------
 // For 20..31 varying bits: the top H = 15 bits split the array into 32768 buckets (~4 K words
 // each at 10^8 keys below 10^8 -- keys rarely fill their top bit's range, so H leaves room);
@@ -2471,14 +2335,6 @@ constexpr int P1_TM = QE_P1_TM;
 static_assert(P1_TM == 1 || (P1_TM == 2 && TL_TPG % 2 == 0), "paired tiles stay inside one group");
 constexpr int p1_tm(bool unstable, int carry) { return unstable && carry != X_NONE ? P1_TM : 1; }
 
-static bool p1_resident_on() {   // A/B knob: QE_P1_RESIDENT=0 launches a workgroup per tile pair
-    static bool on = [] {
-        const char* s = getenv("QE_P1_RESIDENT");
-        return !(s && s[0] == '0');
-    }();
-    return on;
-}
-
 static bool cs_single_on() {   // A/B knob: QE_CS_SINGLE=0 keeps the three-launch count scans
     static bool on = [] {
         const char* s = getenv("QE_CS_SINGLE");
@@ -2684,15 +2540,6 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
             hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN_KIOTA, OUT_W32, true, 8, RTILE / pre_nt(true), pre_nt(true) * p1_tm(true, X_NONE), true, X_NONE, true, p1_tm(true, X_NONE)>),
                                dim3(xcd_grid((nt + p1_tm(true, X_NONE) - 1) / p1_tm(true, X_NONE))), dim3(pre_nt(true) * p1_tm(true, X_NONE)), 0, c->stream, kn, nullptr, nullptr, nullptr, w1, vout, n,
                                32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr);
-        else if (vt && xt && p1_resident_on()) {   // the resident form (p1_resident_kernel)
-            static const uint32_t grid = [&] {
-                int ncu = 0;
-                QE_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
-                return (uint32_t)std::max(8, ncu / 8 * 8);   // one workgroup per CU (its 144 KiB of LDS)
-            }();
-            hipLaunchKernelGGL(p1_resident_kernel<IN_KV>, dim3(grid), dim3(1024), 0, c->stream, kn, vt, w1, n, 32 + L, f,
-                               tcnt, xt, reinterpret_cast<uint32_t*>(x1));
-        }
         else if (vt && xt) QE_P1N(IN_KV, X32, vt, xt);
         else if (vt) QE_P1N(IN_KV, X_NONE, vt, nullptr);
         else if (xt) QE_P1N(IN_KIOTA, X32, nullptr, xt);
