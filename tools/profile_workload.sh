@@ -13,8 +13,12 @@ A="--workload $W --steps 2 --warmup 1 --no-cpu $PROFILE_EXTRA"
 # C4: a crash under the profiler leaves the fault address, PC and /proc/self/maps here (tools/crashmaps.c)
 [ "$W" = c4 ] && export QE_CRASH_MAPS=$O/${TAG}_crashmaps.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${TAG}_trace -o run -- python3 $R/bench.py $A > $O/${TAG}_trace.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/${TAG}_fetch -o run -- python3 $R/bench.py $A > $O/${TAG}_fetch.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/${TAG}_write -o run -- python3 $R/bench.py $A > $O/${TAG}_write.log 2>&1
+# C4's counter passes run without the lanes' HIP-event stage table (QE_BENCH_EVENTS=0): under
+# --pmc a lane's hipEventRecord has faulted inside librocprofiler-sdk; the counters
+# need no events
+PMC_ENV=; [ "$W" = c4 ] && PMC_ENV="QE_BENCH_EVENTS=0"
+env $PMC_ENV timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/${TAG}_fetch -o run -- python3 $R/bench.py $A > $O/${TAG}_fetch.log 2>&1
+env $PMC_ENV timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/${TAG}_write -o run -- python3 $R/bench.py $A > $O/${TAG}_write.log 2>&1
 echo profile-done
 # summaries on the box (a batch workload's raw traces can exceed what gpurun brings back)
 cd $R

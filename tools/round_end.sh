@@ -18,9 +18,9 @@ c45)
   timeout -k 10 500 bash tools/profile_workload.sh ${T}c5 c5 || exit 1
   cp gpurun_out/${T}c5_traffic.json profiles/${T}c5_traffic.json || exit 1
   timeout -k 10 300 python bench.py --workload c5 > gpurun_out/${T}_c5_bench.json 2> gpurun_out/${T}_c5_bench.err || exit 1
-  timeout -k 10 500 bash tools/profile_workload.sh ${T}c4 c4 || exit 1
-  cp gpurun_out/${T}c4_traffic.json profiles/${T}c4_traffic.json || exit 1
+  # C4: the bench line first, then its profile (best effort: see the c4 case)
   timeout -k 10 400 python bench.py --workload c4 > gpurun_out/${T}_c4_bench.json 2> gpurun_out/${T}_c4_bench.err || exit 1
+  timeout -k 10 500 bash tools/profile_workload.sh ${T}c4 c4 || echo "c4 profile failed (rc $?)"
   ;;
 c4)
   # the bench line first (no profiler), then the trace + PMC passes as best effort: the 8 lanes'
