@@ -10,8 +10,12 @@ O=$R/gpurun_out
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 A="--workload $W --steps 2 --warmup 1 --no-cpu $PROFILE_EXTRA"
-# C4: a crash under the profiler leaves the fault address, PC and /proc/self/maps here (tools/crashmaps.c)
-[ "$W" = c4 ] && export QE_CRASH_MAPS=$O/${TAG}_crashmaps.txt
+# C4: a crash under the profiler leaves the fault address, PC and /proc/self/maps here (tools/crashmaps.c).
+# Under the profiler C4 runs ONE lane (QE_WORKERS=1): with eight lanes submitting at once the
+# profiler's HSA queue interception has faulted past its own 1 MiB buffer (in the trace
+# pass and in the counter pass alike); a kernel's bytes do not depend on the lane count, and the
+# C4 line itself is measured without the profiler at eight lanes
+[ "$W" = c4 ] && export QE_CRASH_MAPS=$O/${TAG}_crashmaps.txt QE_WORKERS=1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${TAG}_trace -o run -- python3 $R/bench.py $A > $O/${TAG}_trace.log 2>&1
 # C4's counter passes run without the lanes' HIP-event stage table (QE_BENCH_EVENTS=0): under
 # --pmc a lane's hipEventRecord has faulted inside librocprofiler-sdk; the counters
