@@ -1364,9 +1364,6 @@ constexpr int TL2_WCH = QE_TL2_WCH;   // write-out chunk (slots whose LDS reads 
 constexpr int TL2_WPE = QE_TL2_WPE;
 static_assert(TL2_ITEMS % TL2_WCH == 0, "whole chunks");
 
-#ifndef QE_P2_RES
-#define QE_P2_RES 0   // (build knob: 1 = pass 2 may run as a resident grid, QE_P2_RESIDENT=K)
-#endif
 // CARRY: the payloads of pass 1 (xin, in pass-1 order; X64: 64-bit, X32: 32-bit) follow the words
 // to xout, staged in the words' LDS slots after the words have left (as in radix_pass_kernel).
 // W32: the words are u32 fields (a key-only first pass, OUT_W32): loaded into the high half, stored back as u32
@@ -1386,13 +1383,8 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
     __shared__ uint32_t bexcl[BINS];
     __shared__ uint32_t gofs[BINS];
     __shared__ uint32_t wsum[NW];
-    // a workgroup per segment, or (QE_P2_RES builds, a resident grid: p2_grid) workgroups that
-    // walk segments it, it + gridDim.x, ...: item it is segment (it % 8) * (T / 8) + it / 8 either
-    // way, so an XCD's workgroups take a contiguous range (gridDim.x is a multiple of 8)
-    const uint32_t T = 8u * ((256u * G + 7u) / 8u);
-    for (uint32_t it = blockIdx.x; it < T; it += gridDim.x) {
-    const uint32_t s = (it & 7u) * (T >> 3) + (it >> 3);
-    if (s >= 256u * G) continue;   // the XCD grid's padding items (block-uniform)
+    const uint32_t s = xcd_item(blockIdx.x);
+    if (s >= 256u * G) return;   // the XCD grid's padding blocks (block-uniform)
     // the segment's bounds from the compact table column_scans wrote (48 KB at 1e8 keys, L2-hot):
     // reading them from the 12.5 MB tile-count matrix put a far dependent load before every word load
 #ifdef QE_DIAG_STAMPS
@@ -1636,8 +1628,6 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
         }
         __syncthreads();   // stage / whist / gofs are rewritten by the next sub-tile
         if (base == start) QE_SORT_STAMP(s, 6);
-    }
-    if constexpr (!QE_P2_RES) break;   // (one segment per workgroup: the loop form spilled)
     }
 }
 
@@ -2345,21 +2335,6 @@ constexpr int P1_TM = QE_P1_TM;
 static_assert(P1_TM == 1 || (P1_TM == 2 && TL_TPG % 2 == 0), "paired tiles stay inside one group");
 constexpr int p1_tm(bool unstable, int carry) { return unstable && carry != X_NONE ? P1_TM : 1; }
 
-// pass 2's grid: a workgroup per segment, or QE_P2_RESIDENT=K: K resident workgroups per CU walking
-// the segments (A/B knob)
-static uint32_t p2_grid(qe_ctx* c, uint32_t nseg) {
-    static const uint32_t resident = [&] {
-        const char* v = getenv("QE_P2_RESIDENT");
-        const int k = v ? atoi(v) : 0;
-        if (k <= 0 || !QE_P2_RES) return 0u;
-        int ncu = 0;
-        QE_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
-        return (uint32_t)std::max(8, ncu * k / 8 * 8);
-    }();
-    const uint32_t all = xcd_grid(nseg);
-    return resident && resident < all ? resident : all;
-}
-
 static bool cs_single_on() {   // A/B knob: QE_CS_SINGLE=0 keeps the three-launch count scans
     static bool on = [] {
         const char* s = getenv("QE_CS_SINGLE");
@@ -2625,7 +2600,7 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
 #ifdef QE_DIAG_STAMPS
         stamp_select(c, "p2", n);
 #endif
-        hipLaunchKernelGGL(kern, dim3(p2_grid(c, nseg)), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8, seg, gcnt, G,
+        hipLaunchKernelGGL(kern, dim3(xcd_grid(nseg)), dim3(TL2_NT), 0, c->stream, w1, w2, n, 32 + L + 8, seg, gcnt, G,
                            x1, x2);
         QE_HIP(hipGetLastError());
         if (xm) dfree(c, x1);
