@@ -316,7 +316,10 @@ int e_keys(void* u, uint32_t rel, uint32_t col, qe_h rows, qe_h* out) {
     return guard(e, [&] {
         qe_list l = as_list(A(rows));
         qe_pairs p{};
-        ck(qe_gather_pairs(e->c, column(e->c, rel, col), &l, &p), e->c);
+        e->c->gather_k32 = true;   // the keys go to a join's sort (or an exchange, which widens them)
+        const int rc = qe_gather_pairs(e->c, column(e->c, rel, col), &l, &p);
+        e->c->gather_k32 = false;
+        ck(rc, e->c);
         DArr* k = new_arr(e->c, p.key, p.n, true);
         k->bits = (p.flags & QE_PAIRS_BITS) != 0;
         k->kor = p.kor;
@@ -352,7 +355,10 @@ int e_keys_of(void* u, uint32_t rel, uint32_t col, qe_h vals, qe_h* out) {
         const uint64_t n = v->n;
         uint64_t* k = dalloc_t<uint64_t>(c, std::max<uint64_t>(n, 1));
         const uint32_t* vd = static_cast<const uint32_t*>(v->d);
-        if (n && !widen_with_hist(c, vd, n, kor, kand, k)) {
+        c->gather_k32 = true;
+        const bool fused = n && widen_with_hist(c, vd, n, kor, kand, k);
+        c->gather_k32 = false;
+        if (n && !fused) {
             Timed t(c, "widen_keys", 12.0 * n);
             hipLaunchKernelGGL(widen_u32_kernel, dim3(grid_for(n, 256 * 8, 8192)), dim3(256), 0, c->stream, vd, n, k);
             QE_HIP(hipGetLastError());
@@ -431,6 +437,7 @@ int e_exchange_start(void* u, qe_h keys, const qe_h* cols, int ncols, qe_h* tick
         const int W = e->world;
         DArr* k = A(keys);
         const uint64_t n = k->n;
+        keys_need_u64(c, k->d);   // (keys gathered as u32 for a sort: the partition reads u64)
         // more than 4 rowid columns: an index rides through the partition, the columns follow it
         const bool via_idx = ncols > 4;
         std::vector<const uint32_t*> in;

@@ -92,6 +92,11 @@ struct PreHist {
     uint32_t* gcnt = nullptr;   // per (digit, group) segment digit counts
     int lo = 0, L = 0;
     uint64_t fmask = 0;
+    // the keys as u32 (keys below 2^32, gathered for the plan's deferred sort): the u64 key buffer
+    // was NOT written -- its sort's first pass reads these; anything else that reads the keys
+    // calls keys_need_u64 first, which widens them into the buffer
+    uint32_t* k32 = nullptr;
+    uint64_t n = 0;
 };
 
 }  // namespace qe
@@ -174,6 +179,7 @@ struct qe_ctx {
     const uint64_t* sort_v64 = nullptr;
     // ... or keep the key fields only (u32 words): the next deferred sort's rows are never read
     bool sort_keys_only = false;
+    bool gather_k32 = false;   // (set by the plan engine around its key gathers: see PreHist::k32)
     std::vector<qe::PendingEvent> pending;
     std::vector<hipEvent_t> event_pool;
     std::vector<qe::KStat> kstats;
@@ -271,7 +277,9 @@ SortOut radix_sort_u64(qe_ctx* c, const uint64_t* keys, const uint32_t* vals /*n
 // not applicable -- the caller completes both sorts and merges as usual)
 void pairs_need_keys(qe_ctx* c, const qe_pairs* p);
 void pairs_need_vals(qe_ctx* c, const qe_pairs* p);
-void pairs_drop_deferred(qe_ctx* c, const qe_pairs* p);   // (also drops a gathered histogram)
+// (also drops a gathered histogram; keep_k32: a key buffer the pairs only borrow keeps its u32
+// keys, PreHist::k32, for another sort of it -- its owner's release frees them)
+void pairs_drop_deferred(qe_ctx* c, const qe_pairs* p, bool keep_k32 = false);
 // keys = col[rows] for a list whose sort will be the lookback-free two-level one: the sort's
 // histogram is built in the same pass (false: not that sort -- the caller gathers plainly)
 bool gather_with_hist(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint64_t n, uint64_t kor, uint64_t kand,
@@ -298,6 +306,8 @@ bool join_pairs_carry(qe_ctx* c, qe_pairs* R, qe_pairs* S, const uint32_t* xa, c
 // keys = (u64) vals for a list whose sort will be the lookback-free two-level one, with that
 // sort's histogram (gather_with_hist without the gather); false: not that sort
 bool widen_with_hist(qe_ctx* c, const uint32_t* vals, uint64_t n, uint64_t kor, uint64_t kand, uint64_t* keys);
+// a key buffer gathered as u32 only (PreHist::k32): widen it into the buffer now (no-op otherwise)
+void keys_need_u64(qe_ctx* c, const void* keys);
 // the join's checksums without its pairs (the plan's last join): sums[k] = sum over pairs of
 // col_k[S-side rowid], the rowid being S's val (src 0) or the low / high half of its carried
 // payload (src 1 / 2); *pairs = the pair count.  False: not applicable (geometry, a bucket

@@ -1644,7 +1644,7 @@ static void sort_pairs_raw(qe_ctx* c, qe_pairs* p, bool defer) {
     uint64_t bits[2] = {p->kor, p->kand};
     SortOut so = radix_sort_u64(c, p->key, p->val, p->n, true, (p->flags & QE_PAIRS_BITS) ? bits : nullptr, defer);
     if (so.keys_new) {
-        pairs_drop_deferred(c, p);   // a gathered histogram the sort did not take dies with the keys
+        pairs_drop_deferred(c, p, !(p->owns & 1));   // a gathered histogram the sort did not take dies with the keys
         if (p->owns & 1) dfree(c, p->key);
         p->key = (uint64_t*)so.keys;
         p->owns |= 1;
@@ -1929,7 +1929,7 @@ int qe_sort_pairs(qe_ctx* c, qe_pairs* p) {
     uint64_t bits[2] = {p->kor, p->kand};
     SortOut so = radix_sort_u64(c, p->key, p->val, p->n, true, (p->flags & QE_PAIRS_BITS) ? bits : nullptr, false);
     if (so.keys_new) {
-        pairs_drop_deferred(c, p);   // a gathered histogram the sort did not take dies with the keys
+        pairs_drop_deferred(c, p, !(p->owns & 1));   // a gathered histogram the sort did not take dies with the keys
         if (p->owns & 1) dfree(c, p->key);
         p->key = (uint64_t*)so.keys;
         p->owns |= 1;

@@ -925,7 +925,9 @@ int qe_pairs_to_host(qe_ctx* c, const qe_pairs* p, uint64_t* key, uint32_t* val)
 
 void qe_pairs_free(qe_ctx* c, qe_pairs* p) {
     if (!c || !p) return;
-    pairs_drop_deferred(c, p);
+    // (pairs that only borrow their key buffer leave its u32 keys, PreHist::k32, to its owner:
+    // a join that gives its inputs back is followed by another sort of the same buffer)
+    pairs_drop_deferred(c, p, !(p->owns & 1));
     if (p->owns & 1) dfree(c, p->key);
     if (p->owns & 2) dfree(c, p->val);
     if (p->owns & 4) dfree(c, p->match);

@@ -1076,7 +1076,8 @@ __global__ void __launch_bounds__(1024) tl_gather_hist_kernel(const uint64_t* __
                                                               uint64_t* __restrict__ keys, Field f, int L, uint32_t nt,
                                                               uint32_t G, uint32_t Q, uint32_t* __restrict__ tcnt,
                                                               uint32_t* __restrict__ gout,
-                                                              const uint32_t* __restrict__ col32 = nullptr) {
+                                                              const uint32_t* __restrict__ col32 = nullptr,
+                                                              uint32_t* __restrict__ k32out = nullptr) {
     __shared__ alignas(16) uint32_t h[TL_BUCKETS];
     __shared__ uint32_t th[2][256];
     for (int i = threadIdx.x; i < TL_BUCKETS; i += 1024) h[i] = 0;
@@ -1117,7 +1118,8 @@ __global__ void __launch_bounds__(1024) tl_gather_hist_kernel(const uint64_t* __
         for (int j = 0; j < 8; j++) {
             const uint64_t i = base + (uint64_t)j * 1024 + threadIdx.x;
             if (i < n) {
-                keys[i] = k[j];
+                if (k32out) k32out[i] = (uint32_t)k[j];   // (grid-uniform: keys below 2^32, PreHist::k32)
+                else keys[i] = k[j];
                 const uint32_t b = (uint32_t)((((k[j] >> f.lo) & f.fmask) >> L) & (TL_BUCKETS - 1));
                 atomicAdd(&h[((b & 255u) << 7) | (b >> 8)], 1u);
                 atomicAdd(&th[par][b & 255u], 1u);
@@ -2335,6 +2337,14 @@ constexpr int P1_TM = QE_P1_TM;
 static_assert(P1_TM == 1 || (P1_TM == 2 && TL_TPG % 2 == 0), "paired tiles stay inside one group");
 constexpr int p1_tm(bool unstable, int carry) { return unstable && carry != X_NONE ? P1_TM : 1; }
 
+static bool gather_k32_on() {   // A/B knob: QE_GATHER_K32=0 gathers the plan's keys as u64
+    static bool on = [] {
+        const char* s = getenv("QE_GATHER_K32");
+        return !(s && s[0] == '0');
+    }();
+    return on;
+}
+
 static bool cs_single_on() {   // A/B knob: QE_CS_SINGLE=0 keeps the three-launch count scans
     static bool on = [] {
         const char* s = getenv("QE_CS_SINGLE");
@@ -2464,13 +2474,29 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     auto ph = c->prehist.find(keys);   // counted while the keys were gathered?
     const bool have = ph != c->prehist.end() && ph->second.lo == f.lo && ph->second.L == L &&
                       ph->second.fmask == f.fmask;
+    // keys gathered as u32 only (PreHist::k32): this sort's first pass reads them when it is the
+    // unstable deferred form that reads u32 keys with u32 values (its rowids) -- else they are
+    // widened into the key buffer first
+    const uint32_t* k32 = nullptr;
+    {
+        const bool k32_ok = have && ph->second.k32 && dfr && vals && sort_unstable_on() && !c->carry_c64 &&
+                            !c->sort_v64;
+        if (k32_ok) k32 = ph->second.k32;
+        else if (ph != c->prehist.end()) keys_need_u64(c, keys);
+    }
     if (have) {
         dfree(c, tcnt);
         dfree(c, gcnt);
         tcnt = ph->second.tcnt;
         gcnt = ph->second.gcnt;
-        c->prehist.erase(ph);
+        if (k32) {   // the u32 keys stay with the key buffer: a later sort of the same buffer (a
+            ph->second.tcnt = ph->second.gcnt = nullptr;   // join's fallback) widens them, and
+            ph->second.lo = -1;                            // the buffer's release frees them
+        } else {
+            c->prehist.erase(ph);
+        }
     }
+    if (k32) kn = k32;
     {
         Timed t(c, "sort_hist", have ? 0.0 : (kn ? 4.0 : (double)sizeof(K)) * n);
         uint32_t* gout = have ? gcnt : hist_slices(c, gcnt, Q, nseg);
@@ -2523,27 +2549,30 @@ static bool sort_two_level_pre(qe_ctx* c, const K* keys, const uint32_t* vals, u
     hipLaunchKernelGGL((radix_pass_kernel<K, IN, OUT_WORD, true, 8, RTILE / pre_nt(UN), pre_nt(UN) * p1_tm(UN, CR), true, CR, UN, p1_tm(UN, CR)>),  \
                        dim3(xcd_grid((nt + p1_tm(UN, CR) - 1) / p1_tm(UN, CR))), dim3(pre_nt(UN) * p1_tm(UN, CR)), 0, c->stream, keys, nullptr, vals, kout, w1, vout, n, 32 + L, \
                        255u, f, tcnt, nullptr, nullptr, 0u, XA, XB, XO)
-#define QE_P1N(IN, CR, VIN, XA)                                                                                         \
+#define QE_P1N(IN, CR, VIN, XA, XB)                                                                                     \
     hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN, OUT_WORD, true, 8, RTILE / pre_nt(true), pre_nt(true) * p1_tm(true, CR), true, CR, true, p1_tm(true, CR)>),      \
                        dim3(xcd_grid((nt + p1_tm(true, CR) - 1) / p1_tm(true, CR))), dim3(pre_nt(true) * p1_tm(true, CR)), 0, c->stream, kn, nullptr, VIN, nullptr, w1, vout, n, 32 + L,     \
-                       255u, f, tcnt, nullptr, nullptr, 0u, XA, nullptr, x1)
+                       255u, f, tcnt, nullptr, nullptr, 0u, XA, XB, x1)
 #ifdef QE_DIAG_STAMPS
     stamp_select(c, "p1", n);
 #endif
     if (kn && uns) {
-        // u32 key (+ u32 value) (+ u32 payload) in, word (+ payload) out
-        const uint32_t* vt = cv64 ? narrow_of(c, cv64, n) : nullptr;
+        // u32 key (+ u32 value: a base column's values riding as rows, or a gathered side's rowids)
+        // (+ u32 payload, or X64's one or two u32 columns) in, word (+ payload) out
+        const uint32_t* vt = vals ? vals : cv64 ? narrow_of(c, cv64, n) : nullptr;
         const uint32_t* xt = xm == XCOL ? narrow_of(c, reinterpret_cast<const uint64_t*>(cxa), n) : xm == X32 ? cxa : nullptr;
-        Timed t(c, xm ? "sort_pass_carry" : name, (4.0 + (vt ? 4.0 : 0.0) + (xt ? 4.0 : 0.0) + (w32 ? 4.0 : 8.0) +
-                                                   (xt ? 4.0 : 0.0)) * n);
-        if (w32)
+        const double xin = xm == X64 ? 4.0 + (cxb ? 4.0 : 0.0) : xt ? 4.0 : 0.0, xout = xm == X64 ? 8.0 : xt ? 4.0 : 0.0;
+        Timed t(c, xm ? "sort_pass_carry" : name, (4.0 + (vt ? 4.0 : 0.0) + xin + (w32 ? 4.0 : 8.0) + xout) * n);
+        if (xm == X64 && vt) QE_P1N(IN_KV, X64, vt, cxa, cxb);
+        else if (xm == X64) QE_P1N(IN_KIOTA, X64, nullptr, cxa, cxb);
+        else if (w32)
             hipLaunchKernelGGL((radix_pass_kernel<uint32_t, IN_KIOTA, OUT_W32, true, 8, RTILE / pre_nt(true), pre_nt(true) * p1_tm(true, X_NONE), true, X_NONE, true, p1_tm(true, X_NONE)>),
                                dim3(xcd_grid((nt + p1_tm(true, X_NONE) - 1) / p1_tm(true, X_NONE))), dim3(pre_nt(true) * p1_tm(true, X_NONE)), 0, c->stream, kn, nullptr, nullptr, nullptr, w1, vout, n,
                                32 + L, 255u, f, tcnt, nullptr, nullptr, 0u, nullptr, nullptr, nullptr);
-        else if (vt && xt) QE_P1N(IN_KV, X32, vt, xt);
-        else if (vt) QE_P1N(IN_KV, X_NONE, vt, nullptr);
-        else if (xt) QE_P1N(IN_KIOTA, X32, nullptr, xt);
-        else QE_P1N(IN_KIOTA, X_NONE, nullptr, nullptr);
+        else if (vt && xt) QE_P1N(IN_KV, X32, vt, xt, nullptr);
+        else if (vt) QE_P1N(IN_KV, X_NONE, vt, nullptr, nullptr);
+        else if (xt) QE_P1N(IN_KIOTA, X32, nullptr, xt, nullptr);
+        else QE_P1N(IN_KIOTA, X_NONE, nullptr, nullptr, nullptr);
         QE_HIP(hipGetLastError());
     } else if (w32) {
         Timed t(c, name, ((double)sizeof(K) + 4.0) * n);
@@ -2841,10 +2870,25 @@ static SortOut sort_kv_unpacked(qe_ctx* c, const K* keys, const uint32_t* vals, 
     return SortOut{kbuf[last], vbuf[last], true, true};
 }
 
+// true when radix_sort_impl's plan for these keys is the lookback-free two-level sort (the one that
+// may read a gathered side's u32 keys, PreHist::k32) -- the conditions gather_hist_impl checks
+static bool takes_pre_two_level(uint64_t n, const uint64_t* bits, bool with_vals, bool defer) {
+    if (!bits || !with_vals || !defer || n < 2 || n >= 0xFFFFFFFFull) return false;
+    const uint64_t vary = bits[0] & ~bits[1];
+    if (!vary) return false;
+    const int lo = __builtin_ctzll(vary), hi = 64 - __builtin_clzll(vary), nb = hi - lo;
+    if (nb > 32 || !two_level_on() || n <= (uint64_t)TL_CAP) return false;
+    if (nb >= 12 && nb <= 8 + 24 && n <= 700000) return false;
+    if (!(nb >= 20 && nb <= TL_H + 16 && n >= (1u << 20) && n <= 4000ull * TL_BUCKETS)) return false;
+    return sort_pre_on() && n >= sort_pre_min();
+}
+
 template <typename K>
 static SortOut radix_sort_impl(qe_ctx* c, const K* keys, const uint32_t* vals, uint64_t n, bool with_vals,
                                const char* name, const uint64_t* bits, bool defer = false) {
     SortOut so{(void*)keys, (uint32_t*)vals, false, false};
+    // keys gathered as u32 only: widened now unless the sort that reads them comes next
+    if (sizeof(K) == 8 && !c->prehist.empty() && !takes_pre_two_level(n, bits, with_vals, defer)) keys_need_u64(c, keys);
     if (n < 2) return so;
     if (n >= 0xFFFFFFFFull) throw Error(QE_EINVAL, "sort input too large");
     uint64_t kb[2];
@@ -3125,13 +3169,19 @@ void pairs_need_keys(qe_ctx* c, const qe_pairs* p) {
 
 void pairs_need_vals(qe_ctx* c, const qe_pairs* p) { pairs_need_keys(c, p); }
 
-void pairs_drop_deferred(qe_ctx* c, const qe_pairs* p) {
+void pairs_drop_deferred(qe_ctx* c, const qe_pairs* p, bool keep_k32) {
     if (!p || !p->key) return;
     auto ph = c->prehist.find(p->key);   // gathered with a histogram but never sorted (a scan join)
     if (ph != c->prehist.end()) {
         dfree(c, ph->second.tcnt);
         dfree(c, ph->second.gcnt);
-        c->prehist.erase(ph);
+        if (keep_k32 && ph->second.k32) {
+            ph->second.tcnt = ph->second.gcnt = nullptr;
+            ph->second.lo = -1;
+        } else {
+            if (ph->second.k32) dfree(c, ph->second.k32);
+            c->prehist.erase(ph);
+        }
     }
     auto it = c->deferred.find(p->key);
     if (it == c->deferred.end()) return;
@@ -3161,15 +3211,19 @@ static bool gather_hist_impl(qe_ctx* c, const uint64_t* col, const uint32_t* row
     uint32_t* tcnt = dalloc_t<uint32_t>(c, (size_t)nt * 256);
     uint32_t* gcnt = dalloc_t<uint32_t>(c, (size_t)nseg * 128);
     uint32_t* gout = hist_slices(c, gcnt, Q, nseg);
+    // the plan engine's keys below 2^32 are gathered as u32 (PreHist::k32): its deferred sort's
+    // first pass reads 4 B per key instead of 8, and the gather writes 4
+    uint32_t* k32 = c->gather_k32 && !(kor >> 32) && gather_k32_on() ? dalloc_t<uint32_t>(c, n) : nullptr;
+    const double kw = k32 ? 4.0 : 8.0;
     if (col) {
-        Timed t(c, "gather_keys", (col32 ? 8.0 : 12.0) * n + 8.0 * n);
+        Timed t(c, "gather_keys", (col32 ? 8.0 : 12.0) * n + kw * n);
         hipLaunchKernelGGL(tl_gather_hist_kernel<false>, dim3(G * Q), dim3(1024), 0, c->stream, col, rows, n, keys, f, L,
-                           nt, G, Q, tcnt, gout, col32);
+                           nt, G, Q, tcnt, gout, col32, k32);
         QE_HIP(hipGetLastError());
     } else {
-        Timed t(c, "widen_keys", 12.0 * n);
+        Timed t(c, "widen_keys", 4.0 * n + kw * n);
         hipLaunchKernelGGL(tl_gather_hist_kernel<true>, dim3(G * Q), dim3(1024), 0, c->stream, nullptr, rows, n, keys, f,
-                           L, nt, G, Q, tcnt, gout);
+                           L, nt, G, Q, tcnt, gout, nullptr, k32);
         QE_HIP(hipGetLastError());
     }
     hist_fold(c, gout, Q, G, gcnt, nullptr);   // (the sort that reads these counts makes the histogram)
@@ -3179,8 +3233,29 @@ static bool gather_hist_impl(qe_ctx* c, const uint64_t* col, const uint32_t* row
     ph.lo = lo;
     ph.L = L;
     ph.fmask = fmask;
+    ph.k32 = k32;
+    ph.n = n;
     c->prehist[keys] = ph;
     return true;
+}
+
+__global__ void __launch_bounds__(256) widen_keys_kernel(const uint32_t* __restrict__ k32, uint64_t n,
+                                                         uint64_t* __restrict__ keys) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) keys[i] = k32[i];
+}
+
+void keys_need_u64(qe_ctx* c, const void* keys) {
+    auto it = c->prehist.find(keys);
+    if (it == c->prehist.end() || !it->second.k32) return;
+    PreHist& ph = it->second;
+    if (ph.n) {
+        Timed t(c, "widen_keys", 12.0 * ph.n);
+        hipLaunchKernelGGL(widen_keys_kernel, dim3(grid_for(ph.n, 256 * 8, 8192)), dim3(256), 0, c->stream, ph.k32, ph.n,
+                           static_cast<uint64_t*>(const_cast<void*>(keys)));
+        QE_HIP(hipGetLastError());
+    }
+    dfree(c, ph.k32);
+    ph.k32 = nullptr;
 }
 
 bool gather_with_hist(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint64_t n, uint64_t kor, uint64_t kand,
