@@ -311,14 +311,24 @@ int e_refine(void* u, uint32_t rel, uint32_t col, qe_h rows, char op, uint64_t v
     });
 }
 
+// the plan engine's key gathers may leave their keys as u32 (PreHist::k32): set for the call only,
+// cleared on every exit (a throw included) -- the faithful executor's gathers never see it
+struct K32Scope {
+    qe_ctx* c;
+    explicit K32Scope(qe_ctx* cc) : c(cc) { c->gather_k32 = true; }
+    ~K32Scope() { c->gather_k32 = false; }
+};
+
 int e_keys(void* u, uint32_t rel, uint32_t col, qe_h rows, qe_h* out) {
     Eng* e = E(u);
     return guard(e, [&] {
         qe_list l = as_list(A(rows));
         qe_pairs p{};
-        e->c->gather_k32 = true;   // the keys go to a join's sort (or an exchange, which widens them)
-        const int rc = qe_gather_pairs(e->c, column(e->c, rel, col), &l, &p);
-        e->c->gather_k32 = false;
+        int rc;
+        {
+            K32Scope k32(e->c);   // the keys go to a join's sort (or an exchange, which widens them)
+            rc = qe_gather_pairs(e->c, column(e->c, rel, col), &l, &p);
+        }
         ck(rc, e->c);
         DArr* k = new_arr(e->c, p.key, p.n, true);
         k->bits = (p.flags & QE_PAIRS_BITS) != 0;
@@ -355,9 +365,11 @@ int e_keys_of(void* u, uint32_t rel, uint32_t col, qe_h vals, qe_h* out) {
         const uint64_t n = v->n;
         uint64_t* k = dalloc_t<uint64_t>(c, std::max<uint64_t>(n, 1));
         const uint32_t* vd = static_cast<const uint32_t*>(v->d);
-        c->gather_k32 = true;
-        const bool fused = n && widen_with_hist(c, vd, n, kor, kand, k);
-        c->gather_k32 = false;
+        bool fused;
+        {
+            K32Scope k32(c);
+            fused = n && widen_with_hist(c, vd, n, kor, kand, k);
+        }
         if (n && !fused) {
             Timed t(c, "widen_keys", 12.0 * n);
             hipLaunchKernelGGL(widen_u32_kernel, dim3(grid_for(n, 256 * 8, 8192)), dim3(256), 0, c->stream, vd, n, k);
