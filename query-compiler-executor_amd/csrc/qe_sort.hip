@@ -981,42 +981,15 @@ __device__ inline void tl_store_counts(const uint32_t* h, uint32_t g, uint32_t q
             *reinterpret_cast<const uint4*>(h + i);
 }
 
-#ifndef QE_HIST_WROWS
-#define QE_HIST_WROWS 0
-#endif
 template <typename K>
 __global__ void __launch_bounds__(1024) tl_hist_tiles_kernel(const K* __restrict__ keys, uint64_t n, Field f, int L,
                                                              uint32_t nt, uint32_t G, uint32_t Q,
                                                              uint32_t* __restrict__ tcnt, uint32_t* __restrict__ gout) {
     __shared__ alignas(16) uint32_t h[TL_BUCKETS];   // index d1 * 128 + d2: 128 KiB, one block per CU
-#if QE_HIST_WROWS
-    // (build knob) the tile's d1 counts per wave, two 16-bit counters per word (a wave counts at
-    // most 512 keys of a tile): the 16 waves' atomics meet on 16 rows instead of one
-    __shared__ uint32_t th[2][16][128];
-    for (int i = threadIdx.x; i < 2 * 16 * 128; i += 1024) (&th[0][0][0])[i] = 0;
-#else
     __shared__ uint32_t th[2][256];      // the tile's d1 counts, double-buffered: one barrier per tile
-    if (threadIdx.x < 512) (&th[0][0])[threadIdx.x] = 0;
-#endif
     for (int i = threadIdx.x; i < TL_BUCKETS; i += 1024) h[i] = 0;
+    if (threadIdx.x < 512) (&th[0][0])[threadIdx.x] = 0;
     __syncthreads();
-    // tile t's count of digit d = threadIdx.x (< 256), the counters then zeroed for the tile after next
-    auto flush = [&](uint32_t t, uint32_t pb) {
-#if QE_HIST_WROWS
-        const uint32_t d = threadIdx.x, sh = (d & 1u) * 16u;
-        uint32_t sum = 0;
-#pragma unroll
-        for (int ww = 0; ww < 16; ww++) sum += (th[pb][ww][d >> 1] >> sh) & 0xFFFFu;
-        tcnt[(uint64_t)t * 256 + d] = sum;
-        if (!(d & 1u)) {   // (the odd lane of the pair read these words earlier in this wave's order)
-#pragma unroll
-            for (int ww = 0; ww < 16; ww++) th[pb][ww][d >> 1] = 0;
-        }
-#else
-        tcnt[(uint64_t)t * 256 + threadIdx.x] = th[pb][threadIdx.x];
-        th[pb][threadIdx.x] = 0;
-#endif
-    };
     const uint32_t g = blockIdx.x / Q, q = blockIdx.x % Q;   // Q blocks share group g's tiles
     const uint32_t t_end = (g + 1) * TL_TPG < nt ? (g + 1) * TL_TPG : nt;
     // (a tile's counts do not depend on which thread counts which key: u32 keys are loaded two per
@@ -1063,17 +1036,16 @@ __global__ void __launch_bounds__(1024) tl_hist_tiles_kernel(const K* __restrict
     uint32_t prev = 0, par = 0;
     // count tile t (keys k, mask vm): flush the previous tile's d1 counts first (its barrier passed)
     auto count = [&](uint32_t t, const uint64_t (&k)[8], uint32_t vm) {
-        if (t != t0 && threadIdx.x < 256) flush(prev, par ^ 1u);
+        if (t != t0 && threadIdx.x < 256) {
+            tcnt[(uint64_t)prev * 256 + threadIdx.x] = th[par ^ 1u][threadIdx.x];
+            th[par ^ 1u][threadIdx.x] = 0;
+        }
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             if ((vm >> j) & 1u) {
                 const uint32_t b = (uint32_t)((((k[j] >> f.lo) & f.fmask) >> L) & (TL_BUCKETS - 1));
                 atomicAdd(&h[((b & 255u) << 7) | (b >> 8)], 1u);
-#if QE_HIST_WROWS
-                atomicAdd(&th[par][wave_id()][(b & 255u) >> 1], 1u << ((b & 1u) * 16u));
-#else
                 atomicAdd(&th[par][b & 255u], 1u);
-#endif
             }
         }
         __syncthreads();
@@ -1089,7 +1061,7 @@ __global__ void __launch_bounds__(1024) tl_hist_tiles_kernel(const K* __restrict
         va = load(t + 2 * Q, ka, t + 2 * Q < t_end);
         count(t + Q, kb, vb);
     }
-    if (g * TL_TPG + q < t_end && threadIdx.x < 256) flush(prev, par ^ 1u);
+    if (g * TL_TPG + q < t_end && threadIdx.x < 256) tcnt[(uint64_t)prev * 256 + threadIdx.x] = th[par ^ 1u][threadIdx.x];
     __syncthreads();
     tl_store_counts(h, g, q, G, gout);
 }
