@@ -633,6 +633,37 @@ __global__ void __launch_bounds__(1024) tl_hist_kernel(const K* __restrict__ key
         if (h[i]) atomicAdd(&hist[i], h[i]);
 }
 
+// A 32 K-bucket table held by one 1024-thread block, 32 consecutive buckets per thread (the scans'
+// layout), moved between global memory and registers through LDS padded by one word per 32:
+// lane-contiguous global accesses and conflict-free row reads (stride 33 words).  Each thread
+// reading its own 32 words from global memory was 32 instructions of 64 cache lines each -- the
+// single-block scans took 9.7-14.7 us per sort that way (profiles/r05qc4_kernel_stats.csv).
+constexpr int TP_WORDS = TL_BUCKETS + TL_BUCKETS / 32;
+__device__ __forceinline__ uint32_t tp_at(uint32_t i) { return i + (i >> 5); }
+// v <- the thread's row of g (zero: g is cleared behind the read); ends with sp readable again
+__device__ __forceinline__ void rows_in(uint32_t* g, uint32_t* sp, uint32_t (&v)[32], bool zero) {
+#pragma unroll 8
+    for (int j = 0; j < 32; j++) {
+        const uint32_t i = (uint32_t)j * 1024u + threadIdx.x;
+        sp[tp_at(i)] = g[i];
+        if (zero) g[i] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 32; k++) v[k] = sp[threadIdx.x * 33u + k];
+}
+// g <- the threads' rows v (every read of sp done before the call: it is overwritten)
+__device__ __forceinline__ void rows_out(uint32_t* g, uint32_t* sp, const uint32_t (&v)[32]) {
+#pragma unroll
+    for (int k = 0; k < 32; k++) sp[threadIdx.x * 33u + k] = v[k];
+    __syncthreads();
+#pragma unroll 8
+    for (int j = 0; j < 32; j++) {
+        const uint32_t i = (uint32_t)j * 1024u + threadIdx.x;
+        g[i] = sp[tp_at(i)];
+    }
+}
+
 // one block: bucket starts (+ the end) and the largest bucket only -- the lookback-free form
 // computes its digit bases in the count scans, so it needs none of tl_scan_kernel's marginals
 // (whose serial loops made that kernel ~22 us per sort)
@@ -644,14 +675,15 @@ __global__ void __launch_bounds__(1024) tl_bstart_kernel(const uint32_t* __restr
                                                          const uint32_t* __restrict__ d1part = nullptr) {
     constexpr int PER = TL_BUCKETS / 1024;
     static_assert(PER == 32 && TL_BUCKETS == 128 * 256, "thread t holds buckets t * 32 .. t * 32 + 31");
+    __shared__ uint32_t sp[TP_WORDS];
     __shared__ uint32_t wsum[16], wmax[16];
     const int t = threadIdx.x;
     uint4 dp = make_uint4(0, 0, 0, 0);
     if (cbase && t < 256) dp = reinterpret_cast<const uint4*>(d1part)[t];
     uint32_t v[PER], mine = 0, mx = 0;
+    rows_in(const_cast<uint32_t*>(hist), sp, v, false);
 #pragma unroll
     for (int k = 0; k < PER; k++) {
-        v[k] = hist[t * PER + k];
         mine += v[k];
         mx = v[k] > mx ? v[k] : mx;
     }
@@ -665,9 +697,11 @@ __global__ void __launch_bounds__(1024) tl_bstart_kernel(const uint32_t* __restr
     const uint32_t bstart_first = run;
 #pragma unroll
     for (int k = 0; k < PER; k++) {
-        bstart[t * PER + k] = run;
-        run += v[k];
+        const uint32_t x = v[k];
+        v[k] = run;
+        run += x;
     }
+    rows_out(bstart, sp, v);
     if (t == 1023) bstart[TL_BUCKETS] = run;
     if (t == 0) {
         uint32_t m = 0;
@@ -694,21 +728,18 @@ __global__ void __launch_bounds__(1024) tl_scan_kernel(uint32_t* __restrict__ hi
                                                        uint32_t* __restrict__ base1, uint32_t* __restrict__ base2,
                                                        uint64_t* __restrict__ maxb) {
     constexpr int PER = TL_BUCKETS / 1024;
-    __shared__ alignas(16) uint32_t h[TL_BUCKETS];
+    __shared__ uint32_t h[TP_WORDS];   // the histogram, padded (tp_at)
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t c1[256], c2[128];
     __shared__ uint32_t wmax[16];
     const int t = threadIdx.x;
-    uint32_t v[PER], mine = 0, mx = 0;
+    uint32_t v[PER], bs[PER], mine = 0, mx = 0;
+    rows_in(hist, h, v, true);
 #pragma unroll
     for (int k = 0; k < PER; k++) {
-        v[k] = hist[t * PER + k];
-        h[t * PER + k] = v[k];
         mine += v[k];
         mx = v[k] > mx ? v[k] : mx;
     }
-#pragma unroll
-    for (int k = 0; k < PER; k++) hist[t * PER + k] = 0;
     uint32_t inc = wave_incl_scan_u32(mine);
     mx = wave_max_u32(mx);
     if (lane_id() == 63) wsum[wave_id()] = inc;
@@ -718,7 +749,7 @@ __global__ void __launch_bounds__(1024) tl_scan_kernel(uint32_t* __restrict__ hi
     for (int w = 0; w < wave_id(); w++) run += wsum[w];
 #pragma unroll
     for (int k = 0; k < PER; k++) {
-        bstart[t * PER + k] = run;
+        bs[k] = run;
         run += v[k];
     }
     if (t == 1023) bstart[TL_BUCKETS] = run;
@@ -735,7 +766,7 @@ __global__ void __launch_bounds__(1024) tl_scan_kernel(uint32_t* __restrict__ hi
         const int d1 = t & 255, q = t >> 8;
         uint32_t a = 0;
 #pragma unroll 8
-        for (int d2 = q * 32; d2 < q * 32 + 32; d2++) a += h[d2 * 256 + d1];
+        for (int d2 = q * 32; d2 < q * 32 + 32; d2++) a += h[tp_at(d2 * 256 + d1)];
         part[q][d1] = a;
     }
     // c2[d2]: row d2 = the 256 buckets of threads 8*d2 .. 8*d2 + 7 (their `mine`), one shuffle tree
@@ -745,6 +776,7 @@ __global__ void __launch_bounds__(1024) tl_scan_kernel(uint32_t* __restrict__ hi
     if ((t & 7) == 0) c2[t >> 3] = r8;
     __syncthreads();
     if (t < 256) c1[t] = part[0][t] + part[1][t] + part[2][t] + part[3][t];
+    rows_out(bstart, h, bs);   // (every read of h passed the barrier above)
     __syncthreads();
     if (t < 64) {   // one wave scans both: 4 digits of base1 and 2 of base2 per lane
         uint32_t a[4], sa = 0;
