@@ -1931,17 +1931,30 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
     __shared__ uint32_t tab[HJ_I * NW];
     __shared__ uint64_t s_excl;
     __shared__ uint32_t s_total, s_long;
+    // The bucket's bounds are read before the loop as two 8-B scalar loads with the kernel
+    // arguments: the straight-line form compiled to three serialized scalar round trips (bounds,
+    // then argument pointers, each behind an lgkmcnt(0) wait) before the first word load -- the
+    // loop form issues them together (145 -> 93 waits): bucket_join 1.08 -> 1.01 ms per C3 query
+    // (profiles/r05w_*, r05x_*).  A grid below TL_BUCKETS (QE_HJ_PERSIST=1) walks the buckets b,
+    // b + gridDim.x, ... with the next bucket's bounds in flight -- measured slower (hj_grid).
+    uint32_t nr0 = bsR[blockIdx.x], nrE = bsR[blockIdx.x + 1], ns0 = bsS[blockIdx.x], nsE = bsS[blockIdx.x + 1];
+    for (uint32_t b = blockIdx.x; b < (uint32_t)TL_BUCKETS; b += gridDim.x) {   // (block-uniform)
+    if (b != blockIdx.x) __syncthreads();   // every LDS read of the previous bucket done
 #ifdef QE_DIAG_STAMPS
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-#endif
-    const uint32_t b = blockIdx.x;
-#ifdef QE_DIAG_STAMPS
     if (threadIdx.x == 0 && b < STAMP_TILES) g_hj_stamps[(uint64_t)b * STAMP_SLOTS] = t_start;
 #endif
-    const uint32_t r0 = bsR[b], mR = bsR[b + 1] - r0, s0 = bsS[b], mS = bsS[b + 1] - s0;
+    const uint32_t r0 = nr0, mR = nrE - nr0, s0 = ns0, mS = nsE - ns0;
+    if (b + gridDim.x < (uint32_t)TL_BUCKETS) {
+        const uint32_t bn = b + gridDim.x;
+        nr0 = bsR[bn];
+        nrE = bsR[bn + 1];
+        ns0 = bsS[bn];
+        nsE = bsS[bn + 1];
+    }
     if (mR > (uint32_t)(NT * HJ_I) || mS > (uint32_t)(NT * HJ_I)) {   // beyond LDS (the sorts were not checked): flag it
         if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(total_out + 1), 1ull);
-        return;
+        continue;
     }
     const uint32_t D = 1u << L, dmask = D - 1u;
     const int w = wave_id(), l = lane_id();
@@ -2015,7 +2028,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
     QE_STAMP(g_hj_stamps, b, 3);
     if (s_long) {   // block-uniform: a chain too long to emit by walking (the sorts + merge take the join)
         if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(total_out + 1), 1ull);
-        return;
+        continue;
     }
     if (w == 0) {   // (row group, wave) totals in row order -> bucket offsets; one atomic per bucket
         constexpr uint32_t E = HJ_I * NW;
@@ -2033,7 +2046,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
     __syncthreads();
     QE_STAMP(g_hj_stamps, b, 4);
     const uint64_t gofs = s_excl;
-    if (gofs + s_total > cap) return;   // outgrew the buffers: the host re-runs with the exact size
+    if (gofs + s_total > cap) continue;   // outgrew the buffers: the host re-runs with the exact size
 #pragma unroll
     for (int j = 0; j < HJ_I; j++) {   // wave-cooperative emission, as tl_hjoin_kernel's
         const uint32_t pj = pre[j], all = tot[j];
@@ -2069,6 +2082,19 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
         }
     }
     QE_STAMP(g_hj_stamps, b, 5);
+    }
+}
+
+// the chain join's grid: one block per bucket, or (QE_HJ_PERSIST=1, A/B knob) two per CU walking
+// the buckets with the next bucket's bounds in flight -- bucket_join 1.013 -> 1.081 ms per C3
+// query and C4 3845 -> 3690 q/s on one box (profiles/r05w_*): the grid of one block per bucket
+// keeps every CU's two slots refilled by the dispatcher as buckets finish, whatever their sizes
+static unsigned hj_grid() {
+    static const unsigned g = [] {
+        const char* s = getenv("QE_HJ_PERSIST");
+        return s && s[0] == '1' ? 512u : (unsigned)TL_BUCKETS;
+    }();
+    return g;
 }
 
 static bool hj_chain_on() {
@@ -3376,37 +3402,37 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
             Timed t(c, "bucket_join", 8.0 * (double)(nR + nS) + (carry ? (s32 ? 4.0 : 8.0) * (double)nS : 0.0) +
                                           (rx ? 4.0 * (double)nR : 0.0));
             if (s32 && rx) {
-                hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, true, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
+                hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, true, true>), dim3(hj_grid()), dim3(HJ_NT), 0,
                                    c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
                                    c->d_scratch + 17, nullptr, x0, nullptr, dR.x32, xr, dS.x32);
             } else if (s32) {
-                hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, false, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
+                hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, false, true>), dim3(hj_grid()), dim3(HJ_NT), 0,
                                    c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
                                    c->d_scratch + 17, nullptr, x0, nullptr, nullptr, nullptr, dS.x32);
             } else if (rx) {
                 const uint64_t* xs = carry ? dS.x : nullptr;
                 if (carry)
-                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
+                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, true>), dim3(hj_grid()), dim3(HJ_NT), 0,
                                        c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
                                        c->d_scratch + 17, xs, x0, x1, dR.x32, xr);
                 else
-                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, false, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
+                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, false, true>), dim3(hj_grid()), dim3(HJ_NT), 0,
                                        c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
                                        c->d_scratch + 17, nullptr, nullptr, nullptr, dR.x32, xr);
             } else if (hj_chain_on()) {
                 if (carry && dR.L <= 12)
-                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream,
+                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true>), dim3(hj_grid()), dim3(HJ_NT), 0, c->stream,
                                        dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17,
                                        dS.x, x0, x1);
                 else if (carry)
-                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<HJ_DBITS, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0,
+                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<HJ_DBITS, true>), dim3(hj_grid()), dim3(HJ_NT), 0,
                                        c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
                                        c->d_scratch + 17, dS.x, x0, x1);
                 else if (dR.L <= 12)
-                    hipLaunchKernelGGL(tl_hjoin_chain_kernel<12>, dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream, dR.words,
+                    hipLaunchKernelGGL(tl_hjoin_chain_kernel<12>, dim3(hj_grid()), dim3(HJ_NT), 0, c->stream, dR.words,
                                        dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17);
                 else
-                    hipLaunchKernelGGL(tl_hjoin_chain_kernel<HJ_DBITS>, dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream,
+                    hipLaunchKernelGGL(tl_hjoin_chain_kernel<HJ_DBITS>, dim3(hj_grid()), dim3(HJ_NT), 0, c->stream,
                                        dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap, c->d_scratch + 17);
             } else if (carry && dR.L <= 12)
                 hipLaunchKernelGGL((tl_hjoin_kernel<12, true>), dim3(TL_BUCKETS), dim3(HJ_NT), 0, c->stream, dR.words,
