@@ -193,7 +193,7 @@ def run_dist(args):
     gen_chain(ctx, total, args.seed, total)       # replicated on every rank
     ctx.sync()
     t_part = None
-    if multi:   # load-time layout: this rank's hash bucket of every base column (qe_partition_columns)
+    if multi:   # partitioned layout: a join-key column's hash bucket is kept from its first use (warmup)
         t1 = time.time()
         ctx.partition_columns(world, rank)
         t_part = time.time() - t1
@@ -248,6 +248,25 @@ def run_dist(args):
     faithful = None
     if rank == 0 and not args.no_faithful:
         faithful, _ = ctx.run(QUERY)              # in-run parity: the drop-in executor, same relations
+    # 3) the same plan with the query's last join materialised (QE_PLAN_AGG=0: its pairs made by the
+    #    chain bucket join, then summed by the checksum gathers) -- the line's own last join counts
+    #    its pairs in aggregate form and never writes them; every rank runs it (it is collective)
+    mat_line = None
+    if not args.no_materialised and not args.no_faithful:   # (profiling runs: the measured plan only)
+        agg_env = os.environ.get("QE_PLAN_AGG")
+        os.environ["QE_PLAN_AGG"] = "0"
+        try:
+            dtm, out_m, _, _ = timed_steps()
+        finally:
+            if agg_env is None:
+                del os.environ["QE_PLAN_AGG"]
+            else:
+                os.environ["QE_PLAN_AGG"] = agg_env
+        mat_line = {"last_join": "materialised: every result pair written (rowid pairs + carried columns), "
+                                 "then the checksums gather the select columns",
+                    "ms_per_step": round(dtm / args.steps * 1e3, 3),
+                    "value": round(ctx.last_result_rows() * args.steps / dtm, 1),
+                    "stdout_identical": out_m == out}
     if rank == 0:
         if faithful is not None and not multi:   # N = 1: the faithful executor timed too, for the record
             torch.cuda.synchronize()
@@ -280,7 +299,10 @@ def run_dist(args):
                                    "RCCL grouped send/recv per exchange, all-reduced sums",
                        "refused_queries": refused, "exchanges_per_step": exchanges / max(1, args.steps + args.warmup),
                        "parallelism": f"hash-partitioned dp{world}" if multi else "partitioned plan, one rank",
+                       "last_join": "aggregate (the last join's pairs counted, not materialised: only "
+                                    "print_sums reads them; see materialised_last_join)",
                        "load_partition_s": round(t_part, 4) if t_part is not None else None},
+            "materialised_last_join": mat_line,
             "faithful_executor": faithful_line,
             "roofline": roofline({dominant: stats[dominant]} if dominant in stats else stats,
                                  traffic, args.steps),
@@ -499,8 +521,10 @@ def main():
     ap.add_argument("--cpu-rows-c5", type=int, default=1_000_000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-faithful", action="store_true",
-                    help="skip the faithful executor's parity run and timing (profiling runs: only the "
-                         "measured executor's kernels in the trace)")
+                    help="skip the faithful executor's parity run and timing and the materialised-last-join "
+                         "timing (profiling runs: only the measured executor's kernels in the trace)")
+    ap.add_argument("--no-materialised", action="store_true",
+                    help="c3: skip the materialised-last-join timing (QE_PLAN_AGG=0) reported beside the line")
     ap.add_argument("--workload", choices=["c3", "c4", "c5"], default="c3",
                     help="c3 (default): the headline 4-relation chain join; c4: the SIGMOD-style batch; "
                          "c5: the skewed (Zipf 0.9) 2-relation join at 1e9 rows")

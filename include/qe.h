@@ -254,14 +254,15 @@ int qe_join_indices(qe_ctx*, const uint64_t* keysA, uint64_t nA, const uint64_t*
  * of a join side that is a whole base relation: every rank holds the column. */
 int qe_bucket_select(qe_ctx*, qe_col col, uint32_t nparts, uint32_t part, const uint64_t* heavy, uint32_t nheavy,
                      qe_pairs* out);
-/* Load-time hash partitioning of the base relations (north star "relations
- * hash-partition across the GPUs"): for every column of every loaded relation, this rank's hash
- * bucket (part of nparts) as qe_bucket_select leaves it, kept in the ctx until the relations are
- * dropped.  The partitioned plan's join sides that are whole base columns then read it instead of
- * scanning the replicated column once per join (qe_run_queries_dist at nparts ranks: ~0.18 ms per
- * 1e8-row side on every rank, at any rank count).  Time and bytes join qe_load_stats.  Columns
- * stay replicated (the faithful fallback runs on rank 0).  Replaces nothing in the reference (it
- * has no multi-GPU path); the row set per bucket is qe_bucket_select's. */
+/* Hash-partitioned layout of the base relations (north star "relations
+ * hash-partition across the GPUs"): from this call on, the partitioned plan at nparts ranks keeps,
+ * per base column it joins as a whole base side, this rank's hash bucket (part of nparts) as
+ * qe_bucket_select leaves it -- selected the first time a join reads that column, kept in the ctx
+ * until the relations are dropped -- instead of scanning the replicated column once per join
+ * (~0.18 ms per 1e8-row side on every rank, at any rank count).  Columns never read that way (payload
+ * columns, broadcast joins' base sides) hold no bucket.  Columns stay replicated (the faithful
+ * fallback runs on rank 0).  Fails only on bad arguments.  Replaces nothing in the reference (it has
+ * no multi-GPU path); the row set per bucket is qe_bucket_select's. */
 int qe_partition_columns(qe_ctx*, uint32_t nparts, uint32_t part);
 /* Skew path (C5): over rows [start, end) of `keys`, counts[h] = #rows whose key is heavy[h]
  * (host arrays, heavy sorted, <= 1024) and, when weights != NULL,

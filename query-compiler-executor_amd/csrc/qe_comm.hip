@@ -417,8 +417,18 @@ int e_base_side(void* u, uint32_t rel, uint32_t col, qe_h* keys, qe_h* rowids) {
             return;
         }
         if (c->bparts_n == (uint32_t)e->world && c->bparts_p == (uint32_t)e->rank) {
-            auto it = c->bparts.find(q.d);     // partitioned at load (qe_partition_columns): no scan
-            if (it != c->bparts.end()) {
+            // partitioned layout (qe_partition_columns): this column's bucket is selected the first
+            // time a join reads it as a whole base side and kept until the relations are dropped, so
+            // only join-key columns ever hold one (columns read only as payloads or by broadcast
+            // joins never do)
+            auto it = c->bparts.find(q.d);
+            if (it == c->bparts.end()) {
+                qe_pairs p{};
+                bucket_select_dev(c, q, (uint32_t)e->world, (uint32_t)e->rank, nullptr, 0, nullptr, &p);
+                it = c->bparts.emplace(q.d, p).first;
+                c->load_bytes += 8.0 * (double)q.n + 12.0 * (double)p.n;
+            }
+            {
                 DArr* k = new_arr(c, it->second.key, it->second.n, true, false);
                 k->bits = true;
                 k->kor = kor;

@@ -555,21 +555,12 @@ int qe_partition_columns(qe_ctx* c, uint32_t nparts, uint32_t part) {
     if (nparts < 1 || part >= nparts) throw Error(QE_EINVAL, "part out of range");
     drop_partitions(c);
     if (nparts == 1) return 0;   // (one rank reads the columns themselves)
-    const auto t0 = std::chrono::steady_clock::now();
-    double bytes = 0;
-    for (const auto& r : c->rels)
-        for (size_t k = 0; k < r.cols.size(); k++) {
-            qe_col q{r.cols[k], r.rows};
-            qe_pairs p{};
-            bucket_select_dev(c, q, nparts, part, nullptr, 0, nullptr, &p);
-            c->bparts[r.cols[k]] = p;
-            bytes += 8.0 * (double)r.rows + 12.0 * (double)p.n;
-        }
+    // nothing is selected here: a column's bucket is made the first time the partitioned plan reads
+    // it as a whole base join side (e_base_side) and cached until the relations are dropped -- a
+    // column that is never a partitioned join key (a payload, or a broadcast join's base side)
+    // never holds one, and no allocation can fail at load
     c->bparts_n = nparts;
     c->bparts_p = part;
-    sync(c);
-    c->load_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    c->load_bytes += bytes;
     return 0;
     QE_API_END(c)
 }

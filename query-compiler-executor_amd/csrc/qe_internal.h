@@ -198,10 +198,13 @@ inline const uint32_t* narrow_of(const qe_ctx* c, const void* col, uint64_t n) {
     return nullptr;
 }
 
-// every device buffer a kernel reads is libqe's own -- a dalloc block, a relation column or its
-// u32 copy (no entry point takes a caller's device pointer) -- and each is followed by
-// DALLOC_SLACK allocated bytes: the soffset-strided buffer loads (qe_device.h) may read up to a
-// tile's stride past a buffer's end, never past its allocation
+// every data buffer a kernel reads through the soffset-strided buffer loads (qe_device.h) is
+// libqe's own -- a dalloc block, a relation column or its u32 copy (no entry point takes a caller's
+// device pointer) -- and each is followed by DALLOC_SLACK allocated bytes: such a load may read up
+// to a tile's stride past a buffer's end, never past its allocation (the strides are checked
+// against it by a static_assert in qe_sort.hip).  The few fixed-size control words allocated with
+// a plain hipMalloc (lookback status, tickets, scratch, the zero histogram, the comm's reduction
+// words) are read only by ordinary indexed loads within their sizes
 constexpr size_t DALLOC_SLACK = 64u << 10;
 void* dalloc(qe_ctx* c, size_t bytes);
 bool alloc_log_on();   // QE_ALLOC_LOG=1 (placement A/Bs)

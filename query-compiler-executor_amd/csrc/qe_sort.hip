@@ -1397,6 +1397,12 @@ constexpr int TL2_WCH = QE_TL2_WCH;   // write-out chunk (slots whose LDS reads 
 #endif
 constexpr int TL2_WPE = QE_TL2_WPE;
 static_assert(TL2_ITEMS % TL2_WCH == 0, "whole chunks");
+// the strided buffer loads' soffset is not range-checked (qe_device.h): the largest stride a lane
+// adds past its buffer -- pass 2's TL2_ITEMS x 512 B, pass 1's R_ITEMS x 512 B (u64 words) or
+// R_ITEMS / 4 x 1 KiB (V4) -- must stay inside the allocation's slack
+static_assert((size_t)TL2_ITEMS * 512u < DALLOC_SLACK && (size_t)R_ITEMS * 512u < DALLOC_SLACK &&
+                  (size_t)(R_ITEMS / 4) * 1024u < DALLOC_SLACK,
+              "a strided load's soffset can pass DALLOC_SLACK");
 
 // CARRY: the payloads of pass 1 (xin, in pass-1 order; X64: 64-bit, X32: 32-bit) follow the words
 // to xout, staged in the words' LDS slots after the words have left (as in radix_pass_kernel).
@@ -3207,6 +3213,9 @@ void partition_words_kv(qe_ctx* c, const uint64_t* keys, const uint64_t* v64, co
 
 void pairs_need_keys(qe_ctx* c, const qe_pairs* p) {
     if (!p || !p->key) return;
+    // keys gathered as u32 for a deferred sort that has not run (PreHist::k32): the u64 buffer is
+    // unwritten until widened -- every reader of p->key comes through here, so none sees it
+    keys_need_u64(c, p->key);
     auto it = c->deferred.find(p->key);
     if (it == c->deferred.end()) return;
     const DeferredSort d = it->second;

@@ -343,6 +343,10 @@ typedef struct {
     int agg;
     uint64_t agg_size;
     uint64_t agg_sums[64];
+    /* the plan's switches, read once per query (QE_PLAN_BCAST: 0 never broadcast, 2 always, 1 the
+     * cost model; QE_DIST_REORDER=0: joins in query order), and whether the ranks were checked to
+     * agree on them -- the first all-reduce of a query carries them (plan_allreduce) */
+    int bcast_mode, reorder, agreed;
 } plan_t;
 
 #define ECHK(call)                                   \
@@ -367,10 +371,35 @@ static uint64_t rel_rows(const plan_t* P, uint32_t rel) {
 /* a join's global pair count beyond the materialisation limit (the reference's DArray bound) */
 static int over_limit(const plan_t* P, uint64_t pairs) { return P->e->mat_limit && pairs > *P->e->mat_limit; }
 
-static int allreduce1(plan_t* P, uint64_t* v) {
-    if (P->e->world == 1) return 0;
-    return P->e->allreduce(P->e->u, v, 1);
+/* all-reduce v[0, nv) (nv <= 2; the engine's u64 sum).  The query's first one also carries every
+ * rank's switches (mode and its square, so W * sum(x^2) == sum(x)^2 holds exactly when all ranks
+ * agree): a rank whose environment differs would take a broadcast join where its peers exchange,
+ * or join in another order, and the collectives would no longer pair up -- every rank fails the
+ * query together instead.  It runs before the first collective a switch can change: filters'
+ * counts come first, and do_join calls it (nv = 0) before its first side is started. */
+static int plan_allreduce(plan_t* P, uint64_t* v, int nv) {
+    const qe_engine* e = P->e;
+    if (e->world == 1) return 0;
+    if (P->agreed) return nv ? e->allreduce(e->u, v, nv) : 0;
+    uint64_t w[6] = {0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < nv; i++) w[i] = v[i];
+    w[nv] = (uint64_t)P->bcast_mode;
+    w[nv + 1] = (uint64_t)(P->bcast_mode * P->bcast_mode);
+    w[nv + 2] = (uint64_t)P->reorder;
+    w[nv + 3] = (uint64_t)(P->reorder * P->reorder);
+    const int rc = e->allreduce(e->u, w, nv + 4);
+    if (rc) return rc;
+    P->agreed = 1;
+    for (int i = 0; i < nv; i++) v[i] = w[i];
+    const uint64_t W = e->world;
+    if (W * w[nv + 1] != w[nv] * w[nv] || W * w[nv + 3] != w[nv + 2] * w[nv + 2]) {
+        fprintf(stderr, "[qe_plan] rank %u: QE_PLAN_BCAST / QE_DIST_REORDER differ across ranks\n", e->rank);
+        return QE_EINVAL;
+    }
+    return 0;
 }
+
+static int allreduce1(plan_t* P, uint64_t* v) { return plan_allreduce(P, v, 1); }
 
 static void rel(plan_t* P, qe_h h) {
     if (h != NONE) P->e->release(P->e->u, h);
@@ -582,8 +611,7 @@ static int bcast_join(const plan_t* P, int A, int B) {
     if (e->world <= 1 || !e->base_side_all) return 0;
     const int wa = is_whole(&P->C[A]), wb = is_whole(&P->C[B]);
     if (wa == wb) return 0;                                  /* both derived, or both whole: no */
-    const char* m = getenv("QE_PLAN_BCAST");   /* (read per join: tests switch it) */
-    const int mode = m && (m[0] == '0' || m[0] == '2') ? m[0] - '0' : 1;
+    const int mode = P->bcast_mode;            /* (read once per query, agreed across ranks) */
     if (mode != 1) return mode == 2;
     const double G = (double)e->world;
     const double R = (double)(wa ? P->C[A].size : P->C[B].size), D = (double)(wa ? P->C[B].size : P->C[A].size);
@@ -627,6 +655,7 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* s
         }
     }
     side_t sa, sb;
+    ECHK(plan_allreduce(P, NULL, 0));                        /* (the switches agreed, once per query) */
     const int bc = bcast_join(P, A, B);
     /* derived sides first, so their exchanges overlap the base side's local bucket scan */
     if (is_whole(&P->C[A])) {
@@ -679,7 +708,7 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* s
                 return jr;
             }
             v[1] = jr == QE_ETOOBIG;
-            if (P->e->world > 1) ECHK(P->e->allreduce(P->e->u, v, 2));   /* every rank takes one branch */
+            ECHK(plan_allreduce(P, v, 2));                  /* every rank takes one branch */
             if (over_limit(P, v[0])) v[1] = 1;
             rel(P, sa.keys);
             rel(P, sb.keys);
@@ -747,7 +776,7 @@ static int do_join(plan_t* P, const pred_t* p, const uint8_t* need, const int* s
          * leave the query together (the fallback then runs it) -- one all-reduce with the size */
         uint64_t v[2] = {0, jr == QE_ETOOBIG};
         if (jr == 0) ECHK(e->length(e->u, oa, &v[0]));
-        if (P->e->world > 1) ECHK(P->e->allreduce(P->e->u, v, 2));
+        ECHK(plan_allreduce(P, v, 2));
         if (over_limit(P, v[0])) v[1] = 1;
         if (v[1]) {
             rel(P, oa);
@@ -863,7 +892,10 @@ static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t*
     P->list = (qe_h*)calloc(nb, sizeof(qe_h));
     P->list_size = (uint64_t*)calloc(nb, sizeof(uint64_t));
     for (size_t i = 0; i < nb; i++) P->comp_of[i] = -1;
-    const int reorder = !(getenv("QE_DIST_REORDER") && getenv("QE_DIST_REORDER")[0] == '0');
+    const char* bm = getenv("QE_PLAN_BCAST");
+    P->bcast_mode = bm && (bm[0] == '0' || bm[0] == '2') ? bm[0] - '0' : 1;
+    P->reorder = !(getenv("QE_DIST_REORDER") && getenv("QE_DIST_REORDER")[0] == '0');
+    const int reorder = P->reorder;
     uint8_t* need = (uint8_t*)calloc(nb, 1);
     int* sel1 = (int*)calloc(nb, sizeof(int));
     int* kcol1 = (int*)calloc(nb, sizeof(int));

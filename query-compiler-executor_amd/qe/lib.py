@@ -501,8 +501,8 @@ class Ctx:
         return p
 
     def partition_columns(self, nparts: int, part: int):
-        """keep this rank's hash bucket of every loaded base column (qe_partition_columns: load-time
-        layout for the partitioned plan at nparts ranks; counted in load_stats)"""
+        """the partitioned layout for the plan at nparts ranks (qe_partition_columns): each base column
+        a partitioned join reads as a whole side keeps this rank's hash bucket from its first use on"""
         self._chk(self.lib.qe_partition_columns(self.h, nparts, part))
 
     def heavy_stats(self, keys: Col, start: int, end: int, heavy, vals: Col | None = None, weights=None):

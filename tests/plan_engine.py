@@ -376,9 +376,12 @@ def worker(rank, world, port, rels, queries, outq, limits=None, global_limit=Non
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    opts = dict(opts or {})
+    for k, v in (opts.pop("env", None) or {}).get(rank, {}).items():   # this rank's own environment
+        os.environ[k] = v
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        eng = NumpyPlanEngine(rels, rank, world, **(opts or {}))
+        eng = NumpyPlanEngine(rels, rank, world, **opts)
         if limits:
             eng.mat_limit = limits[rank]
         if global_limit is not None:

@@ -571,9 +571,11 @@ def test_checksums_batched(ctx):
 @pytest.mark.parametrize("extra", [13, 4096 + 3, 8191])
 def test_partial_last_tile_at_the_end_of_exact_allocations(ctx, extra):
     """relations of 2^22 + extra rows (the lookback-free two-level sort's floor, a partial last
-    tile): every column and its u32 copy is an exactly-sized hipMalloc, so the last tile's strided
-    buffer loads end at an allocation's end (the stride rides in the range-checked
-    offset) -- the planned C3 query equals the faithful executor's bytes"""
+    tile): the last tile's masked lanes and its strided buffer loads run past the columns' ends
+    into their DALLOC_SLACK (the soffset stride is not range-checked; a static_assert in qe_sort.hip
+    keeps every stride below the slack) -- the planned C3 query equals the faithful executor's
+    bytes.  (This checks the partial-tile masking; it cannot catch an over-read that stays inside
+    the slack.)"""
     rows = (1 << 22) + extra
     q = "0 1 2 3|0.1=1.0&1.1=2.0&2.1=3.0&3.2>1000000000&3.2<3000000000|1.2 2.2 3.2\n"
     ctx.drop_relations()

@@ -166,3 +166,24 @@ def test_global_pair_count_is_what_the_limit_bounds():
     assert one.run(q2)[1] == -5
     res, _, _ = _run_world(rels, [q2], 2, global_limit=limit, opts={"join_agg": False})
     assert res[0][1] == -5
+
+
+def test_ranks_with_different_plan_switches_fail_together(monkeypatch):
+    """QE_PLAN_BCAST / QE_DIST_REORDER are read once per query on each rank; a rank whose
+    environment differs would broadcast a join its peer exchanges and the collectives would no
+    longer pair up (a hang).  The query's first all-reduce carries the switches: every rank fails
+    the query with QE_EINVAL together, and the next query (switches agreed) still runs"""
+    monkeypatch.delenv("QE_PLAN_BCAST", raising=False)
+    rows = 20_000
+    rels = dg.make_relations(dg.chain_spec(4, rows), 1)
+    q2 = "0 1|0.1=1.0|0.2 1.2\n"
+    want = pe.NumpyPlanEngine(rels, 0, 1, join_agg=False).run(q2)[0]
+    env = {0: {"QE_PLAN_BCAST": "0"}, 1: {"QE_PLAN_BCAST": "2"}}
+    res, _, _ = _run_world(rels, [C3, q2], 2, opts={"env": env, "join_agg": False})
+    assert res[0][1] == -1 and res[1][1] == -1
+    env = {0: {"QE_DIST_REORDER": "0"}, 1: {"QE_DIST_REORDER": "1"}}
+    res, _, _ = _run_world(rels, [C3], 2, opts={"env": env})
+    assert res[0][1] == -1
+    env = {0: {"QE_PLAN_BCAST": "0"}, 1: {"QE_PLAN_BCAST": "0"}}
+    res, _, _ = _run_world(rels, [q2], 2, opts={"env": env, "join_agg": False})
+    assert res[0][:2] == (want, 0)

@@ -10,6 +10,7 @@
 #include <signal.h>
 #include <stdint.h>
 #include <string.h>
+#include <sys/syscall.h>
 #include <ucontext.h>
 #include <unistd.h>
 
@@ -31,12 +32,16 @@ static void handler(int sig, siginfo_t* si, void* uc_) {
         put(fd, sig == SIGSEGV ? "=== SIGSEGV" : "=== SIGBUS");
         put(fd, " addr ");
         put_hex(fd, (uint64_t)(uintptr_t)si->si_addr);
+#if defined(__x86_64__)
         put(fd, " pc ");
         put_hex(fd, (uint64_t)uc->uc_mcontext.gregs[REG_RIP]);
         put(fd, " sp ");
         put_hex(fd, (uint64_t)uc->uc_mcontext.gregs[REG_RSP]);
+#else
+        (void)uc;   /* (the PC / SP registers are x86-64 names; elsewhere the maps alone) */
+#endif
         put(fd, " tid ");
-        put_hex(fd, (uint64_t)gettid());
+        put_hex(fd, (uint64_t)syscall(SYS_gettid));
         put(fd, "\n");
         const int m = open("/proc/self/maps", O_RDONLY);
         if (m >= 0) {
@@ -56,7 +61,10 @@ static void handler(int sig, siginfo_t* si, void* uc_) {
 int qecrash_install(const char* path) {
     if (!path || strlen(path) >= sizeof g_path) return -1;
     strcpy(g_path, path);
-    static char alt[1 << 16];   /* a signal stack: the faulting thread's may be the problem */
+    /* a signal stack: the faulting thread's may be the problem.  sigaltstack is per thread, so
+     * only the installing thread gets it; other threads' faults run the handler on their own
+     * stacks (enough for a stack-intact fault such as a bad pointer) */
+    static char alt[1 << 16];
     stack_t ss = {.ss_sp = alt, .ss_size = sizeof alt, .ss_flags = 0};
     sigaltstack(&ss, NULL);
     struct sigaction sa;
