@@ -42,7 +42,7 @@ struct LocalGroup {
     bool broken = false;
     double timeout_s = 600;
     std::vector<std::array<uint64_t, 64>> red, cnt;
-    std::vector<const uint64_t*> keys;
+    std::vector<const void*> keys;   // each rank's partitioned keys (u64, or u32: Ticket::k32)
     std::vector<std::vector<const uint32_t*>> cols;
     void barrier() {
         std::unique_lock<std::mutex> lk(mu);
@@ -165,6 +165,7 @@ struct DArr : Obj {
 
 struct Ticket : Obj {
     DArr* keys = nullptr;
+    void* keys32 = nullptr;           // the received keys as u32 (k32 exchange), widened at finish
     std::vector<DArr*> cols;
     std::vector<void*> send;          // partitioned send buffers, freed once the exchange is done
     hipEvent_t done = nullptr;
@@ -450,7 +451,21 @@ int e_base_side(void* u, uint32_t rel, uint32_t col, qe_h* keys, qe_h* rowids) {
 }
 
 // partition (ctx stream, no host sync) -> counts all-to-all + the grouped send/recv of every array
-// on the comm stream; the ctx stream carries on with the other join side meanwhile
+// on the comm stream; the ctx stream carries on with the other join side meanwhile.
+// Keys below 2^32 (the side's bounds: column statistics, the same on every rank) travel as u32:
+// partitioned from the side's pending u32 copy when it has one (PreHist::k32), sent as 4 B a key
+// instead of 8, and at the receiver widened only where the join's sort needs it (exchange_finish).
+// Every rank's choice rides in the top bit of its count words, checked before any byte moves.
+static bool exchange_k32_on() {
+    const char* s = getenv("QE_EXCHANGE_K32");   // (A/B: 0 sends u64 keys)
+    return !(s && s[0] == '0');
+}
+constexpr uint64_t K32_FLAG = 1ull << 63;
+// marks this rank's send counts (cnt[0, W), after the scatter has read its cursors) as u32 keys
+__global__ void __launch_bounds__(64) flag_counts_kernel(unsigned long long* cnt, int W) {
+    if ((int)threadIdx.x < W) cnt[threadIdx.x] |= (unsigned long long)K32_FLAG;
+}
+
 int e_exchange_start(void* u, qe_h keys, const qe_h* cols, int ncols, qe_h* ticket) {
     Eng* e = E(u);
     return guard(e, [&] {
@@ -459,7 +474,10 @@ int e_exchange_start(void* u, qe_h keys, const qe_h* cols, int ncols, qe_h* tick
         const int W = e->world;
         DArr* k = A(keys);
         const uint64_t n = k->n;
-        keys_need_u64(c, k->d);   // (keys gathered as u32 for a sort: the partition reads u64)
+        const bool k32 = k->bits && !(k->kor >> 32) && exchange_k32_on();
+        const uint32_t* kin32 = k32 ? keys_pending_u32(c, k->d) : nullptr;
+        if (!kin32) keys_need_u64(c, k->d);   // (keys gathered as u32 for a sort, sent as u64: widened)
+        const size_t kw = k32 ? 4 : 8;
         // more than 4 rowid columns: an index rides through the partition, the columns follow it
         const bool via_idx = ncols > 4;
         std::vector<const uint32_t*> in;
@@ -473,11 +491,16 @@ int e_exchange_start(void* u, qe_h keys, const qe_h* cols, int ncols, qe_h* tick
             for (int i = 0; i < ncols; i++) in.push_back(static_cast<const uint32_t*>(A(cols[i])->d));
         }
         const int np = (int)in.size();
-        uint64_t* sk = dalloc_t<uint64_t>(c, std::max<uint64_t>(n, 1));
+        void* sk = dalloc(c, std::max<uint64_t>(n, 1) * kw);
         std::vector<uint32_t*> sc(np);
         for (int i = 0; i < np; i++) sc[i] = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
         unsigned long long* cnt = dalloc_t<unsigned long long>(c, 4 * 64);   // [send | cursors | recv | -]
-        partition_dev(c, static_cast<const uint64_t*>(k->d), n, in.data(), np, (uint32_t)W, cnt, sk, sc.data());
+        partition_dev(c, static_cast<const uint64_t*>(k->d), n, in.data(), np, (uint32_t)W, cnt,
+                      static_cast<uint64_t*>(sk), sc.data(), kin32, k32);
+        if (k32) {
+            hipLaunchKernelGGL(flag_counts_kernel, dim3(1), dim3(64), 0, c->stream, cnt, W);
+            QE_HIP(hipGetLastError());
+        }
         Ticket* t = new Ticket;
         t->send.push_back(sk);
         for (auto* p : sc) t->send.push_back(p);
@@ -507,7 +530,7 @@ int e_exchange_start(void* u, qe_h keys, const qe_h* cols, int ncols, qe_h* tick
         if (g) {   // counts all-to-all: post this rank's send counts and segments, read the peers'
             QE_HIP(hipMemcpyAsync(hc, cnt, 64 * sizeof(uint64_t), hipMemcpyDeviceToHost, m->stream));
             QE_HIP(hipStreamSynchronize(m->stream));   // (the partitioned segments are complete too)
-            std::copy(hc, hc + W, g->cnt[e->rank].begin());
+            std::copy(hc, hc + W, g->cnt[e->rank].begin());   // (flagged on the device, as below)
             g->keys[e->rank] = sk;
             g->cols[e->rank].assign(scols.begin(), scols.end());
             g->barrier();
@@ -521,6 +544,15 @@ int e_exchange_start(void* u, qe_h keys, const qe_h* cols, int ncols, qe_h* tick
             QE_HIP(hipMemcpyAsync(hc + 64, cnt + 128, 64 * sizeof(uint64_t), hipMemcpyDeviceToHost, m->stream));
             QE_HIP(hipStreamSynchronize(m->stream));   // the one host round trip: receive sizes
         }
+        // every peer must send keys of this rank's width: a mismatch (ranks disagreeing on the
+        // switch) is seen by every rank of the exchange -- each has a peer of the other width --
+        // so all of them stop here, before the grouped send/recv
+        for (int p = 0; p < W; p++) {
+            if (((hc[64 + p] & K32_FLAG) != 0) != k32)
+                throw Error(QE_EINVAL, "exchange: ranks send keys of different widths (QE_EXCHANGE_K32 differs)");
+            hc[p] &= ~K32_FLAG;
+            hc[64 + p] &= ~K32_FLAG;
+        }
         uint64_t soff[64], roff[64], total = 0, run = 0;
         for (int p = 0; p < W; p++) {
             soff[p] = run;
@@ -529,7 +561,9 @@ int e_exchange_start(void* u, qe_h keys, const qe_h* cols, int ncols, qe_h* tick
             total += hc[64 + p];
         }
         if (run != n) throw Error(QE_EINVAL, "internal: partition counts do not add up");
-        DArr* rk = new_arr(c, dalloc_t<uint64_t>(c, std::max<uint64_t>(total, 1)), total, true);
+        void* rkd = dalloc(c, std::max<uint64_t>(total, 1) * kw);
+        DArr* rk = new_arr(c, k32 ? nullptr : rkd, total, true);
+        if (k32) t->keys32 = rkd;
         rk->bits = k->bits;
         rk->kor = k->kor;
         rk->kand = k->kand;
@@ -541,8 +575,9 @@ int e_exchange_start(void* u, qe_h keys, const qe_h* cols, int ncols, qe_h* tick
                 const uint64_t nr = hc[64 + p];
                 if (!nr) continue;
                 uint64_t so = 0;                       // the sender's segment offset for this rank
-                for (int q = 0; q < e->rank; q++) so += g->cnt[p][q];
-                QE_HIP(hipMemcpyAsync(static_cast<uint64_t*>(rk->d) + roff[p], g->keys[p] + so, nr * 8,
+                for (int q = 0; q < e->rank; q++) so += g->cnt[p][q] & ~K32_FLAG;
+                QE_HIP(hipMemcpyAsync(static_cast<char*>(rkd) + roff[p] * kw,
+                                      static_cast<const char*>(g->keys[p]) + so * kw, nr * kw,
                                       hipMemcpyDeviceToDevice, m->stream));
                 for (int i = 0; i < ncols; i++)
                     QE_HIP(hipMemcpyAsync(static_cast<uint32_t*>(t->cols[i]->d) + roff[p], g->cols[p][i] + so, nr * 4,
@@ -551,11 +586,11 @@ int e_exchange_start(void* u, qe_h keys, const qe_h* cols, int ncols, qe_h* tick
             QE_HIP(hipStreamSynchronize(m->stream));
             g->barrier();                              // every peer has its segments: sends may be freed
         } else {
+            const ncclDataType_t kt = k32 ? ncclUint32 : ncclUint64;
             QE_NCCL(ncclGroupStart());
             for (int p = 0; p < W; p++) {
-                QE_NCCL(ncclSend(sk + soff[p], hc[p], ncclUint64, p, m->comm, m->stream));
-                QE_NCCL(ncclRecv(static_cast<uint64_t*>(rk->d) + roff[p], hc[64 + p], ncclUint64, p, m->comm,
-                                 m->stream));
+                QE_NCCL(ncclSend(static_cast<char*>(sk) + soff[p] * kw, hc[p], kt, p, m->comm, m->stream));
+                QE_NCCL(ncclRecv(static_cast<char*>(rkd) + roff[p] * kw, hc[64 + p], kt, p, m->comm, m->stream));
                 for (int i = 0; i < ncols; i++) {
                     QE_NCCL(ncclSend(scols[i] + soff[p], hc[p], ncclUint32, p, m->comm, m->stream));
                     QE_NCCL(ncclRecv(static_cast<uint32_t*>(t->cols[i]->d) + roff[p], hc[64 + p], ncclUint32, p,
@@ -567,7 +602,7 @@ int e_exchange_start(void* u, qe_h keys, const qe_h* cols, int ncols, qe_h* tick
         QE_HIP(hipEventCreateWithFlags(&t->done, hipEventDisableTiming));
         QE_HIP(hipEventRecord(t->done, m->stream));
         m->exchanges++;
-        m->bytes_sent += (n - hc[e->rank]) * (8 + 4 * (uint64_t)ncols);
+        m->bytes_sent += (n - hc[e->rank]) * (kw + 4 * (uint64_t)ncols);
         delete k;                                      // the inputs are consumed
         for (int i = 0; i < ncols; i++) delete A(cols[i]);
         *ticket = H(t);
@@ -577,10 +612,34 @@ int e_exchange_start(void* u, qe_h keys, const qe_h* cols, int ncols, qe_h* tick
 int e_exchange_finish(void* u, qe_h ticket, qe_h* keys, qe_h* cols) {
     Eng* e = E(u);
     return guard(e, [&] {
+        qe_ctx* c = e->c;
         Ticket* t = reinterpret_cast<Ticket*>(ticket);
-        QE_HIP(hipStreamWaitEvent(e->c->stream, t->done, 0));   // later ctx work sees the bucket
+        QE_HIP(hipStreamWaitEvent(c->stream, t->done, 0));   // later ctx work sees the bucket
         QE_HIP(hipEventDestroy(t->done));
-        for (void* p : t->send) dfree(e->c, p);                  // stream-ordered after the wait
+        for (void* p : t->send) dfree(c, p);                  // stream-ordered after the wait
+        if (t->keys32) {
+            // u32 keys received: the join's sort takes them as its u32 copy with their histogram
+            // (widen_with_hist adopts the buffer: no copy, the u64 buffer stays unwritten), or
+            // they are widened into the u64 buffer
+            DArr* rk = t->keys;
+            const uint64_t n = rk->n;
+            const uint32_t* r32 = static_cast<const uint32_t*>(t->keys32);
+            uint64_t* kb = dalloc_t<uint64_t>(c, std::max<uint64_t>(n, 1));
+            rk->d = kb;
+            bool fused = false, adopted = false;
+            if (n) {
+                K32Scope k32(c);
+                fused = widen_with_hist(c, r32, n, rk->kor, rk->kand, kb, &adopted);
+            }
+            if (n && !fused) {
+                Timed tm(c, "widen_keys", 12.0 * n);
+                hipLaunchKernelGGL(widen_u32_kernel, dim3(grid_for(n, 256 * 8, 8192)), dim3(256), 0, c->stream, r32, n,
+                                   kb);
+                QE_HIP(hipGetLastError());
+            }
+            if (!adopted) dfree(c, t->keys32);
+            t->keys32 = nullptr;
+        }
         *keys = H(t->keys);
         for (size_t i = 0; i < t->cols.size(); i++) cols[i] = H(t->cols[i]);
         delete t;

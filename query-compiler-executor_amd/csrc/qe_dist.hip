@@ -45,7 +45,10 @@ __device__ __forceinline__ uint64_t dest_peers(uint32_t d, bool ok, int dbits) {
 
 // rows per destination: per-wave match-any, one LDS add per (wave, item, distinct dest), one
 // global add per (block, dest)
-__global__ void __launch_bounds__(PB) part_count_kernel(const uint64_t* __restrict__ keys, uint64_t n, uint32_t nparts,
+// KI: the keys' width in memory (u32: a side gathered as u32 keys, PreHist::k32) -- the destination
+// is the value's, whatever the width (part_of of the value widened)
+template <typename KI>
+__global__ void __launch_bounds__(PB) part_count_kernel(const KI* __restrict__ keys, uint64_t n, uint32_t nparts,
                                                         int dbits, unsigned long long* __restrict__ counts) {
     // a capped grid (one global add per (block, dest): ~88 adds per us per word) walking tiles of
     // PTILE x 2 rows, 16-B loads, the next tile's loads issued before this one is counted
@@ -60,9 +63,15 @@ __global__ void __launch_bounds__(PB) part_count_kernel(const uint64_t* __restri
         for (int j = 0; j < P_ITEMS; j++) {
             const uint64_t i = tile + (uint64_t)j * (2 * PB) + 2ull * threadIdx.x;
             if (i + 1 < n) {
-                ulonglong2 x = *reinterpret_cast<const ulonglong2*>(keys + i);
-                k[j][0] = x.x;
-                k[j][1] = x.y;
+                if constexpr (sizeof(KI) == 8) {
+                    ulonglong2 x = *reinterpret_cast<const ulonglong2*>(keys + i);
+                    k[j][0] = x.x;
+                    k[j][1] = x.y;
+                } else {
+                    uint2 x = *reinterpret_cast<const uint2*>(keys + i);
+                    k[j][0] = x.x;
+                    k[j][1] = x.y;
+                }
             } else {
                 k[j][0] = i < n ? keys[i] : 0;
                 k[j][1] = 0;
@@ -107,11 +116,13 @@ struct PartCols {
 // staged in LDS in destination order, each destination's range in the send buffer reserved with
 // one atomic on its cursor (cursor[d] starts at d's segment start), and written as runs of
 // ~PTILE / nparts rows.  Order inside a segment is not kept (the receiver sorts).
-template <int NC>
-__global__ void __launch_bounds__(PB) part_scatter_kernel(const uint64_t* __restrict__ keys, uint64_t n,
+// KI / KO: the keys' width in and out (KO = u32: keys below 2^32 leave as 4 B -- half the key bytes
+// of the send buffer, the link and the receive buffer)
+template <int NC, typename KI = uint64_t, typename KO = uint64_t>
+__global__ void __launch_bounds__(PB) part_scatter_kernel(const KI* __restrict__ keys, uint64_t n,
                                                           uint32_t nparts, int dbits,
                                                           unsigned long long* __restrict__ cursor, PartCols pc,
-                                                          uint64_t* __restrict__ okeys) {
+                                                          KO* __restrict__ okeys) {
     __shared__ uint64_t s_key[PTILE];
     __shared__ uint32_t s_col[NC > 0 ? NC : 1][PTILE];
     __shared__ uint8_t s_dest[PTILE];
@@ -182,7 +193,7 @@ __global__ void __launch_bounds__(PB) part_scatter_kernel(const uint64_t* __rest
     for (uint32_t i = threadIdx.x; i < total; i += PB) {
         const uint32_t d = s_dest[i];
         const uint64_t o = gbase[d] + (i - toff[d]);
-        okeys[o] = s_key[i];
+        okeys[o] = (KO)s_key[i];
 #pragma unroll
         for (int c = 0; c < NC; c++) pc.out[c][o] = s_col[c][i];
     }
@@ -406,7 +417,8 @@ __global__ void part_starts_kernel(const unsigned long long* __restrict__ cnt, u
 }
 
 void partition_dev(qe_ctx* c, const uint64_t* keys, uint64_t n, const uint32_t* const* cols, int ncols,
-                   uint32_t nparts, unsigned long long* d_cnt, uint64_t* out_keys, uint32_t* const* out_cols) {
+                   uint32_t nparts, unsigned long long* d_cnt, uint64_t* out_keys, uint32_t* const* out_cols,
+                   const uint32_t* keys32, bool out32) {
     if (nparts < 1 || nparts > (uint32_t)PMAX) throw Error(QE_EINVAL, "nparts must be in [1, 64]");
     if (ncols < 0 || ncols > 4) throw Error(QE_EINVAL, "at most 4 rowid columns per partition call");
     if (n >= 0xFFFFFFFFull) throw Error(QE_EINVAL, "partition input too large");
@@ -420,21 +432,34 @@ void partition_dev(qe_ctx* c, const uint64_t* keys, uint64_t n, const uint32_t* 
         pc.in[i] = cols[i];
         pc.out[i] = out_cols[i];
     }
+    const double kin = keys32 ? 4.0 : 8.0, kout = out32 ? 4.0 : 8.0;
     {
-        Timed t(c, "partition_count", 8.0 * n);
-        hipLaunchKernelGGL(part_count_kernel, dim3(std::min<uint32_t>(nb, 1024)), dim3(PB), 0, c->stream, keys, n,
-                           nparts, dbits, d_cnt);
+        Timed t(c, "partition_count", kin * n);
+        if (keys32)
+            hipLaunchKernelGGL(part_count_kernel<uint32_t>, dim3(std::min<uint32_t>(nb, 1024)), dim3(PB), 0, c->stream,
+                               keys32, n, nparts, dbits, d_cnt);
+        else
+            hipLaunchKernelGGL(part_count_kernel<uint64_t>, dim3(std::min<uint32_t>(nb, 1024)), dim3(PB), 0, c->stream,
+                               keys, n, nparts, dbits, d_cnt);
         QE_HIP(hipGetLastError());
     }
     hipLaunchKernelGGL(part_starts_kernel, dim3(1), dim3(64), 0, c->stream, d_cnt, d_cnt + PMAX, nparts);
     QE_HIP(hipGetLastError());
     {
-        Timed t(c, "partition", (8.0 + 4.0 * ncols) * 2.0 * n);
+        Timed t(c, "partition", (kin + kout + 8.0 * ncols) * n);
+        uint32_t* ok32 = reinterpret_cast<uint32_t*>(out_keys);
         switch (ncols) {
 #define QE_PS(NC)                                                                                                 \
     case NC:                                                                                                      \
-        hipLaunchKernelGGL(part_scatter_kernel<NC>, dim3(nb), dim3(PB), 0, c->stream, keys, n, nparts, dbits,    \
-                           d_cnt + PMAX, pc, out_keys);                                                           \
+        if (keys32 && out32)                                                                                      \
+            hipLaunchKernelGGL((part_scatter_kernel<NC, uint32_t, uint32_t>), dim3(nb), dim3(PB), 0, c->stream,    \
+                               keys32, n, nparts, dbits, d_cnt + PMAX, pc, ok32);                                 \
+        else if (out32)                                                                                           \
+            hipLaunchKernelGGL((part_scatter_kernel<NC, uint64_t, uint32_t>), dim3(nb), dim3(PB), 0, c->stream,    \
+                               keys, n, nparts, dbits, d_cnt + PMAX, pc, ok32);                                   \
+        else                                                                                                      \
+            hipLaunchKernelGGL((part_scatter_kernel<NC>), dim3(nb), dim3(PB), 0, c->stream, keys, n, nparts,       \
+                               dbits, d_cnt + PMAX, pc, out_keys);                                                \
         break;
             QE_PS(0) QE_PS(1) QE_PS(2) QE_PS(3) QE_PS(4)
 #undef QE_PS

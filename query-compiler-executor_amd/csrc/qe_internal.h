@@ -101,9 +101,37 @@ struct PreHist {
 
 }  // namespace qe
 
+// The per-stream working state queued work addresses: the stream, its lookback status words and
+// tickets, scalar scratch and result words.  A ctx owns two: the main one (in the ctx's own fields)
+// and a side one (qe_ctx::side) that SideFork (qe_join.hip) swaps in while one join side's sort is
+// queued on the side stream, concurrently with the other side's.
+struct StreamState {
+    hipStream_t stream = nullptr;
+    uint64_t* lb_status = nullptr;
+    size_t lb_status_words = 0;
+    uint32_t* lb_tickets = nullptr;
+    uint32_t lb_epoch = 0;
+    uint64_t* d_scratch = nullptr;
+    uint32_t* d_zhist = nullptr;
+    bool zhist_dirty = false;
+    uint64_t* h_scratch = nullptr;
+    hipEvent_t wait_ev = nullptr;
+    uint64_t* h_ret = nullptr;
+    uint64_t* d_ret = nullptr;
+    uint64_t ret_seq = 0;
+};
+
 struct qe_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // the side stream's state (swapped with the fields above while a side is queued on it), and
+    // the frees held back while two streams run: a block freed by one stream's queued work must
+    // not be handed to the other stream's before they meet (released by SideFork::join)
+    StreamState side;
+    bool side_in = false;      // the side state is the one in the ctx's fields
+    int hold_frees = 0;
+    std::vector<void*> held;
+    hipEvent_t fork_ev[2] = {nullptr, nullptr};
     std::string err;
     std::string late_err;   // an internal violation found where no throw is allowed (dfree), surfaced later
 
@@ -221,6 +249,29 @@ struct LBSlot {
 };
 LBSlot lb_acquire(qe_ctx* c, size_t words);
 
+// One join side's sort queued on the ctx's side stream while the other side's sort is queued on the
+// ctx stream, so the two run concurrently (a histogram's LDS atomics, a gather's latency and the
+// small scan launches of one side beside the other's streaming passes).
+//   SideFork f(c, big);  f.enter(); <queue side A>  f.leave();  <queue side B>  f.join();  <consumer>
+// The side stream waits for the ctx stream's work queued before the fork; join() makes the ctx
+// stream wait for the side stream's; frees in between are held and recycled at join() (a block one
+// stream frees must not be reused by the other's queued work).  The side state (stream, lookback
+// words, scratch, result words) is swapped into the ctx's fields between enter() and leave(), so
+// everything queued there addresses it unchanged.  The destructor joins.  QE_SIDE_STREAM=1: on
+// (off by default: see side_stream_on).
+struct SideFork {
+    qe_ctx* c;
+    bool on = false;
+    SideFork(qe_ctx* c, bool want);
+    ~SideFork();
+    void enter();
+    void leave();
+    void join();
+    SideFork(const SideFork&) = delete;
+    SideFork& operator=(const SideFork&) = delete;
+};
+bool side_stream_on();
+
 // profiling-aware launch bracket
 void add_bytes(qe_ctx* c, const char* stage, double bytes);
 
@@ -308,7 +359,10 @@ bool join_pairs_carry(qe_ctx* c, qe_pairs* R, qe_pairs* S, const uint32_t* xa, c
                       const uint64_t* rc64 = nullptr, qe_list* outRX = nullptr, const uint64_t* rv64 = nullptr);
 // keys = (u64) vals for a list whose sort will be the lookback-free two-level one, with that
 // sort's histogram (gather_with_hist without the gather); false: not that sort
-bool widen_with_hist(qe_ctx* c, const uint32_t* vals, uint64_t n, uint64_t kor, uint64_t kand, uint64_t* keys);
+// adopted (nullable): vals is a dalloc block of the keys as u32 that the caller gives up if the sort
+// keeps its keys as u32 (PreHist::k32 = vals, no copy); *adopted = whether it did
+bool widen_with_hist(qe_ctx* c, const uint32_t* vals, uint64_t n, uint64_t kor, uint64_t kand, uint64_t* keys,
+                     bool* adopted = nullptr);
 // a key buffer gathered as u32 only (PreHist::k32): widen it into the buffer now (no-op otherwise)
 void keys_need_u64(qe_ctx* c, const void* keys);
 // the join's checksums without its pairs (the plan's last join): sums[k] = sum over pairs of
@@ -330,9 +384,14 @@ SortOut radix_sort_u32(qe_ctx* c, const uint32_t* keys, const uint32_t* vals, ui
                        const uint64_t* bits = nullptr);
 // multi-GPU (qe_dist.hip): hash-partition rows into per-destination segments of out_keys /
 // out_cols; d_cnt (2 x 64 words, device) receives the per-destination counts (then the cursors).
-// Queued on the ctx stream, no host synchronisation.
+// Queued on the ctx stream, no host synchronisation.  keys32 (nullable): read these u32 keys instead
+// of `keys`; out32: write the keys as u32 into out_keys (every key below 2^32).  A key's destination
+// is its value's, whatever the width.
 void partition_dev(qe_ctx* c, const uint64_t* keys, uint64_t n, const uint32_t* const* cols, int ncols,
-                   uint32_t nparts, unsigned long long* d_cnt, uint64_t* out_keys, uint32_t* const* out_cols);
+                   uint32_t nparts, unsigned long long* d_cnt, uint64_t* out_keys, uint32_t* const* out_cols,
+                   const uint32_t* keys32 = nullptr, bool out32 = false);
+// the keys' pending u32 copy (PreHist::k32: gathered as u32, the u64 buffer not yet written), or null
+const uint32_t* keys_pending_u32(qe_ctx* c, const void* keys);
 // OR / AND of n keys -> host out[2] (synchronises)
 void key_bits_u64(qe_ctx* c, const uint64_t* keys, uint64_t n, uint64_t* out);
 // (key field << 32 | (uint32_t) val) words of a base column, stable-sorted by the field

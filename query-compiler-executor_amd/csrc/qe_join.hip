@@ -1809,6 +1809,13 @@ static bool sort_cached(qe_ctx* c, qe_pairs* p, bool defer) {
     return true;
 }
 
+// the two sides of a join sorted concurrently (SideFork): both large enough for the lookback-free
+// two-level sort, outside a batch's shared sorts (the lanes are the concurrency there)
+static bool fork_sides(const qe_ctx* c, const qe_pairs* R, const qe_pairs* S) {
+    return !c->scache && R->n >= (1u << 22) && S->n >= (1u << 22) && !(R->flags & PF_SORTED) &&
+           !(S->flags & PF_SORTED);
+}
+
 static void sort_pairs(qe_ctx* c, qe_pairs* p, bool defer) {
     if (p->flags & PF_SORTED) return;
     if (sort_cached(c, p, defer)) return;
@@ -1879,8 +1886,13 @@ int qe_join_pairs(qe_ctx* c, qe_pairs* R, qe_pairs* S, qe_list* outR, qe_list* o
     // 2529-2533 queries/s same box, 155 bucket joins per batch instead of 104 (profiles/r03_c4_knobs_ab.log)
     static const bool unify = !(getenv("QE_JOIN_UNIFY") && getenv("QE_JOIN_UNIFY")[0] == '0');
     if (unify) unify_geometry(R, S);
-    sort_pairs(c, R, true);
-    sort_pairs(c, S, true);
+    {
+        SideFork fk(c, fork_sides(c, R, S));
+        fk.enter();
+        sort_pairs(c, R, true);
+        fk.leave();
+        sort_pairs(c, S, true);
+    }
     if (bucket_join(c, R, S, outR, outS)) return 0;
     pairs_need_keys(c, R);
     pairs_need_keys(c, S);
@@ -1905,7 +1917,10 @@ bool join_pairs_carry(qe_ctx* c, qe_pairs* R, qe_pairs* S, const uint32_t* xa, c
     c->carry_x32 = rx32;
     c->carry_c64 = rc64;
     c->sort_v64 = rv64;
+    SideFork fk(c, fork_sides(c, R, S));   // R's sort on the side stream, S's beside it
+    fk.enter();
     sort_pairs(c, R, true);
+    fk.leave();
     c->carry_x32 = nullptr;   // (consumed by R's sort; cleared in any case)
     c->carry_c64 = nullptr;
     c->sort_v64 = nullptr;
@@ -1922,6 +1937,7 @@ bool join_pairs_carry(qe_ctx* c, qe_pairs* R, qe_pairs* S, const uint32_t* xa, c
     c->carry_x32 = xb ? nullptr : xa;
     sort_pairs(c, S, true);
     c->carry_xa = c->carry_xb = c->carry_x32 = nullptr;   // (consumed by S's sort; cleared in any case)
+    fk.join();
     if (bucket_join(c, R, S, outR, outS, xa ? outX0 : nullptr, xa && xb ? outX1 : nullptr, rpay ? outRX : nullptr))
         return true;
     // a bucket beyond LDS: drop both deferred sorts, give the caller its inputs back
@@ -1937,14 +1953,19 @@ bool join_pairs_sums(qe_ctx* c, qe_pairs* R, qe_pairs* S, const uint32_t* xa, co
     if (!carry_eligible(R, S)) return false;
     const qe_pairs R0 = *R, S0 = *S;
     if ((R0.owns | S0.owns) & 7) return false;
-    c->sort_keys_only = !R->val;   // R's keys are only counted: its rows never travel
-    sort_pairs(c, R, true);
-    c->sort_keys_only = false;
-    c->carry_xa = xb ? xa : nullptr;   // (null: no payload; one column: 32-bit)
-    c->carry_xb = xb;
-    c->carry_x32 = xb ? nullptr : xa;
-    sort_pairs(c, S, true);
-    c->carry_xa = c->carry_xb = c->carry_x32 = nullptr;
+    {
+        SideFork fk(c, fork_sides(c, R, S));   // R's sort on the side stream, S's beside it
+        c->sort_keys_only = !R->val;   // R's keys are only counted: its rows never travel
+        fk.enter();
+        sort_pairs(c, R, true);
+        fk.leave();
+        c->sort_keys_only = false;
+        c->carry_xa = xb ? xa : nullptr;   // (null: no payload; one column: 32-bit)
+        c->carry_xb = xb;
+        c->carry_x32 = xb ? nullptr : xa;
+        sort_pairs(c, S, true);
+        c->carry_xa = c->carry_xb = c->carry_x32 = nullptr;
+    }
     if (bucket_join_sums(c, R, S, sc, pairs, sums)) return true;
     qe_pairs_free(c, R);
     qe_pairs_free(c, S);

@@ -107,6 +107,10 @@ void dfree(qe_ctx* c, void* p) {
         if (c->late_err.empty()) c->late_err = "internal: dfree of a shared sort's buffer";
         return;
     }
+    if (c->hold_frees) {   // two streams in flight: recycled once they have met (SideFork::join)
+        c->held.push_back(p);
+        return;
+    }
     auto it = c->live.find(p);
     if (it == c->live.end()) return;   // not ours (e.g. a relation column)
     size_t sz = it->second;
@@ -125,6 +129,90 @@ void drop_partitions(qe_ctx* c) {
     }
     c->bparts.clear();
     c->bparts_n = c->bparts_p = 0;
+}
+
+// ---- the side stream (SideFork): one join side's sort queued beside the other's -------------------
+static void swap_state(qe_ctx* c) {
+    StreamState& s = c->side;
+    std::swap(c->stream, s.stream);
+    std::swap(c->lb_status, s.lb_status);
+    std::swap(c->lb_status_words, s.lb_status_words);
+    std::swap(c->lb_tickets, s.lb_tickets);
+    std::swap(c->lb_epoch, s.lb_epoch);
+    std::swap(c->d_scratch, s.d_scratch);
+    std::swap(c->d_zhist, s.d_zhist);
+    std::swap(c->zhist_dirty, s.zhist_dirty);
+    std::swap(c->h_scratch, s.h_scratch);
+    std::swap(c->wait_ev, s.wait_ev);
+    std::swap(c->h_ret, s.h_ret);
+    std::swap(c->d_ret, s.d_ret);
+    std::swap(c->ret_seq, s.ret_seq);
+    c->side_in = !c->side_in;
+}
+
+bool side_stream_on() {
+    // QE_SIDE_STREAM=1: on.  Off by default: C3 6.30 -> 6.15 ms per query on one box (-2.4 %,
+    // profiles/r06d_c3_bench.log), but the two sides' kernels then share the GPU, so a launch's
+    // duration no longer measures that kernel alone -- the line's per-launch roofline would not mean
+    // what it says (sort_pass_carry 3.05 -> 4.22 ms of overlapped launch time per query)
+    const char* s = getenv("QE_SIDE_STREAM");   // (read per join: tests switch it)
+    return s && s[0] == '1';
+}
+
+SideFork::SideFork(qe_ctx* cc, bool want) : c(cc) {
+    if (!want || !side_stream_on() || c->side_in || c->hold_frees) return;   // (no nesting)
+    StreamState& s = c->side;
+    if (!s.stream) {   // made once per ctx, on first use
+        QE_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+        QE_HIP(hipMalloc(&s.lb_tickets, LB_MAX_COUNTERS * sizeof(uint32_t)));
+        QE_HIP(hipMemsetAsync(s.lb_tickets, 0, LB_MAX_COUNTERS * sizeof(uint32_t), s.stream));
+        QE_HIP(hipMalloc(&s.d_scratch, 64 * sizeof(uint64_t)));
+        QE_HIP(hipHostMalloc((void**)&s.h_scratch, 64 * sizeof(uint64_t), hipHostMallocDefault));
+        for (auto& e : c->fork_ev) QE_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    // the side stream starts after everything queued on the ctx stream so far (its inputs)
+    QE_HIP(hipEventRecord(c->fork_ev[0], c->stream));
+    QE_HIP(hipStreamWaitEvent(s.stream, c->fork_ev[0], 0));
+    c->hold_frees++;
+    on = true;
+}
+
+void SideFork::enter() {
+    if (on && !c->side_in) swap_state(c);
+}
+
+void SideFork::leave() {
+    if (on && c->side_in) swap_state(c);
+}
+
+void SideFork::join() {
+    if (!on) return;
+    leave();
+    on = false;
+    // the ctx stream goes on after the side stream's work; then both streams' frees are safe
+    QE_HIP(hipEventRecord(c->fork_ev[1], c->side.stream));
+    QE_HIP(hipStreamWaitEvent(c->stream, c->fork_ev[1], 0));
+    if (--c->hold_frees == 0) {
+        std::vector<void*> h;
+        h.swap(c->held);
+        for (void* p : h) dfree(c, p);
+    }
+}
+
+SideFork::~SideFork() {
+    if (!on) return;
+    try {
+        join();
+    } catch (...) {   // (a failed event call: wait for both streams instead)
+        if (c->side_in) swap_state(c);
+        (void)hipStreamSynchronize(c->side.stream);
+        (void)hipStreamSynchronize(c->stream);
+        if (--c->hold_frees == 0) {
+            std::vector<void*> h;
+            h.swap(c->held);
+            for (void* p : h) dfree(c, p);
+        }
+    }
 }
 
 LBSlot lb_acquire(qe_ctx* c, size_t words) {
@@ -593,6 +681,7 @@ void qe_fini(qe_ctx* c) {
     c->workers.clear();
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    if (c->side.stream) (void)hipStreamSynchronize(c->side.stream);
     for (auto& r : c->rels) free_relation(r);
     for (auto& kv : c->free_blocks) hfree(c, kv.second);
     for (auto& kv : c->live) hfree(c, kv.first);
@@ -608,6 +697,20 @@ void qe_fini(qe_ctx* c) {
     if (c->h_scratch) (void)hipHostFree(c->h_scratch);
     if (c->h_ret) (void)hipHostFree(c->h_ret);
     if (c->wait_ev) (void)hipEventDestroy(c->wait_ev);
+    {   // the side stream's state (never swapped in here: SideFork restores the main one)
+        StreamState& s = c->side;
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+        if (s.lb_status) (void)hipFree(s.lb_status);
+        if (s.lb_tickets) (void)hipFree(s.lb_tickets);
+        if (s.d_scratch) (void)hipFree(s.d_scratch);
+        if (s.d_zhist) (void)hipFree(s.d_zhist);
+        if (s.h_scratch) (void)hipHostFree(s.h_scratch);
+        if (s.h_ret) (void)hipHostFree(s.h_ret);
+        if (s.wait_ev) (void)hipEventDestroy(s.wait_ev);
+        if (s.stream) (void)hipStreamDestroy(s.stream);
+        for (auto e : c->fork_ev)
+            if (e) (void)hipEventDestroy(e);
+    }
     for (int k = 0; k < qe_ctx::STAGE_SLOTS; k++) {
         if (c->h_stage[k]) (void)hipHostFree(c->h_stage[k]);
         if (c->stage_ev[k]) (void)hipEventDestroy(c->stage_ev[k]);

@@ -1150,7 +1150,9 @@ __global__ void __launch_bounds__(1024) tl_gather_hist_kernel(const uint64_t* __
         for (int j = 0; j < 8; j++) {
             const uint64_t i = base + (uint64_t)j * 1024 + threadIdx.x;
             if (i < n) {
-                if (k32out) k32out[i] = (uint32_t)k[j];   // (grid-uniform: keys below 2^32, PreHist::k32)
+                if (k32out) {   // (grid-uniform: keys below 2^32, PreHist::k32)
+                    if (k32out != rows) k32out[i] = (uint32_t)k[j];   // (== rows: DIRECT adopts its input)
+                }
                 else keys[i] = k[j];
                 const uint32_t b = (uint32_t)((((k[j] >> f.lo) & f.fmask) >> L) & (TL_BUCKETS - 1));
                 atomicAdd(&h[((b & 255u) << 7) | (b >> 8)], 1u);
@@ -3256,8 +3258,13 @@ void pairs_drop_deferred(qe_ctx* c, const qe_pairs* p, bool keep_k32) {
     c->deferred.erase(it);
 }
 
+// adopt (DIRECT only, nullable): `rows` are the keys as u32 in a dalloc block the caller hands over --
+// they become the PreHist::k32 copy as they are (no write) when the keys are kept as u32; *adopted
+// says whether they were (else the caller still owns the block)
 static bool gather_hist_impl(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint64_t n, uint64_t kor,
-                             uint64_t kand, uint64_t* keys, const uint32_t* col32 = nullptr) {
+                             uint64_t kand, uint64_t* keys, const uint32_t* col32 = nullptr, bool adopt = false,
+                             bool* adopted = nullptr) {
+    if (adopted) *adopted = false;
     // exactly the plan radix_sort_impl will choose for these keys and bounds: the packed
     // two-level sort in its lookback-free form
     if (n < 2 || n >= 0xFFFFFFFFull) return false;
@@ -3280,8 +3287,11 @@ static bool gather_hist_impl(qe_ctx* c, const uint64_t* col, const uint32_t* row
     uint32_t* gout = hist_slices(c, gcnt, Q, nseg);
     // the plan engine's keys below 2^32 are gathered as u32 (PreHist::k32): its deferred sort's
     // first pass reads 4 B per key instead of 8, and the gather writes 4
-    uint32_t* k32 = c->gather_k32 && !(kor >> 32) && gather_k32_on() ? dalloc_t<uint32_t>(c, n) : nullptr;
-    const double kw = k32 ? 4.0 : 8.0;
+    const bool keep32 = c->gather_k32 && !(kor >> 32) && gather_k32_on();
+    const bool take = adopt && !col && keep32;
+    uint32_t* k32 = take ? const_cast<uint32_t*>(rows) : keep32 ? dalloc_t<uint32_t>(c, n) : nullptr;
+    if (adopted) *adopted = take;
+    const double kw = take ? 0.0 : k32 ? 4.0 : 8.0;
     if (col) {
         Timed t(c, "gather_keys", (col32 ? 8.0 : 12.0) * n + kw * n);
         hipLaunchKernelGGL(tl_gather_hist_kernel<false>, dim3(G * Q), dim3(1024), 0, c->stream, col, rows, n, keys, f, L,
@@ -3311,6 +3321,11 @@ __global__ void __launch_bounds__(256) widen_keys_kernel(const uint32_t* __restr
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) keys[i] = k32[i];
 }
 
+const uint32_t* keys_pending_u32(qe_ctx* c, const void* keys) {
+    auto it = c->prehist.find(keys);
+    return it == c->prehist.end() ? nullptr : it->second.k32;
+}
+
 void keys_need_u64(qe_ctx* c, const void* keys) {
     auto it = c->prehist.find(keys);
     if (it == c->prehist.end() || !it->second.k32) return;
@@ -3330,8 +3345,9 @@ bool gather_with_hist(qe_ctx* c, const uint64_t* col, const uint32_t* rows, uint
     return gather_hist_impl(c, col, rows, n, kor, kand, keys, narrow_of(c, col, col_rows));
 }
 
-bool widen_with_hist(qe_ctx* c, const uint32_t* vals, uint64_t n, uint64_t kor, uint64_t kand, uint64_t* keys) {
-    return gather_hist_impl(c, nullptr, vals, n, kor, kand, keys);
+bool widen_with_hist(qe_ctx* c, const uint32_t* vals, uint64_t n, uint64_t kor, uint64_t kand, uint64_t* keys,
+                     bool* adopted) {
+    return gather_hist_impl(c, nullptr, vals, n, kor, kand, keys, nullptr, adopted != nullptr, adopted);
 }
 
 // the bucket geometry radix_sort_impl would give a deferred sort of p (its pass plan, from the

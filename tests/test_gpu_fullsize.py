@@ -46,3 +46,20 @@ def test_c2_pair_100m(ctx, full):
     assert rc == 0
     assert out == f"{s0} {s1} \n"
     assert ctx.last_result_rows() == pairs
+
+
+@pytest.mark.parametrize("side_stream", ["0", "1"])
+def test_c3_planned_with_and_without_the_side_stream(ctx, full, side_stream, monkeypatch):
+    """the partitioned plan on C3 with each join's two sorts on one stream, and (QE_SIDE_STREAM=1)
+    with one side's sort on the ctx's side stream concurrently with the other's (SideFork: the side
+    stream's own lookback words and scratch, frees held until the streams meet): the same bytes as
+    the aggregate truth, three times in a row (the held blocks recycled between queries)"""
+    monkeypatch.setenv("QE_SIDE_STREAM", side_stream)
+    c2 = full[3][2]
+    mask = (c2 > np.uint64(1000000000)) & (c2 < np.uint64(3000000000))
+    cnt, rows, sums = agg_truth.chain4_sums(full, N, mask)
+    want = f"{cnt}\n" + "".join(f"{s} " for s in sums) + "\n"
+    for _ in range(3):
+        out, rc, refused = ctx.run_dist(C3)
+        assert (out, rc, refused) == (want, 0, 0)
+        assert ctx.last_result_rows() == rows

@@ -119,3 +119,22 @@ def test_local_ranks_c3_100m(ctx, world):
         assert (sent > 0) == (world == 8)
     finally:
         ctx.drop_relations()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_sends_u32_keys_when_they_fit(ctx, world, monkeypatch):
+    """keys below 2^32 cross ranks as 4 B (QE_EXCHANGE_K32, default on): the same bytes printed as
+    with 8-B keys, fewer bytes sent -- C3's exchanged sides carry a key + 1-2 rowid/value columns,
+    so 8 + 4c -> 4 + 4c bytes a row (the receiver's sort takes the u32 keys as they arrive)"""
+    monkeypatch.setenv("QE_PLAN_BCAST", "0")
+    doc = goldens.load(f"{goldens.GOLDEN_DIR}/headline.json")
+    _load(ctx, doc["dataset"])
+    case = next(c for c in doc["cases"] if c["input"] == C3)
+    monkeypatch.setenv("QE_EXCHANGE_K32", "0")
+    out64, rc64, _, sent64 = ctx.run_local(C3, world)
+    monkeypatch.setenv("QE_EXCHANGE_K32", "1")
+    out32, rc32, _, sent32 = ctx.run_local(C3, world)
+    assert (out64, rc64) == (case["stdout"], 0)
+    assert (out32, rc32) == (case["stdout"], 0)
+    assert 0 < sent32 < sent64
+    assert sent32 <= sent64 * 3 // 4 + 1               # at least a key's 4 B of every 16-B row
