@@ -251,22 +251,34 @@ def run_dist(args):
     # 3) the same plan with the query's last join materialised (QE_PLAN_AGG=0: its pairs made by the
     #    chain bucket join, then summed by the checksum gathers) -- the line's own last join counts
     #    its pairs in aggregate form and never writes them; every rank runs it (it is collective)
-    mat_line = None
-    if not args.no_materialised and not args.no_faithful:   # (profiling runs: the measured plan only)
-        agg_env = os.environ.get("QE_PLAN_AGG")
-        os.environ["QE_PLAN_AGG"] = "0"
+    def timed_with(var, val):
+        old = os.environ.get(var)
+        os.environ[var] = val
         try:
-            dtm, out_m, _, _ = timed_steps()
+            return timed_steps()
         finally:
-            if agg_env is None:
-                del os.environ["QE_PLAN_AGG"]
+            if old is None:
+                del os.environ[var]
             else:
-                os.environ["QE_PLAN_AGG"] = agg_env
+                os.environ[var] = old
+
+    mat_line = side_line = None
+    if not args.no_materialised and not args.no_faithful:   # (profiling runs: the measured plan only)
+        dtm, out_m, _, _ = timed_with("QE_PLAN_AGG", "0")
         mat_line = {"last_join": "materialised: every result pair written (rowid pairs + carried columns), "
                                  "then the checksums gather the select columns",
                     "ms_per_step": round(dtm / args.steps * 1e3, 3),
                     "value": round(ctx.last_result_rows() * args.steps / dtm, 1),
                     "stdout_identical": out_m == out}
+        # 4) the same plan with each join's two sorts on two streams (QE_SIDE_STREAM=1, SideFork):
+        #    faster end to end, but its kernels share the GPU, so the line's per-launch roofline is
+        #    measured with it off (the default)
+        if os.environ.get("QE_SIDE_STREAM", "0") != "1":
+            dts, out_s, _, _ = timed_with("QE_SIDE_STREAM", "1")
+            side_line = {"side_stream": "one join side's sort on a second HIP stream beside the other's",
+                         "ms_per_step": round(dts / args.steps * 1e3, 3),
+                         "value": round(ctx.last_result_rows() * args.steps / dts, 1),
+                         "stdout_identical": out_s == out}
     if rank == 0:
         if faithful is not None and not multi:   # N = 1: the faithful executor timed too, for the record
             torch.cuda.synchronize()
@@ -303,6 +315,7 @@ def run_dist(args):
                                     "print_sums reads them; see materialised_last_join)",
                        "load_partition_s": round(t_part, 4) if t_part is not None else None},
             "materialised_last_join": mat_line,
+            "two_stream_sorts": side_line,
             "faithful_executor": faithful_line,
             "roofline": roofline({dominant: stats[dominant]} if dominant in stats else stats,
                                  traffic, args.steps),

@@ -151,8 +151,9 @@ static void swap_state(qe_ctx* c) {
 }
 
 bool side_stream_on() {
-    // QE_SIDE_STREAM=1: on.  Off by default: C3 6.30 -> 6.15 ms per query on one box (-2.4 %,
-    // profiles/r06d_c3_bench.log), but the two sides' kernels then share the GPU, so a launch's
+    // QE_SIDE_STREAM=1: on.  Off by default: C3 6.30 -> 6.15 / 6.29 -> 5.93 ms per query on two
+    // boxes (-2.4 / -5.8 %, profiles/r06d_c3_bench.log, r06e_c3_bench.log; bench.py reports it as
+    // `two_stream_sorts`), but the two sides' kernels then share the GPU, so a launch's
     // duration no longer measures that kernel alone -- the line's per-launch roofline would not mean
     // what it says (sort_pass_carry 3.05 -> 4.22 ms of overlapped launch time per query)
     const char* s = getenv("QE_SIDE_STREAM");   // (read per join: tests switch it)

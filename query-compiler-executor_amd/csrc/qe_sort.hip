@@ -3689,6 +3689,9 @@ bool bucket_join_sums(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const HjS
             return (uint32_t)std::max(1, 2 * ncu);
         }();
         static const bool persist = !(getenv("QE_HJ_SUMS_PERSIST") && getenv("QE_HJ_SUMS_PERSIST")[0] == '0');
+        // (one barrier per bucket -- three count tables used round robin -- with or without the next
+        // bucket's loads in flight at one workgroup per CU measured slower: 0.375 -> 0.424 / 0.431 ms
+        // per C3 query, profiles/r06e_c3_bench.log)
         const uint32_t grid = persist ? std::min<uint32_t>(resident, TL_BUCKETS) : (uint32_t)TL_BUCKETS;
         // S's payload as the kernel holds it: none when no select reads one, else u32 or u64
         const int xk = !carry ? 0 : dS.x32 ? 1 : 2;

@@ -598,14 +598,26 @@ static void free_comp(plan_t* P, int cid) {
 }
 
 /* Broadcast or partitioned, for a join of a derived side D with a whole base relation of R rows at
- * G > 1 ranks (DESIGN §5's per-rank budget).  Partitioned (the default plan): D
- * is exchanged -- per rank D/G rows hash-partitioned (~13 ps a row) and 1/G of them to each peer
- * over its own xGMI link (16 B a row at ~150 GB/s: D*16/(G^2 * 150 GB/s)) -- and joined with the
- * rank's bucket of the base column (R/G rows).  Broadcast: D stays where it lies and is joined with
- * the WHOLE column, so the base side's sort does not shrink with G: (1 - 1/G) * R rows more at
- * ~10 ps a row (a two-level sort of 1e8 keys ~1 ms).  Broadcast wins at G = 2 (one link between the
- * two GPUs carries a quarter of D), partitioned from G = 4.  QE_PLAN_BCAST: 0 never, 2 always
- * (tests), otherwise this model.  Every rank decides on the same global sizes. */
+ * G > 1 ranks (DESIGN §5's per-rank budget).  Per rank:
+ *   partitioned: D/G rows hash-partitioned (COST_PART_PS a row), 1/G of them to each peer over its
+ *     own xGMI link (D * B / (G^2 * COST_LINK_GBS), B = a u32 key + 4 B per carried column), one
+ *     counts all-to-all + host round trip (COST_EXCHANGE_PS); the base side is the rank's hash
+ *     bucket (R/G rows, selected once per column and kept: free from the second query on);
+ *   broadcast: D stays where it lies and is joined with the WHOLE column: (1 - 1/G) * R rows more
+ *     through the base side's sort and the bucket join than the partitioned form's R/G.
+ * Broadcast iff (1 - 1/G) * R * (COST_BASE_SORT_PS + COST_JOIN_PS) < the partitioned form's extra.
+ * The per-row costs are this code's, measured on one MI355X (profiles/r06b_launches.txt: one C3
+ * query's kernels -- the 1e8-row carried base side's histogram + scans + two passes 0.97 ms, the
+ * chain bucket join 0.48 ms for 1e8 + 4.66e7 rows; profiles/r06e_cost_constants.json: partition_dev
+ * of a 4.66e7-row side with 8-B keys and two columns); the link figure is the MI355X_MICROARCH.md
+ * per-link rate, projected (no box here has two GPUs).  C3 then: broadcast at G = 2, partitioned
+ * from G = 4.  QE_PLAN_BCAST: 0 never, 2 always (tests), otherwise this model.  Every rank decides
+ * on the same global sizes (and the same switches: plan_allreduce). */
+#define COST_BASE_SORT_PS 9.7
+#define COST_JOIN_PS 3.3
+#define COST_PART_PS 9.0
+#define COST_LINK_GBS 153.0
+#define COST_EXCHANGE_PS 5.0e7
 static int bcast_join(const plan_t* P, int A, int B) {
     const qe_engine* e = P->e;
     if (e->world <= 1 || !e->base_side_all) return 0;
@@ -614,9 +626,11 @@ static int bcast_join(const plan_t* P, int A, int B) {
     const int mode = P->bcast_mode;            /* (read once per query, agreed across ranks) */
     if (mode != 1) return mode == 2;
     const double G = (double)e->world;
-    const double R = (double)(wa ? P->C[A].size : P->C[B].size), D = (double)(wa ? P->C[B].size : P->C[A].size);
-    const double bcast_ps = (1.0 - 1.0 / G) * R * 10.0;
-    const double part_ps = D / G * 13.0 + D * 16.0 / (G * G) / 150e9 * 1e12;
+    const comp_t* Dc = wa ? &P->C[B] : &P->C[A];
+    const double R = (double)(wa ? P->C[A].size : P->C[B].size), D = (double)Dc->size;
+    const double bytes = 4.0 + 4.0 * (double)(Dc->n < 3 ? Dc->n : 3);   /* u32 key + carried columns */
+    const double bcast_ps = (1.0 - 1.0 / G) * R * (COST_BASE_SORT_PS + COST_JOIN_PS);
+    const double part_ps = D / G * COST_PART_PS + D * bytes / (G * G) / (COST_LINK_GBS * 1e9) * 1e12 + COST_EXCHANGE_PS;
     return bcast_ps < part_ps;
 }
 
