@@ -1,17 +1,19 @@
-# sort_pass_carry's spread across runs on one box: the GPU's clocks, power and temperature sampled
-# (read-only rocm-smi) while the C3 line runs three times back to back -> gpurun_out/TAG_clocks.log
+# The box state the C3 line runs in: a read-only rocm-smi snapshot (power cap, perf level, VBIOS,
+# product), then the C3 query looped ~5 s twice while rocm-smi samples sclk / mclk / power / junction
+# temperature continuously beside it -> gpurun_out/TAG_clocks.log; the RESULT lines carry the line's
+# ms per query and the sort passes' time, so slow and fast boxes can be told apart by their clocks.
+#   tools/clock_probe.sh TAG [STEPS]
 set -o pipefail
 mkdir -p gpurun_out
-T=${1:-r05zb}
+T=${1:-clk}; S=${2:-400}
 O=gpurun_out/${T}_clocks.log
-: > $O
-for rep in 1 2 3; do
-  ( for i in $(seq 120); do echo "t=$(date +%s.%N | cut -c1-14) rep=$rep"; rocm-smi --showclocks --showpower --showtemp 2>/dev/null | grep -E "sclk|mclk|fclk|Power|Temperature" ; sleep 0.5; done ) >> $O 2>&1 &
-  smi=$!
-  echo "== run $rep" >> $O
-  timeout -k 10 240 python bench.py --no-cpu --no-faithful --steps 10 --warmup 2 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); s=d['stages']; print('RESULT', d['ms_per_step'], d['kernel_ms_per_step'], {k: v['ms_per_step'] for k, v in list(s.items())[:4]})" >> $O 2>&1
-  rc=$?
-  kill $smi 2>/dev/null; wait $smi 2>/dev/null
-  [ $rc -eq 0 ] || exit 1
+{ echo "== box"; rocm-smi --showmaxpower --showperflevel --showvbios --showproductname --showdriverversion 2>/dev/null | grep -vE "^=+|^$"; } > $O
+( while true; do echo "t=$(date +%s.%N | cut -c1-14)"; rocm-smi --showclocks --showpower --showtemp 2>/dev/null | grep -E "sclk|mclk|fclk|Package Power|junction"; done ) >> $O 2>&1 &
+SMI=$!
+trap 'kill $SMI 2>/dev/null' EXIT
+for rep in 1 2; do
+  echo "== run $rep start $(date +%s.%N | cut -c1-14)" >> $O
+  timeout -k 10 240 python bench.py --no-cpu --no-faithful --steps $S --warmup 2 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); s=d['stages']; print('RESULT', d['ms_per_step'], d['kernel_ms_per_step'], d['roofline']['frac'], {k: v['ms_per_step'] for k, v in list(s.items())[:4]})" >> $O 2>&1 || exit 1
+  echo "== run $rep end $(date +%s.%N | cut -c1-14)" >> $O
 done
 echo all-done
