@@ -252,9 +252,13 @@ def run_dist(args):
     #    chain bucket join, then summed by the checksum gathers) -- the line's own last join counts
     #    its pairs in aggregate form and never writes them; every rank runs it (it is collective)
     def timed_with(var, val):
+        """the timed loop with one switch flipped, after its own untimed warmup (a form's first
+        queries allocate the buffers its allocator then reuses)"""
         old = os.environ.get(var)
         os.environ[var] = val
         try:
+            for _ in range(max(1, args.warmup)):
+                ctx.run_dist(QUERY, comm)
             return timed_steps()
         finally:
             if old is None:
