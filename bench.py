@@ -333,7 +333,7 @@ def run_dist(args):
             "stage_roofline": stage_roofline(stage_stats, traffic, args.steps),
             "pmc_source": traffic.get("_file") if traffic else None,
         }
-        if not args.no_cpu:
+        if not args.no_cpu and not multi:   # (rank 0 at N = 1 only: the baseline is per host, not per rank)
             res["cpu_baseline"] = cpu_baseline(args.cpu_rows, args.seed, ctx)
         else:
             res["cpu_baseline"] = None

@@ -3644,6 +3644,94 @@ tl_hjoin_sums_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict
     }
 }
 
+// The aggregate join with small workgroups (the default; QE_HJ_SUMS_SMALL=0: the 1024-thread form
+// above): 256 threads, eight resident per CU, each bucket's rows STREAMED in chunks (4 rows a thread
+// in flight) instead of held in registers -- a bucket's three barriers stall an eighth of a CU's
+// waves, not half of them.  bucket_join_sums 0.373 -> 0.262 ms per C3 query, same box
+// (profiles/r06i_c3_bench.log).
+#ifndef QE_HJS_NT
+#define QE_HJS_NT 256
+#endif
+#ifndef QE_HJS_U
+#define QE_HJS_U 4
+#endif
+constexpr int HJS_NT = QE_HJS_NT, HJS_NW = HJS_NT / 64, HJS_U = QE_HJS_U;
+template <int XK>
+__global__ void __launch_bounds__(HJS_NT) __attribute__((amdgpu_waves_per_eu(8)))
+tl_hjoin_sums_small_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict__ bsR,
+                           const uint64_t* __restrict__ wS, const uint32_t* __restrict__ bsS, int L,
+                           const uint64_t* __restrict__ xS, HjSums sc, uint64_t* __restrict__ part,
+                           unsigned long long* __restrict__ flag, const uint32_t* __restrict__ xS32, int r32) {
+    __shared__ alignas(16) uint32_t cnt[1 << 12];
+    __shared__ uint64_t red[HJS_NW][HJ_SUMS + 1];
+    const uint32_t D = 1u << L, dmask = D - 1u;
+    const int w = wave_id(), l = lane_id();
+    uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, ap = 0;
+#define QE_ACC(s) (*((s) == 0 ? &a0 : (s) == 1 ? &a1 : (s) == 2 ? &a2 : &a3))
+    const uint32_t* wR32 = reinterpret_cast<const uint32_t*>(wR);
+    for (uint32_t b = blockIdx.x; b < (uint32_t)TL_BUCKETS; b += gridDim.x) {   // block-uniform
+        const uint32_t r0 = bsR[b], mR = bsR[b + 1] - r0, s0 = bsS[b], mS = bsS[b + 1] - s0;
+        if (mR > (uint32_t)TL_CAP || mS > (uint32_t)TL_CAP) {
+            if (threadIdx.x == 0) atomicOr(flag, 1ull);
+            continue;
+        }
+        if (b != blockIdx.x) __syncthreads();   // the previous bucket's lookups are done with cnt
+        for (uint32_t v = threadIdx.x * 4u; v < D; v += HJS_NT * 4u)
+            *reinterpret_cast<uint4*>(&cnt[v]) = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        for (uint32_t i0 = 0; i0 < mR; i0 += HJS_NT * HJS_U) {
+            uint32_t f[HJS_U];
+#pragma unroll
+            for (int u = 0; u < HJS_U; u++) {
+                const uint32_t i = i0 + (uint32_t)u * HJS_NT + threadIdx.x;
+                f[u] = i < mR ? (r32 ? wR32[r0 + i] : wR32[2u * (r0 + i) + 1u]) : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < HJS_U; u++)
+                if (i0 + (uint32_t)u * HJS_NT + threadIdx.x < mR) atomicAdd(&cnt[f[u] & dmask], 1u);
+        }
+        __syncthreads();
+        for (uint32_t i0 = 0; i0 < mS; i0 += HJS_NT * HJS_U) {
+            uint64_t ws[HJS_U], xv[HJS_U];
+#pragma unroll
+            for (int u = 0; u < HJS_U; u++) {
+                const uint32_t i = i0 + (uint32_t)u * HJS_NT + threadIdx.x;
+                ws[u] = i < mS ? wS[s0 + i] : 0ull;
+                if constexpr (XK == 1) xv[u] = i < mS ? xS32[s0 + i] : 0u;
+                else if constexpr (XK == 2) xv[u] = i < mS ? xS[s0 + i] : 0ull;
+                else xv[u] = 0;
+            }
+#pragma unroll
+            for (int u = 0; u < HJS_U; u++) {
+                const uint32_t i = i0 + (uint32_t)u * HJS_NT + threadIdx.x;
+                const uint32_t c = i < mS ? cnt[(uint32_t)(ws[u] >> 32) & dmask] : 0u;
+                ap += c;
+#pragma unroll
+                for (int s = 0; s < HJ_SUMS; s++) {
+                    if (s < sc.n) {   // block-uniform
+                        const int src = sc.src[s] & 3;
+                        const uint32_t id = src == 0 ? (uint32_t)ws[u] : src == 1 ? (uint32_t)xv[u] : (uint32_t)(xv[u] >> 32);
+                        if (sc.src[s] & 4) QE_ACC(s) += (uint64_t)c * id;
+                        else if (c) QE_ACC(s) += (uint64_t)c * sc.col[s][id];
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int s = 0; s <= HJ_SUMS; s++) {
+        const uint64_t t = wave_sum_u64(s == HJ_SUMS ? ap : QE_ACC(s));
+        if (l == 0) red[w][s] = t;
+    }
+#undef QE_ACC
+    __syncthreads();
+    if (threadIdx.x <= HJ_SUMS) {
+        uint64_t t = 0;
+        for (int ww = 0; ww < HJS_NW; ww++) t += red[ww][threadIdx.x];
+        part[(uint64_t)blockIdx.x * (HJ_SUMS + 1) + threadIdx.x] = t;
+    }
+}
+
 // out[k] = sum over blocks of part[b][k] (mod 2^64), one workgroup per k
 __global__ void __launch_bounds__(256) hjoin_sums_reduce_kernel(const uint64_t* __restrict__ part, uint32_t nb,
                                                                 uint64_t* __restrict__ out) {
@@ -3689,10 +3777,12 @@ bool bucket_join_sums(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const HjS
             return (uint32_t)std::max(1, 2 * ncu);
         }();
         static const bool persist = !(getenv("QE_HJ_SUMS_PERSIST") && getenv("QE_HJ_SUMS_PERSIST")[0] == '0');
+        const bool small = dR.L <= 12 && !(getenv("QE_HJ_SUMS_SMALL") && getenv("QE_HJ_SUMS_SMALL")[0] == '0');
         // (one barrier per bucket -- three count tables used round robin -- with or without the next
         // bucket's loads in flight at one workgroup per CU measured slower: 0.375 -> 0.424 / 0.431 ms
         // per C3 query, profiles/r06e_c3_bench.log)
-        const uint32_t grid = persist ? std::min<uint32_t>(resident, TL_BUCKETS) : (uint32_t)TL_BUCKETS;
+        const uint32_t grid = small ? std::min<uint32_t>(resident * (1024 / HJS_NT), TL_BUCKETS)
+                              : persist ? std::min<uint32_t>(resident, TL_BUCKETS) : (uint32_t)TL_BUCKETS;
         // S's payload as the kernel holds it: none when no select reads one, else u32 or u64
         const int xk = !carry ? 0 : dS.x32 ? 1 : 2;
         auto go = [&](auto kern) {
@@ -3701,7 +3791,16 @@ bool bucket_join_sums(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, const HjS
                                reinterpret_cast<unsigned long long*>(out + HJ_SUMS + 1), carry ? dS.x32 : nullptr,
                                dR.w32 ? 1 : 0);
         };
-        if (persist)
+        auto gos = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(HJS_NT), 0, c->stream, dR.words, dR.bstart, dS.words, dS.bstart,
+                               dR.L, carry ? dS.x : nullptr, sc, part,
+                               reinterpret_cast<unsigned long long*>(out + HJ_SUMS + 1), carry ? dS.x32 : nullptr,
+                               dR.w32 ? 1 : 0);
+        };
+        if (small)
+            xk == 0 ? gos(tl_hjoin_sums_small_kernel<0>) : xk == 1 ? gos(tl_hjoin_sums_small_kernel<1>)
+                                                         : gos(tl_hjoin_sums_small_kernel<2>);
+        else if (persist)
             xk == 0 ? go(tl_hjoin_sums_kernel<true, 0>) : xk == 1 ? go(tl_hjoin_sums_kernel<true, 1>)
                                                         : go(tl_hjoin_sums_kernel<true, 2>);
         else

@@ -1,6 +1,8 @@
-# round 6 working call: large-block backing A/B (contiguous pages / one arena) on the C3 line
+# round 6 working call: GPU tests on the small-workgroup sums default, then its shape sweep
 set -o pipefail
 mkdir -p gpurun_out
-T=${1:-r06h}
-REPS=2 bash tools/gpu_ab.sh $T c3 "base:QE_NOTHING=1" "contig:QE_ALLOC_CONTIG=1" "arena:QE_ALLOC_ARENA_GB=48" || exit 1
+T=${1:-r06j}
+V=$PWD/query-compiler-executor_amd/build/var
+TESTS="tests/test_gpu_bucket_join.py tests/test_gpu_comm.py tests/test_gpu_fullsize.py tests/test_gpu_primitives.py tests/test_gpu_skew.py" \
+REPS=2 bash tools/gpu_ab.sh $T c3 "nt256u4:QE_NOTHING=1" "old:QE_HJ_SUMS_SMALL=0" "nt256u8:QE_LIB_PATH=$V/libqe_nt256u8.so" "nt128u4:QE_LIB_PATH=$V/libqe_nt128u4.so" "nt512u4:QE_LIB_PATH=$V/libqe_nt512u4.so" || exit 1
 echo all-done
