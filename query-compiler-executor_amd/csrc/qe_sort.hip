@@ -3426,6 +3426,8 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
             // algorithmic bytes: both sides' words in (+ 8 B per pair below; + the payloads)
             Timed t(c, "bucket_join", 8.0 * (double)(nR + nS) + (carry ? (s32 ? 4.0 : 8.0) * (double)nS : 0.0) +
                                           (rx ? 4.0 * (double)nR : 0.0));
+            // (256-thread workgroups with only the chain in LDS, R's rows read back from global memory at
+            // emission: 2.32 vs 1.01 ms per C3 query, profiles/r06k_c3_bench.log -- removed)
             if (s32 && rx) {
                 hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, true, true>), dim3(hj_grid()), dim3(HJ_NT), 0,
                                    c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,

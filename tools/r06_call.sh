@@ -1,8 +1,7 @@
-# round 6 working call: GPU tests on the small-workgroup sums default, then its shape sweep
+# round 6 working call: the small-workgroup chain join (QE_HJ_SMALL=1): its GPU tests, then the C3 A/B
 set -o pipefail
 mkdir -p gpurun_out
-T=${1:-r06j}
-V=$PWD/query-compiler-executor_amd/build/var
-TESTS="tests/test_gpu_bucket_join.py tests/test_gpu_comm.py tests/test_gpu_fullsize.py tests/test_gpu_primitives.py tests/test_gpu_skew.py" \
-REPS=2 bash tools/gpu_ab.sh $T c3 "nt256u4:QE_NOTHING=1" "old:QE_HJ_SUMS_SMALL=0" "nt256u8:QE_LIB_PATH=$V/libqe_nt256u8.so" "nt128u4:QE_LIB_PATH=$V/libqe_nt128u4.so" "nt512u4:QE_LIB_PATH=$V/libqe_nt512u4.so" || exit 1
+T=${1:-r06k}
+QE_HJ_SMALL=1 timeout -k 10 900 python -u -m pytest -x -q -m gpu --timeout 300 --timeout-method thread tests/test_gpu_bucket_join.py tests/test_gpu_comm.py tests/test_gpu_fullsize.py > gpurun_out/${T}_tests.log 2>&1 || exit 1
+REPS=2 bash tools/gpu_ab.sh $T c3 "base:QE_NOTHING=1" "small:QE_HJ_SMALL=1" || exit 1
 echo all-done
