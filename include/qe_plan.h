@@ -77,8 +77,10 @@ typedef struct qe_engine {
     int (*fallback)(void* u, void* query, void* out);
     /* a1 then a2 on the same binding, fused (nullable): rowids r in [start, end) with
      * col1[r] op1 v1 and col2[r] op2 v2, in no particular order -- one pass over the column(s) instead of a
-     * scan and a refine gathering through its list.  values = 1: the plan expects to ask for col1's
-     * values of this list later (`values` below) -- the engine may emit them from the same pass */
+     * scan and a refine gathering through its list.  values bit 0: the plan expects to ask for col1's
+     * values of this list later (`values` below) -- the engine may emit them from the same pass;
+     * bits 8..15 (nonzero): 1 + the column every join of this binding keys on -- the engine may
+     * emit those values too and take them for the binding's key side (`keys`) without a gather */
     int (*scan2)(void* u, uint32_t rel, uint32_t col1, char op1, uint64_t v1, uint32_t col2, char op2, uint64_t v2,
                  uint64_t start, uint64_t end, int values, qe_h* out);
     /* join, with side b's carried rowid columns cb[0..nb) delivered beside the pairs (nullable):

@@ -151,9 +151,13 @@ struct DArr : Obj {
     // a fused scan's survivors' values of (vrel, vcol) as u32, kept for a later `values` request
     uint32_t* vcache = nullptr;
     uint32_t vrel = 0, vcol = 0;
+    // ... and of (krel, kcol), the binding's join key column, for its key side (e_keys): no gather
+    uint32_t* kcache = nullptr;
+    uint32_t krel = 0, kcol = 0;
     bool colview = false;   // a base column (e_column): d is the column, n its rows
     ~DArr() override {
         if (vcache) dfree(c, vcache);
+        if (kcache) dfree(c, kcache);
         if (owned && d) {
             qe_pairs p{};
             p.key = static_cast<uint64_t*>(d);   // drops a gathered histogram kept for this key buffer
@@ -268,19 +272,36 @@ int e_scan2(void* u, uint32_t rel, uint32_t col1, char op1, uint64_t v1, uint32_
         uint64_t kor = 0, kand = 0;
         // the survivors' col1 values come out of the same pass when the plan expects to ask for them
         // (4 more bytes written per survivor)
-        const bool vals = values && !(getenv("QE_SCAN_VALUES") && getenv("QE_SCAN_VALUES")[0] == '0') &&
+        const bool vals = (values & 1) && !(getenv("QE_SCAN_VALUES") && getenv("QE_SCAN_VALUES")[0] == '0') &&
                           qe_relation_column_bits(c, (int)rel, (int)col1, &kor, &kand) == 0 && !(kor >> 32);
         const qe_col q1 = column(c, rel, col1), q2 = column(c, rel, col2);
         if (t > q1.n || t > q2.n || s > t) throw Error(QE_EINVAL, "bad row range");
         const uint64_t n = t - s;
+        // ... and the survivors' values of the binding's join key column (values >> 8 = 1 + it), read
+        // from its u32 copy: the join's key side then widens them with its sort's histogram instead
+        // of gathering the column through the list (QE_SCAN_KEYS=0: gathered -- A/B)
+        const uint32_t kc = ((uint32_t)values >> 8) & 0xFFu;
+        const uint32_t* k32 = nullptr;
+        if (kc && !(getenv("QE_SCAN_KEYS") && getenv("QE_SCAN_KEYS")[0] == '0')) {
+            const qe_col qk = column(c, rel, kc - 1);
+            k32 = narrow_of(c, qk.d, qk.n);
+            if (t > qk.n) k32 = nullptr;
+        }
         uint32_t* d = dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1));
         uint32_t* dv = vals ? dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1)) : nullptr;
-        const uint64_t m = filter_scan2_unordered(c, q1.d + s, op1, v1, q2.d + s, op2, v2, n, (uint32_t)s, d, dv);
+        uint32_t* dk = k32 ? dalloc_t<uint32_t>(c, std::max<uint64_t>(n, 1)) : nullptr;
+        const uint64_t m = filter_scan2_unordered(c, q1.d + s, op1, v1, q2.d + s, op2, v2, n, (uint32_t)s, d, dv,
+                                                  k32 ? k32 + s : nullptr, dk);
         DArr* a = new_arr(c, d, m, false);
         if (vals) {
             a->vcache = dv;
             a->vrel = rel;
             a->vcol = col1;
+        }
+        if (dk) {
+            a->kcache = dk;
+            a->krel = rel;
+            a->kcol = kc - 1;
         }
         *out = H(a);
     });
@@ -303,6 +324,10 @@ int e_refine(void* u, uint32_t rel, uint32_t col, qe_h rows, char op, uint64_t v
             dfree(e->c, a->vcache);
             a->vcache = nullptr;
         }
+        if (a->kcache) {
+            dfree(e->c, a->kcache);
+            a->kcache = nullptr;
+        }
         qe_list l = as_list(a);
         l.flags = QE_LIST_DISTINCT;
         ck(qe_filter_refine(e->c, column(e->c, rel, col), op, v, &l), e->c);
@@ -322,6 +347,34 @@ struct K32Scope {
 
 int e_keys(void* u, uint32_t rel, uint32_t col, qe_h rows, qe_h* out) {
     Eng* e = E(u);
+    DArr* r = A(rows);
+    if (r->kcache && r->krel == rel && r->kcol == col) {   // the scan that made the list emitted the keys
+        return guard(e, [&] {
+            qe_ctx* c = e->c;
+            uint64_t kor = 0, kand = 0;
+            ck(qe_relation_column_bits(c, (int)rel, (int)col, &kor, &kand), c);
+            const uint64_t n = r->n;
+            uint32_t* kv = r->kcache;
+            r->kcache = nullptr;
+            uint64_t* k = dalloc_t<uint64_t>(c, std::max<uint64_t>(n, 1));
+            bool fused = false, adopted = false;
+            if (n) {
+                K32Scope k32(c);
+                fused = widen_with_hist(c, kv, n, kor, kand, k, &adopted);
+            }
+            if (n && !fused) {
+                Timed t(c, "widen_keys", 12.0 * n);
+                hipLaunchKernelGGL(widen_u32_kernel, dim3(grid_for(n, 256 * 8, 8192)), dim3(256), 0, c->stream, kv, n, k);
+                QE_HIP(hipGetLastError());
+            }
+            if (!adopted) dfree(c, kv);
+            DArr* a = new_arr(c, k, n, true);
+            a->bits = true;
+            a->kor = kor;
+            a->kand = kand;
+            *out = H(a);
+        });
+    }
     return guard(e, [&] {
         qe_list l = as_list(A(rows));
         qe_pairs p{};

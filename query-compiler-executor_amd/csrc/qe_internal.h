@@ -302,9 +302,11 @@ uint64_t filter_scan2(qe_ctx* c, const uint64_t* c1, char op1, uint64_t v1, cons
 uint64_t filter_scan2_vals(qe_ctx* c, const uint64_t* c1, char op1, uint64_t v1, const uint64_t* c2, char op2,
                            uint64_t v2, uint64_t n, uint32_t* out, uint32_t* outv);
 // the partitioned plan's scans: the same rows, in no particular order (one atomic per wave tile
-// instead of a lookback); rowids numbered from row_base; outv (nullable): c1's low words, aligned
+// instead of a lookback); rowids numbered from row_base; outv (nullable): c1's low words, aligned;
+// kin / outk (nullable): the survivors' values of the u32 column kin (row i = element i), aligned
 uint64_t filter_scan2_unordered(qe_ctx* c, const uint64_t* c1, char op1, uint64_t v1, const uint64_t* c2, char op2,
-                                uint64_t v2, uint64_t n, uint32_t row_base, uint32_t* out, uint32_t* outv);
+                                uint64_t v2, uint64_t n, uint32_t row_base, uint32_t* out, uint32_t* outv,
+                                const uint32_t* kin = nullptr, uint32_t* outk = nullptr);
 uint64_t filter_refine(qe_ctx* c, const uint64_t* col, const uint32_t* in, uint64_t n, char op, uint64_t v,
                        uint32_t* out);
 uint64_t scan_join_k(qe_ctx* c, const uint64_t* rk, const uint32_t* rv, const uint64_t* sk, const uint32_t* sv,

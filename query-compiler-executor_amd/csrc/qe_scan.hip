@@ -529,10 +529,15 @@ static uint64_t run_wscan(qe_ctx* c, double bytes, const FilterScan2Op& op, uint
 #endif
 constexpr int US_B = QE_US_B, US_STEPS = QE_US_STEPS;
 
-template <int STEPS, bool TWO, bool VALS>
+// KEYS: a third output -- the survivors' values of another u32 column (kin, the binding's next join
+// key: its key side then needs no gather), loaded for the surviving lanes only, right after the
+// predicate, so their latency runs under the workgroup's barrier and output reservation
+template <int STEPS, bool TWO, bool VALS, bool KEYS = false>
 __global__ void __launch_bounds__(US_B) uscan_kernel(FilterScan2Op op, uint64_t n, uint32_t row_base,
                                                     uint32_t* __restrict__ out0, uint32_t* __restrict__ out1,
-                                                    unsigned long long* __restrict__ counter) {
+                                                    unsigned long long* __restrict__ counter,
+                                                    const uint32_t* __restrict__ kin = nullptr,
+                                                    uint32_t* __restrict__ out2 = nullptr) {
     constexpr int NW = US_B / WAVE;
     __shared__ uint32_t s_wtot[NW];
     __shared__ uint64_t s_base;
@@ -557,6 +562,11 @@ __global__ void __launch_bounds__(US_B) uscan_kernel(FilterScan2Op op, uint64_t 
         total += (uint32_t)__popcll(__ballot(f));
         if (VALS) val[j] = (uint32_t)x[j];
     }
+    uint32_t kv[KEYS ? STEPS : 1];
+    if constexpr (KEYS) {
+#pragma unroll
+        for (int j = 0; j < STEPS; j++) kv[j] = (fb >> j) & 1u ? kin[base + (uint64_t)j * WAVE] : 0u;
+    }
     if (l == 0) s_wtot[w] = total;
     __syncthreads();
     if (w == 0) {   // the waves' exclusive offsets inside the workgroup's run; one atomic for the run
@@ -578,17 +588,19 @@ __global__ void __launch_bounds__(US_B) uscan_kernel(FilterScan2Op op, uint64_t 
             const uint64_t o = off + (uint64_t)__popcll(m & lt);
             out0[o] = row0 + (uint32_t)(j * WAVE);
             if (VALS) out1[o] = val[j];
+            if constexpr (KEYS) out2[o] = kv[j];
         }
         off += (uint64_t)__popcll(m);
     }
 }
 
 uint64_t filter_scan2_unordered(qe_ctx* c, const uint64_t* c1, char op1, uint64_t v1, const uint64_t* c2, char op2,
-                                uint64_t v2, uint64_t n, uint32_t row_base, uint32_t* out, uint32_t* outv) {
+                                uint64_t v2, uint64_t n, uint32_t row_base, uint32_t* out, uint32_t* outv,
+                                const uint32_t* kin, uint32_t* outk) {
     if (n == 0) return 0;
     const FilterScan2Op op{c1, c2, v1, v2, op_code(op1), op_code(op2)};
     static const bool ordered = getenv("QE_PLAN_USCAN") && getenv("QE_PLAN_USCAN")[0] == '0';   // A/B knob
-    if (ordered && row_base == 0) return run_wscan(c, (c1 == c2 ? 8.0 : 16.0) * n, op, n, out, outv);
+    if (ordered && row_base == 0 && !outk) return run_wscan(c, (c1 == c2 ? 8.0 : 16.0) * n, op, n, out, outv);
     const bool two = c2 != c1;
     constexpr uint64_t TILE = (uint64_t)US_STEPS * US_B;   // rows per workgroup
     const uint64_t nt = (n + TILE - 1) / TILE;
@@ -602,7 +614,15 @@ uint64_t filter_scan2_unordered(qe_ctx* c, const uint64_t* c1, char op1, uint64_
 #define QE_US_LAUNCH(TWO, VALS)                                                                                \
     hipLaunchKernelGGL((uscan_kernel<US_STEPS, TWO, VALS>), dim3(grid), dim3(US_B), 0, c->stream, op, n,       \
                        row_base, out, outv, d_cnt)
-        if (two) {
+#define QE_USK_LAUNCH(TWO, VALS)                                                                               \
+    hipLaunchKernelGGL((uscan_kernel<US_STEPS, TWO, VALS, true>), dim3(grid), dim3(US_B), 0, c->stream, op, n, \
+                       row_base, out, outv, d_cnt, kin, outk)
+        if (outk) {
+            if (two && outv) QE_USK_LAUNCH(true, true);
+            else if (two) QE_USK_LAUNCH(true, false);
+            else if (outv) QE_USK_LAUNCH(false, true);
+            else QE_USK_LAUNCH(false, false);
+        } else if (two) {
             if (outv) QE_US_LAUNCH(true, true);
             else QE_US_LAUNCH(true, false);
         } else {
@@ -610,10 +630,11 @@ uint64_t filter_scan2_unordered(qe_ctx* c, const uint64_t* c1, char op1, uint64_
             else QE_US_LAUNCH(false, false);
         }
 #undef QE_US_LAUNCH
+#undef QE_USK_LAUNCH
         QE_HIP(hipGetLastError());
     }
     const uint64_t m = read_u64(c, reinterpret_cast<uint64_t*>(d_cnt));
-    add_bytes(c, "filter_scan", (outv ? 8.0 : 4.0) * m);
+    add_bytes(c, "filter_scan", (4.0 + (outv ? 4.0 : 0.0) + (outk ? 8.0 : 0.0)) * m);   // (keys: 4 B read, 4 written)
     return m;
 }
 

@@ -894,6 +894,25 @@ static int values_hint(const query_t* q, int b, uint64_t col) {
     return joins == 1 && sels > 0;
 }
 
+/* 1 + the column every join of binding b keys on (0: b joins on several columns, or not at all):
+ * a fused scan of b may emit those values with its rowids (scan2's `values` bits 8..15), and b's
+ * key side then takes them instead of gathering them through the list */
+static int join_key_hint(const query_t* q, int b) {
+    int kc = 0;
+    for (size_t i = 0; i < q->npreds; i++) {
+        const pred_t* p = &q->preds[i];
+        if (p->type != 0) continue;
+        for (int side = 0; side < 2; side++) {
+            const int rb = (int)(side ? p->srel : p->frel);
+            const int c = (int)(side ? p->scol : p->fcol) + 1;
+            if (rb != b) continue;
+            if (kc && kc != c) return 0;
+            kc = c;
+        }
+    }
+    return kc < 256 ? kc : 0;
+}
+
 static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t* rows_out) {
     plan_t PP;
     plan_t* P = &PP;
@@ -936,8 +955,9 @@ static int plan_query(const qe_engine* e, const query_t* q, FILE* out, uint64_t*
                 const pred_t* p2 = &q->preds[k + 1];
                 uint64_t s, t;
                 owned_range(P, rel_rows(P, relid), &s, &t);
+                const int vh = values_hint(q, b, p->fcol) && e->values != NULL;
                 rc = e->scan2(e->u, relid, (uint32_t)p->fcol, p->op, p->cval, (uint32_t)p2->fcol, p2->op, p2->cval, s,
-                              t, values_hint(q, b, p->fcol) && e->values != NULL, &P->list[b]);
+                              t, vh | join_key_hint(q, b) << 8, &P->list[b]);
                 uint64_t n = 0;
                 if (!rc) rc = e->length(e->u, P->list[b], &n);
                 if (!rc) rc = allreduce1(P, &n);

@@ -186,7 +186,7 @@ class NumpyPlanEngine:
         out[0] = self.put(self._unordered(np.nonzero(_OPS[op.decode()](c, np.uint64(v)))[0] + s))
 
     def cb_scan2(self, u, rel, c1, op1, v1, c2, op2, v2, s, t, values, out):
-        self.scan2_values += bool(values)
+        self.scan2_values += bool(values & 1)      # (bits 8..15: a join-key hint this engine ignores)
         a = self.rels[rel][c1][s:t]
         b = self.rels[rel][c2][s:t]
         m = _OPS[op1.decode()](a, np.uint64(v1)) & _OPS[op2.decode()](b, np.uint64(v2))

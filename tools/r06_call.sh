@@ -1,7 +1,7 @@
-# round 6 working call: the small-workgroup chain join (QE_HJ_SMALL=1): its GPU tests, then the C3 A/B
+# round 6 working call: the fused scan emitting the join-key values (QE_SCAN_KEYS): GPU tests, C3 A/B
 set -o pipefail
 mkdir -p gpurun_out
-T=${1:-r06k}
-QE_HJ_SMALL=1 timeout -k 10 900 python -u -m pytest -x -q -m gpu --timeout 300 --timeout-method thread tests/test_gpu_bucket_join.py tests/test_gpu_comm.py tests/test_gpu_fullsize.py > gpurun_out/${T}_tests.log 2>&1 || exit 1
-REPS=2 bash tools/gpu_ab.sh $T c3 "base:QE_NOTHING=1" "small:QE_HJ_SMALL=1" || exit 1
+T=${1:-r06m}
+TESTS="tests/test_gpu_comm.py tests/test_gpu_local_ranks.py tests/test_gpu_fullsize.py" \
+REPS=2 bash tools/gpu_ab.sh $T c3 "keys:QE_NOTHING=1" "gather:QE_SCAN_KEYS=0" || exit 1
 echo all-done
