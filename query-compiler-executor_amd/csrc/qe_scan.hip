@@ -532,6 +532,9 @@ constexpr int US_B = QE_US_B, US_STEPS = QE_US_STEPS;
 // KEYS: a third output -- the survivors' values of another u32 column (kin, the binding's next join
 // key: its key side then needs no gather), loaded for the surviving lanes only, right after the
 // predicate, so their latency runs under the workgroup's barrier and output reservation
+#ifndef QE_USCAN_KEYS_EARLY
+#define QE_USCAN_KEYS_EARLY 0
+#endif
 template <int STEPS, bool TWO, bool VALS, bool KEYS = false>
 __global__ void __launch_bounds__(US_B) uscan_kernel(FilterScan2Op op, uint64_t n, uint32_t row_base,
                                                     uint32_t* __restrict__ out0, uint32_t* __restrict__ out1,
@@ -546,11 +549,13 @@ __global__ void __launch_bounds__(US_B) uscan_kernel(FilterScan2Op op, uint64_t 
     const uint64_t lt = lanemask_lt();
     const uint64_t base = tile * (STEPS * WAVE) + (uint64_t)l;
     uint64_t x[STEPS], y[TWO ? STEPS : 1];
+    uint32_t kv[KEYS ? STEPS : 1];
 #pragma unroll
     for (int j = 0; j < STEPS; j++) {
         const uint64_t i = base + (uint64_t)j * WAVE;
         x[j] = i < n ? __builtin_nontemporal_load(op.c1 + i) : 0;
         if (TWO) y[j] = i < n ? __builtin_nontemporal_load(op.c2 + i) : 0;
+        if (KEYS && QE_USCAN_KEYS_EARLY) kv[j] = i < n ? kin[i] : 0u;   // (build knob: every row's key, with the rest)
     }
     uint32_t fb = 0, total = 0;
     uint32_t val[VALS ? STEPS : 1];
@@ -562,8 +567,7 @@ __global__ void __launch_bounds__(US_B) uscan_kernel(FilterScan2Op op, uint64_t 
         total += (uint32_t)__popcll(__ballot(f));
         if (VALS) val[j] = (uint32_t)x[j];
     }
-    uint32_t kv[KEYS ? STEPS : 1];
-    if constexpr (KEYS) {
+    if constexpr (KEYS && !QE_USCAN_KEYS_EARLY) {
 #pragma unroll
         for (int j = 0; j < STEPS; j++) kv[j] = (fb >> j) & 1u ? kin[base + (uint64_t)j * WAVE] : 0u;
     }

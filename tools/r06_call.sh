@@ -1,7 +1,8 @@
-# round 6 working call: the fused scan emitting the join-key values (QE_SCAN_KEYS): GPU tests, C3 A/B
+# round 6 working call: the fused scan's key loads issued with the predicate columns (every row) vs
+# by the surviving lanes after the predicate
 set -o pipefail
 mkdir -p gpurun_out
-T=${1:-r06m}
-TESTS="tests/test_gpu_comm.py tests/test_gpu_local_ranks.py tests/test_gpu_fullsize.py" \
-REPS=2 bash tools/gpu_ab.sh $T c3 "keys:QE_NOTHING=1" "gather:QE_SCAN_KEYS=0" || exit 1
+T=${1:-r06n}
+V=$PWD/query-compiler-executor_amd/build/var
+REPS=2 bash tools/gpu_ab.sh $T c3 "late:QE_NOTHING=1" "early:QE_LIB_PATH=$V/libqe_kearly.so" || exit 1
 echo all-done
