@@ -555,7 +555,9 @@ __global__ void __launch_bounds__(US_B) uscan_kernel(FilterScan2Op op, uint64_t 
         const uint64_t i = base + (uint64_t)j * WAVE;
         x[j] = i < n ? __builtin_nontemporal_load(op.c1 + i) : 0;
         if (TWO) y[j] = i < n ? __builtin_nontemporal_load(op.c2 + i) : 0;
-        if (KEYS && QE_USCAN_KEYS_EARLY) kv[j] = i < n ? kin[i] : 0u;   // (build knob: every row's key, with the rest)
+        // (build knob: every row's key loaded with the predicate columns -- neutral, 0.311-0.312 vs
+        // 0.314-0.316 ms of filter_scan per C3 query, profiles/r06n_c3_bench.log)
+        if (KEYS && QE_USCAN_KEYS_EARLY) kv[j] = i < n ? kin[i] : 0u;
     }
     uint32_t fb = 0, total = 0;
     uint32_t val[VALS ? STEPS : 1];
