@@ -1,8 +1,6 @@
-# round 6 working call: the fused scan's key loads issued with the predicate columns (every row) vs
-# by the surviving lanes after the predicate
+# round 6 working call: C4 knobs on this round's build (longest-first lane order, scan keys, sums form)
 set -o pipefail
 mkdir -p gpurun_out
-T=${1:-r06n}
-V=$PWD/query-compiler-executor_amd/build/var
-REPS=2 bash tools/gpu_ab.sh $T c3 "late:QE_NOTHING=1" "early:QE_LIB_PATH=$V/libqe_kearly.so" || exit 1
+T=${1:-r06o}
+bash tools/gpu_ab.sh $T c4 "base:QE_NOTHING=1" "inorder:QE_LANE_ORDER=0" "gatherkeys:QE_SCAN_KEYS=0" "oldsums:QE_HJ_SUMS_SMALL=0" || exit 1
 echo all-done
