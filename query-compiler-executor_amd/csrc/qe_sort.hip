@@ -1919,8 +1919,9 @@ static_assert(TL_CAP < HJ_NONE, "chain links are 16-bit row indices");
 // NT: threads per bucket (HJ_NT; 256 for C4-sized joins measured 2 % slower on the batch's wall
 // time -- its bucket joins 99 -> 62 ms of kernel time, but 41 re-runs of overflowing buckets and
 // more interference with the other lanes, profiles/r03_c4_hjsmall_ab.log)
-template <int DBITS, bool CARRY = false, bool RX = false, bool S32 = false, int NT = HJ_NT>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8)))
+// IT: rows per thread per side (NT * IT = the largest bucket side it takes; a larger one is flagged)
+template <int DBITS, bool CARRY = false, bool RX = false, bool S32 = false, int NT = HJ_NT, int IT = HJ_I>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT >= 1024 ? 8 : 6)))
 tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict__ bsR, const uint64_t* __restrict__ wS,
                       const uint32_t* __restrict__ bsS, int L, uint32_t* __restrict__ outR, uint32_t* __restrict__ outS,
                       uint64_t cap, uint64_t* total_out, const uint64_t* __restrict__ xS = nullptr,
@@ -1928,15 +1929,15 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
                       const uint32_t* __restrict__ xR = nullptr, uint32_t* __restrict__ outRX = nullptr,
                       const uint32_t* __restrict__ xS32 = nullptr) {
     __shared__ uint32_t head[1 << DBITS];   // per key value: the last R row inserted (HJ_NONE: none)
-    __shared__ uint16_t nxt[NT * HJ_I];        // per R row: the previous row of its value
+    __shared__ uint16_t nxt[NT * IT];        // per R row: the previous row of its value
 #if QE_HJ_RR_GLOBAL
     uint32_t* rr = nullptr;                 // (R's rowids re-read from its words, L2-hot, at emission)
 #else
-    __shared__ uint32_t rr[NT * HJ_I];         // per R row: its rowid
+    __shared__ uint32_t rr[NT * IT];         // per R row: its rowid
 #endif
-    __shared__ uint32_t rx[RX ? NT * HJ_I : 1];  // per R row: its payload
+    __shared__ uint32_t rx[RX ? NT * IT : 1];  // per R row: its payload
     constexpr int NW = NT / 64;
-    __shared__ uint32_t tab[HJ_I * NW];
+    __shared__ uint32_t tab[IT * NW];
     __shared__ uint64_t s_excl;
     __shared__ uint32_t s_total, s_long;
     // The bucket's bounds are read before the loop as two 8-B scalar loads with the kernel
@@ -1960,35 +1961,35 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
         ns0 = bsS[bn];
         nsE = bsS[bn + 1];
     }
-    if (mR > (uint32_t)(NT * HJ_I) || mS > (uint32_t)(NT * HJ_I)) {   // beyond LDS (the sorts were not checked): flag it
+    if (mR > (uint32_t)(NT * IT) || mS > (uint32_t)(NT * IT)) {   // beyond LDS (the sorts were not checked): flag it
         if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(total_out + 1), 1ull);
         continue;
     }
     const uint32_t D = 1u << L, dmask = D - 1u;
     const int w = wave_id(), l = lane_id();
-    uint64_t wr[HJ_I], ws[HJ_I];
+    uint64_t wr[IT], ws[IT];
 #pragma unroll
-    for (int j = 0; j < HJ_I; j++) {
+    for (int j = 0; j < IT; j++) {
         const uint32_t i = (uint32_t)j * NT + threadIdx.x;
         wr[j] = i < mR ? wR[r0 + i] : 0;
     }
 #pragma unroll
-    for (int j = 0; j < HJ_I; j++) {
+    for (int j = 0; j < IT; j++) {
         const uint32_t i = (uint32_t)j * NT + threadIdx.x;
         ws[j] = i < mS ? wS[s0 + i] : 0;
     }
-    uint64_t xv[CARRY ? HJ_I : 1];
+    uint64_t xv[CARRY ? IT : 1];
     if constexpr (CARRY) {
 #pragma unroll
-        for (int j = 0; j < HJ_I; j++) {
+        for (int j = 0; j < IT; j++) {
             const uint32_t i = (uint32_t)j * NT + threadIdx.x;
             xv[j] = i < mS ? (S32 ? (uint64_t)xS32[s0 + i] : xS[s0 + i]) : 0ull;
         }
     }
-    uint32_t xr[RX ? HJ_I : 1];
+    uint32_t xr[RX ? IT : 1];
     if constexpr (RX) {
 #pragma unroll
-        for (int j = 0; j < HJ_I; j++) {
+        for (int j = 0; j < IT; j++) {
             const uint32_t i = (uint32_t)j * NT + threadIdx.x;
             xr[j] = i < mR ? xR[r0 + i] : 0u;
         }
@@ -1998,7 +1999,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
     __syncthreads();
     QE_STAMP(g_hj_stamps, b, 1);
 #pragma unroll
-    for (int j = 0; j < HJ_I; j++) {
+    for (int j = 0; j < IT; j++) {
         const uint32_t i = (uint32_t)j * NT + threadIdx.x;
         if (i < mR) {
             nxt[i] = (uint16_t)atomicExch(&head[fld(wr[j]) & dmask], i);
@@ -2008,9 +2009,9 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
     }
     __syncthreads();
     QE_STAMP(g_hj_stamps, b, 2);
-    uint32_t pre[HJ_I], hd[HJ_I], tot[HJ_I];
+    uint32_t pre[IT], hd[IT], tot[IT];
 #pragma unroll
-    for (int j = 0; j < HJ_I; j++) {
+    for (int j = 0; j < IT; j++) {
         if (QE_HJ_SKIP && (uint32_t)j * NT + (uint32_t)w * 64u >= mS) {   // (wave-uniform) no S row of this item in this
             hd[j] = HJ_NONE;                                  // wave: skip its walk and scan (a C3 bucket
             pre[j] = tot[j] = 0;                              // fills 1.4 of the 5 items)
@@ -2039,7 +2040,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
         continue;
     }
     if (w == 0) {   // (row group, wave) totals in row order -> bucket offsets; one atomic per bucket
-        constexpr uint32_t E = HJ_I * NW;
+        constexpr uint32_t E = IT * NW;
         const uint32_t a0 = 2u * l < E ? tab[2 * l] : 0u, a1 = 2u * l + 1 < E ? tab[2 * l + 1] : 0u;
         const uint32_t inc = wave_incl_scan_u32(a0 + a1);
         const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
@@ -2056,7 +2057,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
     const uint64_t gofs = s_excl;
     if (gofs + s_total > cap) continue;   // outgrew the buffers: the host re-runs with the exact size
 #pragma unroll
-    for (int j = 0; j < HJ_I; j++) {   // wave-cooperative emission, as tl_hjoin_kernel's
+    for (int j = 0; j < IT; j++) {   // wave-cooperative emission, as tl_hjoin_kernel's
         const uint32_t pj = pre[j], all = tot[j];
         const uint64_t ob = gofs + tab[j * NW + w];
         const uint32_t srow = (uint32_t)ws[j];
@@ -3414,6 +3415,10 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
     if (rx && (!dR.x32 || !hj_chain_on() || dR.L > 12)) return false;
     const uint64_t nR = R->n, nS = S->n;
     uint64_t cap = nR + nS;   // optimistic (fan-out ~1); an outgrown launch re-runs with the exact size
+    // QE_HJ_NT512=1 (A/B): 512-thread workgroups taking bucket sides of <= 3584 rows (51 KiB of LDS:
+    // three per CU instead of two 1024-thread ones); a larger bucket re-runs the join as below
+    const char* e512 = getenv("QE_HJ_NT512");
+    bool use512 = e512 && e512[0] == '1' && hj_chain_on() && dR.L <= 12 && rx && (s32 || !carry);
     for (int attempt = 0; attempt < 2; attempt++) {
         uint32_t* oR = dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1));
         uint32_t* oS = dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1));
@@ -3428,7 +3433,16 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
                                           (rx ? 4.0 * (double)nR : 0.0));
             // (256-thread workgroups with only the chain in LDS, R's rows read back from global memory at
             // emission: 2.32 vs 1.01 ms per C3 query, profiles/r06k_c3_bench.log -- removed)
-            if (s32 && rx) {
+            if (use512) {
+                if (s32)
+                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, true, true, 512, 7>), dim3(hj_grid()), dim3(512),
+                                       0, c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
+                                       c->d_scratch + 17, nullptr, x0, nullptr, dR.x32, xr, dS.x32);
+                else
+                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, false, true, false, 512, 7>), dim3(hj_grid()), dim3(512),
+                                       0, c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
+                                       c->d_scratch + 17, nullptr, nullptr, nullptr, dR.x32, xr);
+            } else if (s32 && rx) {
                 hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, true, true>), dim3(hj_grid()), dim3(HJ_NT), 0,
                                    c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
                                    c->d_scratch + 17, nullptr, x0, nullptr, dR.x32, xr, dS.x32);
@@ -3479,6 +3493,16 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
         uint64_t h[2];
         read_words(c, c->d_scratch + 17, h, 2);   // the ONE round trip of the join
         const uint64_t P = h[0];
+        if (h[1] && use512) {   // a bucket beyond the 512-thread form: the 1024-thread one takes the join
+            dfree(c, oR);
+            dfree(c, oS);
+            dfree(c, x0);
+            dfree(c, x1);
+            dfree(c, xr);
+            use512 = false;
+            attempt--;
+            continue;
+        }
         if (h[1]) {   // a bucket beyond LDS (skew): the sides complete their sorts, the merge joins them
             dfree(c, oR);
             dfree(c, oS);
