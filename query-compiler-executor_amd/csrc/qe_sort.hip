@@ -3415,10 +3415,8 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
     if (rx && (!dR.x32 || !hj_chain_on() || dR.L > 12)) return false;
     const uint64_t nR = R->n, nS = S->n;
     uint64_t cap = nR + nS;   // optimistic (fan-out ~1); an outgrown launch re-runs with the exact size
-    // QE_HJ_NT512=1 (A/B): 512-thread workgroups taking bucket sides of <= 3584 rows (51 KiB of LDS:
-    // three per CU instead of two 1024-thread ones); a larger bucket re-runs the join as below
-    const char* e512 = getenv("QE_HJ_NT512");
-    bool use512 = e512 && e512[0] == '1' && hj_chain_on() && dR.L <= 12 && rx && (s32 || !carry);
+    // (512-thread workgroups taking bucket sides of <= 3584 rows, three per CU, measured 1.63 vs
+    // 1.00 ms per C3 query: profiles/r06q_c3_bench.log)
     for (int attempt = 0; attempt < 2; attempt++) {
         uint32_t* oR = dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1));
         uint32_t* oS = dalloc_t<uint32_t>(c, std::max<uint64_t>(cap, 1));
@@ -3433,16 +3431,7 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
                                           (rx ? 4.0 * (double)nR : 0.0));
             // (256-thread workgroups with only the chain in LDS, R's rows read back from global memory at
             // emission: 2.32 vs 1.01 ms per C3 query, profiles/r06k_c3_bench.log -- removed)
-            if (use512) {
-                if (s32)
-                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, true, true, 512, 7>), dim3(hj_grid()), dim3(512),
-                                       0, c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
-                                       c->d_scratch + 17, nullptr, x0, nullptr, dR.x32, xr, dS.x32);
-                else
-                    hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, false, true, false, 512, 7>), dim3(hj_grid()), dim3(512),
-                                       0, c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
-                                       c->d_scratch + 17, nullptr, nullptr, nullptr, dR.x32, xr);
-            } else if (s32 && rx) {
+            if (s32 && rx) {
                 hipLaunchKernelGGL((tl_hjoin_chain_kernel<12, true, true, true>), dim3(hj_grid()), dim3(HJ_NT), 0,
                                    c->stream, dR.words, dR.bstart, dS.words, dS.bstart, dR.L, oR, oS, cap,
                                    c->d_scratch + 17, nullptr, x0, nullptr, dR.x32, xr, dS.x32);
@@ -3493,16 +3482,6 @@ bool bucket_join(qe_ctx* c, const qe_pairs* R, const qe_pairs* S, qe_list* outR,
         uint64_t h[2];
         read_words(c, c->d_scratch + 17, h, 2);   // the ONE round trip of the join
         const uint64_t P = h[0];
-        if (h[1] && use512) {   // a bucket beyond the 512-thread form: the 1024-thread one takes the join
-            dfree(c, oR);
-            dfree(c, oS);
-            dfree(c, x0);
-            dfree(c, x1);
-            dfree(c, xr);
-            use512 = false;
-            attempt--;
-            continue;
-        }
         if (h[1]) {   // a bucket beyond LDS (skew): the sides complete their sorts, the merge joins them
             dfree(c, oR);
             dfree(c, oS);
