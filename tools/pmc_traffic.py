@@ -47,7 +47,7 @@ STAGES = [
     (r"take_u32_kernel", "take_u32"),
     (r"heavy_stats_kernel", "heavy_stats"),
     (r"key_bits_kernel", "sort_keybits"),
-    (r"tl_hjoin_sums_kernel|hjoin_sums_reduce_kernel", "bucket_join_sums"),
+    (r"tl_hjoin_sums_kernel|tl_hjoin_sums_small_kernel|hjoin_sums_reduce_kernel", "bucket_join_sums"),
     (r"gather_u32_kernel", "gather_values"),
     (r"sum_u32_kernel", "checksum"),
     (r"tl_hjoin_kernel|tl_hjoin_chain_kernel", "bucket_join"),
