@@ -1,7 +1,7 @@
-# round 6 working call: the chain join in 512-thread workgroups (three per CU) vs 1024 (two)
+# round 6 working call: the plan's fused scan at 512 threads a workgroup / 8 steps a wave
 set -o pipefail
 mkdir -p gpurun_out
-T=${1:-r06q}
-QE_HJ_NT512=1 timeout -k 10 900 python -u -m pytest -x -q -m gpu --timeout 300 --timeout-method thread tests/test_gpu_bucket_join.py tests/test_gpu_fullsize.py > gpurun_out/${T}_tests.log 2>&1 || exit 1
-REPS=2 bash tools/gpu_ab.sh $T c3 "base:QE_NOTHING=1" "nt512:QE_HJ_NT512=1" || exit 1
+T=${1:-r06s}
+V=$PWD/query-compiler-executor_amd/build/var
+REPS=2 bash tools/gpu_ab.sh $T c3 "base:QE_NOTHING=1" "usb512:QE_LIB_PATH=$V/libqe_usb512.so" "uss8:QE_LIB_PATH=$V/libqe_uss8.so" || exit 1
 echo all-done
