@@ -415,14 +415,19 @@ int e_keys_of(void* u, uint32_t rel, uint32_t col, qe_h vals, qe_h* out) {
         qe_ctx* c = e->c;
         uint64_t kor = 0, kand = 0;
         ck(qe_relation_column_bits(c, (int)rel, (int)col, &kor, &kand), c);
-        const DArr* v = A(vals);
+        DArr* v = A(vals);
         const uint64_t n = v->n;
         uint64_t* k = dalloc_t<uint64_t>(c, std::max<uint64_t>(n, 1));
         const uint32_t* vd = static_cast<const uint32_t*>(v->d);
         bool fused;
         {
             K32Scope k32(c);
-            fused = n && widen_with_hist(c, vd, n, kor, kand, k);
+            // an owned value list (the join's carried key values, released by the plan right after)
+            // is handed to the sort as its u32 key copy (no copy written); a borrowed one is copied
+            const bool own = v->owned && !v->colview;
+            bool adopted = false;
+            fused = n && widen_with_hist(c, vd, n, kor, kand, k, own ? &adopted : nullptr);
+            if (adopted) v->d = nullptr;   // (the sort's PreHist owns the block now)
         }
         if (n && !fused) {
             Timed t(c, "widen_keys", 12.0 * n);
