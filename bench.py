@@ -232,6 +232,9 @@ def run_dist(args):
     dt_stages, _, _, _ = timed_steps()
     stage_stats = ctx.kernel_stats()
     ctx.set_profiling(False)
+    # QE_RT_SITES=1: the host round trips by call site (zero-time stages "rt@file:line")
+    rt_sites = {k[3:]: stage_stats.pop(k)["launches"] / args.steps for k in
+                [k for k in stage_stats if k.startswith("rt@")]}
     dominant = max(((k, v) for k, v in stage_stats.items() if v["ms"] > 0), key=lambda kv: kv[1]["ms"])[0]
     # 2) the timed region: HIP events around the dominant kernel's launches only (its roofline)
     ctx.set_profiling_only(dominant)
@@ -326,6 +329,7 @@ def run_dist(args):
             # the stage table's loop (every launch timed): kernel time and host round trips per step
             "kernel_ms_per_step": round(sum(s["ms"] for _, s in kern) / args.steps, 3),
             "host_round_trips_per_step": stage_stats.get("host_round_trip", {}).get("launches", 0) / args.steps,
+            **({"round_trip_sites_per_step": dict(sorted(rt_sites.items(), key=lambda kv: -kv[1]))} if rt_sites else {}),
             "stage_table_loop_ms_per_step": round(dt_stages / args.steps * 1e3, 3),
             "stages": {k: {"ms_per_step": round(s["ms"] / args.steps, 3)} for k, s in kern[:12]},
             # every stage against the same roofline (algorithmic bytes per launch / mean launch time

@@ -284,9 +284,11 @@ struct Timed {
     ~Timed();
 };
 
-void sync(qe_ctx* c);
-uint64_t read_u64(qe_ctx* c, const uint64_t* d);
-void read_words(qe_ctx* c, const uint64_t* d, uint64_t* h, int n);
+// (the call site is recorded with each host round trip when QE_RT_SITES=1 and profiling is on)
+void sync(qe_ctx* c, const char* file = __builtin_FILE(), int line = __builtin_LINE());
+uint64_t read_u64(qe_ctx* c, const uint64_t* d, const char* file = __builtin_FILE(), int line = __builtin_LINE());
+void read_words(qe_ctx* c, const uint64_t* d, uint64_t* h, int n, const char* file = __builtin_FILE(),
+                int line = __builtin_LINE());
 
 inline unsigned grid_for(uint64_t n, unsigned per_block, unsigned cap = 0x7fffffffu) {
     uint64_t g = (n + per_block - 1) / per_block;

@@ -306,15 +306,14 @@ Timed::~Timed() {
 
 // profiling: a host round trip (the host waits for the GPU) counts as one "launch" of the
 // zero-time stage host_round_trip, so bench.py reports round trips per query beside the kernels
-static void count_round_trip(qe_ctx* c) {
-    if (!c->prof) return;
-    auto it = c->kindex.find("host_round_trip");
+static void count_stage(qe_ctx* c, const std::string& name) {
+    auto it = c->kindex.find(name);
     int k;
     if (it == c->kindex.end()) {
         k = (int)c->kstats.size();
-        c->kindex["host_round_trip"] = k;
+        c->kindex[name] = k;
         KStat s;
-        s.name = "host_round_trip";
+        s.name = name;
         c->kstats.push_back(s);
     } else {
         k = it->second;
@@ -322,8 +321,19 @@ static void count_round_trip(qe_ctx* c) {
     c->kstats[k].launches++;
 }
 
-void sync(qe_ctx* c) {
-    count_round_trip(c);
+// QE_RT_SITES=1: each round trip also counts under "rt@<file>:<line>" (which calls make them)
+static void count_round_trip(qe_ctx* c, const char* file, int line) {
+    if (!c->prof) return;
+    count_stage(c, "host_round_trip");
+    static const bool sites = getenv("QE_RT_SITES") && getenv("QE_RT_SITES")[0] == '1';
+    if (sites) {
+        const char* b = strrchr(file, '/');
+        count_stage(c, std::string("rt@") + (b ? b + 1 : file) + ":" + std::to_string(line));
+    }
+}
+
+void sync(qe_ctx* c, const char* file, int line) {
+    count_round_trip(c, file, line);
     QE_HIP(hipStreamSynchronize(c->stream));
 }
 
@@ -369,8 +379,8 @@ static void wait_event(qe_ctx* c) {
 }
 
 // h[0..n) = d[0..n) (device words), the one host round trip of a result
-void read_words(qe_ctx* c, const uint64_t* d, uint64_t* h, int n) {
-    count_round_trip(c);
+void read_words(qe_ctx* c, const uint64_t* d, uint64_t* h, int n, const char* file, int line) {
+    count_round_trip(c, file, line);
     const int mode = wait_mode();
     if (mode != WAIT_FLAG || n > RET_WORDS) {
         QE_HIP(hipMemcpyAsync(c->h_scratch, d, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
@@ -402,9 +412,9 @@ void read_words(qe_ctx* c, const uint64_t* d, uint64_t* h, int n) {
     for (int i = 0; i < n; i++) h[i] = __atomic_load_n(&c->h_ret[1 + i], __ATOMIC_RELAXED);
 }
 
-uint64_t read_u64(qe_ctx* c, const uint64_t* d) {
+uint64_t read_u64(qe_ctx* c, const uint64_t* d, const char* file, int line) {
     uint64_t v;
-    read_words(c, d, &v, 1);
+    read_words(c, d, &v, 1, file, line);
     return v;
 }
 
