@@ -5,7 +5,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 T=${1:-stamps}
-export QE_LIB_PATH=${QE_LIB_PATH:-$PWD/query-compiler-executor_amd/build/diag/libqe_STAMPS.so}
+export QE_LIB_PATH=${QE_LIB_PATH:-$PWD/query-compiler-executor_amd/build/var/libqe_STAMPS.so}
 ( for k in 1 2 3 4 5 6; do
     echo "=== p1:$k"; QE_STAMP_SEL=p1:$k timeout -k 10 120 python tools/stamps.py --what c3p1 2>&1 | grep -v "^\[stamps\] p2" || exit 1
   done
