@@ -1910,6 +1910,9 @@ constexpr uint32_t HJ_CHAIN_MAX = 64;
 #ifndef QE_HJ_RR_GLOBAL
 #define QE_HJ_RR_GLOBAL 0
 #endif
+#ifndef QE_LB_MAXB_LATE   // (build knob, A/B: 0 reads the lookback-form sort's largest bucket before its passes)
+#define QE_LB_MAXB_LATE 1
+#endif
 #ifndef QE_HJ_SKIP
 #define QE_HJ_SKIP 1   // (build knob, A/B: 0 walks and scans every item of every wave)
 #endif
@@ -2796,11 +2799,13 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
         QE_HIP(hipGetLastError());
         c->zhist_dirty = false;
     }
+#if !QE_LB_MAXB_LATE
     const uint64_t maxb = dfr ? 0 : read_u64(c, d_max);
     if (!dfr && maxb > (uint64_t)TL_CAP) {
         dfree(c, bstart);
         return false;
     }
+#endif
     const uint64_t nt = (n + RTILE - 1) / RTILE;
     uint64_t* w1 = dalloc_t<uint64_t>(c, n);
     uint64_t* w2 = H == TL_H ? dalloc_t<uint64_t>(c, n) : nullptr;
@@ -2838,6 +2843,20 @@ static bool sort_two_level(qe_ctx* c, const K* keys, const uint32_t* vals, uint6
                                sl.status, sl.ticket, sl.epoch);
         QE_HIP(hipGetLastError());
     }
+#if QE_LB_MAXB_LATE
+    // the passes are valid whatever the bucket sizes (their digit bases come from the histogram):
+    // queued before the host reads the largest bucket, as in the lookback-free form, so the GPU
+    // works through the round trip instead of waiting for the next launch
+    const uint64_t maxb = dfr ? 0 : read_u64(c, d_max);
+    if (!dfr && maxb > (uint64_t)TL_CAP) {   // a bucket beyond LDS (skew): plain LSD passes
+        dfree(c, w1);
+        if (w2) dfree(c, w2);
+        dfree(c, kout);
+        dfree(c, vout);
+        dfree(c, bstart);
+        return false;
+    }
+#endif
     if constexpr (sizeof(K) == 8) {
         if (dfr) {   // the per-bucket step waits for the consumer (bucket_join / pairs_need_keys)
             DeferredSort d;
