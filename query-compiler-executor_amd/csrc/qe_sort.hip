@@ -65,6 +65,16 @@ __device__ uint64_t g_store_sink[64];
         if (ok) QE_ST((ptr), (v)); \
     } while (0)
 #endif
+// the two-level second pass's stores (QE_NT_STORE2=1, A/B build: non-temporal there only -- round 3
+// measured them slower in the first pass, 2 % faster in the second)
+#ifdef QE_NT_STORE2
+#define QE_STS2(ok, ptr, sinkp, v)                               \
+    do {                                                         \
+        if (ok) __builtin_nontemporal_store((v), (ptr));         \
+    } while (0)
+#else
+#define QE_STS2(ok, ptr, sinkp, v) QE_STS(ok, ptr, sinkp, v)
+#endif
 
 
 constexpr int RB = 256;          // block
@@ -1569,7 +1579,7 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
 #else
                 const uint32_t p = gofs[dd] + i;
 #endif
-                QE_STS(i < m && (uint64_t)p < n, &wout[p], &g_store_sink[l], wd);
+                QE_STS2(i < m && (uint64_t)p < n, &wout[p], &g_store_sink[l], wd);
                 if (k & 3) dg[k >> 2] |= dd << (8 * (k & 3));
                 else dg[k >> 2] = dd;
                 if (k % 6 == 5) __builtin_amdgcn_sched_barrier(0);   // six slots' LDS reads in flight, not 18
@@ -1583,7 +1593,7 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
             for (int k = 0; k < TL2_ITEMS; k++) {
                 const uint32_t i = (uint32_t)k * TL2_NT + threadIdx.x;
                 const uint32_t p = gofs[(dg[k >> 2] >> (8 * (k & 3))) & 0xFFu] + i;
-                QE_STS(i < m && (uint64_t)p < n, &xout[p], &g_store_sink[l], stage[i]);
+                QE_STS2(i < m && (uint64_t)p < n, &xout[p], &g_store_sink[l], stage[i]);
                 if (k % 6 == 5) __builtin_amdgcn_sched_barrier(0);
             }
         } else if constexpr (CARRY != X_NONE) {
@@ -1608,7 +1618,7 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
                 for (int q = 0; q < TL2_WCH; q++) {
                     const uint32_t i = (uint32_t)(k0 + q) * TL2_NT + threadIdx.x;
                     const bool ok = i < m && (uint64_t)p[q] < n;
-                    QE_STS(ok, &wout[p[q]], &g_store_sink[l], wd[q]);   // (every store issued: counted waits)
+                    QE_STS2(ok, &wout[p[q]], &g_store_sink[l], wd[q]);   // (every store issued: counted waits)
                     if (i < m) reinterpret_cast<uint32_t*>(stage)[2 * i] = p[q];   // slot i now holds its destination
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -1620,7 +1630,7 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
                 for (int j = 0; j < TL2_ITEMS; j++) {   // payload j goes straight to its slot's destination
                     const uint32_t sl = (pos2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
                     const uint32_t dst = reinterpret_cast<const uint32_t*>(stage)[2 * sl];
-                    QE_STS(j * 64 < lim && (uint64_t)dst < n, &xout[dst], &g_store_sink[l], word[j]);
+                    QE_STS2(j * 64 < lim && (uint64_t)dst < n, &xout[dst], &g_store_sink[l], word[j]);
                 }
             } else {
                 // a 32-bit payload joins its destination in the slot's other half, and the slots
@@ -1639,7 +1649,7 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
                         dv[q] = reinterpret_cast<const uint2*>(stage)[(uint32_t)(k0 + q) * TL2_NT + threadIdx.x];
 #pragma unroll
                     for (int q = 0; q < TL2_WCH; q++)
-                        QE_STS((uint32_t)(k0 + q) * TL2_NT + threadIdx.x < m && (uint64_t)dv[q].x < n, &xo[dv[q].x], reinterpret_cast<uint32_t*>(&g_store_sink[l]), dv[q].y);
+                        QE_STS2((uint32_t)(k0 + q) * TL2_NT + threadIdx.x < m && (uint64_t)dv[q].x < n, &xo[dv[q].x], reinterpret_cast<uint32_t*>(&g_store_sink[l]), dv[q].y);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
@@ -1662,8 +1672,8 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
                     const uint32_t i = (uint32_t)(k0 + q) * TL2_NT + threadIdx.x;
                     const bool ok = i < m && (uint64_t)p[q] < n;   // (p < n: never false with consistent offsets)
                     if constexpr (W32)
-                        QE_STS(ok, &reinterpret_cast<uint32_t*>(wout)[p[q]], reinterpret_cast<uint32_t*>(&g_store_sink[l]), (uint32_t)(wd[q] >> 32));
-                    else QE_STS(ok, &wout[p[q]], &g_store_sink[l], wd[q]);
+                        QE_STS2(ok, &reinterpret_cast<uint32_t*>(wout)[p[q]], reinterpret_cast<uint32_t*>(&g_store_sink[l]), (uint32_t)(wd[q] >> 32));
+                    else QE_STS2(ok, &wout[p[q]], &g_store_sink[l], wd[q]);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -1910,6 +1920,9 @@ constexpr uint32_t HJ_CHAIN_MAX = 64;
 #ifndef QE_HJ_RR_GLOBAL
 #define QE_HJ_RR_GLOBAL 0
 #endif
+#ifndef QE_HJ_BUFLOAD
+#define QE_HJ_BUFLOAD 0   // (build knob, A/B: 1 = buffer loads, skipped per wave past the bucket)
+#endif
 #ifndef QE_LB_MAXB_LATE   // (build knob, A/B: 0 reads the lookback-form sort's largest bucket before its passes)
 #define QE_LB_MAXB_LATE 1
 #endif
@@ -1971,6 +1984,47 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
     const uint32_t D = 1u << L, dmask = D - 1u;
     const int w = wave_id(), l = lane_id();
     uint64_t wr[IT], ws[IT];
+#if QE_HJ_BUFLOAD
+    // (A/B build) buffer loads -- rows past the bucket read 0 -- skipped only for a wave whose
+    // item lies wholly past the bucket (a wave-uniform branch), R's words and payloads first
+    uint64_t xv[CARRY ? IT : 1];
+    uint32_t xr[RX ? IT : 1];
+    {
+        const uint32_t wb = (uint32_t)w * 64u;
+        const auto rw = buf_rsrc(wR + r0, mR * 8u);
+        const auto rx4 = buf_rsrc(RX ? xR + r0 : reinterpret_cast<const uint32_t*>(wR), RX ? mR * 4u : 0u);
+        const auto sw = buf_rsrc(wS + s0, mS * 8u);
+        const auto sx = S32 ? buf_rsrc(xS32 + s0, mS * 4u) : buf_rsrc(CARRY ? xS + s0 : wS, CARRY ? mS * 8u : 0u);
+#pragma unroll
+        for (int j = 0; j < IT; j++) {
+            const uint32_t i = (uint32_t)j * NT + threadIdx.x;
+            wr[j] = 0;
+            if constexpr (RX) xr[j] = 0;
+            if ((uint32_t)j * NT + wb < mR) {
+                const uint2 v = buf_load_u2(rw, i * 8u, 0u);
+                wr[j] = (uint64_t)v.y << 32 | v.x;
+                if constexpr (RX) xr[j] = buf_load_u32(rx4, i * 4u, 0u);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < IT; j++) {
+            const uint32_t i = (uint32_t)j * NT + threadIdx.x;
+            ws[j] = 0;
+            if constexpr (CARRY) xv[j] = 0;
+            if ((uint32_t)j * NT + wb < mS) {
+                const uint2 v = buf_load_u2(sw, i * 8u, 0u);
+                ws[j] = (uint64_t)v.y << 32 | v.x;
+                if constexpr (CARRY) {
+                    if constexpr (S32) xv[j] = buf_load_u32(sx, i * 4u, 0u);
+                    else {
+                        const uint2 x = buf_load_u2(sx, i * 8u, 0u);
+                        xv[j] = (uint64_t)x.y << 32 | x.x;
+                    }
+                }
+            }
+        }
+    }
+#else
 #pragma unroll
     for (int j = 0; j < IT; j++) {
         const uint32_t i = (uint32_t)j * NT + threadIdx.x;
@@ -1997,6 +2051,7 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
             xr[j] = i < mR ? xR[r0 + i] : 0u;
         }
     }
+#endif
     for (uint32_t v = threadIdx.x; v < D; v += NT) head[v] = HJ_NONE;
     if (threadIdx.x == 0) s_long = 0;
     __syncthreads();
