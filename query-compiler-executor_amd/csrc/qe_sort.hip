@@ -65,8 +65,9 @@ __device__ uint64_t g_store_sink[64];
         if (ok) QE_ST((ptr), (v)); \
     } while (0)
 #endif
-// the two-level second pass's stores (QE_NT_STORE2=1, A/B build: non-temporal there only -- round 3
-// measured them slower in the first pass, 2 % faster in the second)
+// the two-level second pass's stores (QE_NT_STORE2=1, A/B build: non-temporal there only).  Round 6,
+// same box: sort_pass_carry 3.04 -> 3.67 ms per C3 query, while the kernels reading its output got
+// faster (bucket_join_sums 0.262 -> 0.204) -- a net loss (profiles/r06zc_c3_bench.log)
 #ifdef QE_NT_STORE2
 #define QE_STS2(ok, ptr, sinkp, v)                               \
     do {                                                         \
@@ -1920,9 +1921,6 @@ constexpr uint32_t HJ_CHAIN_MAX = 64;
 #ifndef QE_HJ_RR_GLOBAL
 #define QE_HJ_RR_GLOBAL 0
 #endif
-#ifndef QE_HJ_BUFLOAD
-#define QE_HJ_BUFLOAD 0   // (build knob, A/B: 1 = buffer loads, skipped per wave past the bucket)
-#endif
 #ifndef QE_LB_MAXB_LATE   // (build knob, A/B: 0 reads the lookback-form sort's largest bucket before its passes)
 #define QE_LB_MAXB_LATE 1
 #endif
@@ -1984,47 +1982,6 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
     const uint32_t D = 1u << L, dmask = D - 1u;
     const int w = wave_id(), l = lane_id();
     uint64_t wr[IT], ws[IT];
-#if QE_HJ_BUFLOAD
-    // (A/B build) buffer loads -- rows past the bucket read 0 -- skipped only for a wave whose
-    // item lies wholly past the bucket (a wave-uniform branch), R's words and payloads first
-    uint64_t xv[CARRY ? IT : 1];
-    uint32_t xr[RX ? IT : 1];
-    {
-        const uint32_t wb = (uint32_t)w * 64u;
-        const auto rw = buf_rsrc(wR + r0, mR * 8u);
-        const auto rx4 = buf_rsrc(RX ? xR + r0 : reinterpret_cast<const uint32_t*>(wR), RX ? mR * 4u : 0u);
-        const auto sw = buf_rsrc(wS + s0, mS * 8u);
-        const auto sx = S32 ? buf_rsrc(xS32 + s0, mS * 4u) : buf_rsrc(CARRY ? xS + s0 : wS, CARRY ? mS * 8u : 0u);
-#pragma unroll
-        for (int j = 0; j < IT; j++) {
-            const uint32_t i = (uint32_t)j * NT + threadIdx.x;
-            wr[j] = 0;
-            if constexpr (RX) xr[j] = 0;
-            if ((uint32_t)j * NT + wb < mR) {
-                const uint2 v = buf_load_u2(rw, i * 8u, 0u);
-                wr[j] = (uint64_t)v.y << 32 | v.x;
-                if constexpr (RX) xr[j] = buf_load_u32(rx4, i * 4u, 0u);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < IT; j++) {
-            const uint32_t i = (uint32_t)j * NT + threadIdx.x;
-            ws[j] = 0;
-            if constexpr (CARRY) xv[j] = 0;
-            if ((uint32_t)j * NT + wb < mS) {
-                const uint2 v = buf_load_u2(sw, i * 8u, 0u);
-                ws[j] = (uint64_t)v.y << 32 | v.x;
-                if constexpr (CARRY) {
-                    if constexpr (S32) xv[j] = buf_load_u32(sx, i * 4u, 0u);
-                    else {
-                        const uint2 x = buf_load_u2(sx, i * 8u, 0u);
-                        xv[j] = (uint64_t)x.y << 32 | x.x;
-                    }
-                }
-            }
-        }
-    }
-#else
 #pragma unroll
     for (int j = 0; j < IT; j++) {
         const uint32_t i = (uint32_t)j * NT + threadIdx.x;
@@ -2051,7 +2008,6 @@ tl_hjoin_chain_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restric
             xr[j] = i < mR ? xR[r0 + i] : 0u;
         }
     }
-#endif
     for (uint32_t v = threadIdx.x; v < D; v += NT) head[v] = HJ_NONE;
     if (threadIdx.x == 0) s_long = 0;
     __syncthreads();
