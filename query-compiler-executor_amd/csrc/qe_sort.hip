@@ -3690,6 +3690,18 @@ tl_hjoin_sums_kernel(const uint64_t* __restrict__ wR, const uint32_t* __restrict
 #ifndef QE_HJS_U
 #define QE_HJS_U 4
 #endif
+// Both sides' words are read once, as non-temporal loads: bucket_join_sums 0.260-0.265 -> 0.239 ms
+// per C3 query, same box, two rounds (profiles/r06ze_c3_bench.log; the next query's filter scan,
+// the kernel after it, +0.007).  QE_HJS_NTLOAD=0 (A/B build): default-policy loads.  (The chain
+// join's loads as non-temporal: neutral there, and the kernel after it slower -- not used.)
+#ifndef QE_HJS_NTLOAD
+#define QE_HJS_NTLOAD 1
+#endif
+#if QE_HJS_NTLOAD
+#define QE_HJS_LD(p) __builtin_nontemporal_load(p)
+#else
+#define QE_HJS_LD(p) (*(p))
+#endif
 constexpr int HJS_NT = QE_HJS_NT, HJS_NW = HJS_NT / 64, HJS_U = QE_HJS_U;
 template <int XK>
 __global__ void __launch_bounds__(HJS_NT) __attribute__((amdgpu_waves_per_eu(8)))
@@ -3719,7 +3731,7 @@ tl_hjoin_sums_small_kernel(const uint64_t* __restrict__ wR, const uint32_t* __re
 #pragma unroll
             for (int u = 0; u < HJS_U; u++) {
                 const uint32_t i = i0 + (uint32_t)u * HJS_NT + threadIdx.x;
-                f[u] = i < mR ? (r32 ? wR32[r0 + i] : wR32[2u * (r0 + i) + 1u]) : 0u;
+                f[u] = i < mR ? QE_HJS_LD(r32 ? &wR32[r0 + i] : &wR32[2u * (r0 + i) + 1u]) : 0u;
             }
 #pragma unroll
             for (int u = 0; u < HJS_U; u++)
@@ -3731,9 +3743,9 @@ tl_hjoin_sums_small_kernel(const uint64_t* __restrict__ wR, const uint32_t* __re
 #pragma unroll
             for (int u = 0; u < HJS_U; u++) {
                 const uint32_t i = i0 + (uint32_t)u * HJS_NT + threadIdx.x;
-                ws[u] = i < mS ? wS[s0 + i] : 0ull;
-                if constexpr (XK == 1) xv[u] = i < mS ? xS32[s0 + i] : 0u;
-                else if constexpr (XK == 2) xv[u] = i < mS ? xS[s0 + i] : 0ull;
+                ws[u] = i < mS ? QE_HJS_LD(&wS[s0 + i]) : 0ull;
+                if constexpr (XK == 1) xv[u] = i < mS ? QE_HJS_LD(&xS32[s0 + i]) : 0u;
+                else if constexpr (XK == 2) xv[u] = i < mS ? QE_HJS_LD(&xS[s0 + i]) : 0ull;
                 else xv[u] = 0;
             }
 #pragma unroll
