@@ -310,6 +310,18 @@ constexpr uint32_t AB_CHUNK = 1u << 16;   // giant path: rows per workgroup
 
 __device__ __forceinline__ uint32_t ab_val(uint64_t w, uint32_t dmask) { return (uint32_t)(w >> 32) & dmask; }
 
+// NT: the rows' last read (non-temporal loads: MI355X_MICROARCH "nt-weights"; the aggregate last
+// join's words measured 0.26 -> 0.239 ms per C3 query that way, profiles/r06ze_c3_bench.log)
+#ifndef QE_AB_NT
+#define QE_AB_NT 1   // (build knob, A/B: 0 = default-policy loads on the second read too)
+#endif
+template <bool NT = false>
+__device__ __forceinline__ uint64_t ab_ld(const uint64_t* p) {
+    if constexpr (NT && QE_AB_NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+template <bool NT = false>
 __device__ __forceinline__ void ab_count(const uint64_t* __restrict__ w, uint32_t m, uint32_t dmask,
                                          uint32_t* __restrict__ cnt) {
     const int l = lane_id();
@@ -318,7 +330,7 @@ __device__ __forceinline__ void ab_count(const uint64_t* __restrict__ w, uint32_
 #pragma unroll
         for (int u = 0; u < AB_U; u++) {
             const uint32_t i = i0 + (uint32_t)u * AB_NT;
-            x[u] = i < m ? w[i] : 0;
+            x[u] = i < m ? ab_ld<NT>(&w[i]) : 0;
         }
 #pragma unroll
         for (int u = 0; u < AB_U; u++) {
@@ -339,6 +351,7 @@ __device__ __forceinline__ void ab_count(const uint64_t* __restrict__ w, uint32_
 }
 
 // rows of w[0..m): a0 += cnt[k], a1 += (u32) value * cnt[k]
+template <bool NT = false>
 __device__ __forceinline__ void ab_lookup(const uint64_t* __restrict__ w, uint32_t m, uint32_t dmask,
                                           const uint32_t* __restrict__ cnt, uint64_t& a0, uint64_t& a1) {
     for (uint32_t i0 = threadIdx.x; i0 < m; i0 += AB_NT * AB_U) {
@@ -346,7 +359,7 @@ __device__ __forceinline__ void ab_lookup(const uint64_t* __restrict__ w, uint32
 #pragma unroll
         for (int u = 0; u < AB_U; u++) {
             const uint32_t i = i0 + (uint32_t)u * AB_NT;
-            x[u] = i < m ? w[i] : 0;
+            x[u] = i < m ? ab_ld<NT>(&w[i]) : 0;
         }
 #pragma unroll
         for (int u = 0; u < AB_U; u++) {
@@ -419,9 +432,9 @@ __global__ void __launch_bounds__(AB_NT) ab_bucket_kernel(const uint64_t* __rest
     __syncthreads();
     ab_zero(cnt, D);
     __syncthreads();
-    ab_count(bR, mR, dmask, cnt);
+    ab_count<true>(bR, mR, dmask, cnt);   // (each side's second and last read)
     __syncthreads();
-    ab_lookup(bS, mS, dmask, cnt, dummy, sS);
+    ab_lookup<true>(bS, mS, dmask, cnt, dummy, sS);
     ab_reduce3(pairs, sR, sS, part + (uint64_t)b * 3, false);
 }
 
