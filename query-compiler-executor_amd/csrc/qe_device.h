@@ -57,12 +57,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, uint32
     const uint32_t n = __builtin_amdgcn_readfirstlane(bytes);
     return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, (int)n, 0x00020000);
 }
+template <int AUX = QE_LOAD_AUX>
 __device__ __forceinline__ uint2 buf_load_u2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    const qe_v2u x = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, QE_LOAD_AUX);
+    const qe_v2u x = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, AUX);
     return make_uint2(x.x, x.y);
 }
+template <int AUX = QE_LOAD_AUX>
 __device__ __forceinline__ uint32_t buf_load_u32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, QE_LOAD_AUX);
+    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, AUX);
 }
 typedef unsigned int qe_v4u __attribute__((ext_vector_type(4)));
 // (a 16-B load that crosses the end of the range: use it only where the range is whole 16-B units)

@@ -867,6 +867,12 @@ struct LocalRounds {
 // UN0: the first round ranks unstably (one LDS atomic per element instead of up to 8 ballots) -- a
 // deferred sort's completion, whose consumer (the plan's merge) needs no order among equal keys;
 // later rounds stay stable (they must keep the earlier rounds' order)
+// (A/B build: QE_LOCAL_NT=1 reads the bucket's words -- their last read -- non-temporal)
+#ifdef QE_LOCAL_NT
+#define QE_LOCAL_LD(p) __builtin_nontemporal_load(p)
+#else
+#define QE_LOCAL_LD(p) (*(p))
+#endif
 template <typename K, int IN, int NT = TL_NT, bool UN0 = false>
 __global__ void __launch_bounds__(NT) tl_local_kernel(const uint64_t* __restrict__ win, const K* __restrict__ kin,
                                                          const uint32_t* __restrict__ vin, K* __restrict__ kout,
@@ -891,7 +897,7 @@ __global__ void __launch_bounds__(NT) tl_local_kernel(const uint64_t* __restrict
         const uint32_t i = wbase + (uint32_t)j * 64 + l;
         const bool ok = (uint32_t)j < jm && i < m;
         if (IN == IN_WORD) {
-            word[j] = ok ? win[s0 + i] : 0;
+            word[j] = ok ? QE_LOCAL_LD(&win[s0 + i]) : 0;
         } else {
             const uint64_t k = ok ? (uint64_t)kin[i] : 0;
             const uint32_t v = IN == IN_KV ? (ok ? vin[i] : 0u) : i;
@@ -1398,6 +1404,12 @@ __global__ void __launch_bounds__(1024) cs_single_kernel(CSJobs js, const uint32
 #ifndef QE_TL2_NT
 #define QE_TL2_NT 512
 #endif
+// (A/B build: QE_P2_LOAD_NT=1 reads the first pass's words and payloads -- their last read --
+// with non-temporal loads)
+#ifndef QE_P2_LOAD_NT
+#define QE_P2_LOAD_NT 0
+#endif
+constexpr int QE_P2_AUX = QE_P2_LOAD_NT ? 2 : QE_LOAD_AUX;
 constexpr int TL2_NT = QE_TL2_NT, TL2_ITEMS = QE_TL2_ITEMS, TL2_TILE = TL2_NT * TL2_ITEMS;   // 9216: mean 8192 + 11 sd
 #ifndef QE_TL2_WCH
 #define QE_TL2_WCH 6
@@ -1466,9 +1478,9 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
             const auto rw = W32 ? buf_rsrc(reinterpret_cast<const uint32_t*>(win) + base, m * 4u) : buf_rsrc(win + base, m * 8u);
 #pragma unroll
             for (int j = 0; j < TL2_ITEMS; j++) {
-                if constexpr (W32) word[j] = (uint64_t)buf_load_u32(rw, o0 * 4u, (uint32_t)j * 256u) << 32;
+                if constexpr (W32) word[j] = (uint64_t)buf_load_u32<QE_P2_AUX>(rw, o0 * 4u, (uint32_t)j * 256u) << 32;
                 else {
-                    const uint2 v = buf_load_u2(rw, o0 * 8u, (uint32_t)j * 512u);
+                    const uint2 v = buf_load_u2<QE_P2_AUX>(rw, o0 * 8u, (uint32_t)j * 512u);
                     word[j] = (uint64_t)v.y << 32 | v.x;
                 }
             }
@@ -1559,10 +1571,10 @@ __global__ void __launch_bounds__(TL2_NT, TL2_WPE) tl_pass2_kernel(const uint64_
 #pragma unroll
             for (int j = 0; j < TL2_ITEMS; j++) {
                 if constexpr (CARRY == X64) {
-                    const uint2 v = buf_load_u2(rx, o0 * 8u, (uint32_t)j * 512u);
+                    const uint2 v = buf_load_u2<QE_P2_AUX>(rx, o0 * 8u, (uint32_t)j * 512u);
                     word[j] = (uint64_t)v.y << 32 | v.x;
                 } else {
-                    xw[j] = buf_load_u32(rx, o0 * 4u, (uint32_t)j * 256u);
+                    xw[j] = buf_load_u32<QE_P2_AUX>(rx, o0 * 4u, (uint32_t)j * 256u);
                 }
             }
         }
