@@ -867,12 +867,6 @@ struct LocalRounds {
 // UN0: the first round ranks unstably (one LDS atomic per element instead of up to 8 ballots) -- a
 // deferred sort's completion, whose consumer (the plan's merge) needs no order among equal keys;
 // later rounds stay stable (they must keep the earlier rounds' order)
-// (A/B build: QE_LOCAL_NT=1 reads the bucket's words -- their last read -- non-temporal)
-#ifdef QE_LOCAL_NT
-#define QE_LOCAL_LD(p) __builtin_nontemporal_load(p)
-#else
-#define QE_LOCAL_LD(p) (*(p))
-#endif
 template <typename K, int IN, int NT = TL_NT, bool UN0 = false>
 __global__ void __launch_bounds__(NT) tl_local_kernel(const uint64_t* __restrict__ win, const K* __restrict__ kin,
                                                          const uint32_t* __restrict__ vin, K* __restrict__ kout,
@@ -897,7 +891,7 @@ __global__ void __launch_bounds__(NT) tl_local_kernel(const uint64_t* __restrict
         const uint32_t i = wbase + (uint32_t)j * 64 + l;
         const bool ok = (uint32_t)j < jm && i < m;
         if (IN == IN_WORD) {
-            word[j] = ok ? QE_LOCAL_LD(&win[s0 + i]) : 0;
+            word[j] = ok ? win[s0 + i] : 0;
         } else {
             const uint64_t k = ok ? (uint64_t)kin[i] : 0;
             const uint32_t v = IN == IN_KV ? (ok ? vin[i] : 0u) : i;
